@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Headline benchmark: multi-command utterances through the on-GPU voice pipeline.
+
+BASELINE.json metric: "ms per added command (multi-cmd utterance) + utterances/sec
+at 1/2/4/8 MI355X"; config 4: 64 concurrent audio streams, Whisper-large-v3 +
+Llama-3-8B intent, DP=8 (8 streams per GPU -> weak scaling: per-GPU work fixed).
+
+One step = every rank processes its batch of B utterances end to end:
+  rank-0 router scatters the step's PCM16 over RCCL -> fused PCM convert/RMS ->
+  log-mel -> Whisper-large-v3 encoder + teacher-forced greedy decode ->
+  wake-word strip -> ONE grammar-constrained Llama-3-8B multi-command decode
+  (verbatim reference prompt, jump-forward JSON) -> command queue with rollback
+  -> NATS publishes (embedded broker) -> per-utterance records all_gathered.
+
+Prints ONE JSON line (rank 0). ``value`` = utterances/s over all GPUs;
+ms-per-added-command (both BASELINE.md definitions) is reported alongside.
+Random-init weights, synthetic speech-like audio (no network / checkpoints).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from loqa_hub_amd.engine.llm_engine import LLMEngine  # noqa: E402
+from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline, added_command_stats  # noqa: E402
+from loqa_hub_amd.engine.stt_engine import STTEngine  # noqa: E402
+from loqa_hub_amd.engine.synthetic import make_batch  # noqa: E402
+from loqa_hub_amd.messaging.nats_server import NATSServer  # noqa: E402
+from loqa_hub_amd.messaging.nats_service import NATSService  # noqa: E402
+from loqa_hub_amd.models.configs import llama_config, whisper_config  # noqa: E402
+from loqa_hub_amd.parallel import dist as pdist  # noqa: E402
+from loqa_hub_amd.parallel.dp_router import gather_records, scatter_pcm, slot_len_for  # noqa: E402
+
+BASELINE_MS_PER_ADDED_COMMAND = 200.0
+
+
+def start_broker() -> tuple[int, threading.Thread]:
+    ready = threading.Event()
+    box = {}
+
+    def run():
+        loop = asyncio.new_event_loop()
+        srv = loop.run_until_complete(NATSServer("127.0.0.1", 0).start())
+        box["port"] = srv.port
+        ready.set()
+        loop.run_forever()
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    ready.wait(10)
+    return box["port"], t
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch-per-gpu", type=int, default=8)
+    ap.add_argument("--stt", default="whisper-large-v3")
+    ap.add_argument("--llm", default="llama3-8b")
+    ap.add_argument("--mix", default="1,2,3,4", help="commands per utterance, cycled")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
+    args = ap.parse_args(argv)
+
+    if args.cpu_smoke:
+        args.stt, args.llm = "test-whisper", "test-tiny"
+    info = pdist.init_distributed(prefer_gpu=not args.cpu_smoke)
+    dev = info.device
+    if dev.type == "cuda":
+        torch.backends.cuda.matmul.allow_tf32 = False
+
+    # event bus: embedded NATS broker on rank 0, every rank connects
+    port = start_broker()[0] if info.rank == 0 else 0
+    if info.world > 1:
+        obj = [port]
+        torch.distributed.broadcast_object_list(obj, src=0)
+        port = obj[0]
+    loop = asyncio.new_event_loop()
+    nats = NATSService(f"nats://127.0.0.1:{port}")
+    loop.run_until_complete(nats.connect())
+
+    B = args.batch_per_gpu
+    mix = [int(x) for x in args.mix.split(",")]
+    t_init = time.perf_counter()
+    stt = STTEngine(whisper_config(args.stt), dev, seed=args.seed, max_batch=max(B, 8))
+    llm = LLMEngine(llama_config(args.llm), dev, seed=args.seed, max_seqs=max(B, 8), max_seq_len=1024,
+                    use_graphs=not args.no_graphs)
+    pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_init = time.perf_counter() - t_init
+
+    utts = make_batch(args.seed, info.world * B, mix)
+    mine = utts[info.rank * B:(info.rank + 1) * B]
+    per_rank = [[u.pcm for u in utts[r * B:(r + 1) * B]] for r in range(info.world)]
+    slot = slot_len_for(per_rank)
+    all_jobs: list[PipelineJob] = []
+
+    def step(record: bool) -> None:
+        dpcm = scatter_pcm(info, per_rank if info.rank == 0 else None, slot)
+        jobs = [PipelineJob(u.relay_id, f"req-{info.rank}-{i}", u.pcm, transcript_hint=u.text)
+                for i, u in enumerate(mine)]
+        loop.run_until_complete(pipe.process(jobs, device_pcm=dpcm))
+        rec = torch.tensor([[j.n_commands, j.n_expected, float(j.queue is not None and j.queue.success),
+                             (j.t.get("queue_done", j.t["start"]) - j.t["start"]) * 1e3]
+                            for j in jobs], dtype=torch.float64)
+        gathered = gather_records(info, rec)
+        if record:
+            all_jobs.extend(jobs)
+            step.records.append(gathered.cpu())
+
+    step.records = []
+    for _ in range(args.warmup):
+        step(False)
+    pdist.barrier(info)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    pdist.barrier(info)
+    elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
+
+    stats = added_command_stats(all_jobs)
+    recs = torch.cat(step.records, 0) if step.records else torch.zeros(0, 4)
+    total_utts = info.world * B * args.steps
+    value = total_utts / elapsed
+    ok = float(recs[:, 2].mean()) if len(recs) else 0.0
+    cmd_match = float((recs[:, 0] == recs[:, 1]).double().mean()) if len(recs) else 0.0
+    e2e = stats["e2e_marginal_ms_per_added_command"]
+    e2e = pdist.max_over_ranks(info, e2e if e2e is not None else -1.0)
+    ref = stats["ref_equiv_ms_per_added_command"]
+    ref = pdist.max_over_ranks(info, ref if ref is not None else -1.0)
+    if info.is_main:
+        out = {
+            "metric": "utterances_per_sec (multi-command utterances; ms per added command reported alongside)",
+            "value": round(value, 3),
+            "unit": "utterances/s",
+            "n_gpus": info.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT, grammar-constrained LLM)",
+            "config": {"model": f"{args.stt} + {args.llm}", "global_batch": info.world * B,
+                       "seq_len": 1500, "parallelism": f"dp{info.world}",
+                       "commands_mix": mix, "baseline_config": 4},
+            "ms_per_added_command_e2e_marginal": None if e2e < 0 else round(e2e, 3),
+            "ms_per_added_command_ref_equiv": None if ref < 0 else round(ref, 4),
+            "baseline_ms_per_added_command": BASELINE_MS_PER_ADDED_COMMAND,
+            "added_command_speedup_vs_baseline": None if e2e <= 0 else round(BASELINE_MS_PER_ADDED_COMMAND / e2e, 3),
+            "queue_success_rate": round(ok, 4),
+            "command_count_match_rate": round(cmd_match, 4),
+            "llm_stats": llm.stats,
+            "init_s": round(t_init, 2),
+        }
+        print(json.dumps(out), flush=True)
+    loop.run_until_complete(nats.close())
+    pdist.shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,339 @@
+// Flash attention forward for CDNA4.
+//
+// One kernel family covers every attention in the hub:
+//   * PREFILL mode  - 128 query rows of ONE head per workgroup (Whisper encoder,
+//                     Llama prompt prefill, VITS text encoder). Causal or not.
+//   * GROUPED mode  - all query heads of ONE kv head x a few query tokens per
+//                     workgroup (decode / jump-forward extend, GQA), with
+//                     split-K over the context and a separate combine kernel.
+// K/V come either from a contiguous [T, H_kv, D] tensor (cu_k offsets) or from
+// the paged KV cache [n_blocks, H_kv, BLK, D] through a block table.
+//
+// MFMA formulation (v_mfma_f32_32x32x16_bf16, 4 waves, 32 query rows per wave):
+//   S^T = K * Q^T  : A = K rows (ds_read_b128 from a padded LDS tile),
+//                    B = Q^T fragment kept in VGPRs for the whole KV loop.
+//                    The query lands on the MFMA lane, so the softmax row
+//                    max/sum is in-register + one lane^32 exchange.
+//   O^T += V^T * P^T : the S^T accumulator, exp2'ed and packed to bf16, IS the B
+//                    operand (guide §3 "accumulator tile as next operand"); the
+//                    V^T fragment comes from ds_read_b64_tr_b16 transposed reads
+//                    of the row-major V tile (guide T10). O^T also has the
+//                    query on the lane, so the online-softmax rescale is a
+//                    per-lane scalar multiply.
+// LDS rows are padded (K: +16 B, V: +64 B) so that both the b128 row reads and
+// the tr_b16 reads are bank-conflict free (guide §2, G4).
+#include "common.h"
+
+#define ATT_THREADS 256
+#define ATT_WAVES 4
+#define KV_TILE 64
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+struct AttnParams {
+  const bf16_t* q;
+  long long q_stride;  // elements between consecutive query tokens (head stride = D)
+  const bf16_t* k;
+  const bf16_t* v;
+  long long kv_stride;  // contiguous mode: elements between tokens
+  bf16_t* o;
+  long long o_stride;
+  const int* cu_q;          // [B+1]
+  const int* cu_k;          // [B+1] contiguous mode (or [B] starts when ctx_lens given)
+  const int* ctx_lens;      // [B]   paged mode
+  const int* block_tables;  // [B, max_blocks]
+  int max_blocks;
+  int blk;
+  int Hq, Hkv;
+  float scale_log2;
+  int causal;
+  int split_keys;  // GROUPED: keys per split (multiple of KV_TILE)
+  int num_splits;
+  float* part_o;   // [num_splits, Tq, Hq, D]
+  float* part_ml;  // [num_splits, Tq, Hq, 2]
+  int total_q;
+};
+
+template <int D>
+struct AttnSmem {
+  bf16_t k[KV_TILE][D + 8];
+  bf16_t v[KV_TILE][D + 32];
+};
+
+__device__ __forceinline__ float16v mfma32(const bf16x8& a, const bf16x8& b, const float16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int D, bool PAGED, bool GROUPED>
+__global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) AttnSmem<D> sm;
+  constexpr int NS = D / 16;  // k-slices of the QK^T product
+  constexpr int NDT = D / 32; // 32-wide d tiles of O^T
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = lane >> 5;
+  const int b = blockIdx.z;
+  const int q0 = p.cu_q[b];
+  const int qlen = p.cu_q[b + 1] - q0;
+  int k0 = 0, klen;
+  if (PAGED) {
+    klen = p.ctx_lens[b];
+  } else {
+    // contiguous K/V: start cu_k[b]; length ctx_lens[b] if given, else cu_k[b+1]-cu_k[b]
+    k0 = p.cu_k[b];
+    klen = p.ctx_lens ? p.ctx_lens[b] : p.cu_k[b + 1] - k0;
+  }
+  const int G = p.Hq / p.Hkv;
+
+  // ---- row mapping: this lane's query row (token index within seq, head)
+  const int r = wave * 32 + (lane & 31);
+  int qi, head, kvh;
+  int row_lo, row_hi;  // token range covered by the workgroup (for causal bound)
+  if (GROUPED) {
+    kvh = blockIdx.y;
+    qi = r / G;
+    head = kvh * G + (r - qi * G);
+    row_lo = 0;
+    row_hi = min(qlen, (ATT_WAVES * 32) / G) - 1;
+  } else {
+    head = blockIdx.y;
+    kvh = head / G;
+    qi = blockIdx.x * (ATT_WAVES * 32) + r;
+    row_lo = blockIdx.x * (ATT_WAVES * 32);
+    row_hi = min(qlen - 1, row_lo + ATT_WAVES * 32 - 1);
+  }
+  if (!GROUPED && row_lo >= qlen) return;
+  const bool row_valid = GROUPED ? (qi < qlen && (ATT_WAVES * 32) / G > 0 && r < (ATT_WAVES * 32 / G) * G)
+                                 : (qi < qlen);
+  const int qpos = klen - qlen + qi;  // absolute position for causal masking
+
+  // ---- key range of this workgroup
+  int kbeg = 0, kend = klen;
+  int split = 0;
+  if (GROUPED) {
+    split = blockIdx.x;
+    kbeg = split * p.split_keys;
+    kend = min(klen, kbeg + p.split_keys);
+  }
+  if (p.causal) kend = min(kend, klen - qlen + row_hi + 1);
+
+  // ---- Q^T fragments (B operand): lane (query, h) holds Q[q][16s + 8h .. +7]
+  bf16x8 qf[NS];
+  {
+    const bf16_t* qrow = p.q + (size_t)(q0 + (row_valid ? qi : 0)) * p.q_stride + (size_t)head * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4 v = row_valid ? *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      qf[s] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+
+  float16v acc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  const int* btab = PAGED ? p.block_tables + (size_t)b * p.max_blocks : nullptr;
+  constexpr int CH = D / 8;  // 16-byte chunks per row
+
+  for (int kt = kbeg; kt < kend; kt += KV_TILE) {
+    // ---- stage K and V tile (64 keys) into LDS
+    __syncthreads();
+#pragma unroll
+    for (int c = threadIdx.x; c < KV_TILE * CH; c += ATT_THREADS) {
+      const int kr = c / CH, cc = (c - kr * CH) * 8;
+      const int key = kt + kr;
+      uint4 kv4 = make_uint4(0, 0, 0, 0), vv4 = make_uint4(0, 0, 0, 0);
+      if (key < kend) {
+        size_t off;
+        if (PAGED) {
+          const int bi = key / p.blk, bo = key - bi * p.blk;
+          off = (((size_t)btab[bi] * p.Hkv + kvh) * p.blk + bo) * D + cc;
+        } else {
+          off = (size_t)(k0 + key) * p.kv_stride + (size_t)kvh * D + cc;
+        }
+        kv4 = *reinterpret_cast<const uint4*>(p.k + off);
+        vv4 = *reinterpret_cast<const uint4*>(p.v + off);
+      }
+      *reinterpret_cast<uint4*>(&sm.k[kr][cc]) = kv4;
+      *reinterpret_cast<uint4*>(&sm.v[kr][cc]) = vv4;
+    }
+    __syncthreads();
+
+    // ---- S^T = K Q^T for the two 32-key halves
+    float16v st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sm.k[32 * t + (lane & 31)][16 * s + 8 * h]);
+        st[t] = mfma32(a, qf[s], st[t]);
+      }
+    }
+    // ---- mask + online softmax (row = this lane's query)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int key = kt + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * h;
+        float sv = st[t][j] * p.scale_log2;
+        if (key >= kend || (p.causal && key > qpos)) sv = -INFINITY;
+        st[t][j] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = exp2f(st[t][8 * s2 + j] - m_new);
+          ls += e;
+          pf[t][s2][j] = (__bf16)e;
+        }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+
+    // ---- O^T += V^T P^T
+    const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int c0 = 32 * dt + 16 * (g & 1) + 4 * (li & 3);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int kb = 32 * t + 16 * s2 + 4 * h + (li >> 2);
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(&sm.v[kb][c0]));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(&sm.v[kb + 8][c0]));
+          short8 a8;
+          a8[0] = lo[0]; a8[1] = lo[1]; a8[2] = lo[2]; a8[3] = lo[3];
+          a8[4] = hi[0]; a8[5] = hi[1]; a8[6] = hi[2]; a8[7] = hi[3];
+          acc[dt] = mfma32(*reinterpret_cast<bf16x8*>(&a8), pf[t][s2], acc[dt]);
+        }
+    }
+  }
+
+  if (!row_valid) return;
+  const size_t tok = (size_t)(q0 + qi);
+  if (GROUPED && p.num_splits > 1) {
+    // unnormalised partial result + (m, l) for the combine kernel
+    float* po = p.part_o + (((size_t)split * p.total_q + tok) * p.Hq + head) * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(po + d0) =
+            make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+      }
+    if (h == 0) {
+      float* pm = p.part_ml + (((size_t)split * p.total_q + tok) * p.Hq + head) * 2;
+      pm[0] = m_run;
+      pm[1] = l_run;
+    }
+    return;
+  }
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16_t* orow = p.o + tok * p.o_stride + (size_t)head * D;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      uint2 w;
+      w.x = pack_bf16x2(acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv);
+      w.y = pack_bf16x2(acc[dt][4 * g4 + 2] * inv, acc[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<uint2*>(orow + d0) = w;
+    }
+}
+
+// Combine split-K partials: one workgroup of D threads per (token, head).
+__global__ void attn_combine_kernel(const float* __restrict__ part_o,
+                                    const float* __restrict__ part_ml, bf16_t* __restrict__ o,
+                                    long long o_stride, int total_q, int Hq, int D,
+                                    int num_splits) {
+  const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
+  float mstar = -1e30f;
+  for (int s = 0; s < num_splits; ++s)
+    mstar = fmaxf(mstar, part_ml[(((size_t)s * total_q + tok) * Hq + head) * 2]);
+  float l = 0.f, acc = 0.f;
+  for (int s = 0; s < num_splits; ++s) {
+    const size_t idx = ((size_t)s * total_q + tok) * Hq + head;
+    const float w = exp2f(part_ml[idx * 2] - mstar);
+    l += w * part_ml[idx * 2 + 1];
+    acc += w * part_o[idx * D + d];
+  }
+  o[(size_t)tok * o_stride + (size_t)head * D + d] = f2bf(l > 0.f ? acc / l : 0.f);
+}
+
+template <int D, bool PAGED, bool GROUPED>
+static int launch_attn(const AttnParams& p, int B, int max_q, hipStream_t s) {
+  dim3 grid;
+  if (GROUPED)
+    grid = dim3(p.num_splits, p.Hkv, B);
+  else
+    grid = dim3((max_q + ATT_WAVES * 32 - 1) / (ATT_WAVES * 32), p.Hq, B);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, PAGED, GROUPED>), grid, dim3(ATT_THREADS), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+// mode: 0 = prefill (rows = q tokens of one head), 1 = grouped decode/extend.
+extern "C" int loqa_attention(const void* q, long long q_stride, const void* k, const void* v,
+                              long long kv_stride, void* o, long long o_stride, const int* cu_q,
+                              const int* cu_k, const int* ctx_lens, const int* block_tables,
+                              int max_blocks, int blk, int B, int max_q, int Hq, int Hkv, int D,
+                              float scale, int causal, int mode, int split_keys, int num_splits,
+                              float* part_o, float* part_ml, int total_q, hipStream_t s) {
+  if (B <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  const bool paged = block_tables != nullptr;
+  if (paged && (!ctx_lens || blk <= 0)) return (int)hipErrorInvalidValue;
+  if (!paged && !cu_k) return (int)hipErrorInvalidValue;
+  if (mode == 1) {
+    if ((ATT_WAVES * 32) / (Hq / Hkv) < max_q) return (int)hipErrorInvalidValue;
+    if (num_splits < 1 || split_keys % KV_TILE != 0) return (int)hipErrorInvalidValue;
+    if (num_splits > 1 && (!part_o || !part_ml)) return (int)hipErrorInvalidValue;
+  }
+  AttnParams p;
+  p.q = (const bf16_t*)q; p.q_stride = q_stride;
+  p.k = (const bf16_t*)k; p.v = (const bf16_t*)v; p.kv_stride = kv_stride;
+  p.o = (bf16_t*)o; p.o_stride = o_stride;
+  p.cu_q = cu_q; p.cu_k = cu_k; p.ctx_lens = ctx_lens; p.block_tables = block_tables;
+  p.max_blocks = max_blocks; p.blk = blk; p.Hq = Hq; p.Hkv = Hkv;
+  p.scale_log2 = scale * 1.4426950408889634f; p.causal = causal;
+  p.split_keys = split_keys; p.num_splits = num_splits; p.part_o = part_o; p.part_ml = part_ml;
+  p.total_q = total_q;
+  int rc;
+#define DISPATCH(DD)                                                                    \
+  if (mode == 0) rc = paged ? launch_attn<DD, true, false>(p, B, max_q, s)              \
+                            : launch_attn<DD, false, false>(p, B, max_q, s);            \
+  else rc = paged ? launch_attn<DD, true, true>(p, B, max_q, s)                         \
+                  : launch_attn<DD, false, true>(p, B, max_q, s);
+  if (D == 64) { DISPATCH(64) } else { DISPATCH(128) }
+#undef DISPATCH
+  if (rc != 0) return rc;
+  if (mode == 1 && num_splits > 1) {
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(total_q, Hq), dim3(D), 0, s, part_o, part_ml,
+                       (bf16_t*)o, o_stride, total_q, Hq, D, num_splits);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
+}

@@ -1,0 +1,276 @@
+// Memory-bound fused elementwise kernels:
+//   K1  pcm16 -> f32 conversion fused with the per-utterance sum of squares used
+//       by wake-word arbitration RMS (reference: audio_service.go:1048-1101 and
+//       :818-852 do these as two per-sample Go loops).
+//   K6  bias + GELU (+ sinusoidal position add) epilogue for Whisper conv/MLP.
+//   K11 RoPE on q/k + paged KV-cache append (K16), reading the fused QKV GEMM
+//       output in place.
+//   K14 SwiGLU gate: silu(gate) * up.
+//   K15 grammar-masked argmax over the vocabulary (jump-forward JSON decoding).
+// All bf16 traffic is 8-16 bytes per lane (guide G13).
+#include "common.h"
+#include <float.h>
+
+// ---------------------------------------------------------------- K14 SwiGLU
+// in: [T, 2F] = [gate | up], out: [T, F]
+__global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                int F, long long total_vec) {
+  const int fv = F >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / fv;
+    const int c = (int)(i - row * fv);
+    const uint4* g = reinterpret_cast<const uint4*>(in + row * 2 * F) + c;
+    const uint4* u = reinterpret_cast<const uint4*>(in + row * 2 * F + F) + c;
+    float a[8], b[8], o[8];
+    unpack8(*g, a);
+    unpack8(*u, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
+    reinterpret_cast<uint4*>(out + row * F)[c] = pack8(o);
+  }
+}
+
+extern "C" int loqa_silu_mul(const void* in, void* out, long long rows, int F, hipStream_t s) {
+  if (F % 8 != 0 || rows <= 0) return (int)hipErrorInvalidValue;
+  const long long tv = rows * (F / 8);
+  const int threads = 256;
+  long long blocks = (tv + threads - 1) / threads;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(threads), 0, s,
+                     (const bf16_t*)in, (bf16_t*)out, F, tv);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ K6 bias+GELU(+pos)
+// x[T, F] <- gelu(x + bias) + pos[(t % pos_period), :]   (bias, pos optional)
+__global__ void gelu_bias_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ bias,
+                                 const bf16_t* __restrict__ pos, int F, int pos_period,
+                                 long long total_vec) {
+  const int fv = F >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / fv;
+    const int c = (int)(i - row * fv);
+    uint4* p = reinterpret_cast<uint4*>(x + row * F) + c;
+    float v[8];
+    unpack8(*p, v);
+    if (bias) {
+      float b[8];
+      unpack8(reinterpret_cast<const uint4*>(bias)[c], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += b[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+    if (pos) {
+      float q[8];
+      const long long prow = row % pos_period;
+      unpack8(reinterpret_cast<const uint4*>(pos + prow * F)[c], q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += q[j];
+    }
+    *p = pack8(v);
+  }
+}
+
+extern "C" int loqa_gelu_bias(void* x, const void* bias, const void* pos, long long rows, int F,
+                              int pos_period, hipStream_t s) {
+  if (F % 8 != 0 || rows <= 0 || (pos && pos_period <= 0)) return (int)hipErrorInvalidValue;
+  const long long tv = rows * (F / 8);
+  long long blocks = (tv + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(gelu_bias_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (bf16_t*)x,
+                     (const bf16_t*)bias, (const bf16_t*)pos, F, pos_period, tv);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------ K11/K16 RoPE + KV append
+// qkv: [T, stride] with q at [0, Hq*D), k at [Hq*D, (Hq+Hkv)*D), v after it.
+// q (and k) are rotated in place (NeoX rotate-half pairing i <-> i + D/2);
+// k and v are then written to the paged cache [nblocks, Hkv, blk, D] at
+// slot = slots[t] (= block * blk + offset). cs == nullptr disables the rotation
+// (Whisper decoder, learned positions). slots[t] < 0 skips the append (padding).
+__global__ void rope_kv_append_kernel(bf16_t* __restrict__ qkv, int stride,
+                                      const int* __restrict__ positions,
+                                      const float2* __restrict__ cs, bf16_t* __restrict__ kc,
+                                      bf16_t* __restrict__ vc, const int* __restrict__ slots,
+                                      int Hq, int Hkv, int D, int blk) {
+  const int t = blockIdx.x;
+  bf16_t* row = qkv + (size_t)t * stride;
+  const int half = D >> 1;
+  const int pv = half >> 2;  // 4-element groups per half-head
+  const int slot = slots ? slots[t] : -1;
+  const float2* csr = cs ? cs + (size_t)positions[t] * half : nullptr;
+  const int nq = Hq * pv, nk = Hkv * pv;
+  // q and k rotation (k rotation only materialised into the cache).
+  for (int i = threadIdx.x; i < nq + nk; i += blockDim.x) {
+    const bool isk = i >= nq;
+    const int ii = isk ? i - nq : i;
+    const int h = ii / pv, c = (ii - h * pv) * 4;
+    bf16_t* base = row + (isk ? Hq * D : 0) + h * D;
+    uint2 lo = *reinterpret_cast<const uint2*>(base + c);
+    uint2 hi = *reinterpret_cast<const uint2*>(base + c + half);
+    if (csr) {
+      float a[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xffff0000u),
+                    __uint_as_float(lo.y << 16), __uint_as_float(lo.y & 0xffff0000u)};
+      float b[4] = {__uint_as_float(hi.x << 16), __uint_as_float(hi.x & 0xffff0000u),
+                    __uint_as_float(hi.y << 16), __uint_as_float(hi.y & 0xffff0000u)};
+      float ra[4], rb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float2 e = csr[c + j];
+        ra[j] = a[j] * e.x - b[j] * e.y;
+        rb[j] = b[j] * e.x + a[j] * e.y;
+      }
+      lo.x = pack_bf16x2(ra[0], ra[1]);
+      lo.y = pack_bf16x2(ra[2], ra[3]);
+      hi.x = pack_bf16x2(rb[0], rb[1]);
+      hi.y = pack_bf16x2(rb[2], rb[3]);
+    }
+    if (!isk) {
+      *reinterpret_cast<uint2*>(base + c) = lo;
+      *reinterpret_cast<uint2*>(base + c + half) = hi;
+    } else if (slot >= 0) {
+      const int b = slot / blk, o = slot - b * blk;
+      bf16_t* dst = kc + (((size_t)b * Hkv + h) * blk + o) * D;
+      *reinterpret_cast<uint2*>(dst + c) = lo;
+      *reinterpret_cast<uint2*>(dst + c + half) = hi;
+    }
+  }
+  if (slot >= 0) {
+    const int b = slot / blk, o = slot - b * blk;
+    const int dv = D >> 3;
+    for (int i = threadIdx.x; i < Hkv * dv; i += blockDim.x) {
+      const int h = i / dv, c = (i - h * dv) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(row + (Hq + Hkv) * D + h * D + c);
+      *reinterpret_cast<uint4*>(vc + (((size_t)b * Hkv + h) * blk + o) * D + c) = v;
+    }
+  }
+}
+
+extern "C" int loqa_rope_kv_append(void* qkv, int stride, const int* positions, const void* cs,
+                                   void* kc, void* vc, const int* slots, int T, int Hq, int Hkv,
+                                   int D, int blk, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (D % 8 != 0 || stride < (Hq + 2 * Hkv) * D || (cs && !positions)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rope_kv_append_kernel, dim3(T), dim3(128), 0, s, (bf16_t*)qkv, stride,
+                     positions, (const float2*)cs, (bf16_t*)kc, (bf16_t*)vc, slots, Hq, Hkv, D,
+                     blk);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------- K1 PCM16 -> f32 + sum of squares
+// pcm: concatenated int16 samples of S segments (offsets[S+1] in samples).
+// out: f32 samples (x / 32767, as audio_service.go:1078), sumsq[S] accumulates.
+#define PCM_CHUNK 8192
+__global__ void pcm16_f32_sumsq_kernel(const int16_t* __restrict__ pcm, float* __restrict__ out,
+                                       const long long* __restrict__ offsets,
+                                       float* __restrict__ sumsq) {
+  __shared__ float scratch[4];
+  const int seg = blockIdx.y;
+  const long long beg = offsets[seg], end = offsets[seg + 1];
+  const long long c0 = beg + (long long)blockIdx.x * PCM_CHUNK;
+  float acc = 0.f;
+  if (c0 < end) {
+    const long long c1 = min(end, c0 + PCM_CHUNK);
+    for (long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+      const float f = (float)pcm[i] * (1.0f / 32767.0f);
+      out[i] = f;
+      acc += f * f;
+    }
+  }
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0 && c0 < end) atomicAdd(sumsq + seg, acc);
+}
+
+extern "C" int loqa_pcm16_f32_sumsq(const void* pcm, float* out, const long long* offsets,
+                                    float* sumsq, int nseg, long long max_seg_len, hipStream_t s) {
+  if (nseg <= 0) return 0;
+  hipError_t e = hipMemsetAsync(sumsq, 0, sizeof(float) * nseg, s);
+  if (e != hipSuccess) return (int)e;
+  const long long chunks = max_seg_len <= 0 ? 1 : (max_seg_len + PCM_CHUNK - 1) / PCM_CHUNK;
+  hipLaunchKernelGGL(pcm16_f32_sumsq_kernel, dim3((unsigned)chunks, nseg), dim3(256), 0, s,
+                     (const int16_t*)pcm, out, offsets, sumsq);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------------- K15 grammar-masked argmax
+// logits: [B, V] (bf16 if is_bf16 else f32), row stride ld elements.
+// mask: [B, W] uint32 bitmask (bit v%32 of word v/32 = token v allowed), or null.
+// mask_rows: optional per-row index into the mask table (so B rows can share
+// precomputed grammar-state masks). out_idx[b] = argmax over allowed (or -1).
+template <bool BF16>
+__global__ __launch_bounds__(1024) void masked_argmax_kernel(
+    const void* __restrict__ logits, long long ld, int V, const uint32_t* __restrict__ mask,
+    const int* __restrict__ mask_rows, int W, int* __restrict__ out_idx,
+    float* __restrict__ out_val) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int b = blockIdx.x;
+  const uint32_t* m = nullptr;
+  if (mask) m = mask + (size_t)(mask_rows ? mask_rows[b] : b) * W;
+  float best = -FLT_MAX;
+  int bi = -1;
+  if (BF16) {
+    const bf16_t* row = reinterpret_cast<const bf16_t*>(logits) + (size_t)b * ld;
+    // 8 tokens per lane per step.
+    for (int v0 = threadIdx.x * 8; v0 < V; v0 += blockDim.x * 8) {
+      if (v0 + 8 <= V && (ld % 8 == 0)) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(row + v0), f);
+        const uint32_t bits = m ? (m[v0 >> 5] >> (v0 & 31)) & 0xffu : 0xffu;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((bits >> j) & 1u) && f[j] > best) { best = f[j]; bi = v0 + j; }
+      } else {
+        for (int v = v0; v < min(V, v0 + 8); ++v) {
+          const bool ok = !m || ((m[v >> 5] >> (v & 31)) & 1u);
+          const float f = bf2f(row[v]);
+          if (ok && f > best) { best = f; bi = v; }
+        }
+      }
+    }
+  } else {
+    const float* row = reinterpret_cast<const float*>(logits) + (size_t)b * ld;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      const bool ok = !m || ((m[v >> 5] >> (v & 31)) & 1u);
+      const float f = row[v];
+      if (ok && f > best) { best = f; bi = v; }
+    }
+  }
+  // wave reduce (ties -> lowest index, matching torch.argmax)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (oi >= 0 && (bi < 0 || ov > best || (ov == best && oi < bi))) { best = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sv[wid] = best; si[wid] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int i = 1; i < nw; ++i)
+      if (si[i] >= 0 && (bi < 0 || sv[i] > best || (sv[i] == best && si[i] < bi))) {
+        best = sv[i];
+        bi = si[i];
+      }
+    out_idx[b] = bi;
+    if (out_val) out_val[b] = best;
+  }
+}
+
+extern "C" int loqa_masked_argmax(const void* logits, int is_bf16, long long ld, int B, int V,
+                                  const uint32_t* mask, const int* mask_rows, int W, int* out_idx,
+                                  float* out_val, hipStream_t s) {
+  if (B <= 0) return 0;
+  if (mask && W * 32 < V) return (int)hipErrorInvalidValue;
+  if (is_bf16)
+    hipLaunchKernelGGL(masked_argmax_kernel<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, mask,
+                       mask_rows, W, out_idx, out_val);
+  else
+    hipLaunchKernelGGL(masked_argmax_kernel<false>, dim3(B), dim3(1024), 0, s, logits, ld, V,
+                       mask, mask_rows, W, out_idx, out_val);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,307 @@
+// Native host runtime for the MI355X voice hub.
+//
+//  * PcmStager   - pinned (hipHostMalloc) host slots that relay PCM frames are
+//                  appended into as they arrive on the gRPC stream, then moved
+//                  to HBM with hipMemcpyAsync on a dedicated H2D stream; a HIP
+//                  event per transfer gates slot reuse (SURVEY §2.4 "Host<->device
+//                  data path"). Replaces the reference's per-sample Go
+//                  conversion loop + WAV/HTTP round trip (audio_service.go:1048,
+//                  stt_client.go:365).
+//  * BlockPool   - paged KV-cache block allocator with per-sequence block tables,
+//                  reference counts and a hash-keyed prefix cache so prompts that
+//                  share the parser template prefix share KV blocks
+//                  (SURVEY §7.2 step 4).
+// Exposed through a flat C ABI (loaded with ctypes after torch, so the process
+// has exactly one HIP runtime).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ PcmStager
+struct Slot {
+  int16_t* host = nullptr;  // pinned
+  int64_t len = 0;          // samples written
+  bool busy = false;        // owned by a producer or in flight
+  hipEvent_t done = nullptr;
+  bool in_flight = false;
+};
+
+struct PcmStager {
+  std::vector<Slot> slots;
+  int64_t cap = 0;  // samples per slot
+  std::mutex mu;
+  hipStream_t h2d = nullptr;
+};
+
+// ------------------------------------------------------------------ BlockPool
+struct Seq {
+  std::vector<int32_t> blocks;
+  int64_t len = 0;  // tokens stored
+};
+
+struct BlockPool {
+  int32_t num_blocks = 0, block_size = 0;
+  std::vector<int32_t> refcnt;
+  std::deque<int32_t> free_list;
+  std::unordered_map<int64_t, Seq> seqs;
+  // prefix cache: chained hash of full blocks -> block id (holds one reference)
+  std::unordered_map<uint64_t, int32_t> prefix;
+  std::unordered_map<int32_t, uint64_t> block_hash;
+  std::mutex mu;
+
+  int32_t take() {
+    if (free_list.empty()) {
+      // evict an unreferenced cached prefix block
+      for (auto it = prefix.begin(); it != prefix.end(); ++it) {
+        if (refcnt[it->second] == 1) {
+          const int32_t b = it->second;
+          block_hash.erase(b);
+          prefix.erase(it);
+          refcnt[b] = 0;
+          return take_fresh(b);
+        }
+      }
+      return -1;
+    }
+    const int32_t b = free_list.front();
+    free_list.pop_front();
+    return take_fresh(b);
+  }
+  int32_t take_fresh(int32_t b) {
+    refcnt[b] = 1;
+    return b;
+  }
+  void release(int32_t b) {
+    if (--refcnt[b] == 0) free_list.push_back(b);
+  }
+};
+
+uint64_t mix_hash(uint64_t h, const int32_t* toks, int n) {
+  // FNV-1a over the token ids, chained from the previous block's hash
+  uint64_t x = h ^ 0xcbf29ce484222325ULL;
+  for (int i = 0; i < n; ++i) {
+    x ^= (uint64_t)(uint32_t)toks[i];
+    x *= 0x100000001b3ULL;
+  }
+  return x;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------- stager API
+void* loqa_stager_create(int nslots, long long samples_per_slot) {
+  auto* s = new PcmStager();
+  s->cap = samples_per_slot;
+  s->slots.resize(nslots);
+  if (hipStreamCreateWithFlags(&s->h2d, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return nullptr;
+  }
+  for (auto& sl : s->slots) {
+    if (hipHostMalloc((void**)&sl.host, sizeof(int16_t) * samples_per_slot, hipHostMallocDefault) !=
+            hipSuccess ||
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+      return nullptr;
+    }
+  }
+  return s;
+}
+
+void loqa_stager_destroy(void* h) {
+  auto* s = static_cast<PcmStager*>(h);
+  if (!s) return;
+  hipStreamSynchronize(s->h2d);
+  for (auto& sl : s->slots) {
+    if (sl.host) hipHostFree(sl.host);
+    if (sl.done) hipEventDestroy(sl.done);
+  }
+  hipStreamDestroy(s->h2d);
+  delete s;
+}
+
+// Acquire a free slot (reclaiming slots whose transfer completed). -1 if none.
+int loqa_stager_acquire(void* h) {
+  auto* s = static_cast<PcmStager*>(h);
+  std::lock_guard<std::mutex> g(s->mu);
+  for (size_t i = 0; i < s->slots.size(); ++i) {
+    Slot& sl = s->slots[i];
+    if (sl.busy && sl.in_flight && hipEventQuery(sl.done) == hipSuccess) {
+      sl.busy = false;
+      sl.in_flight = false;
+    }
+    if (!sl.busy) {
+      sl.busy = true;
+      sl.len = 0;
+      return (int)i;
+    }
+  }
+  return -1;
+}
+
+// Append little-endian PCM16 bytes; an odd trailing byte is dropped (as the
+// reference does). Returns samples appended, or -1 on overflow.
+long long loqa_stager_append(void* h, int slot, const uint8_t* bytes, long long nbytes) {
+  auto* s = static_cast<PcmStager*>(h);
+  Slot& sl = s->slots[slot];
+  const long long n = nbytes / 2;
+  if (sl.len + n > s->cap) return -1;
+  std::memcpy(sl.host + sl.len, bytes, (size_t)n * 2);
+  sl.len += n;
+  return n;
+}
+
+long long loqa_stager_len(void* h, int slot) { return static_cast<PcmStager*>(h)->slots[slot].len; }
+
+const void* loqa_stager_host_ptr(void* h, int slot) {
+  return static_cast<PcmStager*>(h)->slots[slot].host;
+}
+
+// Async H2D of the slot's samples into dst (device) on the stager's H2D stream;
+// `wait_stream` (the compute stream) is made to wait for the copy. The slot is
+// recycled once the copy's event has completed.
+int loqa_stager_upload(void* h, int slot, void* dst, long long max_samples, hipStream_t wait_stream) {
+  auto* s = static_cast<PcmStager*>(h);
+  Slot& sl = s->slots[slot];
+  const long long n = sl.len < max_samples ? sl.len : max_samples;
+  hipError_t e = hipSuccess;
+  if (n > 0) e = hipMemcpyAsync(dst, sl.host, (size_t)n * 2, hipMemcpyHostToDevice, s->h2d);
+  if (e != hipSuccess) return (int)e;
+  e = hipEventRecord(sl.done, s->h2d);
+  if (e != hipSuccess) return (int)e;
+  if (wait_stream) e = hipStreamWaitEvent(wait_stream, sl.done, 0);
+  std::lock_guard<std::mutex> g(s->mu);
+  sl.in_flight = true;
+  return (int)e;
+}
+
+void loqa_stager_release(void* h, int slot) {
+  auto* s = static_cast<PcmStager*>(h);
+  std::lock_guard<std::mutex> g(s->mu);
+  Slot& sl = s->slots[slot];
+  if (!sl.in_flight) sl.busy = false;  // otherwise reclaimed on event completion
+}
+
+// ------------------------------------------------------------- block pool API
+void* loqa_pool_create(int num_blocks, int block_size) {
+  auto* p = new BlockPool();
+  p->num_blocks = num_blocks;
+  p->block_size = block_size;
+  p->refcnt.assign(num_blocks, 0);
+  for (int i = 0; i < num_blocks; ++i) p->free_list.push_back(i);
+  return p;
+}
+
+void loqa_pool_destroy(void* h) { delete static_cast<BlockPool*>(h); }
+
+int loqa_pool_free_blocks(void* h) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  int n = (int)p->free_list.size();
+  for (auto& kv : p->prefix)
+    if (p->refcnt[kv.second] == 1) ++n;
+  return n;
+}
+
+// Register a sequence and try to reuse cached full prefix blocks for `toks`.
+// Returns the number of tokens whose KV is already present (multiple of block
+// size, always < ntok so at least one token is computed), or -1 on error.
+long long loqa_pool_add_seq(void* h, long long seq_id, const int32_t* toks, int ntok) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  if (p->seqs.count(seq_id)) return -1;
+  Seq sq;
+  uint64_t hsh = 0;
+  const int bs = p->block_size;
+  for (int i = 0; i + bs < ntok; i += bs) {  // keep >= 1 token to compute
+    hsh = mix_hash(hsh, toks + i, bs);
+    auto it = p->prefix.find(hsh);
+    if (it == p->prefix.end()) break;
+    p->refcnt[it->second]++;
+    sq.blocks.push_back(it->second);
+    sq.len += bs;
+  }
+  p->seqs.emplace(seq_id, std::move(sq));
+  return p->seqs[seq_id].len;
+}
+
+// Reserve KV slots for n more tokens; writes slot ids (block*bs + off) to out.
+int loqa_pool_append(void* h, long long seq_id, int n, int32_t* out_slots) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  if (it == p->seqs.end()) return -1;
+  Seq& sq = it->second;
+  const int bs = p->block_size;
+  for (int i = 0; i < n; ++i) {
+    const long long pos = sq.len + i;
+    const int bi = (int)(pos / bs);
+    if (bi >= (int)sq.blocks.size()) {
+      const int32_t b = p->take();
+      if (b < 0) return -2;  // out of KV memory
+      sq.blocks.push_back(b);
+    }
+    out_slots[i] = sq.blocks[bi] * bs + (int)(pos % bs);
+  }
+  sq.len += n;
+  return 0;
+}
+
+// Publish the sequence's full blocks of `toks` (its first ntok tokens) to the
+// prefix cache so later prompts with the same prefix can reuse them.
+int loqa_pool_cache_prefix(void* h, long long seq_id, const int32_t* toks, int ntok) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  if (it == p->seqs.end()) return -1;
+  const int bs = p->block_size;
+  uint64_t hsh = 0;
+  for (int i = 0, bi = 0; i + bs <= ntok && bi < (int)it->second.blocks.size(); i += bs, ++bi) {
+    hsh = mix_hash(hsh, toks + i, bs);
+    const int32_t b = it->second.blocks[bi];
+    if (!p->prefix.count(hsh) && !p->block_hash.count(b)) {
+      p->prefix[hsh] = b;
+      p->block_hash[b] = hsh;
+      p->refcnt[b]++;  // the cache's own reference
+    }
+  }
+  return 0;
+}
+
+int loqa_pool_block_table(void* h, long long seq_id, int32_t* out, int max_blocks) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  if (it == p->seqs.end()) return -1;
+  const int n = (int)it->second.blocks.size();
+  if (n > max_blocks) return -2;
+  for (int i = 0; i < n; ++i) out[i] = it->second.blocks[i];
+  return n;
+}
+
+long long loqa_pool_seq_len(void* h, long long seq_id) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  return it == p->seqs.end() ? -1 : it->second.len;
+}
+
+int loqa_pool_free_seq(void* h, long long seq_id) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  if (it == p->seqs.end()) return -1;
+  for (int32_t b : it->second.blocks) p->release(b);
+  p->seqs.erase(it);
+  return 0;
+}
+
+}  // extern "C"

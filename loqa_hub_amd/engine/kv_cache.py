@@ -1,0 +1,182 @@
+"""Paged KV cache: device storage + block pool.
+
+The block pool lives in the native runtime (``csrc/runtime/runtime.cpp``,
+``BlockPool``); a Python twin with the same semantics is used only when the
+native library is not built (CPU unit tests).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ..ops import _lib
+
+
+class PyBlockPool:
+    """Pure-Python twin of the native BlockPool (prefix cache included)."""
+
+    def __init__(self, num_blocks: int, block_size: int):
+        self.num_blocks, self.block_size = num_blocks, block_size
+        self.ref = [0] * num_blocks
+        self.free = list(range(num_blocks))[::-1]
+        self.seqs: dict[int, dict] = {}
+        self.prefix: dict[tuple, int] = {}
+        self.block_key: dict[int, tuple] = {}
+
+    def _take(self) -> int:
+        if not self.free:
+            for k, b in list(self.prefix.items()):
+                if self.ref[b] == 1:
+                    del self.prefix[k]
+                    del self.block_key[b]
+                    self.ref[b] = 1
+                    return b
+            return -1
+        b = self.free.pop()
+        self.ref[b] = 1
+        return b
+
+    def _release(self, b: int) -> None:
+        self.ref[b] -= 1
+        if self.ref[b] == 0:
+            self.free.append(b)
+
+    def free_blocks(self) -> int:
+        return len(self.free) + sum(1 for b in self.prefix.values() if self.ref[b] == 1)
+
+    def add_seq(self, seq_id: int, toks: list[int]) -> int:
+        if seq_id in self.seqs:
+            return -1
+        bs = self.block_size
+        blocks, n = [], 0
+        key: tuple = ()
+        i = 0
+        while i + bs < len(toks):
+            key = key + tuple(toks[i:i + bs])
+            b = self.prefix.get(key)
+            if b is None:
+                break
+            self.ref[b] += 1
+            blocks.append(b)
+            n += bs
+            i += bs
+        self.seqs[seq_id] = {"blocks": blocks, "len": n}
+        return n
+
+    def append(self, seq_id: int, n: int) -> list[int] | None:
+        s = self.seqs[seq_id]
+        bs = self.block_size
+        out = []
+        for i in range(n):
+            pos = s["len"] + i
+            bi = pos // bs
+            if bi >= len(s["blocks"]):
+                b = self._take()
+                if b < 0:
+                    return None
+                s["blocks"].append(b)
+            out.append(s["blocks"][bi] * bs + pos % bs)
+        s["len"] += n
+        return out
+
+    def cache_prefix(self, seq_id: int, toks: list[int]) -> None:
+        s = self.seqs[seq_id]
+        bs = self.block_size
+        key: tuple = ()
+        for bi, i in enumerate(range(0, len(toks) - bs + 1, bs)):
+            if bi >= len(s["blocks"]):
+                break
+            key = key + tuple(toks[i:i + bs])
+            b = s["blocks"][bi]
+            if key not in self.prefix and b not in self.block_key:
+                self.prefix[key] = b
+                self.block_key[b] = key
+                self.ref[b] += 1
+
+    def block_table(self, seq_id: int) -> list[int]:
+        return list(self.seqs[seq_id]["blocks"])
+
+    def seq_len(self, seq_id: int) -> int:
+        return self.seqs[seq_id]["len"]
+
+    def free_seq(self, seq_id: int) -> None:
+        for b in self.seqs.pop(seq_id)["blocks"]:
+            self._release(b)
+
+
+class NativeBlockPool:
+    def __init__(self, num_blocks: int, block_size: int):
+        self.lib = _lib.runtime()
+        self.h = self.lib.loqa_pool_create(num_blocks, block_size)
+        self.num_blocks, self.block_size = num_blocks, block_size
+        self._buf = np.zeros(4096, dtype=np.int32)
+
+    def __del__(self):
+        try:
+            self.lib.loqa_pool_destroy(self.h)
+        except Exception:
+            pass
+
+    def free_blocks(self) -> int:
+        return self.lib.loqa_pool_free_blocks(self.h)
+
+    @staticmethod
+    def _arr(toks) -> np.ndarray:
+        return np.ascontiguousarray(np.asarray(toks, dtype=np.int32))
+
+    def add_seq(self, seq_id: int, toks: list[int]) -> int:
+        a = self._arr(toks)
+        return int(self.lib.loqa_pool_add_seq(self.h, seq_id, a.ctypes.data_as(ctypes.c_void_p), len(a)))
+
+    def append(self, seq_id: int, n: int) -> list[int] | None:
+        out = np.empty(max(n, 1), dtype=np.int32)
+        rc = self.lib.loqa_pool_append(self.h, seq_id, n, out.ctypes.data_as(ctypes.c_void_p))
+        if rc == -2:
+            return None
+        if rc != 0:
+            raise KeyError(seq_id)
+        return out[:n].tolist()
+
+    def cache_prefix(self, seq_id: int, toks: list[int]) -> None:
+        a = self._arr(toks)
+        self.lib.loqa_pool_cache_prefix(self.h, seq_id, a.ctypes.data_as(ctypes.c_void_p), len(a))
+
+    def block_table(self, seq_id: int) -> list[int]:
+        n = self.lib.loqa_pool_block_table(self.h, seq_id,
+                                           self._buf.ctypes.data_as(ctypes.c_void_p), len(self._buf))
+        if n < 0:
+            raise KeyError(seq_id)
+        return self._buf[:n].tolist()
+
+    def seq_len(self, seq_id: int) -> int:
+        return int(self.lib.loqa_pool_seq_len(self.h, seq_id))
+
+    def free_seq(self, seq_id: int) -> None:
+        self.lib.loqa_pool_free_seq(self.h, seq_id)
+
+
+def make_block_pool(num_blocks: int, block_size: int, require_native: bool):
+    try:
+        return NativeBlockPool(num_blocks, block_size)
+    except (_lib.NativeLibraryMissing, OSError):
+        if require_native:
+            raise
+        return PyBlockPool(num_blocks, block_size)
+
+
+class PagedKVCache:
+    def __init__(self, n_layers: int, n_kv: int, head_dim: int, num_blocks: int, block_size: int,
+                 device, dtype=torch.bfloat16):
+        shape = (n_layers, num_blocks, n_kv, block_size, head_dim)
+        self.k = torch.zeros(shape, dtype=dtype, device=device)
+        self.v = torch.zeros(shape, dtype=dtype, device=device)
+        self.block_size = block_size
+        self.num_blocks = num_blocks
+        self.pool = make_block_pool(num_blocks, block_size,
+                                    require_native=torch.device(device).type == "cuda")
+
+    @staticmethod
+    def bytes_per_block(n_layers: int, n_kv: int, head_dim: int, block_size: int) -> int:
+        return 2 * n_layers * n_kv * block_size * head_dim * 2

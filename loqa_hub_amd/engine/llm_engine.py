@@ -1,0 +1,307 @@
+"""Continuous-batching, grammar-constrained LLM engine (one per GPU).
+
+Replaces the up-to-five Ollama HTTP calls per utterance of the reference
+(SURVEY §3.2 observation 2) with ONE constrained multi-command decode whose
+result is shared by the classifier, the bridge, the fallback parser and the
+command queue.
+
+Step anatomy (all on the compute stream):
+  prefill : prompts (+ the schema's opening literal, jump-forwarded) as one
+            flat batch -> flash attention over the paged cache (prefix blocks
+            shared through the native block pool's prefix cache).
+  decode  : every live sequence feeds [sampled token + forced literal tokens]
+            -> grouped split-K paged attention -> lm_head -> fused
+            grammar-masked argmax (one mask row per sequence).  Decode steps
+            are replayed from HIP graphs bucketed by (seqs, tokens).
+Host work per step is the grammar cursor advance (a few dict lookups per
+sequence) plus one small pinned H2D copy of the step metadata.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.configs import LlamaConfig
+from ..models.llama import LlamaModel, LlamaWeights, StepMeta, TPGroup
+from .grammar import GrammarState, GrammarTables
+from .kv_cache import PagedKVCache
+from .tokenizer import get_tokenizer
+
+
+@dataclass
+class GenRequest:
+    prompt: list[int]
+    schema: list
+    seq_id: int = -1
+    # filled by the engine
+    grammar: GrammarState | None = None
+    feed: list[int] = field(default_factory=list)
+    output: str = ""
+    t_submit: float = 0.0
+    t_first: float = 0.0
+    t_done: float = 0.0
+    steps: int = 0
+    token_times: list[float] = field(default_factory=list)
+    done: bool = False
+
+
+def _bucket(n: int, buckets: list[int]) -> int:
+    for b in buckets:
+        if n <= b:
+            return b
+    return n
+
+
+class LLMEngine:
+    SEQ_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128]
+    MAX_DECODE_Q = 16
+
+    def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
+                 max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
+                 tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.tp = tp or TPGroup()
+        self.weights = LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
+        self.model = LlamaModel(self.weights)
+        self.tok = get_tokenizer(cfg.vocab_size)
+        self.grammar = GrammarTables(self.tok, self.device)
+        from .grammar import INTENTS
+        self.grammar.trie(INTENTS)
+        self.grammar.trie(["true", "false"])
+        self.masks = self.grammar.mask_table(self.device)
+        self.max_seqs, self.max_seq_len = max_seqs, max_seq_len
+        self.block_size = block_size
+        self.max_blocks = (max_seq_len + block_size - 1) // block_size
+        if num_blocks is None:
+            num_blocks = max_seqs * self.max_blocks + 64
+        self.kv = PagedKVCache(cfg.n_layers, self.weights.hkv, cfg.head_dim, num_blocks, block_size,
+                               self.device)
+        self.is_gpu = self.device.type == "cuda"
+        self.attn_ws = ops.AttnWorkspace(self.device, max_seqs * self.MAX_DECODE_Q, self.weights.h,
+                                         cfg.head_dim, (max_seq_len + 255) // 256) if self.is_gpu else None
+        self.use_graphs = use_graphs and self.is_gpu
+        self.prefill_chunk = prefill_chunk
+        self._graphs: dict[tuple[int, int], dict] = {}
+        self._next_id = 1
+        self._on_done = None
+        self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
+                      "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0}
+
+    # ------------------------------------------------------------- metadata
+    def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
+              B_pad: int | None = None, T_pad: int | None = None) -> tuple[StepMeta, dict]:
+        B = len(seqs)
+        T = sum(len(f) for f in feeds)
+        B_pad = B_pad or B
+        T_pad = T_pad or T
+        tokens = np.zeros(T_pad, np.int32)
+        positions = np.zeros(T_pad, np.int32)
+        slots = np.full(T_pad, -1, np.int32)
+        cu = np.zeros(B_pad + 1, np.int32)
+        ctx = np.zeros(B_pad, np.int32)
+        bt = np.zeros((B_pad, self.max_blocks), np.int32)
+        lidx = np.zeros(B_pad, np.int64)
+        off = 0
+        max_q = 1
+        max_ctx = 1
+        pool = self.kv.pool
+        for i, (r, f) in enumerate(zip(seqs, feeds)):
+            n = len(f)
+            start = pool.seq_len(r.seq_id)
+            sl = pool.append(r.seq_id, n)
+            if sl is None:
+                raise RuntimeError("KV cache exhausted")
+            tokens[off:off + n] = f
+            positions[off:off + n] = np.arange(start, start + n)
+            slots[off:off + n] = sl
+            off += n
+            cu[i + 1] = off
+            ctx[i] = start + n
+            tab = pool.block_table(r.seq_id)
+            bt[i, :len(tab)] = tab
+            lidx[i] = off - 1
+            max_q = max(max_q, n)
+            max_ctx = max(max_ctx, start + n)
+        cu[B + 1:] = off
+        host = {"tokens": tokens, "positions": positions, "slots": slots, "cu_q": cu,
+                "ctx_lens": ctx, "block_tables": bt, "logit_idx": lidx}
+        return max_q, max_ctx, host
+
+    def _to_device(self, host: dict, dst: dict | None = None) -> dict:
+        out = {}
+        for k, a in host.items():
+            t = torch.from_numpy(a)
+            if self.is_gpu:
+                t = t.pin_memory()
+            if dst is not None:
+                dst[k].copy_(t, non_blocking=True)
+                out[k] = dst[k]
+            else:
+                out[k] = t.to(self.device, non_blocking=True)
+        return out
+
+    # ------------------------------------------------------------ forward
+    def _forward_sample(self, meta: StepMeta, mask_rows: torch.Tensor) -> torch.Tensor:
+        hid = self.model.forward(meta, self.kv.k, self.kv.v, self.attn_ws)
+        logits = self.model.logits(hid)
+        if self.tp.world == 1:
+            return ops.masked_argmax(logits, self.masks, mask_rows)
+        return self._tp_argmax(logits, mask_rows)
+
+    def _tp_argmax(self, logits: torch.Tensor, mask_rows: torch.Tensor) -> torch.Tensor:
+        """Vocab-parallel masked argmax: local (max, idx) then all_gather (D5)."""
+        import torch.distributed as dist
+        V = self.weights.v
+        lo = self.tp.rank * V
+        W = self.masks.shape[1]
+        w0 = lo // 32
+        local_mask = self.masks[:, w0:w0 + (V + 31) // 32].contiguous()
+        idx = ops.masked_argmax(logits, local_mask, mask_rows)
+        val = logits.float().gather(1, idx.clamp(min=0).long()[:, None])[:, 0]
+        val = torch.where(idx >= 0, val, torch.full_like(val, -float("inf")))
+        pair = torch.stack([val, (idx + lo).float()], dim=1)  # idx < 2^24 exact in fp32
+        gathered = [torch.empty_like(pair) for _ in range(self.tp.world)]
+        dist.all_gather(gathered, pair, group=self.tp.group)
+        allp = torch.stack(gathered, 0)  # [W, B, 2]
+        best = allp[:, :, 0].argmax(0)
+        return allp[best, torch.arange(allp.shape[1], device=allp.device), 1].to(torch.int32)
+
+    def _build_meta(self, dev: dict, max_q: int, max_ctx: int, decode: bool) -> StepMeta:
+        return StepMeta(tokens=dev["tokens"], positions=dev["positions"], slots=dev["slots"],
+                        cu_q=dev["cu_q"], ctx_lens=dev["ctx_lens"], block_tables=dev["block_tables"],
+                        logit_idx=dev["logit_idx"], max_q=max_q, max_ctx=max_ctx, decode=decode)
+
+    def _decode_graph(self, B_pad: int, T_pad: int) -> dict:
+        key = (B_pad, T_pad)
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        dev = {
+            "tokens": torch.zeros(T_pad, dtype=torch.int32, device=self.device),
+            "positions": torch.zeros(T_pad, dtype=torch.int32, device=self.device),
+            "slots": torch.full((T_pad,), -1, dtype=torch.int32, device=self.device),
+            "cu_q": torch.zeros(B_pad + 1, dtype=torch.int32, device=self.device),
+            "ctx_lens": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
+            "block_tables": torch.zeros(B_pad, self.max_blocks, dtype=torch.int32, device=self.device),
+            "logit_idx": torch.zeros(B_pad, dtype=torch.int64, device=self.device),
+            "mask_rows": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
+        }
+        meta = self._build_meta(dev, self.MAX_DECODE_Q, self.max_seq_len, True)
+        # warm up (allocator + kernels) on a side stream, then capture
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            out = self._forward_sample(meta, dev["mask_rows"])
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._forward_sample(meta, dev["mask_rows"])
+        g = {"graph": graph, "dev": dev, "out": out}
+        self._graphs[key] = g
+        return g
+
+    # ------------------------------------------------------------ generate
+    def submit(self, req: GenRequest) -> GenRequest:
+        req.seq_id = self._next_id
+        self._next_id += 1
+        req.grammar = GrammarState(self.grammar, req.schema)
+        req.feed = list(req.prompt) + req.grammar.start()
+        req.t_submit = time.perf_counter()
+        hit = self.kv.pool.add_seq(req.seq_id, req.feed)
+        if hit < 0:
+            raise RuntimeError("duplicate sequence id")
+        self.stats["prefix_hit_tokens"] += hit
+        req.feed = req.feed[hit:]
+        req._prompt_full = list(req.prompt) + req.grammar.emitted  # type: ignore[attr-defined]
+        return req
+
+    def _sample_and_advance(self, live: list[GenRequest], nxt: np.ndarray, now: float) -> None:
+        for r, t in zip(live, nxt.tolist()):
+            if r.t_first == 0.0:
+                r.t_first = now
+            r.token_times.append(now)
+            r.steps += 1
+            forced = r.grammar.advance(int(t))
+            self.stats["sampled_tokens"] += 1
+            self.stats["forced_tokens"] += len(forced)
+            if r.grammar.done:
+                r.done = True
+                r.t_done = now
+                r.output = r.grammar.text()
+                r.feed = []
+                if self._on_done is not None:
+                    self._on_done(r)
+            else:
+                r.feed = [int(t)] + forced
+
+    def prefill(self, reqs: list[GenRequest]) -> None:
+        """Run the prompts (chunked) and sample each sequence's first token."""
+        i = 0
+        while i < len(reqs):
+            batch, T = [], 0
+            while i < len(reqs) and (not batch or T + len(reqs[i].feed) <= self.prefill_chunk):
+                batch.append(reqs[i])
+                T += len(reqs[i].feed)
+                i += 1
+            feeds = [r.feed for r in batch]
+            max_q, max_ctx, host = self._meta(batch, feeds, decode=False)
+            rows = np.array([r.grammar.mask_row() for r in batch], np.int32)
+            host["mask_rows"] = rows
+            dev = self._to_device(host)
+            meta = self._build_meta(dev, max_q, max_ctx, False)
+            nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
+            self.stats["prefill_tokens"] += T
+            for r in batch:
+                self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
+            self._sample_and_advance(batch, nxt, time.perf_counter())
+
+    def decode_step(self, live: list[GenRequest]) -> None:
+        feeds = []
+        for r in live:
+            f = r.feed
+            if len(f) > self.MAX_DECODE_Q:  # long forced run: keep the tail for the next step
+                raise RuntimeError("forced literal longer than MAX_DECODE_Q")
+            feeds.append(f)
+        B = len(live)
+        T = sum(len(f) for f in feeds)
+        rows = np.array([r.grammar.mask_row() for r in live], np.int32)
+        if self.use_graphs:
+            B_pad = _bucket(B, self.SEQ_BUCKETS)
+            T_pad = _bucket(T, [B_pad * k for k in (1, 2, 4, 8, 16)])
+            g = self._decode_graph(B_pad, T_pad)
+            max_q, max_ctx, host = self._meta(live, feeds, True, B_pad, T_pad)
+            mr = np.zeros(B_pad, np.int32)
+            mr[:B] = rows
+            host["mask_rows"] = mr
+            self._to_device(host, g["dev"])
+            g["graph"].replay()
+            nxt = g["out"][:B].cpu().numpy()
+        else:
+            max_q, max_ctx, host = self._meta(live, feeds, True)
+            host["mask_rows"] = rows
+            dev = self._to_device(host)
+            meta = self._build_meta(dev, max_q, max_ctx, True)
+            nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += T
+        self._sample_and_advance(live, nxt, time.perf_counter())
+
+    def generate(self, reqs: list[GenRequest], on_done=None) -> list[GenRequest]:
+        """Run the requests to completion. ``on_done(req)`` fires as soon as each
+        sequence finishes (its command queue can start while others decode)."""
+        self._on_done = on_done
+        for r in reqs:
+            self.submit(r)
+        self.prefill(reqs)
+        live = [r for r in reqs if not r.done]
+        while live:
+            self.decode_step(live)
+            live = [r for r in live if not r.done]
+        for r in reqs:
+            self.kv.pool.free_seq(r.seq_id)
+        return reqs

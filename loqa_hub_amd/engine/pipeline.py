@@ -1,0 +1,185 @@
+"""GPU voice pipeline: batched STT -> ONE constrained multi-command parse per
+utterance -> command queue (rollback) -> NATS publish -> voice-event record.
+
+This is the MI355X replacement of the reference's winner path
+(``audio_service.go:590-761``: transcribe, bridge / ParseMultiCommand, TTS,
+NATS), restructured for batching: every stage runs once per *batch* of
+arbitration winners on one GPU, and the command queue of each utterance runs
+as soon as its own decode finishes.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..llm.command_queue import CommandQueue, ExecutionResult
+from ..llm.commands import (Command, MultiCommand, ParseError, detect_compound_utterance,
+                            parse_multi_command_response, parse_response,
+                            split_compound_utterance)
+from ..llm.prompts import build_multi_command_prompt, build_prompt
+from ..llm.transcriber import TranscriptionResult, to_transcription_result
+from ..transport.device_commands import ExecutionContext, NATSCommandExecutor
+from .grammar import multi_command_schema, single_command_schema
+from .llm_engine import GenRequest, LLMEngine
+from .stt_engine import STTEngine, STTRequest
+
+
+@dataclass
+class PipelineJob:
+    relay_id: str
+    request_id: str
+    pcm: np.ndarray
+    transcript_hint: str | None = None     # synthetic ground truth (teacher forcing)
+    # results
+    transcription: TranscriptionResult | None = None
+    raw_text: str = ""
+    rms: float = 0.0
+    multi: MultiCommand | None = None
+    n_expected: int = 0
+    llm_output: str = ""
+    queue: ExecutionResult | None = None
+    error: str = ""
+    t: dict = field(default_factory=dict)   # stage timestamps (perf_counter)
+
+    @property
+    def n_commands(self) -> int:
+        return len(self.multi.commands) if self.multi else 0
+
+
+class VoicePipeline:
+    def __init__(self, stt: STTEngine, llm: LLMEngine, nats=None, *, min_response_tokens: int = 8,
+                 queue_max_duration: float = 0.0, rollback: bool = True, tts=None,
+                 response_audio: bool = False):
+        self.stt, self.llm, self.nats = stt, llm, nats
+        self.min_response_tokens = min_response_tokens
+        self.queue_max_duration = queue_max_duration
+        self.rollback = rollback
+        self.tts = tts
+        self.response_audio = response_audio
+        self._pool: ThreadPoolExecutor | None = None
+
+    # --------------------------------------------------------------- stages
+    def transcribe(self, jobs: list[PipelineJob], device_pcm=None) -> None:
+        reqs = [STTRequest(j.pcm, transcript=j.transcript_hint) for j in jobs]
+        self.stt.transcribe(reqs, device_pcm)
+        now = time.perf_counter()
+        for j, r in zip(jobs, reqs):
+            j.raw_text, j.rms = r.text, r.rms
+            j.transcription = to_transcription_result(r.text)
+            j.t["stt_done"] = now
+
+    def build_request(self, j: PipelineJob) -> GenRequest | None:
+        text = j.transcription.text if j.transcription else ""
+        if not text:
+            j.multi = MultiCommand([], False, text, "I didn't hear anything.")
+            return None
+        tok = self.llm.tok
+        if detect_compound_utterance(text):
+            n = max(1, len(split_compound_utterance(text)))
+            j.n_expected = n
+            prompt = build_multi_command_prompt(text)
+            schema = multi_command_schema(n, min_response_tokens=self.min_response_tokens)
+            r = GenRequest(tok.encode(prompt, bos=True), schema)
+            r.kind = "multi"  # type: ignore[attr-defined]
+        else:
+            j.n_expected = 1
+            schema = single_command_schema(max_response_tokens=12)
+            r = GenRequest(tok.encode(build_prompt(text), bos=True), schema)
+            r.kind = "single"  # type: ignore[attr-defined]
+        return r
+
+    def parse(self, j: PipelineJob, r: GenRequest) -> None:
+        text = j.transcription.text
+        j.llm_output = r.output
+        try:
+            if getattr(r, "kind", "multi") == "multi":
+                j.multi = parse_multi_command_response(r.output, text)
+            else:
+                cmd = parse_response(r.output)
+                j.multi = MultiCommand([cmd], False, text, cmd.response)
+        except ParseError as e:
+            j.error = str(e)
+            j.multi = MultiCommand([Command("unknown", {}, 0.0, "I'm not sure what you want me to do.")],
+                                   False, text, "I'm not sure what you want me to do.")
+
+    async def execute(self, j: PipelineJob) -> None:
+        if not j.multi or not j.multi.commands:
+            return
+        ctx = ExecutionContext(j.relay_id, j.request_id, "", j.transcription.text)
+        q = CommandQueue(j.multi.commands, self.queue_max_duration, self.rollback)
+        j.queue = await q.execute(NATSCommandExecutor(self.nats, ctx))
+        j.t["queue_done"] = time.perf_counter()
+
+    # ------------------------------------------------------------- batch run
+    def _gpu_executor(self) -> ThreadPoolExecutor:
+        if self._pool is None:
+            dev = self.llm.device
+
+            def init():
+                if dev.type == "cuda":
+                    torch.cuda.set_device(dev)
+            self._pool = ThreadPoolExecutor(1, thread_name_prefix="gpu-worker", initializer=init)
+        return self._pool
+
+    async def process(self, jobs: list[PipelineJob], device_pcm=None) -> list[PipelineJob]:
+        """GPU stages run on a dedicated worker thread; each utterance's command
+        queue is scheduled on the event loop the moment its own decode finishes,
+        so command execution/NATS publishing overlaps the remaining decode."""
+        loop = asyncio.get_running_loop()
+        ex = self._gpu_executor()
+        t0 = time.perf_counter()
+        for j in jobs:
+            j.t["start"] = t0
+        await loop.run_in_executor(ex, self.transcribe, jobs, device_pcm)
+        reqs, owners = [], []
+        for j in jobs:
+            r = self.build_request(j)
+            if r is not None:
+                reqs.append(r)
+                owners.append(j)
+        owner_of = {id(r): j for r, j in zip(reqs, owners)}
+        tasks: list[asyncio.Future] = []
+
+        def start_queue(r: GenRequest) -> None:
+            j = owner_of[id(r)]
+            j.t["llm_first"] = r.t_first
+            j.t["llm_done"] = r.t_done
+            self.parse(j, r)
+            tasks.append(asyncio.ensure_future(self.execute(j)))
+
+        def on_done(r: GenRequest) -> None:  # called on the GPU worker thread
+            loop.call_soon_threadsafe(start_queue, r)
+
+        if reqs:
+            await loop.run_in_executor(ex, self.llm.generate, reqs, on_done)
+        await asyncio.sleep(0)  # let the last call_soon_threadsafe callbacks run
+        while len(tasks) < len(reqs):
+            await asyncio.sleep(0.0005)
+        await asyncio.gather(*tasks)
+        return jobs
+
+
+def added_command_stats(jobs: list[PipelineJob]) -> dict:
+    """Both BASELINE.md definitions of 'ms per added command':
+    * reference-equivalent: queue item durations for index >= 1
+      (command_queue.go:119-121: execution + NATS publish);
+    * end-to-end marginal: slope of (utterance completion latency) vs
+      (number of commands) across the batch (decode tokens + execution)."""
+    added = [it.duration * 1e3 for j in jobs if j.queue for it in j.queue.completed_items if it.index >= 1]
+    xs, ys = [], []
+    for j in jobs:
+        if j.queue is not None and "queue_done" in j.t:
+            xs.append(j.n_commands)
+            ys.append((j.t["queue_done"] - j.t["start"]) * 1e3)
+    slope = None
+    if len(set(xs)) >= 2:
+        slope = float(np.polyfit(np.array(xs, float), np.array(ys, float), 1)[0])
+    return {"ref_equiv_ms_per_added_command": float(np.mean(added)) if added else None,
+            "ref_equiv_ms_per_added_command_max": float(np.max(added)) if added else None,
+            "e2e_marginal_ms_per_added_command": slope,
+            "n_added_commands": len(added)}

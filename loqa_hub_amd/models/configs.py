@@ -1,0 +1,116 @@
+"""Model configurations for the on-GPU STT -> intent -> TTS pipeline.
+
+Dimensions are public model-card facts. Weights are always
+seeded random-init (no network, no checkpoints); ``loqa_hub_amd.engine.weights``
+can also map safetensors files when they exist locally.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, replace
+
+
+@dataclass(frozen=True)
+class LlamaConfig:
+    name: str
+    d_model: int
+    n_layers: int
+    n_heads: int
+    n_kv_heads: int
+    head_dim: int
+    ffn_dim: int
+    vocab_size: int
+    rope_theta: float = 500000.0
+    norm_eps: float = 1e-5
+    tie_embeddings: bool = False
+    max_positions: int = 8192
+
+    @property
+    def qkv_dim(self) -> int:
+        return (self.n_heads + 2 * self.n_kv_heads) * self.head_dim
+
+    def n_params(self) -> int:
+        d, f = self.d_model, self.ffn_dim
+        per = d * self.qkv_dim + self.n_heads * self.head_dim * d + 3 * d * f + 2 * d
+        emb = self.vocab_size * d * (1 if self.tie_embeddings else 2)
+        return self.n_layers * per + emb + d
+
+
+LLAMA_CONFIGS = {
+    "tinyllama": LlamaConfig("tinyllama-1.1b", 2048, 22, 32, 4, 64, 5632, 32000, rope_theta=10000.0),
+    "llama3.2-1b": LlamaConfig("llama-3.2-1b", 2048, 16, 32, 8, 64, 8192, 128256, tie_embeddings=True),
+    "llama3.2-3b": LlamaConfig("llama-3.2-3b", 3072, 28, 24, 8, 128, 8192, 128256, tie_embeddings=True),
+    "llama3-8b": LlamaConfig("llama-3-8b", 4096, 32, 32, 8, 128, 14336, 128256),
+    "llama3-70b": LlamaConfig("llama-3-70b", 8192, 80, 64, 8, 128, 28672, 128256),
+    # small shapes for CPU tests / smoke
+    "test-tiny": LlamaConfig("test-tiny", 256, 2, 4, 2, 64, 512, 4096, tie_embeddings=True,
+                             max_positions=2048),
+}
+
+
+@dataclass(frozen=True)
+class WhisperConfig:
+    name: str
+    n_mels: int
+    d_model: int
+    enc_layers: int
+    dec_layers: int
+    n_heads: int
+    vocab_size: int
+    n_audio_ctx: int = 1500
+    n_text_ctx: int = 448
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_heads
+
+    @property
+    def ffn_dim(self) -> int:
+        return 4 * self.d_model
+
+
+WHISPER_CONFIGS = {
+    "whisper-tiny": WhisperConfig("whisper-tiny", 80, 384, 4, 4, 6, 51865),
+    "whisper-base": WhisperConfig("whisper-base", 80, 512, 6, 6, 8, 51865),
+    "whisper-small": WhisperConfig("whisper-small", 80, 768, 12, 12, 12, 51865),
+    "whisper-large-v3": WhisperConfig("whisper-large-v3", 128, 1280, 32, 32, 20, 51866),
+    "test-whisper": WhisperConfig("test-whisper", 80, 128, 2, 2, 2, 4096, n_audio_ctx=1500),
+}
+
+
+@dataclass(frozen=True)
+class VitsConfig:
+    """VITS (text encoder + stochastic duration + flow + HiFi-GAN) at the public
+    'vits-ljs' sizes; sample rate 22.05 kHz, hop 256."""
+    name: str
+    n_symbols: int = 178
+    hidden: int = 192
+    filter_channels: int = 768
+    n_heads: int = 2
+    enc_layers: int = 6
+    kernel_size: int = 3
+    flow_layers: int = 4
+    wn_layers: int = 4
+    inter_channels: int = 192
+    upsample_rates: tuple = (8, 8, 2, 2)
+    upsample_initial: int = 512
+    resblock_kernels: tuple = (3, 7, 11)
+    resblock_dilations: tuple = ((1, 3, 5), (1, 3, 5), (1, 3, 5))
+    sample_rate: int = 22050
+    window: int = 4
+
+
+VITS_CONFIGS = {
+    "vits-ljs": VitsConfig("vits-ljs"),
+    "test-vits": VitsConfig("test-vits", hidden=64, filter_channels=128, enc_layers=2, flow_layers=2,
+                            wn_layers=2, inter_channels=64, upsample_initial=64),
+}
+
+
+def llama_config(name: str, **over) -> LlamaConfig:
+    c = LLAMA_CONFIGS[name]
+    return replace(c, **over) if over else c
+
+
+def whisper_config(name: str, **over) -> WhisperConfig:
+    c = WHISPER_CONFIGS[name]
+    return replace(c, **over) if over else c

@@ -1,0 +1,156 @@
+"""Llama-family decoder (TinyLlama, Llama-3.2-1B/3B, Llama-3-8B/70B) for the
+intent parser that replaces the reference's Ollama call
+(``command_parser.go:223-266``, ``streaming_command_parser.go:339-371``).
+
+Layout is MI355X-first rather than HF-module-first:
+
+* fused QKV weight [(H + 2 Hkv) D, d] and fused gate|up weight [2F, d] so each
+  layer is 4 GEMMs (hipBLASLt) + 4 fused HIP kernels (rmsnorm+residual,
+  rope+paged-KV-append, flash/paged attention, SwiGLU);
+* the residual stream is updated inside the norm kernel;
+* activations are a flat [T, d] token batch (continuous batching), sequence
+  structure lives only in the attention metadata;
+* tensor parallel: QKV/gate-up column-sharded by head / ffn slice, O/down
+  row-sharded with one all-reduce each, vocab-parallel lm_head with a
+  (max, argmax) combine.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..ops.reference import rope_cos_sin
+from .configs import LlamaConfig
+
+
+@dataclass
+class StepMeta:
+    """Device-side metadata of one forward over a flat token batch."""
+    tokens: torch.Tensor        # [T] int32
+    positions: torch.Tensor     # [T] int32
+    slots: torch.Tensor         # [T] int32 (KV slot, -1 = padding row)
+    cu_q: torch.Tensor          # [B+1] int32
+    ctx_lens: torch.Tensor      # [B] int32 (tokens in cache after this step)
+    block_tables: torch.Tensor  # [B, max_blocks] int32
+    logit_idx: torch.Tensor     # [B] int64 rows whose logits are needed
+    max_q: int
+    max_ctx: int
+    decode: bool                # grouped (small-q) attention path
+
+
+class TPGroup:
+    """Tensor-parallel context; world 1 = no-op."""
+
+    def __init__(self, rank: int = 0, world: int = 1, group=None, allreduce=None):
+        self.rank, self.world, self.group = rank, world, group
+        self._allreduce = allreduce
+
+    def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return x
+        if self._allreduce is not None:
+            return self._allreduce(x)
+        import torch.distributed as dist
+        dist.all_reduce(x, group=self.group)
+        return x
+
+
+class LlamaWeights:
+    def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0,
+                 tp: TPGroup | None = None):
+        tp = tp or TPGroup()
+        self.cfg, self.tp = cfg, tp
+        assert cfg.n_heads % tp.world == 0 and cfg.n_kv_heads % tp.world == 0
+        assert cfg.ffn_dim % tp.world == 0 and cfg.vocab_size % tp.world == 0
+        self.h = cfg.n_heads // tp.world
+        self.hkv = cfg.n_kv_heads // tp.world
+        self.f = cfg.ffn_dim // tp.world
+        self.v = cfg.vocab_size // tp.world
+        d, D = cfg.d_model, cfg.head_dim
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1000003 + 17 + tp.rank)  # shards differ; replicas (same rank) identical
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(*shape, dtype=dtype, device=device)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        def ones(n):
+            return torch.ones(n, dtype=dtype, device=device)
+
+        # std 0.02 everywhere keeps activations O(1) through random layers
+        self.embed = rnd(self.v, d)
+        self.layers = []
+        for _ in range(cfg.n_layers):
+            self.layers.append({
+                "attn_norm": ones(d),
+                "wqkv": rnd((self.h + 2 * self.hkv) * D, d),
+                "wo": rnd(d, self.h * D),
+                "mlp_norm": ones(d),
+                "w_gate_up": rnd(2 * self.f, d),
+                "w_down": rnd(d, self.f),
+            })
+        self.final_norm = ones(d)
+        self.lm_head = self.embed if cfg.tie_embeddings else rnd(self.v, d)
+        self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
+
+    def nbytes(self) -> int:
+        n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
+        for L in self.layers:
+            n += sum(t.numel() for t in L.values())
+        return n * 2
+
+
+class LlamaModel:
+    def __init__(self, w: LlamaWeights):
+        self.w = w
+        self.cfg = w.cfg
+
+    def embed(self, tokens: torch.Tensor) -> torch.Tensor:
+        tp = self.w.tp
+        if tp.world == 1:
+            return torch.nn.functional.embedding(tokens.long(), self.w.embed)
+        lo = tp.rank * self.w.v
+        local = tokens.long() - lo
+        inr = (local >= 0) & (local < self.w.v)
+        x = torch.nn.functional.embedding(local.clamp(0, self.w.v - 1), self.w.embed)
+        x = x * inr[:, None].to(x.dtype)
+        return tp.all_reduce_(x)
+
+    def forward(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                attn_ws: ops.AttnWorkspace | None = None) -> torch.Tensor:
+        """Runs all layers; returns final-normed hidden states of ``logit_idx`` rows
+        [B, d]. k_cache/v_cache: [L, n_blocks, Hkv, BLK, D]."""
+        cfg, w, tp = self.cfg, self.w, self.w.tp
+        H, Hkv, D = w.h, w.hkv, cfg.head_dim
+        x = self.embed(meta.tokens)
+        residual = x
+        h = ops.rmsnorm(x, w.layers[0]["attn_norm"], cfg.norm_eps)
+        split_keys = 256
+        num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
+        for li, L in enumerate(w.layers):
+            if li > 0:
+                h = ops.rmsnorm(mlp_out, L["attn_norm"], cfg.norm_eps, residual=residual)
+            qkv = ops.linear(h, L["wqkv"])
+            ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
+                               H, Hkv, D)
+            attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                 head_dim=D, causal=True, max_q=meta.max_q,
+                                 ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
+                                 grouped=meta.decode, split_keys=split_keys,
+                                 num_splits=num_splits if meta.decode else 1,
+                                 workspace=attn_ws, max_k=meta.max_ctx)
+            o = tp.all_reduce_(ops.linear(attn, L["wo"]))
+            h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
+            gu = ops.linear(h, L["w_gate_up"])
+            mlp_out = tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["w_down"]))
+        sel_res = residual.index_select(0, meta.logit_idx)
+        sel_mlp = mlp_out.index_select(0, meta.logit_idx)
+        return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
+                           residual=sel_res.contiguous())
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """Local vocab shard logits [B, V/tp] (bf16)."""
+        return ops.linear(hidden, self.w.lm_head)

@@ -1,0 +1,179 @@
+"""Whisper encoder/decoder (tiny/base/small/large-v3) for on-GPU STT, replacing the
+reference's ``POST {STT_URL}/v1/audio/transcriptions`` (``stt_client.go:157``,
+``model=tiny``, temperature 0 = greedy).
+
+Execution plan per batch of utterances (one GPU):
+  log-mel (f32-MFMA STFT kernel) -> conv stem as im2col + GEMM with fused
+  bias+GELU(+sinusoidal position) epilogue -> L pre-LN encoder blocks (fused
+  QKV GEMM, non-causal flash attention on the contiguous QKV output, fused
+  residual+layernorm) -> cross-attention K/V for every decoder layer computed
+  once -> greedy decode with a paged self-attention cache and split-K
+  cross-attention over the 1500 encoder frames.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops.reference import MelConstants
+from .configs import WhisperConfig
+
+
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> torch.Tensor:
+    lt = math.log(max_timescale) / (channels // 2 - 1)
+    inv = torch.exp(-lt * torch.arange(channels // 2, dtype=torch.float64))
+    t = torch.arange(length, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.cat([t.sin(), t.cos()], dim=1).float()
+
+
+class WhisperWeights:
+    def __init__(self, cfg: WhisperConfig, device, dtype=torch.bfloat16, seed: int = 0):
+        self.cfg = cfg
+        d, f, M = cfg.d_model, cfg.ffn_dim, cfg.n_mels
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 7919 + 3)
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(*shape, dtype=dtype, device=device)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        def zeros(*shape):
+            return torch.zeros(*shape, dtype=dtype, device=device)
+
+        def ones(n):
+            return torch.ones(n, dtype=dtype, device=device)
+
+        self.conv1_w = rnd(d, M * 3)          # [Cout, Cin*3] (torch conv weight flattened)
+        self.conv1_b = zeros(d)
+        self.conv2_w = rnd(d, d * 3)
+        self.conv2_b = zeros(d)
+        self.pos_enc = sinusoids(cfg.n_audio_ctx, d).to(device=device, dtype=dtype)
+        self.enc = []
+        for _ in range(cfg.enc_layers):
+            self.enc.append(self._block(rnd, zeros, ones, d, f, cross=False))
+        self.enc_ln_w, self.enc_ln_b = ones(d), zeros(d)
+        self.tok_embed = rnd(cfg.vocab_size, d)
+        self.dec_pos = rnd(cfg.n_text_ctx, d, std=0.01)
+        self.dec = []
+        for _ in range(cfg.dec_layers):
+            self.dec.append(self._block(rnd, zeros, ones, d, f, cross=True))
+        self.dec_ln_w, self.dec_ln_b = ones(d), zeros(d)
+
+    @staticmethod
+    def _block(rnd, zeros, ones, d, f, cross: bool) -> dict:
+        b = {
+            "ln1_w": ones(d), "ln1_b": zeros(d),
+            "wqkv": rnd(3 * d, d), "bqkv": zeros(3 * d),   # k bias is zero in whisper
+            "wo": rnd(d, d), "bo": zeros(d),
+            "ln2_w": ones(d), "ln2_b": zeros(d),
+            "fc1": rnd(f, d), "fc1_b": zeros(f),
+            "fc2": rnd(d, f), "fc2_b": zeros(d),
+        }
+        if cross:
+            b.update({
+                "lnx_w": ones(d), "lnx_b": zeros(d),
+                "xq": rnd(d, d), "xq_b": zeros(d),
+                "xkv": rnd(2 * d, d), "xkv_b": zeros(2 * d),
+                "xo": rnd(d, d), "xo_b": zeros(d),
+            })
+        return b
+
+
+class WhisperModel:
+    def __init__(self, w: WhisperWeights):
+        self.w = w
+        self.cfg = w.cfg
+        self.mel = MelConstants.create(self.cfg.n_mels)
+
+    # ----------------------------------------------------------------- encoder
+    def encode(self, audio: torch.Tensor) -> torch.Tensor:
+        """audio [B, 480000] f32 (padded 30 s windows) -> encoder states [B*1500, d] bf16."""
+        cfg, w = self.cfg, self.w
+        B = audio.shape[0]
+        d, M = cfg.d_model, cfg.n_mels
+        mel = ops.log_mel(audio, self.mel)  # [B, M, 3000] bf16
+        frames = mel.shape[-1]
+        cols = ops.im2col_k3(mel, (M * frames, frames, 1), B, M, frames, 1)
+        x1 = ops.linear(cols, w.conv1_w)                      # [B*3000, d]
+        ops.gelu_bias_(x1, w.conv1_b)
+        cols2 = ops.im2col_k3(x1, (frames * d, 1, d), B, d, frames, 2)
+        x = ops.linear(cols2, w.conv2_w)                      # [B*1500, d]
+        ops.gelu_bias_(x, w.conv2_b, w.pos_enc)               # + positional embedding
+        T = cfg.n_audio_ctx
+        cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device=audio.device)
+        H, D = cfg.n_heads, cfg.head_dim
+        residual = x
+        h = ops.layernorm(x, w.enc[0]["ln1_w"], w.enc[0]["ln1_b"], 1e-5)
+        delta = None
+        for i, L in enumerate(w.enc):
+            if i > 0:
+                h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
+            qkv = ops.linear(h, L["wqkv"], L["bqkv"])
+            a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
+                              causal=False, max_q=T, cu_k=cu)
+            o = ops.linear(a, L["wo"], L["bo"])
+            h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
+            m = ops.linear(h, L["fc1"], L["fc1_b"])
+            ops.gelu_bias_(m)
+            delta = ops.linear(m, L["fc2"], L["fc2_b"])
+        return ops.layernorm(delta, w.enc_ln_w, w.enc_ln_b, 1e-5, residual=residual)
+
+    def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:
+        """Per decoder layer [B*1500, 2d] cross-attention K|V (computed once)."""
+        return [ops.linear(enc, L["xkv"], L["xkv_b"]) for L in self.w.dec]
+
+    # ----------------------------------------------------------------- decoder
+    def decode_step(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor,
+                    cu_q: torch.Tensor, ctx_lens: torch.Tensor, block_tables: torch.Tensor,
+                    max_q: int, max_ctx: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                    xkv: list[torch.Tensor], enc_starts: torch.Tensor, enc_lens: torch.Tensor,
+                    logit_idx: torch.Tensor, ws: ops.AttnWorkspace | None) -> torch.Tensor:
+        """One decoder forward over a flat token batch; returns logits [B, V] of
+        ``logit_idx`` rows. Self-attn K/V go to the paged cache (no RoPE)."""
+        cfg, w = self.cfg, self.w
+        d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
+        x = torch.nn.functional.embedding(tokens.long(), w.tok_embed)
+        x = x + w.dec_pos.index_select(0, positions.long())
+        residual = x
+        h = ops.layernorm(x, w.dec[0]["ln1_w"], w.dec[0]["ln1_b"], 1e-5)
+        delta = None
+        enc_splits = (cfg.n_audio_ctx + 255) // 256
+        self_splits = max(1, (max_ctx + 255) // 256)
+        grouped = max_q <= 128
+        for i, L in enumerate(w.dec):
+            if i > 0:
+                h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
+            qkv = ops.linear(h, L["wqkv"], L["bqkv"])
+            ops.rope_kv_append(qkv, None, None, k_cache[i], v_cache[i], slots, H, H, D)
+            a = ops.attention(qkv, k_cache[i], v_cache[i], cu_q, n_heads=H, n_kv=H, head_dim=D,
+                              causal=True, max_q=max_q, ctx_lens=ctx_lens,
+                              block_tables=block_tables, grouped=grouped, split_keys=256,
+                              num_splits=self_splits if grouped else 1, workspace=ws,
+                              max_k=max_ctx)
+            o = ops.linear(a, L["wo"], L["bo"])
+            h = ops.layernorm(o, L["lnx_w"], L["lnx_b"], 1e-5, residual=residual)
+            q = ops.linear(h, L["xq"], L["xq_b"])
+            kv = xkv[i]
+            xa = ops.attention(q, kv, kv[:, d:], cu_q, n_heads=H, n_kv=H, head_dim=D, causal=False,
+                               max_q=max_q, cu_k=enc_starts, ctx_lens=enc_lens,
+                               grouped=grouped, split_keys=256,
+                               num_splits=enc_splits if grouped else 1, workspace=ws)
+            xo = ops.linear(xa, L["xo"], L["xo_b"])
+            h = ops.layernorm(xo, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
+            m = ops.linear(h, L["fc1"], L["fc1_b"])
+            ops.gelu_bias_(m)
+            delta = ops.linear(m, L["fc2"], L["fc2_b"])
+        sel_r = residual.index_select(0, logit_idx).contiguous()
+        sel_d = delta.index_select(0, logit_idx).contiguous()
+        hf = ops.layernorm(sel_d, w.dec_ln_w, w.dec_ln_b, 1e-5, residual=sel_r)
+        return ops.linear(hf, w.tok_embed)
+
+
+def pad_or_trim(audio: np.ndarray, n: int = 480000) -> np.ndarray:
+    if len(audio) >= n:
+        return audio[:n]
+    return np.pad(audio, (0, n - len(audio)))

@@ -1,0 +1,289 @@
+"""Hot ops of the voice hub.
+
+Every op has two implementations:
+
+* the **HIP kernel** (``csrc/kernels``, gfx950 MFMA/LDS) used whenever the inputs
+  live on the GPU - a missing native library is a hard error there, never a
+  silent fallback;
+* a plain-PyTorch fp32 **reference** (``loqa_hub_amd.ops.reference``) used for
+  CPU inputs (the CPU test tier, the config-1 plumbing path) and as the
+  numerics oracle in ``tests/test_kernels_gpu.py``.
+
+Plain GEMMs go to hipBLASLt through ``torch.nn.functional.linear``; every fused
+elementwise/normalisation/attention/audio op around them is ours.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import reference as ref
+from ._lib import check, kernels, ptr, stream_ptr
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _bf16_contig(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+# --------------------------------------------------------------------- norms
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float,
+            residual: torch.Tensor | None = None) -> torch.Tensor:
+    """y = rmsnorm(x [+ residual]) * w; if residual is given it is updated in place
+    to x + residual (the fused pre-norm residual stream)."""
+    if not _gpu(x):
+        return ref.rmsnorm(x, w, eps, residual)
+    d = x.shape[-1]
+    rows = x.numel() // d
+    _bf16_contig(x, "x"); _bf16_contig(w, "w")
+    if residual is not None:
+        _bf16_contig(residual, "residual")
+        assert residual.shape == x.shape
+    assert w.numel() == d
+    y = torch.empty_like(x)
+    check(kernels().loqa_rmsnorm(ptr(x), ptr(residual), ptr(w), ptr(y), rows, d, eps,
+                                 stream_ptr(x)), "rmsnorm")
+    return y
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
+              residual: torch.Tensor | None = None) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.layernorm(x, w, b, eps, residual)
+    d = x.shape[-1]
+    rows = x.numel() // d
+    _bf16_contig(x, "x"); _bf16_contig(w, "w"); _bf16_contig(b, "b")
+    if residual is not None:
+        _bf16_contig(residual, "residual")
+        assert residual.shape == x.shape
+    y = torch.empty_like(x)
+    check(kernels().loqa_layernorm(ptr(x), ptr(residual), ptr(w), ptr(b), ptr(y), rows, d, eps,
+                                   stream_ptr(x)), "layernorm")
+    return y
+
+
+# --------------------------------------------------------------- elementwise
+def silu_mul(x: torch.Tensor) -> torch.Tensor:
+    """x: [..., 2F] = [gate | up] -> silu(gate) * up: [..., F]"""
+    if not _gpu(x):
+        return ref.silu_mul(x)
+    _bf16_contig(x, "x")
+    F = x.shape[-1] // 2
+    rows = x.numel() // (2 * F)
+    out = torch.empty(*x.shape[:-1], F, dtype=x.dtype, device=x.device)
+    check(kernels().loqa_silu_mul(ptr(x), ptr(out), rows, F, stream_ptr(x)), "silu_mul")
+    return out
+
+
+def gelu_bias_(x: torch.Tensor, bias: torch.Tensor | None = None,
+               pos: torch.Tensor | None = None) -> torch.Tensor:
+    """In place: x = gelu(x + bias) [+ pos[row % pos.shape[0]]]."""
+    if not _gpu(x):
+        return ref.gelu_bias_(x, bias, pos)
+    _bf16_contig(x, "x")
+    F = x.shape[-1]
+    rows = x.numel() // F
+    if bias is not None:
+        _bf16_contig(bias, "bias"); assert bias.numel() == F
+    period = 0
+    if pos is not None:
+        _bf16_contig(pos, "pos"); assert pos.shape[-1] == F
+        period = pos.shape[0]
+    check(kernels().loqa_gelu_bias(ptr(x), ptr(bias), ptr(pos), rows, F, period, stream_ptr(x)),
+          "gelu_bias")
+    return x
+
+
+def rope_kv_append(qkv: torch.Tensor, positions: torch.Tensor | None, cos_sin: torch.Tensor | None,
+                   k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
+                   n_heads: int, n_kv: int, head_dim: int) -> None:
+    """Rotate q (in place in ``qkv``) and k, and append k/v to the paged cache.
+
+    qkv: [T, >= (H + 2 Hkv) * D] bf16; positions/slots: [T] int32;
+    cos_sin: [max_pos, D/2, 2] f32 or None (no rotation);
+    caches: [n_blocks, Hkv, BLK, D] bf16.
+    """
+    if not _gpu(qkv):
+        return ref.rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, n_heads, n_kv,
+                                  head_dim)
+    T = qkv.shape[0]
+    if T == 0:
+        return None
+    assert qkv.dtype == torch.bfloat16 and qkv.stride(-1) == 1
+    assert qkv.shape[1] >= (n_heads + 2 * n_kv) * head_dim
+    assert slots.dtype == torch.int32 and slots.numel() == T and slots.is_contiguous()
+    if cos_sin is not None:
+        assert positions is not None and positions.dtype == torch.int32 and positions.numel() == T
+        assert cos_sin.dtype == torch.float32 and cos_sin.shape[-2] == head_dim // 2
+    assert k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim and k_cache.is_contiguous()
+    blk = k_cache.shape[2]
+    check(kernels().loqa_rope_kv_append(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin),
+                                        ptr(k_cache), ptr(v_cache), ptr(slots), T, n_heads, n_kv,
+                                        head_dim, blk, stream_ptr(qkv)), "rope_kv_append")
+    return None
+
+
+# ----------------------------------------------------------------- attention
+class AttnWorkspace:
+    """Split-K partial buffers for grouped decode attention (allocated once per
+    engine so the decode step stays graph-capturable)."""
+
+    def __init__(self, device, max_tokens: int, n_heads: int, head_dim: int, max_splits: int):
+        self.max_tokens, self.max_splits = max_tokens, max_splits
+        self.part_o = torch.empty(max_splits * max_tokens * n_heads * head_dim, dtype=torch.float32,
+                                  device=device)
+        self.part_ml = torch.empty(max_splits * max_tokens * n_heads * 2, dtype=torch.float32,
+                                   device=device)
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Tensor, *,
+              n_heads: int, n_kv: int, head_dim: int, causal: bool, max_q: int,
+              cu_k: torch.Tensor | None = None, ctx_lens: torch.Tensor | None = None,
+              block_tables: torch.Tensor | None = None, scale: float | None = None,
+              grouped: bool = False, split_keys: int = 256, num_splits: int = 1,
+              workspace: AttnWorkspace | None = None, out: torch.Tensor | None = None,
+              max_k: int | None = None) -> torch.Tensor:
+    """Varlen flash attention.
+
+    q: [Tq, >=H*D] (row stride may exceed H*D, e.g. a view into the fused QKV
+    output). K/V: contiguous [Tk, >=Hkv*D] with ``cu_k``, or paged caches
+    [n_blocks, Hkv, BLK, D] with ``ctx_lens`` + ``block_tables``.
+    Query i of sequence b sits at absolute position ctx_len_b - q_len_b + i.
+    Returns [Tq, H*D] bf16.
+    """
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    if not _gpu(q):
+        return ref.attention(q, k, v, cu_q, n_heads=n_heads, n_kv=n_kv, head_dim=head_dim,
+                             causal=causal, cu_k=cu_k, ctx_lens=ctx_lens,
+                             block_tables=block_tables, scale=scale, out=out)
+    Tq = q.shape[0]
+    B = cu_q.numel() - 1
+    if out is None:
+        out = torch.empty(Tq, n_heads * head_dim, dtype=torch.bfloat16, device=q.device)
+    if Tq == 0 or B == 0:
+        return out
+    assert q.dtype == torch.bfloat16 and q.stride(-1) == 1 and q.shape[1] >= n_heads * head_dim
+    assert cu_q.dtype == torch.int32 and cu_q.is_contiguous()
+    assert out.stride(-1) == 1 and out.shape[0] == Tq
+    paged = block_tables is not None
+    if paged:
+        assert k.dim() == 4 and k.shape[1] == n_kv and k.shape[3] == head_dim and k.is_contiguous()
+        assert v.shape == k.shape and v.is_contiguous()
+        assert ctx_lens is not None and ctx_lens.dtype == torch.int32 and ctx_lens.numel() == B
+        assert block_tables.dtype == torch.int32 and block_tables.is_contiguous()
+        assert block_tables.shape[0] == B
+        blk, max_blocks, kv_stride = k.shape[2], block_tables.shape[1], 0
+        if max_k is not None:
+            assert max_k <= max_blocks * blk, "context exceeds block table"
+    else:
+        assert cu_k is not None and cu_k.dtype == torch.int32
+        if ctx_lens is None:
+            assert cu_k.numel() == B + 1
+        else:  # explicit per-sequence starts (cu_k) and lengths (ctx_lens)
+            assert cu_k.numel() >= B and ctx_lens.dtype == torch.int32 and ctx_lens.numel() == B
+        assert k.stride(-1) == 1 and v.stride(-1) == 1 and k.stride(0) == v.stride(0)
+        blk, max_blocks, kv_stride = 0, 0, k.stride(0)
+    part_o = part_ml = None
+    if grouped:
+        G = n_heads // n_kv
+        assert max_q * G <= 128, "grouped attention handles at most 128/G query tokens"
+        if num_splits > 1:
+            assert workspace is not None and workspace.max_splits >= num_splits
+            assert workspace.max_tokens >= Tq
+            part_o, part_ml = workspace.part_o, workspace.part_ml
+    check(kernels().loqa_attention(
+        ptr(q), q.stride(0), ptr(k), ptr(v), kv_stride, ptr(out), out.stride(0), ptr(cu_q),
+        ptr(cu_k), ptr(ctx_lens), ptr(block_tables), max_blocks, blk, B, max_q, n_heads, n_kv,
+        head_dim, scale, int(causal), int(grouped), split_keys, num_splits, ptr(part_o),
+        ptr(part_ml), Tq, stream_ptr(q)), "attention")
+    return out
+
+
+# ----------------------------------------------------------------- sampling
+def masked_argmax(logits: torch.Tensor, mask: torch.Tensor | None = None,
+                  mask_rows: torch.Tensor | None = None) -> torch.Tensor:
+    """argmax over tokens allowed by a packed uint32 bitmask (bit v%32 of word
+    v//32). ``mask_rows`` optionally maps each logits row to a mask-table row.
+    Returns int32 [B] (-1 if nothing is allowed)."""
+    if not _gpu(logits):
+        return ref.masked_argmax(logits, mask, mask_rows)
+    assert logits.dim() == 2 and logits.stride(-1) == 1
+    B, V = logits.shape
+    W = 0
+    if mask is not None:
+        assert mask.dtype == torch.int32 and mask.is_contiguous()
+        W = mask.shape[-1]
+        assert W * 32 >= V
+        if mask_rows is not None:
+            assert mask_rows.dtype == torch.int32 and mask_rows.numel() == B
+        else:
+            assert mask.shape[0] >= B
+    is_bf16 = logits.dtype == torch.bfloat16
+    assert is_bf16 or logits.dtype == torch.float32
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    check(kernels().loqa_masked_argmax(ptr(logits), int(is_bf16), logits.stride(0), B, V,
+                                       ptr(mask), ptr(mask_rows), W, ptr(out), None,
+                                       stream_ptr(logits)), "masked_argmax")
+    return out
+
+
+# -------------------------------------------------------------------- audio
+def pcm16_to_f32_sumsq(pcm: torch.Tensor, offsets: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """pcm: int16 [N] (concatenated segments), offsets: int64 [S+1].
+    Returns (f32 samples [N] = x/32767, per-segment sum of squares [S])."""
+    if not _gpu(pcm):
+        return ref.pcm16_to_f32_sumsq(pcm, offsets)
+    assert pcm.dtype == torch.int16 and pcm.is_contiguous()
+    assert offsets.dtype == torch.int64 and offsets.is_contiguous()
+    S = offsets.numel() - 1
+    out = torch.empty(pcm.numel(), dtype=torch.float32, device=pcm.device)
+    sumsq = torch.empty(max(S, 1), dtype=torch.float32, device=pcm.device)
+    seg = offsets.cpu()
+    max_len = int((seg[1:] - seg[:-1]).max()) if S > 0 else 0
+    assert int(seg[-1]) <= pcm.numel()
+    check(kernels().loqa_pcm16_f32_sumsq(ptr(pcm), ptr(out), ptr(offsets), ptr(sumsq), S, max_len,
+                                         stream_ptr(pcm)), "pcm16_f32_sumsq")
+    return out, sumsq[:S]
+
+
+def log_mel(audio: torch.Tensor, consts: "ref.MelConstants") -> torch.Tensor:
+    """audio [B, n_samples] f32 (padded to 30 s) -> whisper log-mel [B, n_mels, frames] bf16."""
+    if not _gpu(audio):
+        return ref.log_mel(audio, consts).to(torch.bfloat16)
+    assert audio.dtype == torch.float32 and audio.is_contiguous() and audio.dim() == 2
+    B, n = audio.shape
+    frames = n // 160
+    c = consts.to(audio.device)
+    work = torch.empty(B, c.n_mels, frames, dtype=torch.float32, device=audio.device)
+    gmax = torch.empty(B, dtype=torch.float32, device=audio.device)
+    out = torch.empty(B, c.n_mels, frames, dtype=torch.bfloat16, device=audio.device)
+    check(kernels().loqa_log_mel(ptr(audio), B, n, ptr(c.window), ptr(c.cos_basis),
+                                 ptr(c.sin_basis), ptr(c.filters), c.n_mels, ptr(work), ptr(gmax),
+                                 ptr(out), frames, stream_ptr(audio)), "log_mel")
+    return out
+
+
+def im2col_k3(x: torch.Tensor, strides: tuple[int, int, int], B: int, C: int, L: int,
+              stride: int) -> torch.Tensor:
+    """Unfold a k=3/pad=1 conv1d input. x element (b,c,t) at
+    b*strides[0] + c*strides[1] + t*strides[2]. Returns [B*Lout, 3C] bf16."""
+    Lout = (L - 1) // stride + 1
+    if not _gpu(x):
+        return ref.im2col_k3(x, strides, B, C, L, stride)
+    assert x.dtype == torch.bfloat16
+    cols = torch.empty(B * Lout, 3 * C, dtype=torch.bfloat16, device=x.device)
+    check(kernels().loqa_im2col_k3(ptr(x), strides[0], strides[1], strides[2], B, C, L, stride,
+                                   ptr(cols), stream_ptr(x)), "im2col_k3")
+    return cols
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """Plain GEMM: hipBLASLt via torch on the GPU."""
+    return torch.nn.functional.linear(x, w, b)

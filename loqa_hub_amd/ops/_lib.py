@@ -1,0 +1,127 @@
+"""ctypes bindings for the in-tree native libraries (``loqa_hub_amd/_native``).
+
+The libraries are loaded lazily, always *after* ``import torch`` so they bind
+to the HIP runtime torch already mapped (same soname ``libamdhip64.so.7``).
+On a GPU box a missing library is a hard error: GPU ops never silently fall
+back to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be imported before the HIP libraries)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_NATIVE = os.path.join(os.path.dirname(_HERE), "_native")
+_lock = threading.Lock()
+_kernels = None
+_runtime = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_float = ctypes.c_float
+
+_KERNEL_SIGS = {
+    "loqa_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "loqa_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                       c_void_p],
+    "loqa_silu_mul": [c_void_p, c_void_p, c_ll, c_int, c_void_p],
+    "loqa_gelu_bias": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_void_p],
+    "loqa_rope_kv_append": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "loqa_pcm16_f32_sumsq": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p],
+    "loqa_masked_argmax": [c_void_p, c_int, c_ll, c_int, c_int, c_void_p, c_void_p, c_int,
+                           c_void_p, c_void_p, c_void_p],
+    "loqa_attention": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_ll, c_void_p,
+                       c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                       c_int, c_float, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                       c_void_p],
+    "loqa_log_mel": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                     c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "loqa_im2col_k3": [c_void_p, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void_p,
+                       c_void_p],
+}
+
+_RUNTIME_SIGS = {
+    "loqa_stager_create": ([c_int, c_ll], c_void_p),
+    "loqa_stager_destroy": ([c_void_p], None),
+    "loqa_stager_acquire": ([c_void_p], c_int),
+    "loqa_stager_append": ([c_void_p, c_int, c_void_p, c_ll], c_ll),
+    "loqa_stager_len": ([c_void_p, c_int], c_ll),
+    "loqa_stager_host_ptr": ([c_void_p, c_int], c_void_p),
+    "loqa_stager_upload": ([c_void_p, c_int, c_void_p, c_ll, c_void_p], c_int),
+    "loqa_stager_release": ([c_void_p, c_int], None),
+    "loqa_pool_create": ([c_int, c_int], c_void_p),
+    "loqa_pool_destroy": ([c_void_p], None),
+    "loqa_pool_free_blocks": ([c_void_p], c_int),
+    "loqa_pool_add_seq": ([c_void_p, c_ll, c_void_p, c_int], c_ll),
+    "loqa_pool_append": ([c_void_p, c_ll, c_int, c_void_p], c_int),
+    "loqa_pool_cache_prefix": ([c_void_p, c_ll, c_void_p, c_int], c_int),
+    "loqa_pool_block_table": ([c_void_p, c_ll, c_void_p, c_int], c_int),
+    "loqa_pool_seq_len": ([c_void_p, c_ll], c_ll),
+    "loqa_pool_free_seq": ([c_void_p, c_ll], c_int),
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def _load(name: str) -> ctypes.CDLL:
+    path = os.path.join(_NATIVE, name)
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} is missing: run `python -m loqa_hub_amd._native.build` (gfx950)")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def kernels() -> ctypes.CDLL:
+    global _kernels
+    if _kernels is None:
+        with _lock:
+            if _kernels is None:
+                lib = _load("libloqa_kernels.so")
+                for fn, sig in _KERNEL_SIGS.items():
+                    f = getattr(lib, fn)
+                    f.argtypes = sig
+                    f.restype = c_int
+                _kernels = lib
+    return _kernels
+
+
+def runtime() -> ctypes.CDLL:
+    global _runtime
+    if _runtime is None:
+        with _lock:
+            if _runtime is None:
+                lib = _load("libloqa_runtime.so")
+                for fn, (args, res) in _RUNTIME_SIGS.items():
+                    f = getattr(lib, fn)
+                    f.argtypes = args
+                    f.restype = res
+                _runtime = lib
+    return _runtime
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except (NativeLibraryMissing, OSError):
+        return False
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream_ptr(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,267 @@
+"""Plain-PyTorch fp32 reference implementations of every hot op.
+
+These are the numerics oracle for the HIP kernels (tests compare kernel output
+against them) and the CPU execution path (no GPU in the CI tier).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+
+def rmsnorm(x, w, eps, residual=None):
+    if residual is not None:
+        s = (x.float() + residual.float()).to(residual.dtype)
+        residual.copy_(s)
+        x = s
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype)
+
+
+def layernorm(x, w, b, eps, residual=None):
+    if residual is not None:
+        s = (x.float() + residual.float()).to(residual.dtype)
+        residual.copy_(s)
+        x = s
+    y = torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(x.dtype)
+
+
+def silu_mul(x):
+    F = x.shape[-1] // 2
+    g, u = x[..., :F].float(), x[..., F:].float()
+    return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+
+def gelu_bias_(x, bias=None, pos=None):
+    y = x.float()
+    if bias is not None:
+        y = y + bias.float()
+    y = torch.nn.functional.gelu(y)
+    if pos is not None:
+        rows = y.reshape(-1, y.shape[-1]).shape[0]
+        idx = torch.arange(rows, device=x.device) % pos.shape[0]
+        y = (y.reshape(-1, y.shape[-1]) + pos.float()[idx]).reshape(y.shape)
+    x.copy_(y.to(x.dtype))
+    return x
+
+
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, device=None) -> torch.Tensor:
+    """[max_pos, D/2, 2] f32 table of (cos, sin) for NeoX rotate-half RoPE."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).float().to(device)
+
+
+def apply_rope(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
+    """x [T, H, D] (any float), cs [T, D/2, 2] -> rotated x (fp32)."""
+    half = x.shape[-1] // 2
+    a, b = x[..., :half].float(), x[..., half:].float()
+    c, s = cs[:, None, :, 0], cs[:, None, :, 1]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+
+
+def rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D):
+    T = qkv.shape[0]
+    if T == 0:
+        return None
+    q = qkv[:, : H * D].view(T, H, D)
+    k = qkv[:, H * D:(H + Hkv) * D].view(T, Hkv, D)
+    v = qkv[:, (H + Hkv) * D:(H + 2 * Hkv) * D].view(T, Hkv, D)
+    if cos_sin is not None:
+        cs = cos_sin[positions.long()]
+        q.copy_(apply_rope(q, cs).to(q.dtype))
+        k = apply_rope(k, cs).to(qkv.dtype)
+    blk = k_cache.shape[2]
+    sl = slots.long()
+    valid = sl >= 0
+    b, o = (sl // blk)[valid], (sl % blk)[valid]
+    k_cache[b, :, o, :] = k[valid].to(k_cache.dtype)
+    v_cache[b, :, o, :] = v[valid].to(v_cache.dtype)
+    return None
+
+
+def attention(q, k, v, cu_q, *, n_heads, n_kv, head_dim, causal, cu_k=None, ctx_lens=None,
+              block_tables=None, scale=None, out=None):
+    H, Hkv, D = n_heads, n_kv, head_dim
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    Tq = q.shape[0]
+    res = torch.zeros(Tq, H * D, dtype=torch.float32, device=q.device)
+    cuq = cu_q.tolist()
+    G = H // Hkv
+    for b in range(len(cuq) - 1):
+        q0, q1 = cuq[b], cuq[b + 1]
+        ql = q1 - q0
+        if ql == 0:
+            continue
+        if block_tables is not None:
+            L = int(ctx_lens[b])
+            blk = k.shape[2]
+            idx = torch.arange(L, device=k.device)
+            bt = block_tables[b].long()[idx // blk]
+            kb = k[bt, :, idx % blk, :].float()  # [L, Hkv, D]
+            vb = v[bt, :, idx % blk, :].float()
+        else:
+            k0 = int(cu_k[b])
+            k1 = k0 + int(ctx_lens[b]) if ctx_lens is not None else int(cu_k[b + 1])
+            L = k1 - k0
+            kb = k[k0:k1, : Hkv * D].reshape(L, Hkv, D).float()
+            vb = v[k0:k1, : Hkv * D].reshape(L, Hkv, D).float()
+        qb = q[q0:q1, : H * D].reshape(ql, H, D).float()
+        kb = kb.repeat_interleave(G, dim=1)
+        vb = vb.repeat_interleave(G, dim=1)
+        s = torch.einsum("qhd,khd->hqk", qb, kb) * scale
+        if causal:
+            qpos = torch.arange(ql, device=q.device) + (L - ql)
+            kpos = torch.arange(L, device=q.device)
+            s = s.masked_fill(kpos[None, None, :] > qpos[None, :, None], float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        p = torch.nan_to_num(p, nan=0.0)
+        res[q0:q1] = torch.einsum("hqk,khd->qhd", p, vb).reshape(ql, H * D)
+    r = res.to(q.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def masked_argmax(logits, mask=None, mask_rows=None):
+    x = logits.float()
+    B, V = x.shape
+    if mask is not None:
+        m = mask if mask_rows is None else mask[mask_rows.long()]
+        bits = unpack_mask(m, V)
+        x = x.masked_fill(~bits, float("-inf"))
+        none = ~bits.any(dim=-1)
+    else:
+        none = torch.zeros(B, dtype=torch.bool, device=x.device)
+    r = x.argmax(dim=-1).to(torch.int32)
+    r[none] = -1
+    return r
+
+
+def unpack_mask(m: torch.Tensor, V: int) -> torch.Tensor:
+    """int32 words [..., W] -> bool [..., V]"""
+    shifts = torch.arange(32, device=m.device, dtype=torch.int32)
+    bits = (m.unsqueeze(-1) >> shifts) & 1
+    return bits.reshape(*m.shape[:-1], -1)[..., :V].bool()
+
+
+def pack_mask(bits: torch.Tensor) -> torch.Tensor:
+    """bool [..., V] -> int32 words [..., ceil(V/32)]"""
+    V = bits.shape[-1]
+    W = (V + 31) // 32
+    pad = torch.zeros(*bits.shape[:-1], W * 32, dtype=torch.int64, device=bits.device)
+    pad[..., :V] = bits.long()
+    w = (pad.reshape(*bits.shape[:-1], W, 32) << torch.arange(32, device=bits.device)).sum(-1)
+    w = torch.where(w >= 2**31, w - 2**32, w)
+    return w.to(torch.int32)
+
+
+def pcm16_to_f32_sumsq(pcm, offsets):
+    f = pcm.float() / 32767.0
+    off = offsets.tolist()
+    ss = torch.tensor([float((f[off[i]:off[i + 1]].double() ** 2).sum()) for i in range(len(off) - 1)],
+                      dtype=torch.float32)
+    return f, ss
+
+
+# ------------------------------------------------------------- log-mel consts
+def _hz_to_mel(f):
+    f = np.asarray(f, dtype=np.float64)
+    f_sp = 200.0 / 3
+    mels = f / f_sp
+    min_log_hz = 1000.0
+    min_log_mel = min_log_hz / f_sp
+    logstep = np.log(6.4) / 27.0
+    return np.where(f >= min_log_hz, min_log_mel + np.log(np.maximum(f, 1e-10) / min_log_hz) / logstep, mels)
+
+
+def _mel_to_hz(m):
+    m = np.asarray(m, dtype=np.float64)
+    f_sp = 200.0 / 3
+    freqs = f_sp * m
+    min_log_hz = 1000.0
+    min_log_mel = min_log_hz / f_sp
+    logstep = np.log(6.4) / 27.0
+    return np.where(m >= min_log_mel, min_log_hz * np.exp(logstep * (m - min_log_mel)), freqs)
+
+
+def mel_filterbank(sr: int = 16000, n_fft: int = 400, n_mels: int = 80) -> np.ndarray:
+    """Slaney-style mel filterbank (librosa defaults, as whisper uses)."""
+    n_freqs = 1 + n_fft // 2
+    fftfreqs = np.linspace(0, sr / 2, n_freqs)
+    mel_f = _mel_to_hz(np.linspace(_hz_to_mel(0.0), _hz_to_mel(sr / 2), n_mels + 2))
+    fdiff = np.diff(mel_f)
+    ramps = mel_f[:, None] - fftfreqs[None, :]
+    lower = -ramps[:-2] / fdiff[:-1, None]
+    upper = ramps[2:] / fdiff[1:, None]
+    w = np.maximum(0, np.minimum(lower, upper))
+    enorm = 2.0 / (mel_f[2: n_mels + 2] - mel_f[:n_mels])
+    return (w * enorm[:, None]).astype(np.float32)
+
+
+@dataclass
+class MelConstants:
+    n_mels: int
+    window: torch.Tensor      # [400]
+    cos_basis: torch.Tensor   # [400, 224]
+    sin_basis: torch.Tensor   # [400, 224]
+    filters: torch.Tensor     # [n_mels, 201]
+
+    @staticmethod
+    def create(n_mels: int = 80) -> "MelConstants":
+        n = np.arange(400)
+        window = (0.5 - 0.5 * np.cos(2 * np.pi * n / 400)).astype(np.float32)  # periodic Hann
+        k = np.arange(224)
+        ang = 2 * np.pi * np.outer(n, k) / 400
+        cosb = np.cos(ang)
+        sinb = -np.sin(ang)
+        cosb[:, 201:] = 0
+        sinb[:, 201:] = 0
+        return MelConstants(n_mels, torch.from_numpy(window), torch.from_numpy(cosb.astype(np.float32)),
+                            torch.from_numpy(sinb.astype(np.float32)),
+                            torch.from_numpy(mel_filterbank(n_mels=n_mels)))
+
+    def to(self, device) -> "MelConstants":
+        device = torch.device(device)
+        if self.window.device == device:
+            return self
+        cache = self.__dict__.setdefault("_dev_cache", {})
+        key = str(device)
+        if key not in cache:
+            cache[key] = MelConstants(self.n_mels, self.window.to(device), self.cos_basis.to(device),
+                                      self.sin_basis.to(device), self.filters.to(device))
+        return cache[key]
+
+
+def log_mel(audio: torch.Tensor, c: MelConstants) -> torch.Tensor:
+    """Whisper log-mel (whisper/audio.py semantics) in fp32: [B, n_mels, n//160]."""
+    win = c.window.to(audio.device)
+    st = torch.stft(audio.float(), 400, 160, window=win, return_complex=True, center=True,
+                    pad_mode="reflect")
+    mag = st[..., :-1].abs() ** 2
+    mel = c.filters.to(audio.device) @ mag
+    lg = torch.clamp(mel, min=1e-10).log10()
+    mx = lg.amax(dim=(-2, -1), keepdim=True)
+    lg = torch.maximum(lg, mx - 8.0)
+    return (lg + 4.0) / 4.0
+
+
+def im2col_k3(x, strides, B, C, L, stride):
+    Lout = (L - 1) // stride + 1
+    flat = x.reshape(-1)
+    b = torch.arange(B, device=x.device)[:, None, None, None]
+    to = torch.arange(Lout, device=x.device)[None, :, None, None]
+    c = torch.arange(C, device=x.device)[None, None, :, None]
+    k = torch.arange(3, device=x.device)[None, None, None, :]
+    t = to * stride + k - 1
+    valid = (t >= 0) & (t < L)
+    idx = b * strides[0] + c * strides[1] + t.clamp(0, L - 1) * strides[2]
+    vals = flat[idx.reshape(-1)].reshape(B, Lout, C, 3)
+    vals = torch.where(valid.expand(B, Lout, C, 3), vals, torch.zeros((), dtype=x.dtype))
+    return vals.reshape(B * Lout, 3 * C)

@@ -1,0 +1,68 @@
+"""Process-group bootstrap: one process per GPU, ``torch.distributed`` over
+RCCL (backend "nccl" on ROCm) across the xGMI mesh, gloo on CPU.
+
+Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    local_rank: int = 0
+    world: int = 1
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_distributed(prefer_gpu: bool = True) -> DistInfo:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    backend = "none"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = {"device_id": device} if use_gpu else {}
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    return DistInfo(rank, local, world, device, backend)
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1:
+        if info.device.type == "cuda":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(info: DistInfo, value: float) -> float:
+    if info.world == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=info.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown(info: DistInfo) -> None:
+    if info.world > 1 and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,229 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the
+same op (ops/reference.py). Shapes follow SURVEY §2.4."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from loqa_hub_amd import ops
+from loqa_hub_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("d,rows", [(4096, 37), (2048, 5), (8192, 3), (384, 64)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(d, rows, with_res):
+    x = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).bfloat16()
+    r1 = torch.randn(rows, d, device=DEV, dtype=torch.bfloat16) if with_res else None
+    r2 = r1.clone() if with_res else None
+    y = ops.rmsnorm(x, w, 1e-5, residual=r1)
+    yr = ref.rmsnorm(x, w, 1e-5, residual=r2)
+    assert _rel(y, yr) < 1e-2
+    if with_res:
+        assert torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("d", [1280, 384, 512])
+def test_layernorm(d):
+    x = torch.randn(300, d, device=DEV, dtype=torch.bfloat16) * 3 + 1
+    w = torch.randn(d, device=DEV).bfloat16()
+    b = torch.randn(d, device=DEV).bfloat16()
+    r1 = torch.randn_like(x)
+    r2 = r1.clone()
+    y = ops.layernorm(x, w, b, 1e-5, residual=r1)
+    yr = ref.layernorm(x, w, b, 1e-5, residual=r2)
+    assert _rel(y, yr) < 1e-2
+
+
+def test_silu_mul_and_gelu():
+    x = torch.randn(77, 2 * 1408, device=DEV, dtype=torch.bfloat16)
+    assert _rel(ops.silu_mul(x), ref.silu_mul(x)) < 1e-2
+    y = torch.randn(3000, 512, device=DEV, dtype=torch.bfloat16)
+    bias = torch.randn(512, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randn(1500, 512, device=DEV, dtype=torch.bfloat16)
+    y2 = y.clone()
+    ops.gelu_bias_(y, bias, pos)
+    ref.gelu_bias_(y2, bias, pos)
+    assert _rel(y, y2) < 1e-2
+
+
+def test_rope_kv_append():
+    H, Hkv, D, blk, T = 8, 2, 128, 16, 21
+    qkv = torch.randn(T, (H + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 500, (T,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(D, 1024, 500000.0, device=DEV)
+    slots = torch.randperm(8 * blk, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1
+    kc1 = torch.zeros(8, Hkv, blk, D, device=DEV, dtype=torch.bfloat16)
+    vc1 = torch.zeros_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    q1, q2 = qkv.clone(), qkv.clone()
+    ops.rope_kv_append(q1, pos, cs, kc1, vc1, slots, H, Hkv, D)
+    ref.rope_kv_append(q2, pos, cs, kc2, vc2, slots, H, Hkv, D)
+    assert _rel(q1, q2) < 1e-2
+    assert _rel(kc1, kc2) < 1e-2
+    assert torch.equal(vc1, vc2)
+
+
+def _paged(kv_tokens, blk, n_blocks):
+    """Scatter per-seq contiguous K [L, Hkv, D] into a random paged layout."""
+    Hkv, D = kv_tokens[0].shape[1:]
+    cache = torch.zeros(n_blocks, Hkv, blk, D, device=DEV, dtype=torch.bfloat16)
+    perm = torch.randperm(n_blocks).tolist()
+    tables = []
+    for kt in kv_tokens:
+        nb = (kt.shape[0] + blk - 1) // blk
+        tab = [perm.pop() for _ in range(nb)]
+        for i in range(kt.shape[0]):
+            cache[tab[i // blk], :, i % blk] = kt[i]
+        tables.append(tab)
+    mb = max(len(t) for t in tables)
+    bt = torch.zeros(len(tables), mb, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = torch.tensor(t)
+    return cache, bt.to(DEV)
+
+
+@pytest.mark.parametrize("D,H,Hkv", [(64, 4, 4), (128, 8, 2)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_prefill_contiguous(D, H, Hkv, causal):
+    lens = [1500, 37, 200]
+    T = sum(lens)
+    q = torch.randn(T, H * D, device=DEV, dtype=torch.bfloat16)
+    kv = torch.randn(T, 2 * Hkv * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int32, device=DEV)
+    k, v = kv[:, : Hkv * D], kv[:, Hkv * D:]
+    o = ops.attention(q, k, v, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=causal, max_q=max(lens), cu_k=cu)
+    orf = ref.attention(q, k, v, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=causal, cu_k=cu)
+    assert _rel(o, orf) < 2e-2
+
+
+@pytest.mark.parametrize("G", [1, 4])
+def test_attention_prefill_paged_with_prefix(G):
+    D, Hkv = 128, 2
+    H = Hkv * G
+    blk = 16
+    ctx = [400, 90, 33]
+    ql = [380, 90, 1]          # seq 0 has a 20-token cached prefix
+    ks = [torch.randn(c, Hkv, D, device=DEV, dtype=torch.bfloat16) for c in ctx]
+    vs = [torch.randn(c, Hkv, D, device=DEV, dtype=torch.bfloat16) for c in ctx]
+    kc, bt = _paged(ks, blk, 64)
+    torch.manual_seed(1)
+    vc, _ = _paged(vs, blk, 64)
+    # same layout for V: rebuild with the same tables
+    vc = torch.zeros_like(kc)
+    for b, vt in enumerate(vs):
+        for i in range(vt.shape[0]):
+            vc[int(bt[b, i // blk]), :, i % blk] = vt[i]
+    q = torch.randn(sum(ql), H * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(ql)), dtype=torch.int32, device=DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    o = ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, max_q=max(ql),
+                      ctx_lens=cl, block_tables=bt)
+    orf = ref.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, ctx_lens=cl,
+                        block_tables=bt)
+    assert _rel(o, orf) < 2e-2
+
+
+@pytest.mark.parametrize("qlens,G,splits", [([1, 1, 1, 1], 4, 4), ([3, 1, 7, 2], 4, 2),
+                                            ([1, 1], 1, 1), ([16, 5], 8, 3)])
+def test_attention_grouped_paged(qlens, G, splits):
+    D, Hkv, blk = 128, 2, 16
+    H = Hkv * G
+    ctx = [700, 65, 300, 1][: len(qlens)]
+    ctx = [max(c, q) for c, q in zip(ctx, qlens)]
+    ks = [torch.randn(c, Hkv, D, device=DEV, dtype=torch.bfloat16) for c in ctx]
+    kc, bt = _paged(ks, blk, 128)
+    vc = torch.randn_like(kc)
+    q = torch.randn(sum(qlens), H * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(qlens)), dtype=torch.int32, device=DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    ws = ops.AttnWorkspace(DEV, 64, H, D, 4)
+    split_keys = 256
+    o = ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, max_q=max(qlens),
+                      ctx_lens=cl, block_tables=bt, grouped=True, split_keys=split_keys,
+                      num_splits=max(splits, math.ceil(max(ctx) / split_keys)), workspace=ws)
+    orf = ref.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, ctx_lens=cl,
+                        block_tables=bt)
+    assert _rel(o, orf) < 2e-2
+
+
+def test_attention_grouped_cross_starts():
+    """Whisper cross-attention: subset of utterances addressed by start/len."""
+    D, H, T = 64, 6, 1500
+    enc = torch.randn(4 * T, 2 * H * D, device=DEV, dtype=torch.bfloat16)
+    live = [0, 2, 3]
+    q = torch.randn(len(live), H * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.arange(len(live) + 1, dtype=torch.int32, device=DEV)
+    starts = torch.tensor([i * T for i in live], dtype=torch.int32, device=DEV)
+    lens = torch.full((len(live),), T, dtype=torch.int32, device=DEV)
+    ws = ops.AttnWorkspace(DEV, 64, H, D, 8)
+    o = ops.attention(q, enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D, causal=False, max_q=1,
+                      cu_k=starts, ctx_lens=lens, grouped=True, split_keys=256, num_splits=6, workspace=ws)
+    orf = ref.attention(q, enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D, causal=False,
+                        cu_k=starts, ctx_lens=lens)
+    assert _rel(o, orf) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_masked_argmax(dtype):
+    B, V = 6, 128256
+    logits = torch.randn(B, V, device=DEV).to(dtype)
+    bits = torch.rand(3, V, device=DEV) < 0.01
+    bits[2] = False
+    bits[2, 12345] = True
+    mask = ref.pack_mask(bits)
+    rows = torch.tensor([0, 1, 2, 0, 1, 2], dtype=torch.int32, device=DEV)
+    a = ops.masked_argmax(logits, mask, rows)
+    b = ref.masked_argmax(logits, mask, rows)
+    assert torch.equal(a.cpu(), b.cpu())
+    assert int(a[2]) == 12345
+    assert torch.equal(ops.masked_argmax(logits).cpu(), logits.float().argmax(-1).int().cpu())
+
+
+def test_pcm16_sumsq():
+    segs = [np.random.randint(-32768, 32767, n).astype(np.int16) for n in (16000, 1, 70001)]
+    cat = torch.from_numpy(np.concatenate(segs)).to(DEV)
+    off = torch.tensor([0, 16000, 16001, 86002], dtype=torch.int64, device=DEV)
+    f, ss = ops.pcm16_to_f32_sumsq(cat, off)
+    fr, ssr = ref.pcm16_to_f32_sumsq(cat.cpu(), off.cpu())
+    assert torch.allclose(f.cpu(), fr)
+    assert torch.allclose(ss.cpu(), ssr, rtol=1e-4)
+
+
+@pytest.mark.parametrize("n_mels", [80, 128])
+def test_log_mel(n_mels):
+    c = ref.MelConstants.create(n_mels)
+    t = np.arange(480000) / 16000
+    a = np.stack([0.3 * np.sin(2 * np.pi * 440 * t) * (t < 3), 0.1 * np.random.randn(480000)])
+    audio = torch.from_numpy(a.astype(np.float32)).to(DEV)
+    m = ops.log_mel(audio, c).float()
+    mr = ref.log_mel(audio, c)
+    assert m.shape == mr.shape == (2, n_mels, 3000)
+    assert float((m - mr).abs().max()) < 0.05
+
+
+def test_im2col():
+    x = torch.randn(2, 80, 3000, device=DEV, dtype=torch.bfloat16)
+    a = ops.im2col_k3(x, (80 * 3000, 3000, 1), 2, 80, 3000, 1)
+    b = ref.im2col_k3(x, (80 * 3000, 3000, 1), 2, 80, 3000, 1)
+    assert torch.equal(a, b)
+    y = torch.randn(2, 3000, 64, device=DEV, dtype=torch.bfloat16)
+    a = ops.im2col_k3(y, (3000 * 64, 1, 64), 2, 64, 3000, 2)
+    b = ref.im2col_k3(y, (3000 * 64, 1, 64), 2, 64, 3000, 2)
+    assert torch.equal(a, b)
