@@ -83,7 +83,7 @@ class LLMEngine:
                                self.device)
         self.is_gpu = self.device.type == "cuda"
         self.attn_ws = ops.AttnWorkspace(self.device, max_seqs * self.MAX_DECODE_Q, self.weights.h,
-                                         cfg.head_dim, (max_seq_len + 255) // 256) if self.is_gpu else None
+                                         cfg.head_dim, (max_seq_len + 63) // 64) if self.is_gpu else None
         self.use_graphs = use_graphs and self.is_gpu
         self.prefill_chunk = prefill_chunk
         self._graphs: dict[tuple[int, int], dict] = {}
@@ -105,7 +105,7 @@ class LLMEngine:
         cu = np.zeros(B_pad + 1, np.int32)
         ctx = np.zeros(B_pad, np.int32)
         bt = np.zeros((B_pad, self.max_blocks), np.int32)
-        lidx = np.zeros(B_pad, np.int64)
+        lidx = np.zeros(max(16, B_pad) if decode else B_pad, np.int64)
         off = 0
         max_q = 1
         max_ctx = 1
@@ -147,8 +147,12 @@ class LLMEngine:
 
     # ------------------------------------------------------------ forward
     def _forward_sample(self, meta: StepMeta, mask_rows: torch.Tensor) -> torch.Tensor:
-        hid = self.model.forward(meta, self.kv.k, self.kv.v, self.attn_ws)
-        logits = self.model.logits(hid)
+        if meta.decode:
+            logits = self.model.forward_decode(meta, self.kv.k, self.kv.v, self.attn_ws)
+            logits = logits[: mask_rows.numel()]
+        else:
+            hid = self.model.forward(meta, self.kv.k, self.kv.v, self.attn_ws)
+            logits = self.model.logits(hid)
         if self.tp.world == 1:
             return ops.masked_argmax(logits, self.masks, mask_rows)
         return self._tp_argmax(logits, mask_rows)
@@ -188,7 +192,7 @@ class LLMEngine:
             "cu_q": torch.zeros(B_pad + 1, dtype=torch.int32, device=self.device),
             "ctx_lens": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
             "block_tables": torch.zeros(B_pad, self.max_blocks, dtype=torch.int32, device=self.device),
-            "logit_idx": torch.zeros(B_pad, dtype=torch.int64, device=self.device),
+            "logit_idx": torch.zeros(max(16, B_pad), dtype=torch.int64, device=self.device),
             "mask_rows": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
         }
         meta = self._build_meta(dev, self.MAX_DECODE_Q, self.max_seq_len, True)
@@ -272,7 +276,7 @@ class LLMEngine:
         rows = np.array([r.grammar.mask_row() for r in live], np.int32)
         if self.use_graphs:
             B_pad = _bucket(B, self.SEQ_BUCKETS)
-            T_pad = _bucket(T, [B_pad * k for k in (1, 2, 4, 8, 16)])
+            T_pad = ops.mpad_for(T)
             g = self._decode_graph(B_pad, T_pad)
             max_q, max_ctx, host = self._meta(live, feeds, True, B_pad, T_pad)
             mr = np.zeros(B_pad, np.int32)
@@ -282,7 +286,7 @@ class LLMEngine:
             g["graph"].replay()
             nxt = g["out"][:B].cpu().numpy()
         else:
-            max_q, max_ctx, host = self._meta(live, feeds, True)
+            max_q, max_ctx, host = self._meta(live, feeds, True, B, ops.mpad_for(T))
             host["mask_rows"] = rows
             dev = self._to_device(host)
             meta = self._build_meta(dev, max_q, max_ctx, True)

@@ -151,6 +151,43 @@ class LlamaModel:
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
                            residual=sel_res.contiguous())
 
+    def forward_decode(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                       attn_ws: ops.AttnWorkspace | None, split_keys: int = 64) -> torch.Tensor:
+        """Decode / jump-forward step for <= 128 padded tokens. Every projection is
+        the weight-streaming skinny MFMA GEMM emitting split-K f32 slabs that the
+        following fused kernel reduces (rmsnorm+residual, RoPE+KV append, SwiGLU).
+        ``meta.tokens`` has Mpad rows; ``meta.logit_idx`` has >= 16 rows.
+        Returns f32 logits [len(logit_idx), V/tp]."""
+        cfg, w, tp = self.cfg, self.w, self.w.tp
+        H, Hkv, D = w.h, w.hkv, cfg.head_dim
+        tp_splits = 1 if tp.world > 1 else None
+        x = self.embed(meta.tokens)
+        residual = x.contiguous()
+        h = ops.rmsnorm(residual, w.layers[0]["attn_norm"], cfg.norm_eps)
+        num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
+        down = None
+        for li, L in enumerate(w.layers):
+            if li > 0:
+                h = ops.slab_rmsnorm(down, residual, L["attn_norm"], cfg.norm_eps)
+            qkv = ops.skinny_gemm(h, L["wqkv"])
+            q = ops.slab_rope_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li],
+                                     meta.slots, H, Hkv, D)
+            attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
+                                 block_tables=meta.block_tables, grouped=True,
+                                 split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
+                                 max_k=meta.max_ctx)
+            o = ops.skinny_gemm(attn, L["wo"], tp_splits)
+            tp.all_reduce_(o)
+            h = ops.slab_rmsnorm(o, residual, L["mlp_norm"], cfg.norm_eps)
+            gu = ops.skinny_gemm(h, L["w_gate_up"])
+            a = ops.slab_silu_mul(gu)
+            down = ops.skinny_gemm(a, L["w_down"], tp_splits)
+            tp.all_reduce_(down)
+        hf = ops.slab_rmsnorm(down, residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx,
+                              write_residual=False)
+        return ops.skinny_gemm(hf, w.lm_head, 1)[0]
+
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """Local vocab shard logits [B, V/tp] (bf16)."""
         return ops.linear(hidden, self.w.lm_head)

@@ -287,3 +287,108 @@ def im2col_k3(x: torch.Tensor, strides: tuple[int, int, int], B: int, C: int, L:
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     """Plain GEMM: hipBLASLt via torch on the GPU."""
     return torch.nn.functional.linear(x, w, b)
+
+
+# ------------------------------------------------- decode GEMM + slab consumers
+MPADS = (16, 32, 64, 128)
+
+
+def mpad_for(m: int) -> int:
+    for p in MPADS:
+        if m <= p:
+            return p
+    raise ValueError(f"skinny GEMM supports at most {MPADS[-1]} rows, got {m}")
+
+
+def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
+    """Split-K factor so the grid has >= ~2 workgroups per CU (256 CUs)."""
+    rt = 2 if Mpad <= 32 else 4
+    tiles = max(1, N // (16 * rt))
+    best = 1
+    for s in (1, 2, 4, 8):
+        if K % (s * 128) != 0:
+            continue
+        best = s
+        if tiles * s >= target_wgs:
+            break
+    return best
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """x [Mpad, K] bf16 (Mpad in 16/32/64/128, padded rows finite) @ w[N, K]^T
+    -> split-K partial slabs [S, Mpad, N] f32 (sum over S = x @ w^T)."""
+    Mpad, K = x.shape
+    N = w.shape[0]
+    S = splits or choose_splits(N, K, Mpad)
+    if not _gpu(x):
+        return ref.skinny_gemm(x, w, S)
+    assert Mpad in MPADS and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    _bf16_contig(w, "w")
+    assert w.shape[1] == K
+    part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device)
+    check(kernels().loqa_skinny_gemm(ptr(x), x.stride(0), ptr(w), ptr(part), Mpad, N, K, S,
+                                     stream_ptr(x)), "skinny_gemm")
+    return part
+
+
+def slab_rmsnorm(part: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                 row_idx: torch.Tensor | None = None, write_residual: bool = True) -> torch.Tensor:
+    """residual[src] += sum_s part[s, src]; y[i] = rmsnorm(residual[src]) * w with
+    src = row_idx[i] (or i). Returns y [rows, d] bf16."""
+    S, Mpad, d = part.shape
+    rows = row_idx.numel() if row_idx is not None else Mpad
+    if not _gpu(part):
+        return ref.slab_rmsnorm(part, residual, w, eps, row_idx, write_residual)
+    assert part.dtype == torch.float32 and part.is_contiguous()
+    _bf16_contig(residual, "residual")
+    assert residual.shape[-1] == d and residual.shape[0] >= Mpad
+    if row_idx is not None:
+        assert row_idx.dtype == torch.int64 and row_idx.is_contiguous()
+    y = torch.empty(rows, d, dtype=torch.bfloat16, device=part.device)
+    check(kernels().loqa_slab_rmsnorm(ptr(part), S, Mpad, ptr(row_idx), rows, ptr(residual),
+                                      int(write_residual), ptr(w), ptr(y), d, eps,
+                                      stream_ptr(part)), "slab_rmsnorm")
+    return y
+
+
+def slab_rope_append(part: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor | None,
+                     k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
+                     n_heads: int, n_kv: int, head_dim: int) -> torch.Tensor:
+    """qkv slabs [S, Mpad, (H+2Hkv)D] -> rotated q [Mpad, H*D] bf16; k/v to cache."""
+    S, Mpad, N = part.shape
+    assert N == (n_heads + 2 * n_kv) * head_dim
+    if not _gpu(part):
+        return ref.slab_rope_append(part, positions, cos_sin, k_cache, v_cache, slots, n_heads,
+                                    n_kv, head_dim)
+    assert slots.dtype == torch.int32 and slots.numel() == Mpad
+    assert positions.dtype == torch.int32 and positions.numel() == Mpad
+    assert k_cache.is_contiguous() and k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim
+    q = torch.empty(Mpad, n_heads * head_dim, dtype=torch.bfloat16, device=part.device)
+    check(kernels().loqa_slab_rope_append(ptr(part), S, Mpad, Mpad, ptr(positions), ptr(cos_sin),
+                                          ptr(q), ptr(k_cache), ptr(v_cache), ptr(slots), n_heads,
+                                          n_kv, head_dim, k_cache.shape[2], stream_ptr(part)),
+          "slab_rope_append")
+    return q
+
+
+def slab_silu_mul(part: torch.Tensor) -> torch.Tensor:
+    S, Mpad, F2 = part.shape
+    F = F2 // 2
+    if not _gpu(part):
+        return ref.slab_silu_mul(part)
+    out = torch.empty(Mpad, F, dtype=torch.bfloat16, device=part.device)
+    check(kernels().loqa_slab_silu_mul(ptr(part), S, Mpad, Mpad, F, ptr(out), stream_ptr(part)),
+          "slab_silu_mul")
+    return out
+
+
+def slab_reduce(part: torch.Tensor) -> torch.Tensor:
+    S, Mpad, N = part.shape
+    if S == 1:
+        return part[0]
+    if not _gpu(part):
+        return part.sum(0)
+    out = torch.empty(Mpad, N, dtype=torch.float32, device=part.device)
+    check(kernels().loqa_slab_reduce(ptr(part), S, Mpad, Mpad, N, ptr(out), stream_ptr(part)),
+          "slab_reduce")
+    return out

@@ -43,6 +43,13 @@ _KERNEL_SIGS = {
                      c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "loqa_im2col_k3": [c_void_p, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void_p,
                        c_void_p],
+    "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "loqa_slab_rmsnorm": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                          c_void_p, c_int, c_float, c_void_p],
+    "loqa_slab_rope_append": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "loqa_slab_silu_mul": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
 _RUNTIME_SIGS = {

@@ -265,3 +265,32 @@ def im2col_k3(x, strides, B, C, L, stride):
     vals = flat[idx.reshape(-1)].reshape(B, Lout, C, 3)
     vals = torch.where(valid.expand(B, Lout, C, 3), vals, torch.zeros((), dtype=x.dtype))
     return vals.reshape(B * Lout, 3 * C)
+
+
+# ----------------------------------------------------------- decode slabs
+def skinny_gemm(x, w, S):
+    Mpad, K = x.shape
+    kc = K // S
+    parts = [x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].float().t() for s in range(S)]
+    return torch.stack(parts, 0)
+
+
+def slab_rmsnorm(part, residual, w, eps, row_idx=None, write_residual=True):
+    tot = part.sum(0)
+    idx = row_idx.long() if row_idx is not None else torch.arange(part.shape[1], device=part.device)
+    s = (tot[idx] + residual[idx].float()).to(residual.dtype)
+    if write_residual:
+        residual[idx] = s
+    xf = s.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(residual.dtype)
+
+
+def slab_rope_append(part, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D):
+    qkv = part.sum(0).to(torch.bfloat16)
+    rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D)
+    return qkv[:, : H * D].contiguous()
+
+
+def slab_silu_mul(part):
+    return silu_mul(part.sum(0).to(torch.bfloat16))

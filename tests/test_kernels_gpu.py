@@ -227,3 +227,72 @@ def test_im2col():
     a = ops.im2col_k3(y, (3000 * 64, 1, 64), 2, 64, 3000, 2)
     b = ref.im2col_k3(y, (3000 * 64, 1, 64), 2, 64, 3000, 2)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("Mpad,N,K", [(16, 6144, 4096), (32, 4096, 14336), (64, 1280, 1280),
+                                      (128, 2560, 2048), (16, 128256, 4096)])
+def test_skinny_gemm(Mpad, N, K):
+    x = torch.randn(Mpad, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
+    part = ops.skinny_gemm(x, w)
+    want = x.float() @ w.float().t()
+    assert part.shape[1:] == (Mpad, N)
+    assert _rel(part.sum(0), want) < 1e-3
+
+
+def test_slab_consumers():
+    Mpad, d, H, Hkv, D, F = 32, 512, 4, 2, 128, 1024
+    part = torch.randn(4, Mpad, d, device=DEV)
+    res1 = torch.randn(Mpad, d, device=DEV, dtype=torch.bfloat16)
+    res2 = res1.clone()
+    w = torch.randn(d, device=DEV).bfloat16()
+    y1 = ops.slab_rmsnorm(part, res1, w, 1e-5)
+    y2 = ref.slab_rmsnorm(part, res2, w, 1e-5)
+    assert _rel(y1, y2) < 1e-2 and torch.equal(res1, res2)
+    idx = torch.tensor([3, 1, 0] + [0] * 13, dtype=torch.int64, device=DEV)
+    z1 = ops.slab_rmsnorm(part, res1, w, 1e-5, row_idx=idx, write_residual=False)
+    z2 = ref.slab_rmsnorm(part, res2, w, 1e-5, row_idx=idx, write_residual=False)
+    assert _rel(z1, z2) < 1e-2
+    qkv = torch.randn(2, Mpad, (H + 2 * Hkv) * D, device=DEV)
+    pos = torch.arange(Mpad, dtype=torch.int32, device=DEV)
+    cs = ref.rope_cos_sin(D, 256, 10000.0, device=DEV)
+    slots = torch.arange(Mpad, dtype=torch.int32, device=DEV)
+    slots[-5:] = -1
+    kc1 = torch.zeros(4, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
+    vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
+    q1 = ops.slab_rope_append(qkv, pos, cs, kc1, vc1, slots, H, Hkv, D)
+    q2 = ref.slab_rope_append(qkv, pos, cs, kc2, vc2, slots, H, Hkv, D)
+    assert _rel(q1, q2) < 1e-2 and _rel(kc1, kc2) < 1e-2 and _rel(vc1, vc2) < 1e-2
+    gu = torch.randn(3, Mpad, 2 * F, device=DEV)
+    assert _rel(ops.slab_silu_mul(gu), ref.slab_silu_mul(gu)) < 1e-2
+    assert _rel(ops.slab_reduce(gu), gu.sum(0)) < 1e-5
+
+
+def test_llama_decode_fast_path_matches_generic():
+    """forward_decode (skinny GEMM + slab ops) == forward (hipBLASLt + generic ops)."""
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), DEV, max_seqs=4, use_graphs=False)
+    tok = torch.randint(10, 4000, (2, 40)).tolist()
+    outs = []
+    for decode in (True, False):
+        pool = eng.kv.pool
+        for sid in (1, 2):
+            pool.add_seq(sid + (10 if decode else 20), [])
+        seqs = []
+        from loqa_hub_amd.engine.llm_engine import GenRequest
+        for i, sid in enumerate((1, 2)):
+            r = GenRequest([], [])
+            r.seq_id = sid + (10 if decode else 20)
+            seqs.append(r)
+        feeds = [t[:5] for t in tok]
+        max_q, max_ctx, host = eng._meta(seqs, feeds, decode, 2, ops.mpad_for(10) if decode else None)
+        host["mask_rows"] = np.zeros(2, np.int32)
+        dev = eng._to_device(host)
+        meta = eng._build_meta(dev, max_q, max_ctx, decode)
+        if decode:
+            lg = eng.model.forward_decode(meta, eng.kv.k, eng.kv.v, eng.attn_ws)[:2]
+        else:
+            lg = eng.model.logits(eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws))
+        outs.append(lg.float())
+    assert _rel(outs[0], outs[1]) < 3e-2
