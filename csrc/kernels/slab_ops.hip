@@ -85,7 +85,20 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
   const float2* csr = cs ? cs + (size_t)positions[t] * half : nullptr;
   const int pv = half >> 2;
   const int nq = H * pv, nk = Hkv * pv;
-  for (int i = threadIdx.x; i < nq + nk; i += blockDim.x) {
+  const int dv = D >> 3;
+  const int total = nq + nk + Hkv * dv;
+  // items: [q rotations | k rotations + append | v appends], spread over gridDim.y blocks
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < total; i += gridDim.y * blockDim.x) {
+    if (i >= nq + nk) {
+      if (slot < 0) continue;
+      const int j = i - nq - nk;
+      const int h = j / dv, c = (j - h * dv) * 8;
+      const int bb = slot / blk, o = slot - bb * blk;
+      float v[8];
+      slab_load8(part, slab_stride, S, (size_t)t * N + (H + Hkv) * D + h * D + c, v);
+      *reinterpret_cast<uint4*>(vc + (((size_t)bb * Hkv + h) * blk + o) * D + c) = pack8(v);
+      continue;
+    }
     const bool isk = i >= nq;
     const int ii = isk ? i - nq : i;
     const int h = ii / pv, c = (ii - h * pv) * 4;
@@ -128,16 +141,6 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
     }
     *reinterpret_cast<uint2*>(dst + c) = lo;
     *reinterpret_cast<uint2*>(dst + c + half) = hi;
-  }
-  if (slot >= 0) {
-    const int bb = slot / blk, o = slot - bb * blk;
-    const int dv = D >> 3;
-    for (int i = threadIdx.x; i < Hkv * dv; i += blockDim.x) {
-      const int h = i / dv, c = (i - h * dv) * 8;
-      float v[8];
-      slab_load8(part, slab_stride, S, (size_t)t * N + (H + Hkv) * D + h * D + c, v);
-      *reinterpret_cast<uint4*>(vc + (((size_t)bb * Hkv + h) * blk + o) * D + c) = pack8(v);
-    }
   }
 }
 
@@ -191,7 +194,8 @@ extern "C" int loqa_slab_rope_append(const float* part, int S, int Mpad, int M, 
                                      hipStream_t st) {
   if (M <= 0) return 0;
   if (D % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(slab_rope_append_kernel, dim3(M), dim3(128), 0, st, part, S, Mpad, positions,
+  const int items = (H + Hkv) * (D / 8) + Hkv * (D / 8);
+  hipLaunchKernelGGL(slab_rope_append_kernel, dim3(M, (items + 127) / 128), dim3(128), 0, st, part, S, Mpad, positions,
                      (const float2*)cs, (bf16_t*)q_out, (bf16_t*)kc, (bf16_t*)vc, slots, H, Hkv, D,
                      blk);
   return (int)hipGetLastError();

@@ -95,6 +95,13 @@ class LlamaWeights:
         self.final_norm = ones(d)
         self.lm_head = self.embed if cfg.tie_embeddings else rnd(self.v, d)
         self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
+        # decode copies in MFMA-fragment order for the weight-streaming skinny GEMM
+        # (prefill keeps the row-major copies for hipBLASLt; 288 GB of HBM makes
+        # the duplicate affordable and each path gets its ideal layout)
+        self.decode_layers = [{k: ops.shuffle_weight(L[k])
+                               for k in ("wqkv", "wo", "w_gate_up", "w_down")}
+                              for L in self.layers]
+        self.lm_head_p = ops.shuffle_weight(self.lm_head)
 
     def nbytes(self) -> int:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
@@ -167,9 +174,10 @@ class LlamaModel:
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
         down = None
         for li, L in enumerate(w.layers):
+            P = w.decode_layers[li]
             if li > 0:
                 h = ops.slab_rmsnorm(down, residual, L["attn_norm"], cfg.norm_eps)
-            qkv = ops.skinny_gemm(h, L["wqkv"])
+            qkv = ops.skinny_gemm(h, P["wqkv"])
             q = ops.slab_rope_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li],
                                      meta.slots, H, Hkv, D)
             attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
@@ -177,16 +185,16 @@ class LlamaModel:
                                  block_tables=meta.block_tables, grouped=True,
                                  split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
                                  max_k=meta.max_ctx)
-            o = ops.skinny_gemm(attn, L["wo"], tp_splits)
+            o = ops.skinny_gemm(attn, P["wo"], tp_splits)
             tp.all_reduce_(o)
             h = ops.slab_rmsnorm(o, residual, L["mlp_norm"], cfg.norm_eps)
-            gu = ops.skinny_gemm(h, L["w_gate_up"])
+            gu = ops.skinny_gemm(h, P["w_gate_up"])
             a = ops.slab_silu_mul(gu)
-            down = ops.skinny_gemm(a, L["w_down"], tp_splits)
+            down = ops.skinny_gemm(a, P["w_down"], tp_splits)
             tp.all_reduce_(down)
         hf = ops.slab_rmsnorm(down, residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx,
                               write_residual=False)
-        return ops.skinny_gemm(hf, w.lm_head, 1)[0]
+        return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """Local vocab shard logits [B, V/tp] (bf16)."""

@@ -314,19 +314,32 @@ def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
     return best
 
 
-def skinny_gemm(x: torch.Tensor, w: torch.Tensor, splits: int | None = None) -> torch.Tensor:
-    """x [Mpad, K] bf16 (Mpad in 16/32/64/128, padded rows finite) @ w[N, K]^T
-    -> split-K partial slabs [S, Mpad, N] f32 (sum over S = x @ w^T)."""
+def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] bf16 -> MFMA-fragment-ordered [N/16, K/32, 64, 8] (skinny GEMM layout)."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0
+    if not _gpu(w):
+        return ref.shuffle_weight(w)
+    _bf16_contig(w, "w")
+    out = torch.empty(N // 16, K // 32, 64, 8, dtype=torch.bfloat16, device=w.device)
+    check(kernels().loqa_shuffle_weight(ptr(w), ptr(out), N, K, stream_ptr(w)), "shuffle_weight")
+    return out
+
+
+def skinny_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """x [Mpad, K] bf16 (Mpad in 16/32/64/128, padded rows finite) @ W^T with W
+    given pre-shuffled (``shuffle_weight``) -> split-K partial slabs
+    [S, Mpad, N] f32 (sum over S = x @ W^T)."""
     Mpad, K = x.shape
-    N = w.shape[0]
+    N = wp.shape[0] * 16
+    assert wp.shape[1] * 32 == K, "weight/activation K mismatch"
     S = splits or choose_splits(N, K, Mpad)
     if not _gpu(x):
-        return ref.skinny_gemm(x, w, S)
+        return ref.skinny_gemm(x, wp, S)
     assert Mpad in MPADS and x.dtype == torch.bfloat16 and x.stride(1) == 1
-    _bf16_contig(w, "w")
-    assert w.shape[1] == K
+    _bf16_contig(wp, "wp")
     part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device)
-    check(kernels().loqa_skinny_gemm(ptr(x), x.stride(0), ptr(w), ptr(part), Mpad, N, K, S,
+    check(kernels().loqa_skinny_gemm(ptr(x), x.stride(0), ptr(wp), ptr(part), Mpad, N, K, S,
                                      stream_ptr(x)), "skinny_gemm")
     return part
 

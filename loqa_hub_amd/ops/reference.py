@@ -268,7 +268,19 @@ def im2col_k3(x, strides, B, C, L, stride):
 
 
 # ----------------------------------------------------------- decode slabs
-def skinny_gemm(x, w, S):
+def shuffle_weight(w):
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(
+        N // 16, K // 32, 64, 8)
+
+
+def unshuffle_weight(wp):
+    T, KS = wp.shape[:2]
+    return wp.reshape(T, KS, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(T * 16, KS * 32)
+
+
+def skinny_gemm(x, wp, S):
+    w = unshuffle_weight(wp)
     Mpad, K = x.shape
     kc = K // S
     parts = [x[:, s * kc:(s + 1) * kc].float() @ w[:, s * kc:(s + 1) * kc].float().t() for s in range(S)]

@@ -234,7 +234,9 @@ def test_im2col():
 def test_skinny_gemm(Mpad, N, K):
     x = torch.randn(Mpad, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.02
-    part = ops.skinny_gemm(x, w)
+    wp = ops.shuffle_weight(w)
+    assert torch.equal(wp.cpu(), ref.shuffle_weight(w.cpu()))
+    part = ops.skinny_gemm(x, wp)
     want = x.float() @ w.float().t()
     assert part.shape[1:] == (Mpad, N)
     assert _rel(part.sum(0), want) < 1e-3
