@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks on the GPU (HIP-event timing, median of N reps).
+
+Decode-step shapes of Llama-3-8B (M = 16/32 tokens): our skinny GEMM at each
+split-K vs hipBLASLt (torch.nn.functional.linear); decode attention; slab ops.
+Prints one JSON line per measurement (also written to gpurun_out/kbench.jsonl).
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from loqa_hub_amd import ops  # noqa: E402
+
+dev = torch.device("cuda")
+out_path = "gpurun_out/kbench.jsonl"
+os.makedirs("gpurun_out", exist_ok=True)
+fout = open(out_path, "w")
+
+
+def timeit(fn, reps=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+    fout.write(json.dumps(kw) + "\n")
+
+
+def gemm_bench():
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+              "lm_head": (128256, 4096)}
+    for M in (16, 32, 64):
+        for name, (N, K) in shapes.items():
+            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+            wp = ops.shuffle_weight(w)
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            gb = N * K * 2 / 1e9
+            t_blas = timeit(lambda: torch.nn.functional.linear(x, w))
+            res = {"kernel": "gemm", "shape": name, "M": M, "N": N, "K": K,
+                   "hipblaslt_us": round(t_blas, 2), "hipblaslt_TBps": round(gb / t_blas * 1e3, 2)}
+            for S in (1, 2, 4, 8):
+                if K % (S * 128):
+                    continue
+                t = timeit(lambda: ops.skinny_gemm(x, wp, S))
+                res[f"skinny_S{S}_us"] = round(t, 2)
+                res[f"skinny_S{S}_TBps"] = round(gb / t * 1e3, 2)
+            res["auto_S"] = ops.choose_splits(N, K, M)
+            emit(**res)
+            del w, wp
+
+
+def attn_bench():
+    H, Hkv, D, blk = 32, 8, 128, 16
+    for B, ctx in ((8, 450), (8, 900), (32, 450)):
+        nblk = B * ((ctx + blk - 1) // blk)
+        kc = torch.randn(nblk, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nblk, dtype=torch.int32, device=dev).view(B, -1)
+        q = torch.randn(B, H * D, device=dev, dtype=torch.bfloat16)
+        cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
+        cl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        ws = ops.AttnWorkspace(dev, 256, H, D, 32)
+        gb = 2 * B * ctx * Hkv * D * 2 / 1e9
+        for sk in (64, 128, 256):
+            ns = (ctx + sk - 1) // sk
+            t = timeit(lambda: ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True,
+                                             max_q=1, ctx_lens=cl, block_tables=bt, grouped=True,
+                                             split_keys=sk, num_splits=ns, workspace=ws))
+            emit(kernel="decode_attn", B=B, ctx=ctx, split_keys=sk, splits=ns, us=round(t, 2),
+                 TBps=round(gb / t * 1e3, 2))
+
+
+def slab_bench():
+    for M, d, S in ((16, 4096, 4), (16, 4096, 2), (32, 4096, 4)):
+        part = torch.randn(S, M, d, device=dev)
+        res = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
+        w = torch.ones(d, device=dev, dtype=torch.bfloat16)
+        emit(kernel="slab_rmsnorm", M=M, d=d, S=S, us=round(timeit(lambda: ops.slab_rmsnorm(part, res, w, 1e-5)), 2))
+    part = torch.randn(1, 16, 2 * 14336, device=dev)
+    emit(kernel="slab_silu_mul", M=16, F=14336, S=1, us=round(timeit(lambda: ops.slab_silu_mul(part)), 2))
+    x = torch.randn(16, 4096, device=dev, dtype=torch.bfloat16)
+    emit(kernel="rmsnorm", M=16, d=4096, us=round(timeit(lambda: ops.rmsnorm(x, w, 1e-5)), 2))
+    emit(kernel="empty_torch_add", us=round(timeit(lambda: x.add_(0)), 2))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["gemm", "attn", "slab"]
+    if "gemm" in which:
+        gemm_bench()
+    if "attn" in which:
+        attn_bench()
+    if "slab" in which:
+        slab_bench()

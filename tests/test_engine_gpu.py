@@ -44,6 +44,8 @@ def test_llm_gpu_matches_cpu_reference_first_tokens():
     # same weights on both
     c.weights.__dict__.update({k: (v.cpu() if torch.is_tensor(v) else v) for k, v in g.weights.__dict__.items()})
     c.weights.layers = [{k: t.cpu() for k, t in L.items()} for L in g.weights.layers]
+    c.weights.decode_layers = [{k: t.cpu() for k, t in L.items()} for L in g.weights.decode_layers]
+    c.weights.cos_sin = g.weights.cos_sin.cpu()
     c.model.w = c.weights
     rg, rc = _gen(g, [2]), _gen(c, [2])
     # bf16 kernels vs fp32 reference may diverge late; the first sampled decisions agree
