@@ -1,0 +1,229 @@
+// Decode / jump-forward attention over the paged KV cache,
+// one wave per workgroup.
+//
+// Decode attention is a pure KV-streaming problem (a few query rows per kv
+// head), and per-CU load bandwidth (~24 GB/s) caps how fast one CU can pull
+// its share, so the work is spread over as many CUs as possible: a workgroup
+// is ONE wave owning (sequence, kv head, key split). All G*q_len query rows of
+// the kv head (<= 32: GQA group x jump-forward tokens) form one 32-row MFMA
+// tile, so K and V are read exactly once per step.
+//
+//   S^T = K Q^T : K rows go straight from HBM into the A fragments (16 B per
+//                 lane per k-slice, no LDS), Q^T is register-resident.
+//   O^T += V^T P^T : V is staged through a double-buffered LDS tile and read
+//                 with ds_read_b64_tr_b16 (guide T10); P^T is the exp2'ed S^T
+//                 accumulator repacked to bf16 in registers.
+// The next 32-key tile's K fragments and V chunk are prefetched into registers
+// while the current tile computes. Split partials (O, m, l) are merged by
+// attn_combine_kernel (attention.hip).
+#include "common.h"
+
+#define DEC_TILE 32
+
+typedef short v4s_ __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float16v mfma32d(const bf16x8& a, const bf16x8& b, const float16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void attn_decode_kernel(
+    const bf16_t* __restrict__ q, long long q_stride, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const int* __restrict__ block_tables, int max_blocks, int blk, int Hq, int Hkv,
+    float scale_log2, int split_keys, int num_splits, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int total_q) {
+  constexpr int NS = D / 16, NDT = D / 32, CH = D / 8;
+  constexpr int VLD = D + 32;                     // padded V row (conflict-free tr reads)
+  constexpr int VPL = DEC_TILE * CH / 64;         // 16-byte V chunks per lane per tile
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][DEC_TILE][VLD];
+  const int lane = threadIdx.x;
+  const int h = lane >> 5, r = lane & 31;
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int G = Hq / Hkv;
+  const int q0 = cu_q[b], qlen = cu_q[b + 1] - q0;
+  const int klen = ctx_lens[b];
+  const int qi = r / G;
+  const int head = kvh * G + (r - qi * G);
+  const bool row_valid = qi < qlen && r < (32 / G) * G;
+  const int qpos = klen - qlen + qi;
+  const int kbeg = split * split_keys;
+  // causal bound of the whole row group: last token's position + 1
+  const int kend = min(min(klen, kbeg + split_keys), klen);
+  const int* bt = block_tables + (size_t)b * max_blocks;
+
+  bf16x8 qf[NS];
+  {
+    const bf16_t* qr = q + (size_t)(q0 + (row_valid ? qi : 0)) * q_stride + (size_t)head * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4 v = row_valid ? *reinterpret_cast<const uint4*>(qr + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      qf[s] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+  float16v acc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  auto key_off = [&](int key) -> size_t {
+    const int bi = key / blk, bo = key - bi * blk;
+    return (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
+  };
+  // prefetch registers
+  uint4 kpre[NS], vpre[VPL];
+  auto load_tile = [&](int kt) {
+    const int key = kt + r;
+    const bool ok = key < kend;
+    const size_t off = ok ? key_off(key) : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      kpre[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      const int kr = c / CH, cc = (c - kr * CH) * 8;
+      const int k2 = kt + kr;
+      vpre[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + key_off(k2) + cc) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_v = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      const int kr = c / CH, cc = (c - kr * CH) * 8;
+      *reinterpret_cast<uint4*>(&vs[buf][kr][cc]) = vpre[i];
+    }
+  };
+
+  if (kbeg < kend) load_tile(kbeg);
+  int buf = 0;
+  for (int kt = kbeg; kt < kend; kt += DEC_TILE) {
+    bf16x8 kf[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) kf[s] = *reinterpret_cast<bf16x8*>(&kpre[s]);
+    store_v(buf);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (kt + DEC_TILE < kend) load_tile(kt + DEC_TILE);  // prefetch next tile
+
+    float16v st;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) st[j] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) st = mfma32d(kf[s], qf[s], st);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int key = kt + (j & 3) + 8 * (j >> 2) + 4 * h;
+      float sv = st[j] * scale_log2;
+      if (key >= kend || key > qpos) sv = -INFINITY;
+      st[j] = sv;
+      mx = fmaxf(mx, sv);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = exp2f(st[8 * s2 + j] - m_new);
+        ls += e;
+        pf[s2][j] = (__bf16)e;
+      }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int c0 = 32 * dt + 16 * (g & 1) + 4 * (li & 3);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kb = 16 * s2 + 4 * h + (li >> 2);
+        const v4s_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_*)(&vs[buf][kb][c0]));
+        const v4s_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_*)(&vs[buf][kb + 8][c0]));
+        short8 a8;
+        a8[0] = lo[0]; a8[1] = lo[1]; a8[2] = lo[2]; a8[3] = lo[3];
+        a8[4] = hi[0]; a8[5] = hi[1]; a8[6] = hi[2]; a8[7] = hi[3];
+        acc[dt] = mfma32d(*reinterpret_cast<bf16x8*>(&a8), pf[s2], acc[dt]);
+      }
+    }
+    buf ^= 1;
+  }
+
+  if (!row_valid) return;
+  const size_t tok = (size_t)(q0 + qi);
+  float* po = part_o + (((size_t)split * total_q + tok) * Hq + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      *reinterpret_cast<float4*>(po + d0) =
+          make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+    }
+  if (h == 0) {
+    float* pm = part_ml + (((size_t)split * total_q + tok) * Hq + head) * 2;
+    pm[0] = m_run;
+    pm[1] = l_run;
+  }
+}
+
+// combine split partials (one workgroup of D threads per (token, head))
+__global__ void attn_decode_combine_kernel(const float* __restrict__ part_o,
+                                           const float* __restrict__ part_ml, bf16_t* __restrict__ o,
+                                           long long o_stride, int total_q, int Hq, int D,
+                                           int num_splits) {
+  const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
+  float mstar = -1e30f;
+  for (int s = 0; s < num_splits; ++s)
+    mstar = fmaxf(mstar, part_ml[(((size_t)s * total_q + tok) * Hq + head) * 2]);
+  float l = 0.f, acc = 0.f;
+  for (int s = 0; s < num_splits; ++s) {
+    const size_t idx = ((size_t)s * total_q + tok) * Hq + head;
+    const float w = exp2f(part_ml[idx * 2] - mstar);
+    l += w * part_ml[idx * 2 + 1];
+    acc += w * part_o[idx * D + d];
+  }
+  o[(size_t)tok * o_stride + (size_t)head * D + d] = f2bf(l > 0.f ? acc / l : 0.f);
+}
+
+// q: [Tq, >=Hq*D] bf16; caches [nb, Hkv, blk, D]; out [Tq, Hq*D] bf16.
+// Requires G * max_q <= 32 and split_keys % 32 == 0.
+extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* kc, const void* vc,
+                                void* o, long long o_stride, const int* cu_q, const int* ctx_lens,
+                                const int* block_tables, int max_blocks, int blk, int B, int max_q,
+                                int Hq, int Hkv, int D, float scale, int split_keys, int num_splits,
+                                float* part_o, float* part_ml, int total_q, hipStream_t s) {
+  if (B <= 0 || total_q <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv || (Hq / Hkv) * max_q > 32 || split_keys % DEC_TILE || num_splits < 1 ||
+      (D != 64 && D != 128) || !part_o || !part_ml)
+    return (int)hipErrorInvalidValue;
+  dim3 grid(num_splits, Hkv, B);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (D == 128)
+    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(64), 0, s, (const bf16_t*)q, q_stride,
+                       (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
+                       blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(64), 0, s, (const bf16_t*)q, q_stride,
+                       (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
+                       blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(total_q, Hq), dim3(D), 0, s, part_o, part_ml,
+                     (bf16_t*)o, o_stride, total_q, Hq, D, num_splits);
+  return (int)hipGetLastError();
+}

@@ -58,7 +58,6 @@ def _bucket(n: int, buckets: list[int]) -> int:
 
 class LLMEngine:
     SEQ_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128]
-    MAX_DECODE_Q = 16
 
     def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
@@ -82,8 +81,10 @@ class LLMEngine:
         self.kv = PagedKVCache(cfg.n_layers, self.weights.hkv, cfg.head_dim, num_blocks, block_size,
                                self.device)
         self.is_gpu = self.device.type == "cuda"
-        self.attn_ws = ops.AttnWorkspace(self.device, max_seqs * self.MAX_DECODE_Q, self.weights.h,
-                                         cfg.head_dim, (max_seq_len + 63) // 64) if self.is_gpu else None
+        # grouped decode attention holds G * q_len <= 32 query rows per kv head
+        self.max_decode_q = max(1, 32 // (self.weights.h // self.weights.hkv))
+        self.attn_ws = ops.AttnWorkspace(self.device, 128, self.weights.h, cfg.head_dim,
+                                         (max_seq_len + 127) // 128) if self.is_gpu else None
         self.use_graphs = use_graphs and self.is_gpu
         self.prefill_chunk = prefill_chunk
         self._graphs: dict[tuple[int, int], dict] = {}
@@ -195,7 +196,7 @@ class LLMEngine:
             "logit_idx": torch.zeros(max(16, B_pad), dtype=torch.int64, device=self.device),
             "mask_rows": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
         }
-        meta = self._build_meta(dev, self.MAX_DECODE_Q, self.max_seq_len, True)
+        meta = self._build_meta(dev, self.max_decode_q, self.max_seq_len, True)
         # warm up (allocator + kernels) on a side stream, then capture
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -224,8 +225,11 @@ class LLMEngine:
         req._prompt_full = list(req.prompt) + req.grammar.emitted  # type: ignore[attr-defined]
         return req
 
-    def _sample_and_advance(self, live: list[GenRequest], nxt: np.ndarray, now: float) -> None:
-        for r, t in zip(live, nxt.tolist()):
+    def _sample_and_advance(self, live: list[GenRequest], nxt: np.ndarray, now: float,
+                            carry: list[bool] | None = None) -> None:
+        for i, (r, t) in enumerate(zip(live, nxt.tolist())):
+            if carry is not None and carry[i]:
+                continue  # long forced run split across steps: logits of this step unused
             if r.t_first == 0.0:
                 r.t_first = now
             r.token_times.append(now)
@@ -265,12 +269,16 @@ class LLMEngine:
             self._sample_and_advance(batch, nxt, time.perf_counter())
 
     def decode_step(self, live: list[GenRequest]) -> None:
-        feeds = []
+        feeds, carry = [], []
         for r in live:
             f = r.feed
-            if len(f) > self.MAX_DECODE_Q:  # long forced run: keep the tail for the next step
-                raise RuntimeError("forced literal longer than MAX_DECODE_Q")
-            feeds.append(f)
+            if len(f) > self.max_decode_q:  # long forced run: feed it over two steps
+                feeds.append(f[: self.max_decode_q])
+                r.feed = f[self.max_decode_q:]
+                carry.append(True)
+            else:
+                feeds.append(f)
+                carry.append(False)
         B = len(live)
         T = sum(len(f) for f in feeds)
         rows = np.array([r.grammar.mask_row() for r in live], np.int32)
@@ -293,7 +301,7 @@ class LLMEngine:
             nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += T
-        self._sample_and_advance(live, nxt, time.perf_counter())
+        self._sample_and_advance(live, nxt, time.perf_counter(), carry)
 
     def generate(self, reqs: list[GenRequest], on_done=None) -> list[GenRequest]:
         """Run the requests to completion. ``on_done(req)`` fires as soon as each

@@ -44,7 +44,9 @@ again didn't anything not sure help with what want do having trouble understandi
 _FRAGMENTS = [
     "{", "}", "[", "]", ":", ",", '"', "\n", "  ", "    ", "      ", "        ", "\n  ", "\n    ",
     "\n      ", "\n        ", '{"', '"}', '":', '": ', '": "', '",', '", "', '"\n', "},", "}]", "]}",
-    "}\n", "},\n", '  "', '    "', '      "', '        "', "0.", "1.", "0", "1", "2", "3", "4", "5",
+    "}\n", "},\n", '  "', '    "', '      "', '        "', ', "', '", "', ': "', ', {"', '"}, "',
+    '}, {"', '"}],', '], "', ': 0.', ': [', ': {', '": {"', '": [', '": 0.', '"},', '"}]',
+    "0.", "1.", "0", "1", "2", "3", "4", "5",
     "6", "7", "8", "9", "00", "95", "90", "85", "80", "75", "50", ".", "!", "?", "'", "-", "_",
     "...", "(", ")", "/", "turn_on", "turn_off", "greeting", "question", "unknown", "true", "false",
     "intent", "entities", "device", "location", "confidence", "response", "commands", "is_multi",

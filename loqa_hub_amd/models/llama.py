@@ -102,6 +102,10 @@ class LlamaWeights:
                                for k in ("wqkv", "wo", "w_gate_up", "w_down")}
                               for L in self.layers]
         self.lm_head_p = ops.shuffle_weight(self.lm_head)
+        if torch.device(device).type == "cuda":
+            for k in ("wqkv", "wo", "w_gate_up", "w_down"):
+                ops.tune_skinny_splits(self.decode_layers[0][k])
+            ops.tune_skinny_splits(self.lm_head_p)
 
     def nbytes(self) -> int:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
@@ -159,7 +163,7 @@ class LlamaModel:
                            residual=sel_res.contiguous())
 
     def forward_decode(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
-                       attn_ws: ops.AttnWorkspace | None, split_keys: int = 64) -> torch.Tensor:
+                       attn_ws: ops.AttnWorkspace | None, split_keys: int = 128) -> torch.Tensor:
         """Decode / jump-forward step for <= 128 padded tokens. Every projection is
         the weight-streaming skinny MFMA GEMM emitting split-K f32 slabs that the
         following fused kernel reduces (rmsnorm+residual, RoPE+KV append, SwiGLU).

@@ -191,6 +191,16 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Ten
         assert k.stride(-1) == 1 and v.stride(-1) == 1 and k.stride(0) == v.stride(0)
         blk, max_blocks, kv_stride = 0, 0, k.stride(0)
     part_o = part_ml = None
+    if grouped and paged and (n_heads // n_kv) * max_q <= 32 and split_keys % 32 == 0:
+        # one-wave-per-workgroup decode kernel (attn_decode.hip)
+        assert workspace is not None and workspace.max_splits >= num_splits
+        assert workspace.max_tokens >= Tq
+        check(kernels().loqa_attn_decode(
+            ptr(q), q.stride(0), ptr(k), ptr(v), ptr(out), out.stride(0), ptr(cu_q), ptr(ctx_lens),
+            ptr(block_tables), max_blocks, blk, B, max_q, n_heads, n_kv, head_dim, scale, split_keys,
+            num_splits, ptr(workspace.part_o), ptr(workspace.part_ml), Tq, stream_ptr(q)),
+            "attn_decode")
+        return out
     if grouped:
         G = n_heads // n_kv
         assert max_q * G <= 128, "grouped attention handles at most 128/G query tokens"
@@ -300,8 +310,50 @@ def mpad_for(m: int) -> int:
     raise ValueError(f"skinny GEMM supports at most {MPADS[-1]} rows, got {m}")
 
 
+_SPLITS: dict[tuple[int, int, int], int] = {}
+
+
+def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
+    """Time the skinny GEMM for every split-K option on the real weight and
+    cache the fastest per (N, K, Mpad). Per-CU bandwidth (~24 GB/s per CU) makes
+    grid balance across the 256 CUs the dominant effect, and it depends on the
+    shape, so it is measured rather than modelled. Run before graph capture."""
+    N, K = wp.shape[0] * 16, wp.shape[1] * 32
+    if not _gpu(wp):
+        return {}
+    out = {}
+    for Mpad in mpads:
+        key = (N, K, Mpad)
+        if key in _SPLITS:
+            out[key] = _SPLITS[key]
+            continue
+        x = torch.randn(Mpad, K, device=wp.device, dtype=torch.bfloat16)
+        best, best_t = 1, float("inf")
+        for s in (1, 2, 4, 8):
+            if K % (s * 128):
+                continue
+            for _ in range(2):
+                skinny_gemm(x, wp, s)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                skinny_gemm(x, wp, s)
+            b.record()
+            b.synchronize()
+            t = a.elapsed_time(b)
+            if t < best_t * 0.98:
+                best, best_t = s, t
+        _SPLITS[key] = best
+        out[key] = best
+    return out
+
+
 def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
-    """Split-K factor so the grid has >= ~2 workgroups per CU (256 CUs)."""
+    """Split-K factor: the tuned value if available, else enough splits for
+    >= ~2 workgroups per CU (256 CUs)."""
+    tuned = _SPLITS.get((N, K, Mpad))
+    if tuned is not None:
+        return tuned
     rt = 2 if Mpad <= 32 else 4
     tiles = max(1, N // (16 * rt))
     best = 1
