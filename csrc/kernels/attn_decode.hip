@@ -1,24 +1,24 @@
-// Decode / jump-forward attention over the paged KV cache,
-// one wave per workgroup.
+// Decode / jump-forward attention over the paged KV cache.
 //
-// Decode attention is a pure KV-streaming problem (a few query rows per kv
-// head), and per-CU load bandwidth (~24 GB/s) caps how fast one CU can pull
-// its share, so the work is spread over as many CUs as possible: a workgroup
-// is ONE wave owning (sequence, kv head, key split). All G*q_len query rows of
-// the kv head (<= 32: GQA group x jump-forward tokens) form one 32-row MFMA
-// tile, so K and V are read exactly once per step.
+// Decode attention is a pure KV-streaming problem: a few query rows per kv
+// head (GQA group x jump-forward tokens <= 32 -> ONE 32-row MFMA tile), so K
+// and V must be read exactly once per step and the reads must be in flight
+// together. A workgroup = 4 waves = (sequence, kv head, 128-key split); each
+// wave owns one 32-key tile, so the whole split's K/V is requested at once
+// (no serial tile-after-tile latency chain):
 //
-//   S^T = K Q^T : K rows go straight from HBM into the A fragments (16 B per
-//                 lane per k-slice, no LDS), Q^T is register-resident.
-//   O^T += V^T P^T : V is staged through a double-buffered LDS tile and read
-//                 with ds_read_b64_tr_b16 (guide T10); P^T is the exp2'ed S^T
-//                 accumulator repacked to bf16 in registers.
-// The next 32-key tile's K fragments and V chunk are prefetched into registers
-// while the current tile computes. Split partials (O, m, l) are merged by
-// attn_combine_kernel (attention.hip).
+//   S^T = K Q^T    : K rows go straight from HBM into the MFMA A fragments
+//                    (16 B per lane per k-slice, no LDS); Q^T is register-resident.
+//   O^T += V^T P^T : V goes through the wave's private LDS tile and is read with
+//                    ds_read_b64_tr_b16 (guide T10); P^T is the exp2'ed S^T
+//                    accumulator repacked to bf16 in registers.
+//   merge          : the 4 waves' (m, l, O^T) are merged through LDS by wave 0,
+//                    which writes one split partial; attn_decode_combine merges
+//                    the splits (sequences longer than split_keys).
 #include "common.h"
 
 #define DEC_TILE 32
+#define DEC_WAVES 4
 
 typedef short v4s_ __attribute__((ext_vector_type(4)));
 
@@ -27,17 +27,23 @@ __device__ __forceinline__ float16v mfma32d(const bf16x8& a, const bf16x8& b, co
 }
 
 template <int D>
-__global__ __launch_bounds__(64) void attn_decode_kernel(
+struct DecSmem {
+  bf16_t v[DEC_WAVES][DEC_TILE][D + 32];          // per-wave V tile (padded rows)
+  float o[DEC_WAVES - 1][D / 32][16][64];          // O^T partials of waves 1..3
+  float ml[DEC_WAVES][2][64];                      // (m, l) per wave per lane
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16_t* __restrict__ q, long long q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, int max_blocks, int blk, int Hq, int Hkv,
     float scale_log2, int split_keys, int num_splits, float* __restrict__ part_o,
     float* __restrict__ part_ml, int total_q) {
   constexpr int NS = D / 16, NDT = D / 32, CH = D / 8;
-  constexpr int VLD = D + 32;                     // padded V row (conflict-free tr reads)
-  constexpr int VPL = DEC_TILE * CH / 64;         // 16-byte V chunks per lane per tile
-  __shared__ __attribute__((aligned(16))) bf16_t vs[2][DEC_TILE][VLD];
-  const int lane = threadIdx.x;
+  constexpr int VPL = DEC_TILE * CH / 64;  // 16-byte V chunks per lane per tile
+  __shared__ __attribute__((aligned(16))) DecSmem<D> sm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, r = lane & 31;
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int G = Hq / Hkv;
@@ -48,8 +54,7 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
   const bool row_valid = qi < qlen && r < (32 / G) * G;
   const int qpos = klen - qlen + qi;
   const int kbeg = split * split_keys;
-  // causal bound of the whole row group: last token's position + 1
-  const int kend = min(min(klen, kbeg + split_keys), klen);
+  const int kend = min(klen, kbeg + split_keys);
   const int* bt = block_tables + (size_t)b * max_blocks;
 
   bf16x8 qf[NS];
@@ -68,52 +73,46 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
-  auto key_off = [&](int key) -> size_t {
-    const int bi = key / blk, bo = key - bi * blk;
-    return (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
-  };
-  // prefetch registers
-  uint4 kpre[NS], vpre[VPL];
-  auto load_tile = [&](int kt) {
-    const int key = kt + r;
-    const bool ok = key < kend;
-    const size_t off = ok ? key_off(key) : 0;
+  for (int kt = kbeg + wave * DEC_TILE; kt < kend; kt += DEC_WAVES * DEC_TILE) {
+    // issue K (-> registers) and V (-> registers -> LDS) loads of this wave's tile
+    uint4 kraw[NS], vraw[VPL];
+    {
+      const int key = kt + r;
+      const bool ok = key < kend;
+      size_t off = 0;
+      if (ok) {
+        const int bi = key / blk, bo = key - bi * blk;
+        off = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
+      }
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      kpre[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      for (int s = 0; s < NS; ++s)
+        kraw[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = lane + 64 * i;
-      const int kr = c / CH, cc = (c - kr * CH) * 8;
-      const int k2 = kt + kr;
-      vpre[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + key_off(k2) + cc) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < VPL; ++i) {
+        const int c = lane + 64 * i;
+        const int kr = c / CH, cc = (c - kr * CH) * 8;
+        const int k2 = kt + kr;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k2 < kend) {
+          const int bi = k2 / blk, bo = k2 - bi * blk;
+          v = *reinterpret_cast<const uint4*>(vc + (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D + cc);
+        }
+        vraw[i] = v;
+      }
     }
-  };
-  auto store_v = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = lane + 64 * i;
-      const int kr = c / CH, cc = (c - kr * CH) * 8;
-      *reinterpret_cast<uint4*>(&vs[buf][kr][cc]) = vpre[i];
-    }
-  };
-
-  if (kbeg < kend) load_tile(kbeg);
-  int buf = 0;
-  for (int kt = kbeg; kt < kend; kt += DEC_TILE) {
-    bf16x8 kf[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) kf[s] = *reinterpret_cast<bf16x8*>(&kpre[s]);
-    store_v(buf);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (kt + DEC_TILE < kend) load_tile(kt + DEC_TILE);  // prefetch next tile
-
+    // S^T = K Q^T
     float16v st;
 #pragma unroll
     for (int j = 0; j < 16; ++j) st[j] = 0.f;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) st = mfma32d(kf[s], qf[s], st);
+    for (int s = 0; s < NS; ++s) st = mfma32d(*reinterpret_cast<bf16x8*>(&kraw[s]), qf[s], st);
+    // V tile -> this wave's LDS region (wave-private: no workgroup barrier)
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      const int kr = c / CH, cc = (c - kr * CH) * 8;
+      *reinterpret_cast<uint4*>(&sm.v[wave][kr][cc]) = vraw[i];
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -143,6 +142,8 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
     for (int i = 0; i < NDT; ++i)
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     const int g = lane >> 4, li = lane & 15;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
@@ -151,18 +152,48 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
       for (int s2 = 0; s2 < 2; ++s2) {
         const int kb = 16 * s2 + 4 * h + (li >> 2);
         const v4s_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s_*)(&vs[buf][kb][c0]));
+            (__attribute__((address_space(3))) v4s_*)(&sm.v[wave][kb][c0]));
         const v4s_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s_*)(&vs[buf][kb + 8][c0]));
+            (__attribute__((address_space(3))) v4s_*)(&sm.v[wave][kb + 8][c0]));
         short8 a8;
         a8[0] = lo[0]; a8[1] = lo[1]; a8[2] = lo[2]; a8[3] = lo[3];
         a8[4] = hi[0]; a8[5] = hi[1]; a8[6] = hi[2]; a8[7] = hi[3];
         acc[dt] = mfma32d(*reinterpret_cast<bf16x8*>(&a8), pf[s2], acc[dt]);
       }
     }
-    buf ^= 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 
+  // ---- merge the 4 waves' online-softmax states through LDS
+  sm.ml[wave][0][lane] = m_run;
+  sm.ml[wave][1][lane] = l_run;
+  if (wave > 0) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sm.o[wave - 1][dt][j][lane] = acc[dt][j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  float mstar = m_run;
+#pragma unroll
+  for (int w = 1; w < DEC_WAVES; ++w) mstar = fmaxf(mstar, sm.ml[w][0][lane]);
+  const float s0 = exp2f(m_run - mstar);
+  float l = l_run * s0;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[dt][j] *= s0;
+#pragma unroll
+  for (int w = 1; w < DEC_WAVES; ++w) {
+    const float sw = exp2f(sm.ml[w][0][lane] - mstar);
+    l += sm.ml[w][1][lane] * sw;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[dt][j] += sw * sm.o[w - 1][dt][j][lane];
+  }
   if (!row_valid) return;
   const size_t tok = (size_t)(q0 + qi);
   float* po = part_o + (((size_t)split * total_q + tok) * Hq + head) * D;
@@ -176,12 +207,13 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
     }
   if (h == 0) {
     float* pm = part_ml + (((size_t)split * total_q + tok) * Hq + head) * 2;
-    pm[0] = m_run;
-    pm[1] = l_run;
+    pm[0] = mstar;
+    pm[1] = l;
   }
 }
 
-// combine split partials (one workgroup of D threads per (token, head))
+// combine split partials (one workgroup of D threads per (token, head)); a
+// single split is a plain normalisation.
 __global__ void attn_decode_combine_kernel(const float* __restrict__ part_o,
                                            const float* __restrict__ part_ml, bf16_t* __restrict__ o,
                                            long long o_stride, int total_q, int Hq, int D,
@@ -214,11 +246,11 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   dim3 grid(num_splits, Hkv, B);
   const float sl2 = scale * 1.4426950408889634f;
   if (D == 128)
-    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(64), 0, s, (const bf16_t*)q, q_stride,
+    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
                        blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
   else
-    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(64), 0, s, (const bf16_t*)q, q_stride,
+    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
                        blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
   hipError_t e = hipGetLastError();

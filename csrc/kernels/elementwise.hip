@@ -197,80 +197,104 @@ extern "C" int loqa_pcm16_f32_sumsq(const void* pcm, float* out, const long long
 
 // --------------------------------------------------- K15 grammar-masked argmax
 // logits: [B, V] (bf16 if is_bf16 else f32), row stride ld elements.
-// mask: [B, W] uint32 bitmask (bit v%32 of word v/32 = token v allowed), or null.
-// mask_rows: optional per-row index into the mask table (so B rows can share
-// precomputed grammar-state masks). out_idx[b] = argmax over allowed (or -1).
+// mask: [*, W] uint32 bitmask (bit v%32 of word v/32 = token v allowed), or null;
+// mask_rows: optional per-row index into the mask table (rows share the
+// precomputed grammar-state masks). Each row is split over ARG_CHUNK-token
+// workgroups (a 128k vocabulary -> 16 workgroups per row, so B=16 rows fill the
+// GPU); each workgroup folds its best (value, index) into one 64-bit atomicMax
+// of (order-preserving float key << 32 | ~index) - ties resolve to the lowest
+// index like torch.argmax. out_idx[b] = argmax over allowed tokens (or -1).
+#define ARG_CHUNK 8192
+#define ARG_THREADS 256
+
+__device__ __forceinline__ unsigned long long argpack(float v, int idx) {
+  const uint32_t bits = __float_as_uint(v);
+  const uint32_t key = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+  return ((unsigned long long)key << 32) | (0xFFFFFFFFu - (uint32_t)idx);
+}
+
 template <bool BF16>
-__global__ __launch_bounds__(1024) void masked_argmax_kernel(
+__global__ __launch_bounds__(ARG_THREADS) void masked_argmax_kernel(
     const void* __restrict__ logits, long long ld, int V, const uint32_t* __restrict__ mask,
-    const int* __restrict__ mask_rows, int W, int* __restrict__ out_idx,
-    float* __restrict__ out_val) {
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  const int b = blockIdx.x;
+    const int* __restrict__ mask_rows, int W, unsigned long long* __restrict__ packed) {
+  __shared__ unsigned long long sbest[ARG_THREADS / 64];
+  const int b = blockIdx.y;
+  const int v_begin = blockIdx.x * ARG_CHUNK;
+  const int v_end = min(V, v_begin + ARG_CHUNK);
   const uint32_t* m = nullptr;
   if (mask) m = mask + (size_t)(mask_rows ? mask_rows[b] : b) * W;
-  float best = -FLT_MAX;
-  int bi = -1;
+  unsigned long long best = 0;
   if (BF16) {
     const bf16_t* row = reinterpret_cast<const bf16_t*>(logits) + (size_t)b * ld;
-    // 8 tokens per lane per step.
-    for (int v0 = threadIdx.x * 8; v0 < V; v0 += blockDim.x * 8) {
-      if (v0 + 8 <= V && (ld % 8 == 0)) {
+    for (int v0 = v_begin + threadIdx.x * 8; v0 < v_end; v0 += ARG_THREADS * 8) {
+      if (v0 + 8 <= v_end && (ld % 8 == 0)) {
         float f[8];
         unpack8(*reinterpret_cast<const uint4*>(row + v0), f);
         const uint32_t bits = m ? (m[v0 >> 5] >> (v0 & 31)) & 0xffu : 0xffu;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (((bits >> j) & 1u) && f[j] > best) { best = f[j]; bi = v0 + j; }
+          if ((bits >> j) & 1u) best = max(best, argpack(f[j], v0 + j));
       } else {
-        for (int v = v0; v < min(V, v0 + 8); ++v) {
-          const bool ok = !m || ((m[v >> 5] >> (v & 31)) & 1u);
-          const float f = bf2f(row[v]);
-          if (ok && f > best) { best = f; bi = v; }
-        }
+        for (int v = v0; v < min(v_end, v0 + 8); ++v)
+          if (!m || ((m[v >> 5] >> (v & 31)) & 1u)) best = max(best, argpack(bf2f(row[v]), v));
       }
     }
   } else {
     const float* row = reinterpret_cast<const float*>(logits) + (size_t)b * ld;
-    for (int v = threadIdx.x; v < V; v += blockDim.x) {
-      const bool ok = !m || ((m[v >> 5] >> (v & 31)) & 1u);
-      const float f = row[v];
-      if (ok && f > best) { best = f; bi = v; }
+    for (int v0 = v_begin + threadIdx.x * 4; v0 < v_end; v0 += ARG_THREADS * 4) {
+      if (v0 + 4 <= v_end && (ld % 4 == 0)) {
+        const float4 f = *reinterpret_cast<const float4*>(row + v0);
+        const uint32_t bits = m ? (m[v0 >> 5] >> (v0 & 31)) & 0xfu : 0xfu;
+        if (bits & 1u) best = max(best, argpack(f.x, v0));
+        if (bits & 2u) best = max(best, argpack(f.y, v0 + 1));
+        if (bits & 4u) best = max(best, argpack(f.z, v0 + 2));
+        if (bits & 8u) best = max(best, argpack(f.w, v0 + 3));
+      } else {
+        for (int v = v0; v < min(v_end, v0 + 4); ++v)
+          if (!m || ((m[v >> 5] >> (v & 31)) & 1u)) best = max(best, argpack(row[v], v));
+      }
     }
   }
-  // wave reduce (ties -> lowest index, matching torch.argmax)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (oi >= 0 && (bi < 0 || ov > best || (ov == best && oi < bi))) { best = ov; bi = oi; }
+    const unsigned long long other = __shfl_xor(best, o, 64);
+    best = max(best, other);
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) { sv[wid] = best; si[wid] = bi; }
+  if ((threadIdx.x & 63) == 0) sbest[threadIdx.x >> 6] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int nw = blockDim.x >> 6;
-    for (int i = 1; i < nw; ++i)
-      if (si[i] >= 0 && (bi < 0 || sv[i] > best || (sv[i] == best && si[i] < bi))) {
-        best = sv[i];
-        bi = si[i];
-      }
-    out_idx[b] = bi;
-    if (out_val) out_val[b] = best;
+    for (int i = 1; i < ARG_THREADS / 64; ++i) best = max(best, sbest[i]);
+    if (best) atomicMax(packed + b, best);
   }
 }
 
+__global__ void argmax_unpack_kernel(const unsigned long long* __restrict__ packed, int B,
+                                     int* __restrict__ out_idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) {
+    const unsigned long long p = packed[b];
+    out_idx[b] = p ? (int)(0xFFFFFFFFu - (uint32_t)(p & 0xFFFFFFFFull)) : -1;
+  }
+}
+
+// workspace: >= B * 8 bytes (device)
 extern "C" int loqa_masked_argmax(const void* logits, int is_bf16, long long ld, int B, int V,
                                   const uint32_t* mask, const int* mask_rows, int W, int* out_idx,
-                                  float* out_val, hipStream_t s) {
+                                  void* workspace, hipStream_t s) {
   if (B <= 0) return 0;
-  if (mask && W * 32 < V) return (int)hipErrorInvalidValue;
+  if ((mask && W * 32 < V) || !workspace) return (int)hipErrorInvalidValue;
+  unsigned long long* packed = (unsigned long long*)workspace;
+  hipError_t e = hipMemsetAsync(packed, 0, sizeof(unsigned long long) * B, s);
+  if (e != hipSuccess) return (int)e;
+  dim3 grid((V + ARG_CHUNK - 1) / ARG_CHUNK, B);
   if (is_bf16)
-    hipLaunchKernelGGL(masked_argmax_kernel<true>, dim3(B), dim3(1024), 0, s, logits, ld, V, mask,
-                       mask_rows, W, out_idx, out_val);
+    hipLaunchKernelGGL(masked_argmax_kernel<true>, grid, dim3(ARG_THREADS), 0, s, logits, ld, V, mask,
+                       mask_rows, W, packed);
   else
-    hipLaunchKernelGGL(masked_argmax_kernel<false>, dim3(B), dim3(1024), 0, s, logits, ld, V,
-                       mask, mask_rows, W, out_idx, out_val);
+    hipLaunchKernelGGL(masked_argmax_kernel<false>, grid, dim3(ARG_THREADS), 0, s, logits, ld, V,
+                       mask, mask_rows, W, packed);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(argmax_unpack_kernel, dim3((B + 63) / 64), dim3(64), 0, s, packed, B, out_idx);
   return (int)hipGetLastError();
 }

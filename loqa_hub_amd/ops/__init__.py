@@ -238,8 +238,9 @@ def masked_argmax(logits: torch.Tensor, mask: torch.Tensor | None = None,
     is_bf16 = logits.dtype == torch.bfloat16
     assert is_bf16 or logits.dtype == torch.float32
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    ws = torch.empty(B, dtype=torch.int64, device=logits.device)
     check(kernels().loqa_masked_argmax(ptr(logits), int(is_bf16), logits.stride(0), B, V,
-                                       ptr(mask), ptr(mask_rows), W, ptr(out), None,
+                                       ptr(mask), ptr(mask_rows), W, ptr(out), ptr(ws),
                                        stream_ptr(logits)), "masked_argmax")
     return out
 
