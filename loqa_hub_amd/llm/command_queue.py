@@ -106,6 +106,8 @@ class CommandQueue:
                     item.error = err
                     res.success = False
                     res.failed_item = item
+                    if isinstance(err, QueueTimeout):  # deadline hit mid-command
+                        res.error, res.cancelled = err, True
                     log.warning("command %d failed: %s", i + 1, err)
                     if self.rollback_enabled and res.completed_items:
                         rb_err = await self._rollback(executor, res.completed_items)

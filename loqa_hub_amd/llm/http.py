@@ -86,6 +86,8 @@ class MockHTTPClient:
     async def request(self, method, url, *, body=None, headers=None, timeout=30.0) -> HTTPResponse:
         self.requests.append((method, url, body))
         r = self._match(url)
+        if callable(r):
+            r = r(body)
         if isinstance(r, Exception):
             raise r
         if r is None:
@@ -95,6 +97,8 @@ class MockHTTPClient:
     async def stream_lines(self, method, url, *, body=None, headers=None, timeout=30.0):
         self.requests.append((method, url, body))
         r = self._match(url)
+        if callable(r):
+            r = r(body)
         if isinstance(r, Exception):
             raise r
         if r is None:
@@ -105,9 +109,12 @@ class MockHTTPClient:
             yield line
 
 
-def create_mock_ollama(response_text: str, status: int = 200) -> MockHTTPClient:
+def create_mock_ollama(response_text, status: int = 200) -> MockHTTPClient:
     """``CreateMockHTTPClient`` equivalent: every /api/generate returns
-    ``{"response": response_text, "done": true}``."""
-    return MockHTTPClient({"/api/generate": HTTPResponse(status, json.dumps(
-        {"response": response_text, "done": True}).encode()),
-        "/api/tags": HTTPResponse(200, b'{"models": []}')})
+    ``{"response": response_text, "done": true}``. ``response_text`` may be a
+    callable ``prompt -> str`` to answer per request."""
+    def gen(body):
+        text = response_text(json.loads(body)["prompt"]) if callable(response_text) else response_text
+        return HTTPResponse(status, json.dumps({"response": text, "done": True}).encode())
+    return MockHTTPClient({"/api/generate": gen,
+                           "/api/tags": HTTPResponse(200, b'{"models": []}')})

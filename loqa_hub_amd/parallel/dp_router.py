@@ -44,7 +44,9 @@ def scatter_pcm(info: DistInfo, per_rank: list[list[np.ndarray]] | None, slot_le
     recv = torch.empty(slot_len, dtype=torch.bfloat16, device=info.device)
     if info.rank == 0:
         packed = np.stack([pack_pcm(p, slot_len) for p in per_rank])
-        src = torch.from_numpy(packed).pin_memory().to(info.device, non_blocking=True)
+        src = torch.from_numpy(packed)
+        if info.device.type == "cuda":
+            src = src.pin_memory().to(info.device, non_blocking=True)
         chunks = list(src.view(torch.bfloat16).unbind(0))
         dist.scatter(recv, chunks, src=0)
     else:

@@ -1,0 +1,207 @@
+"""Engine-level CPU tests: tokenizer, grammar-constrained decoding, paged-KV block
+pools (Python and native C++), torch references of the HIP ops, the LLM / STT
+engines on tiny configs, the voice pipeline, and the DP bench path over gloo."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from loqa_hub_amd.engine.grammar import (Choice, Digits, Free, GrammarState, GrammarTables, Lit,
+                                         multi_command_schema, single_command_schema)
+from loqa_hub_amd.engine.kv_cache import PyBlockPool
+from loqa_hub_amd.engine.tokenizer import get_tokenizer
+from loqa_hub_amd.llm.commands import parse_multi_command_response, parse_response
+from loqa_hub_amd.ops import reference as R
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_tokenizer_roundtrip():
+    tok = get_tokenizer(32000)
+    for s in ['{"intent": "turn_on"}', "turn on the kitchen lights, then play music",
+              "émoji ✓ bytes"]:
+        ids = tok.encode(s)
+        assert tok.decode(ids) == s
+        assert all(0 <= i < tok.vocab_size for i in ids)
+    assert tok.vocab_size == 32000
+
+
+def _walk(state: GrammarState, tables: GrammarTables, rng) -> str:
+    state.start()
+    for _ in range(2000):
+        row = state.mask_row()
+        if row < 0:
+            break
+        allowed = tables.allowed(row).nonzero().flatten().tolist()
+        state.advance(int(rng.choice(allowed)))
+    assert state.done
+    return state.text()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_grammar_random_walk_is_valid_json(n):
+    tok = get_tokenizer(32000)
+    tables = GrammarTables(tok)
+    rng = np.random.default_rng(n)
+    for trial in range(5):
+        text = _walk(GrammarState(tables, multi_command_schema(n)), tables, rng)
+        obj = json.loads(text)
+        assert len(obj["commands"]) == n
+        mc = parse_multi_command_response(text, "x")
+        assert all(c.intent in ("turn_on", "turn_off", "greeting", "question", "unknown")
+                   for c in mc.commands)
+    single = _walk(GrammarState(tables, single_command_schema()), tables, rng)
+    assert parse_response(single).intent
+
+
+def test_grammar_min_length_and_digits():
+    tok = get_tokenizer(32000)
+    tables = GrammarTables(tok)
+    st = GrammarState(tables, [Lit('{"a": "'), Free("a", 4, min_tokens=2), Lit('", "d": 0.'),
+                               Digits(2), Lit("}")])
+    st.start()
+    assert st.mask_row() == tables.ROW_FREE_OPEN  # quote not allowed yet
+    assert not bool(tables.allowed(st.mask_row())[tables.quote])
+    st.advance(tok.token_id("x"))
+    st.advance(tok.token_id("y"))
+    assert st.mask_row() == tables.ROW_FREE
+    st.advance(tables.quote)
+    assert st.mask_row() == tables.ROW_DIGIT
+    st.advance(tok.token_id("4"))
+    st.advance(tok.token_id("2"))
+    assert st.done and json.loads(st.text()) == {"a": "xy", "d": 0.42}
+    # choice trie: forced completion once the prefix is unique
+    st = GrammarState(tables, [Lit('"'), Choice("c", ["turn_on", "turn_off"]), Lit('"')])
+    st.start()
+    while not st.done:
+        st.advance(int(tables.allowed(st.mask_row()).nonzero()[0]))
+    assert json.loads(st.text()) in ("turn_on", "turn_off")
+
+
+def test_mask_pack_roundtrip():
+    m = torch.rand(3, 100) > 0.5
+    packed = R.pack_mask(m)
+    assert packed.dtype == torch.int32 and packed.shape == (3, 4)
+    assert torch.equal(R.unpack_mask(packed, 100), m)
+
+
+def _exercise_pool(pool):
+    toks = list(range(40))
+    assert pool.add_seq(1, toks) == 0
+    slots = pool.append(1, 40)
+    assert len(slots) == 40 and len(set(slots)) == 40
+    assert pool.seq_len(1) == 40 and len(pool.block_table(1)) == 3
+    pool.cache_prefix(1, toks)
+    hit = pool.add_seq(2, toks[:32] + [99, 98])
+    assert hit == 32  # two full blocks shared
+    assert pool.block_table(2)[:2] == pool.block_table(1)[:2]
+    before = pool.free_blocks()
+    pool.append(2, 20)
+    assert pool.seq_len(2) == 52 and pool.free_blocks() < before
+    pool.free_seq(1)
+    pool.free_seq(2)
+    assert pool.add_seq(3, toks[:16] + [7]) == 16  # cached block survives until evicted
+    pool.free_seq(3)
+    # exhausting the pool evicts unreferenced cached blocks instead of failing
+    assert pool.add_seq(4, [5]) == 0
+    assert pool.append(4, 16 * pool_blocks(pool)) is not None
+
+
+def pool_blocks(pool):
+    return 64
+
+
+def test_py_block_pool():
+    _exercise_pool(PyBlockPool(64, 16))
+
+
+def test_native_block_pool_matches():
+    from loqa_hub_amd.engine.kv_cache import NativeBlockPool
+    from loqa_hub_amd.ops import _lib
+    try:
+        _lib.runtime()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native runtime not built: {e}")
+    _exercise_pool(NativeBlockPool(64, 16))
+
+
+def test_skinny_reference_and_shuffle():
+    torch.manual_seed(0)
+    N, K = 64, 256
+    W = torch.randn(N, K).bfloat16()
+    Wp = R.shuffle_weight(W)
+    assert torch.equal(R.unshuffle_weight(Wp), W)
+    x = torch.randn(16, K).bfloat16()
+    part = R.skinny_gemm(x, Wp, 4)
+    assert part.shape == (4, 16, N)
+    assert torch.allclose(part.sum(0), x.float() @ W.float().t(), atol=1e-3, rtol=1e-4)
+
+
+def test_attention_reference_matches_sdpa():
+    torch.manual_seed(0)
+    q = torch.randn(2, 4, 10, 64)
+    k = torch.randn(2, 2, 10, 64)
+    v = torch.randn(2, 2, 10, 64)
+    kk, vv = k.repeat_interleave(2, 1), v.repeat_interleave(2, 1)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, kk, vv, is_causal=True)
+    s = (q @ kk.transpose(-1, -2)) / 8.0
+    s = s.masked_fill(torch.ones(10, 10, dtype=torch.bool).triu(1), float("-inf"))
+    assert torch.allclose(s.softmax(-1) @ vv, ref, atol=1e-5)
+
+
+def test_llm_engine_cpu_generates_valid_json():
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=4,
+                    max_seq_len=512, use_graphs=False)
+    reqs = [GenRequest(eng.tok.encode("turn on the lights and play music", bos=True),
+                       multi_command_schema(n)) for n in (1, 2, 3)]
+    eng.generate(reqs)
+    for n, r in zip((1, 2, 3), reqs):
+        mc = parse_multi_command_response(r.output, "x")
+        assert len(mc.commands) == n
+    assert eng.stats["decode_steps"] > 0
+
+
+def test_stt_engine_cpu_teacher_forced():
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    eng = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4)
+    utts = make_batch(0, 3, [1, 2])
+    reqs = [STTRequest(u.pcm, transcript=u.text) for u in utts]
+    eng.transcribe(reqs)
+    for r, u in zip(reqs, utts):
+        assert r.text == u.text
+
+
+def _run(cmd, timeout=600):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_cpu_smoke_single():
+    out = _run([sys.executable, "bench.py", "--cpu-smoke", "--steps", "1", "--warmup", "0",
+                "--batch-per-gpu", "4"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["n_gpus"] == 1 and out["queue_success_rate"] == 1.0
+    assert out["command_count_match_rate"] == 1.0
+
+
+def test_bench_cpu_smoke_dp2_gloo():
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+                "2", "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py",
+                "--cpu-smoke", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                "--batch-per-gpu", "2"])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 4 and out["queue_success_rate"] == 1.0
