@@ -47,6 +47,9 @@ class GenRequest:
     steps: int = 0
     token_times: list[float] = field(default_factory=list)
     done: bool = False
+    # optional streaming hook: called from the engine thread with each step's
+    # newly emitted token ids (sampled token + jump-forward literal)
+    on_tokens: object = None
 
 
 def _bucket(n: int, buckets: list[int]) -> int:
@@ -215,7 +218,10 @@ class LLMEngine:
         req.seq_id = self._next_id
         self._next_id += 1
         req.grammar = GrammarState(self.grammar, req.schema)
-        req.feed = list(req.prompt) + req.grammar.start()
+        start = req.grammar.start()
+        req.feed = list(req.prompt) + start
+        if req.on_tokens is not None and start:
+            req.on_tokens(list(start))
         req.t_submit = time.perf_counter()
         hit = self.kv.pool.add_seq(req.seq_id, req.feed)
         if hit < 0:
@@ -237,6 +243,8 @@ class LLMEngine:
             forced = r.grammar.advance(int(t))
             self.stats["sampled_tokens"] += 1
             self.stats["forced_tokens"] += len(forced)
+            if r.on_tokens is not None:
+                r.on_tokens([int(t)] + forced)
             if r.grammar.done:
                 r.done = True
                 r.t_done = now
