@@ -128,6 +128,7 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    s0 = dict(llm.stats)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
@@ -137,6 +138,13 @@ def main(argv=None) -> int:
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
 
     stats = added_command_stats(all_jobs)
+    phase_ms = {
+        "stt": round(float(np.mean([(j.t["stt_done"] - j.t["start"]) for j in all_jobs])) * 1e3, 2)
+        if all_jobs else None,
+        "llm_prefill": round((llm.stats["prefill_s"] - s0["prefill_s"]) / args.steps * 1e3, 2),
+        "llm_decode": round((llm.stats["decode_s"] - s0["decode_s"]) / args.steps * 1e3, 2),
+        "llm_decode_steps": (llm.stats["decode_steps"] - s0["decode_steps"]) / args.steps,
+    }
     recs = torch.cat(step.records, 0) if step.records else torch.zeros(0, 4)
     total_utts = info.world * B * args.steps
     value = total_utts / elapsed
@@ -169,6 +177,7 @@ def main(argv=None) -> int:
             "added_command_speedup_vs_baseline": None if e2e <= 0 else round(BASELINE_MS_PER_ADDED_COMMAND / e2e, 3),
             "queue_success_rate": round(ok, 4),
             "command_count_match_rate": round(cmd_match, 4),
+            "phase_ms_per_step": phase_ms,
             "llm_stats": llm.stats,
             "init_s": round(t_init, 2),
         }

@@ -33,12 +33,16 @@ struct DecSmem {
   float ml[DEC_WAVES][2][64];                      // (m, l) per wave per lane
 };
 
+// K/V source: paged caches [nb, Hkv, blk, D] via block_tables, or (block_tables
+// == nullptr) contiguous rows kc/vc[(kv_start[b] + key) * kv_stride + kvh * D]
+// (Whisper cross-attention over the encoder output, read in place).
 template <int D>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16_t* __restrict__ q, long long q_stride, const bf16_t* __restrict__ kc,
-    const bf16_t* __restrict__ vc, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+    const bf16_t* __restrict__ vc, long long kv_stride, const int* __restrict__ kv_start,
+    const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, int max_blocks, int blk, int Hq, int Hkv,
-    float scale_log2, int split_keys, int num_splits, float* __restrict__ part_o,
+    float scale_log2, int causal, int split_keys, int num_splits, float* __restrict__ part_o,
     float* __restrict__ part_ml, int total_q) {
   constexpr int NS = D / 16, NDT = D / 32, CH = D / 8;
   constexpr int VPL = DEC_TILE * CH / 64;  // 16-byte V chunks per lane per tile
@@ -55,7 +59,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int qpos = klen - qlen + qi;
   const int kbeg = split * split_keys;
   const int kend = min(klen, kbeg + split_keys);
-  const int* bt = block_tables + (size_t)b * max_blocks;
+  const bool paged = block_tables != nullptr;
+  const int* bt = paged ? block_tables + (size_t)b * max_blocks : nullptr;
+  const size_t kv0 = paged ? 0 : (size_t)kv_start[b];
 
   bf16x8 qf[NS];
   {
@@ -81,8 +87,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       const bool ok = key < kend;
       size_t off = 0;
       if (ok) {
-        const int bi = key / blk, bo = key - bi * blk;
-        off = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
+        if (paged) {
+          const int bi = key / blk, bo = key - bi * blk;
+          off = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
+        } else {
+          off = (kv0 + key) * (size_t)kv_stride + (size_t)kvh * D;
+        }
       }
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -94,8 +104,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         const int k2 = kt + kr;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (k2 < kend) {
-          const int bi = k2 / blk, bo = k2 - bi * blk;
-          v = *reinterpret_cast<const uint4*>(vc + (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D + cc);
+          size_t voff;
+          if (paged) {
+            const int bi = k2 / blk, bo = k2 - bi * blk;
+            voff = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
+          } else {
+            voff = (kv0 + k2) * (size_t)kv_stride + (size_t)kvh * D;
+          }
+          v = *reinterpret_cast<const uint4*>(vc + voff + cc);
         }
         vraw[i] = v;
       }
@@ -118,7 +134,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int j = 0; j < 16; ++j) {
       const int key = kt + (j & 3) + 8 * (j >> 2) + 4 * h;
       float sv = st[j] * scale_log2;
-      if (key >= kend || key > qpos) sv = -INFINITY;
+      if (key >= kend || (causal && key > qpos)) sv = -INFINITY;
       st[j] = sv;
       mx = fmaxf(mx, sv);
     }
@@ -232,27 +248,33 @@ __global__ void attn_decode_combine_kernel(const float* __restrict__ part_o,
   o[(size_t)tok * o_stride + (size_t)head * D + d] = f2bf(l > 0.f ? acc / l : 0.f);
 }
 
-// q: [Tq, >=Hq*D] bf16; caches [nb, Hkv, blk, D]; out [Tq, Hq*D] bf16.
+// q: [Tq, >=Hq*D] bf16; K/V paged caches [nb, Hkv, blk, D] (block_tables) or
+// contiguous rows (kv_stride, kv_start); out [Tq, Hq*D] bf16.
 // Requires G * max_q <= 32 and split_keys % 32 == 0.
 extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* kc, const void* vc,
-                                void* o, long long o_stride, const int* cu_q, const int* ctx_lens,
+                                long long kv_stride, const int* kv_start, void* o,
+                                long long o_stride, const int* cu_q, const int* ctx_lens,
                                 const int* block_tables, int max_blocks, int blk, int B, int max_q,
-                                int Hq, int Hkv, int D, float scale, int split_keys, int num_splits,
-                                float* part_o, float* part_ml, int total_q, hipStream_t s) {
+                                int Hq, int Hkv, int D, float scale, int causal, int split_keys,
+                                int num_splits, float* part_o, float* part_ml, int total_q,
+                                hipStream_t s) {
   if (B <= 0 || total_q <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv || (Hq / Hkv) * max_q > 32 || split_keys % DEC_TILE || num_splits < 1 ||
       (D != 64 && D != 128) || !part_o || !part_ml)
     return (int)hipErrorInvalidValue;
+  if (!block_tables && (!kv_start || kv_stride % 8)) return (int)hipErrorInvalidValue;
   dim3 grid(num_splits, Hkv, B);
   const float sl2 = scale * 1.4426950408889634f;
   if (D == 128)
     hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
-                       (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
-                       blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
+                       (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
+                       block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
+                       part_o, part_ml, total_q);
   else
     hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
-                       (const bf16_t*)kc, (const bf16_t*)vc, cu_q, ctx_lens, block_tables, max_blocks,
-                       blk, Hq, Hkv, sl2, split_keys, num_splits, part_o, part_ml, total_q);
+                       (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
+                       block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
+                       part_o, part_ml, total_q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(total_q, Hq), dim3(D), 0, s, part_o, part_ml,

@@ -135,3 +135,31 @@ extern "C" int loqa_layernorm(const void* x, void* residual, const void* w, cons
                      (bf16_t*)y, d, eps);
   return (int)hipGetLastError();
 }
+
+// Decoder input embedding: out[r] = bf16(tok_embed[tokens[r]] + pos_embed[positions[r]])
+// (Whisper decoder; feeds layernorm as the first residual).
+__global__ void embed_pos_kernel(const int* __restrict__ tokens, const int* __restrict__ positions,
+                                 const bf16_t* __restrict__ te, const bf16_t* __restrict__ pe,
+                                 bf16_t* __restrict__ out, int d) {
+  const int row = blockIdx.x;
+  const uint4* a = reinterpret_cast<const uint4*>(te + (size_t)tokens[row] * d);
+  const uint4* b = reinterpret_cast<const uint4*>(pe + (size_t)positions[row] * d);
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)row * d);
+  for (int c = threadIdx.x; c < (d >> 3); c += blockDim.x) {
+    float x[8], y[8];
+    unpack8(a[c], x);
+    unpack8(b[c], y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += y[j];
+    o[c] = pack8(x);
+  }
+}
+
+extern "C" int loqa_embed_pos(const int* tokens, const int* positions, const void* tok_embed,
+                              const void* pos_embed, void* out, int rows, int d, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (d % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_pos_kernel, dim3(rows), dim3(128), 0, s, tokens, positions,
+                     (const bf16_t*)tok_embed, (const bf16_t*)pos_embed, (bf16_t*)out, d);
+  return (int)hipGetLastError();
+}

@@ -75,7 +75,7 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
                                         const float2* __restrict__ cs, bf16_t* __restrict__ q_out,
                                         bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
                                         const int* __restrict__ slots, int H, int Hkv, int D,
-                                        int blk) {
+                                        int blk, const bf16_t* __restrict__ bias) {
   const int t = blockIdx.x;
   const int N = (H + 2 * Hkv) * D;
   const size_t slab_stride = (size_t)Mpad * N;
@@ -96,6 +96,12 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
       const int bb = slot / blk, o = slot - bb * blk;
       float v[8];
       slab_load8(part, slab_stride, S, (size_t)t * N + (H + Hkv) * D + h * D + c, v);
+      if (bias) {
+        float bv[8];
+        unpack8(*reinterpret_cast<const uint4*>(bias + (H + Hkv) * D + h * D + c), bv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += bv[j];
+      }
       *reinterpret_cast<uint4*>(vc + (((size_t)bb * Hkv + h) * blk + o) * D + c) = pack8(v);
       continue;
     }
@@ -113,6 +119,13 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
         y = *reinterpret_cast<const float4*>(row + s * slab_stride + base + c + half);
         a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w;
         b[0] += y.x; b[1] += y.y; b[2] += y.z; b[3] += y.w;
+      }
+    }
+    if (bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] += bf2f(bias[base + c + j]);
+        b[j] += bf2f(bias[base + c + half + j]);
       }
     }
     // round to bf16 first: the projection output is a bf16 tensor in the model
@@ -141,6 +154,105 @@ __global__ void slab_rope_append_kernel(const float* __restrict__ part, int S, i
     }
     *reinterpret_cast<uint2*>(dst + c) = lo;
     *reinterpret_cast<uint2*>(dst + c + half) = hi;
+  }
+}
+
+// LayerNorm consumer (Whisper decoder): h = sum_s part + bias (+ residual);
+// residual <- h (bf16); y = (h - mean) / sqrt(var + eps) * w + b.
+__global__ __launch_bounds__(NT) void slab_layernorm_kernel(
+    const float* __restrict__ part, int S, int Mpad, const int64_t* __restrict__ row_idx,
+    const bf16_t* __restrict__ pbias, bf16_t* __restrict__ residual, int write_residual,
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ lb, bf16_t* __restrict__ y, int d,
+    float eps) {
+  __shared__ float scratch[NT / 64];
+  const int row = blockIdx.x;
+  const int src = row_idx ? (int)row_idx[row] : row;
+  const size_t slab_stride = (size_t)Mpad * d;
+  const int nvec = d >> 3;
+  uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)src * d);
+  float v[MAXV][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = threadIdx.x + i * NT;
+    if (c < nvec) {
+      slab_load8(part, slab_stride, S, (size_t)src * d + c * 8, v[i]);
+      float r[8];
+      // the projection output (with bias) is a bf16 tensor in the model
+      if (pbias) {
+        unpack8(reinterpret_cast<const uint4*>(pbias)[c], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(v[i][j]));
+      unpack8(rr[c], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] += r[j];
+      uint4 p = pack8(v[i]);
+      if (write_residual) rr[c] = p;
+      unpack8(p, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[i][j];
+    }
+  }
+  const float mean = block_sum(sum, scratch) / (float)d;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = threadIdx.x + i * NT;
+    if (c < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = v[i][j] - mean;
+        ss += t * t;
+      }
+    }
+  }
+  __syncthreads();
+  const float inv = rsqrtf(block_sum(ss, scratch) / (float)d + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  const uint4* br = reinterpret_cast<const uint4*>(lb);
+  uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * d);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = threadIdx.x + i * NT;
+    if (c < nvec) {
+      float wf[8], bf[8], o[8];
+      unpack8(wr[c], wf);
+      unpack8(br[c], bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * inv * wf[j] + bf[j];
+      yr[c] = pack8(o);
+    }
+  }
+}
+
+// out[m, n] = act(bf16(sum_s part[s][m][n] + bias[n])), act: 0 identity, 1 GELU(erf)
+__global__ void slab_bias_act_kernel(const float* __restrict__ part, int S, int Mpad, int N,
+                                     const bf16_t* __restrict__ bias, int act,
+                                     bf16_t* __restrict__ out, long long total_vec) {
+  const size_t slab_stride = (size_t)Mpad * N;
+  const int nv = N >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % nv) * 8;
+    float v[8];
+    slab_load8(part, slab_stride, S, (size_t)i * 8, v);
+    if (bias) {
+      float bv[8];
+      unpack8(*reinterpret_cast<const uint4*>(bias + c), bv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bv[j];
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = bf2f(f2bf(v[j]));
+        v[j] = 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+      }
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)i * 8) = pack8(v);
   }
 }
 
@@ -191,13 +303,13 @@ extern "C" int loqa_slab_rmsnorm(const float* part, int S, int Mpad, const int64
 extern "C" int loqa_slab_rope_append(const float* part, int S, int Mpad, int M, const int* positions,
                                      const void* cs, void* q_out, void* kc, void* vc,
                                      const int* slots, int H, int Hkv, int D, int blk,
-                                     hipStream_t st) {
+                                     const void* bias, hipStream_t st) {
   if (M <= 0) return 0;
   if (D % 8) return (int)hipErrorInvalidValue;
   const int items = (H + Hkv) * (D / 8) + Hkv * (D / 8);
   hipLaunchKernelGGL(slab_rope_append_kernel, dim3(M, (items + 127) / 128), dim3(128), 0, st, part, S, Mpad, positions,
                      (const float2*)cs, (bf16_t*)q_out, (bf16_t*)kc, (bf16_t*)vc, slots, H, Hkv, D,
-                     blk);
+                     blk, (const bf16_t*)bias);
   return (int)hipGetLastError();
 }
 
@@ -222,5 +334,29 @@ extern "C" int loqa_slab_reduce(const float* part, int S, int Mpad, int M, int N
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, S, Mpad, N,
                      out, tv);
+  return (int)hipGetLastError();
+}
+
+extern "C" int loqa_slab_layernorm(const float* part, int S, int Mpad, const int64_t* row_idx,
+                                   int rows, const void* pbias, void* residual, int write_residual,
+                                   const void* w, const void* b, void* y, int d, float eps,
+                                   hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (d % 8 || d > NT * 8 * MAXV) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(slab_layernorm_kernel, dim3(rows), dim3(NT), 0, st, part, S, Mpad, row_idx,
+                     (const bf16_t*)pbias, (bf16_t*)residual, write_residual, (const bf16_t*)w,
+                     (const bf16_t*)b, (bf16_t*)y, d, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int loqa_slab_bias_act(const float* part, int S, int Mpad, int M, int N,
+                                  const void* bias, int act, void* out, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % 8 || act < 0 || act > 1) return (int)hipErrorInvalidValue;
+  const long long tv = (long long)M * N / 8;
+  long long blocks = (tv + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(slab_bias_act_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, S, Mpad,
+                     N, (const bf16_t*)bias, act, (bf16_t*)out, tv);
   return (int)hipGetLastError();
 }

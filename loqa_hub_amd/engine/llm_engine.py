@@ -94,7 +94,8 @@ class LLMEngine:
         self._next_id = 1
         self._on_done = None
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
-                      "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0}
+                      "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
+                      "prefill_s": 0.0, "decode_s": 0.0}
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
@@ -315,13 +316,17 @@ class LLMEngine:
         """Run the requests to completion. ``on_done(req)`` fires as soon as each
         sequence finishes (its command queue can start while others decode)."""
         self._on_done = on_done
+        t0 = time.perf_counter()
         for r in reqs:
             self.submit(r)
         self.prefill(reqs)
+        t1 = time.perf_counter()
         live = [r for r in reqs if not r.done]
         while live:
             self.decode_step(live)
             live = [r for r in live if not r.done]
+        self.stats["prefill_s"] += t1 - t0
+        self.stats["decode_s"] += time.perf_counter() - t1
         for r in reqs:
             self.kv.pool.free_seq(r.seq_id)
         return reqs

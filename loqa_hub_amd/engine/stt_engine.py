@@ -19,7 +19,7 @@ import torch
 
 from .. import ops
 from ..models.configs import WhisperConfig
-from ..models.whisper import WhisperModel, WhisperWeights
+from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
@@ -41,8 +41,11 @@ class STTRequest:
 
 
 class STTEngine:
+    SEQ_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128]
+    SPLIT_KEYS = 128
+
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
-                 block_size: int = 16):
+                 block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.weights = WhisperWeights(cfg, self.device, seed=seed)
@@ -61,6 +64,19 @@ class STTEngine:
                                     ) if self.is_gpu else None
         self._next = 1
         self.stats = {"utterances": 0, "decode_steps": 0}
+        self.max_batch = max_batch
+        self.fast_decode = fast_decode
+        self.use_graphs = use_graphs and self.is_gpu and fast_decode
+        self.self_splits = (cfg.n_text_ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS
+        if fast_decode and self.is_gpu:
+            self.ws = ops.AttnWorkspace(self.device, 128, cfg.n_heads, cfg.head_dim,
+                                        max(self.self_splits, (cfg.n_audio_ctx + self.SPLIT_KEYS - 1)
+                                            // self.SPLIT_KEYS))
+        # cross-attention K|V of every decoder layer for up to max_batch
+        # utterances, written in place each batch (graph-captured steps read it)
+        self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
+                                device=self.device) for _ in range(cfg.dec_layers)]
+        self._graphs: dict[tuple[int, int], dict] = {}
 
     # ------------------------------------------------------------ front end
     def upload(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
@@ -102,15 +118,150 @@ class STTEngine:
         return audio
 
     # -------------------------------------------------------------- decode
+    def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:
+        rows = enc.shape[0]
+        assert rows <= self.xkv[0].shape[0], "batch exceeds max_batch"
+        for L, buf in zip(self.weights.dec, self.xkv):
+            torch.addmm(L["xkv_b"], enc, L["xkv"].t(), out=buf[:rows])
+        return self.xkv
+
+    def _host_meta(self, reqs, live, feeds, B_pad: int, T_pad: int) -> tuple[int, dict]:
+        T_enc = self.cfg.n_audio_ctx
+        tokens = np.zeros(T_pad, np.int32)
+        positions = np.zeros(T_pad, np.int32)
+        slots = np.full(T_pad, -1, np.int32)
+        cu = np.zeros(B_pad + 1, np.int32)
+        ctx = np.zeros(B_pad, np.int32)
+        bt = np.zeros((B_pad, self.max_blocks), np.int32)
+        enc_starts = np.zeros(B_pad, np.int32)
+        enc_lens = np.zeros(B_pad, np.int32)
+        lidx = np.zeros(max(16, ops.mpad_for(B_pad)), np.int64)
+        off, max_q = 0, 1
+        pool = self.kv.pool
+        for j, i in enumerate(live):
+            r, f = reqs[i], feeds[i]
+            n = len(f)
+            start = pool.seq_len(r.seq_id)
+            sl = pool.append(r.seq_id, n)
+            if sl is None:
+                raise RuntimeError("STT KV cache exhausted")
+            tokens[off:off + n] = f
+            positions[off:off + n] = np.arange(start, start + n)
+            slots[off:off + n] = sl
+            off += n
+            cu[j + 1] = off
+            ctx[j] = start + n
+            tab = pool.block_table(r.seq_id)
+            bt[j, :len(tab)] = tab
+            enc_starts[j] = i * T_enc
+            enc_lens[j] = T_enc
+            lidx[j] = off - 1
+            max_q = max(max_q, n)
+        cu[len(live) + 1:] = off
+        return max_q, {"tokens": tokens, "positions": positions, "slots": slots, "cu_q": cu,
+                       "ctx_lens": ctx, "block_tables": bt, "enc_starts": enc_starts,
+                       "enc_lens": enc_lens, "logit_idx": lidx}
+
+    def _dev(self, host: dict, dst: dict | None = None) -> dict:
+        out = {}
+        for k, a in host.items():
+            t = torch.from_numpy(a)
+            if self.is_gpu:
+                t = t.pin_memory()
+            if dst is not None:
+                dst[k].copy_(t, non_blocking=True)
+                out[k] = dst[k]
+            else:
+                out[k] = t.to(self.device, non_blocking=True)
+        return out
+
+    def _fast_forward(self, dev: dict, max_q: int, B_pad: int) -> torch.Tensor:
+        logits = decode_step_fast(self.model, dev["tokens"], dev["positions"], dev["slots"],
+                                  dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
+                                  self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
+                                  dev["enc_lens"], dev["logit_idx"], self.ws, self.self_splits,
+                                  self.SPLIT_KEYS)
+        return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
+
+    def _graph(self, B_pad: int, T_pad: int) -> dict:
+        key = (B_pad, T_pad)
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        z = lambda *shape, dt=torch.int32: torch.zeros(*shape, dtype=dt, device=self.device)
+        dev = {"tokens": z(T_pad), "positions": z(T_pad),
+               "slots": torch.full((T_pad,), -1, dtype=torch.int32, device=self.device),
+               "cu_q": z(B_pad + 1), "ctx_lens": z(B_pad),
+               "block_tables": z(B_pad, self.max_blocks), "enc_starts": z(B_pad),
+               "enc_lens": z(B_pad), "logit_idx": z(max(16, ops.mpad_for(B_pad)), dt=torch.int64)}
+        max_q = max(1, min(len(self.sot), T_pad))
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._fast_forward(dev, max_q, B_pad)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self._fast_forward(dev, max_q, B_pad)
+        g = {"graph": graph, "dev": dev, "out": out}
+        self._graphs[key] = g
+        return g
+
+    def _step(self, reqs, live, feeds) -> np.ndarray:
+        B = len(live)
+        T = sum(len(feeds[i]) for i in live)
+        if self.fast_decode:
+            B_pad = next((b for b in self.SEQ_BUCKETS if b >= B), B)
+            T_pad = ops.mpad_for(T)
+            if self.use_graphs:
+                g = self._graph(B_pad, T_pad)
+                _, host = self._host_meta(reqs, live, feeds, B_pad, T_pad)
+                self._dev(host, g["dev"])
+                g["graph"].replay()
+                return g["out"][:B].cpu().numpy()
+            max_q, host = self._host_meta(reqs, live, feeds, B_pad, T_pad)
+            return self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
+        return self._eager_step(reqs, live, feeds)
+
+    def _eager_step(self, reqs, live, feeds) -> np.ndarray:
+        """Reference decode path (hipBLASLt GEMMs, eager launches)."""
+        T_enc = self.cfg.n_audio_ctx
+        toks, pos, slots, cu, ctx, lidx = [], [], [], [0], [], []
+        bt = np.zeros((len(live), self.max_blocks), np.int32)
+        max_q, max_ctx = 1, 1
+        for j, i in enumerate(live):
+            r = reqs[i]
+            f = feeds[i]
+            start = self.kv.pool.seq_len(r.seq_id)
+            sl = self.kv.pool.append(r.seq_id, len(f))
+            toks += f
+            pos += list(range(start, start + len(f)))
+            slots += sl
+            cu.append(cu[-1] + len(f))
+            ctx.append(start + len(f))
+            tab = self.kv.pool.block_table(r.seq_id)
+            bt[j, :len(tab)] = tab
+            lidx.append(cu[-1] - 1)
+            max_q = max(max_q, len(f))
+            max_ctx = max(max_ctx, start + len(f))
+        dev = lambda a, dt: torch.tensor(a, dtype=dt).to(self.device, non_blocking=True)
+        enc_starts = dev([i * T_enc for i in live], torch.int32)
+        enc_lens = dev([T_enc] * len(live), torch.int32)
+        logits = self.model.decode_step(
+            dev(toks, torch.int32), dev(pos, torch.int32), dev(slots, torch.int32),
+            dev(cu, torch.int32), dev(ctx, torch.int32), dev(bt, torch.int32), max_q, max_ctx,
+            self.kv.k, self.kv.v, self.xkv, enc_starts, enc_lens, dev(lidx, torch.int64), self.ws)
+        return ops.masked_argmax(logits).cpu().numpy()
+
     def transcribe(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
                    ) -> list[STTRequest]:
         if not reqs:
             return reqs
+        assert len(reqs) <= self.max_batch, "batch exceeds max_batch"
         audio, sumsq = self.upload(reqs, device_pcm)
         enc = self.model.encode(audio)
-        xkv = self.model.cross_kv(enc)
+        self.cross_kv(enc)
         B = len(reqs)
-        T = self.cfg.n_audio_ctx
         targets = []
         for r in reqs:
             r.seq_id = self._next
@@ -124,33 +275,7 @@ class STTEngine:
         live = list(range(B))
         step = 0
         while live:
-            toks, pos, slots, cu, ctx, lidx = [], [], [], [0], [], []
-            bt = np.zeros((len(live), self.max_blocks), np.int32)
-            max_q, max_ctx = 1, 1
-            for j, i in enumerate(live):
-                r = reqs[i]
-                f = feeds[i]
-                start = self.kv.pool.seq_len(r.seq_id)
-                sl = self.kv.pool.append(r.seq_id, len(f))
-                toks += f
-                pos += list(range(start, start + len(f)))
-                slots += sl
-                cu.append(cu[-1] + len(f))
-                ctx.append(start + len(f))
-                tab = self.kv.pool.block_table(r.seq_id)
-                bt[j, :len(tab)] = tab
-                lidx.append(cu[-1] - 1)
-                max_q = max(max_q, len(f))
-                max_ctx = max(max_ctx, start + len(f))
-            dev = lambda a, dt: torch.tensor(a, dtype=dt).to(self.device, non_blocking=True)
-            # cross-attention reads each live utterance's 1500 encoder rows in place
-            enc_starts = dev([i * T for i in live], torch.int32)
-            enc_lens = dev([T] * len(live), torch.int32)
-            logits = self.model.decode_step(
-                dev(toks, torch.int32), dev(pos, torch.int32), dev(slots, torch.int32),
-                dev(cu, torch.int32), dev(ctx, torch.int32), dev(bt, torch.int32), max_q, max_ctx,
-                self.kv.k, self.kv.v, xkv, enc_starts, enc_lens, dev(lidx, torch.int64), self.ws)
-            nxt = ops.masked_argmax(logits).cpu().numpy()
+            nxt = self._step(reqs, live, feeds)
             self.stats["decode_steps"] += 1
             still = []
             for j, i in enumerate(live):

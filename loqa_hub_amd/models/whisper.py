@@ -29,6 +29,9 @@ def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> tor
     return torch.cat([t.sin(), t.cos()], dim=1).float()
 
 
+DEC_PROJ = ("wqkv", "wo", "xq", "xo", "fc1", "fc2")
+
+
 class WhisperWeights:
     def __init__(self, cfg: WhisperConfig, device, dtype=torch.bfloat16, seed: int = 0):
         self.cfg = cfg
@@ -62,6 +65,18 @@ class WhisperWeights:
         for _ in range(cfg.dec_layers):
             self.dec.append(self._block(rnd, zeros, ones, d, f, cross=True))
         self.dec_ln_w, self.dec_ln_b = ones(d), zeros(d)
+        # decode-path copies in MFMA fragment order for the weight-streaming
+        # skinny GEMM; the vocab is zero-padded to a multiple of 32 rows
+        self.vocab_pad = (cfg.vocab_size + 31) // 32 * 32
+        lm = torch.zeros(self.vocab_pad, d, dtype=dtype, device=device)
+        lm[: cfg.vocab_size] = self.tok_embed
+        self.lm_head_p = ops.shuffle_weight(lm)
+        del lm
+        self.dec_p = [{k: ops.shuffle_weight(L[k]) for k in DEC_PROJ} for L in self.dec]
+        if torch.device(device).type == "cuda":
+            for k in DEC_PROJ:
+                ops.tune_skinny_splits(self.dec_p[0][k], mpads=(16, 32))
+            ops.tune_skinny_splits(self.lm_head_p, mpads=(16, 32))
 
     @staticmethod
     def _block(rnd, zeros, ones, d, f, cross: bool) -> dict:
@@ -171,6 +186,55 @@ class WhisperModel:
         sel_d = delta.index_select(0, logit_idx).contiguous()
         hf = ops.layernorm(sel_d, w.dec_ln_w, w.dec_ln_b, 1e-5, residual=sel_r)
         return ops.linear(hf, w.tok_embed)
+
+
+def decode_step_fast(model: "WhisperModel", tokens: torch.Tensor, positions: torch.Tensor,
+                     slots: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor,
+                     block_tables: torch.Tensor, max_q: int, k_cache: torch.Tensor,
+                     v_cache: torch.Tensor, xkv: list[torch.Tensor], enc_starts: torch.Tensor,
+                     enc_lens: torch.Tensor, logit_idx: torch.Tensor, ws,
+                     self_splits: int, split_keys: int = 128) -> torch.Tensor:
+    """Decoder step on the weight-streaming path: every projection is the
+    skinny split-K MFMA GEMM whose f32 slabs are reduced by the fused consumer
+    that follows (bias + residual + LayerNorm, bias + KV append, bias + GELU);
+    self- and cross-attention use the split-key decode kernel (cross-attention
+    reads the encoder K/V rows in place). ``tokens`` has Mpad rows (padding
+    rows carry slot -1); ``logit_idx`` has >= 16 rows. Graph-capturable: no
+    host synchronisation, fixed ``self_splits``. Returns f32 logits
+    [len(logit_idx), vocab_pad]."""
+    cfg, w = model.cfg, model.w
+    d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
+    enc_splits = (cfg.n_audio_ctx + split_keys - 1) // split_keys
+    residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
+    h = ops.layernorm(residual, w.dec[0]["ln1_w"], w.dec[0]["ln1_b"], 1e-5)
+    part = None
+    for i, (L, P) in enumerate(zip(w.dec, w.dec_p)):
+        if i > 0:
+            h = ops.slab_layernorm(part, residual, L["ln1_w"], L["ln1_b"], 1e-5,
+                                   bias=w.dec[i - 1]["fc2_b"])
+        part = ops.skinny_gemm(h, P["wqkv"])
+        q = ops.slab_rope_append(part, positions, None, k_cache[i], v_cache[i], slots, H, H, D,
+                                 bias=L["bqkv"])
+        a = ops.attention(q, k_cache[i], v_cache[i], cu_q, n_heads=H, n_kv=H, head_dim=D,
+                          causal=True, max_q=max_q, ctx_lens=ctx_lens, block_tables=block_tables,
+                          grouped=True, split_keys=split_keys, num_splits=self_splits,
+                          workspace=ws)
+        part = ops.skinny_gemm(a, P["wo"])
+        h = ops.slab_layernorm(part, residual, L["lnx_w"], L["lnx_b"], 1e-5, bias=L["bo"])
+        part = ops.skinny_gemm(h, P["xq"])
+        q = ops.slab_bias_act(part, L["xq_b"])
+        kv = xkv[i]
+        a = ops.attention(q, kv, kv[:, d:], cu_q, n_heads=H, n_kv=H, head_dim=D, causal=False,
+                          max_q=max_q, cu_k=enc_starts, ctx_lens=enc_lens, grouped=True,
+                          split_keys=split_keys, num_splits=enc_splits, workspace=ws)
+        part = ops.skinny_gemm(a, P["xo"])
+        h = ops.slab_layernorm(part, residual, L["ln2_w"], L["ln2_b"], 1e-5, bias=L["xo_b"])
+        part = ops.skinny_gemm(h, P["fc1"])
+        m = ops.slab_bias_act(part, L["fc1_b"], "gelu")
+        part = ops.skinny_gemm(m, P["fc2"])
+    hf = ops.slab_layernorm(part, residual, w.dec_ln_w, w.dec_ln_b, 1e-5,
+                            bias=w.dec[-1]["fc2_b"], row_idx=logit_idx, write_residual=False)
+    return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
 
 
 def pad_or_trim(audio: np.ndarray, n: int = 480000) -> np.ndarray:

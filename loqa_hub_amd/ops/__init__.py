@@ -191,14 +191,19 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Ten
         assert k.stride(-1) == 1 and v.stride(-1) == 1 and k.stride(0) == v.stride(0)
         blk, max_blocks, kv_stride = 0, 0, k.stride(0)
     part_o = part_ml = None
-    if grouped and paged and (n_heads // n_kv) * max_q <= 32 and split_keys % 32 == 0:
-        # one-wave-per-workgroup decode kernel (attn_decode.hip)
+    if grouped and (n_heads // n_kv) * max_q <= 32 and split_keys % 32 == 0 and \
+            (paged or ctx_lens is not None):
+        # split-key decode kernel (attn_decode.hip): paged cache, or contiguous
+        # rows at per-sequence starts cu_k[b] with lengths ctx_lens[b]
         assert workspace is not None and workspace.max_splits >= num_splits
         assert workspace.max_tokens >= Tq
+        kv_stride = 0 if paged else k.stride(0)
         check(kernels().loqa_attn_decode(
-            ptr(q), q.stride(0), ptr(k), ptr(v), ptr(out), out.stride(0), ptr(cu_q), ptr(ctx_lens),
-            ptr(block_tables), max_blocks, blk, B, max_q, n_heads, n_kv, head_dim, scale, split_keys,
-            num_splits, ptr(workspace.part_o), ptr(workspace.part_ml), Tq, stream_ptr(q)),
+            ptr(q), q.stride(0), ptr(k), ptr(v), kv_stride, None if paged else ptr(cu_k),
+            ptr(out), out.stride(0), ptr(cu_q), ptr(ctx_lens),
+            ptr(block_tables) if paged else None, max_blocks, blk, B, max_q, n_heads, n_kv,
+            head_dim, scale, int(causal), split_keys, num_splits, ptr(workspace.part_o),
+            ptr(workspace.part_ml), Tq, stream_ptr(q)),
             "attn_decode")
         return out
     if grouped:
@@ -312,6 +317,9 @@ def mpad_for(m: int) -> int:
 
 
 _SPLITS: dict[tuple[int, int, int], int] = {}
+# K must be a multiple of S * 128 (4 waves x 32-wide k-steps); 5 and 10 cover
+# Whisper's K = 1280 (= 10 * 128)
+SPLIT_CANDIDATES = (1, 2, 4, 5, 8, 10)
 
 
 def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
@@ -330,7 +338,7 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
             continue
         x = torch.randn(Mpad, K, device=wp.device, dtype=torch.bfloat16)
         best, best_t = 1, float("inf")
-        for s in (1, 2, 4, 8):
+        for s in SPLIT_CANDIDATES:
             if K % (s * 128):
                 continue
             for _ in range(2):
@@ -358,7 +366,7 @@ def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
     rt = 2 if Mpad <= 32 else 4
     tiles = max(1, N // (16 * rt))
     best = 1
-    for s in (1, 2, 4, 8):
+    for s in SPLIT_CANDIDATES:
         if K % (s * 128) != 0:
             continue
         best = s
@@ -419,22 +427,79 @@ def slab_rmsnorm(part: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, ep
 
 def slab_rope_append(part: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor | None,
                      k_cache: torch.Tensor, v_cache: torch.Tensor, slots: torch.Tensor,
-                     n_heads: int, n_kv: int, head_dim: int) -> torch.Tensor:
-    """qkv slabs [S, Mpad, (H+2Hkv)D] -> rotated q [Mpad, H*D] bf16; k/v to cache."""
+                     n_heads: int, n_kv: int, head_dim: int,
+                     bias: torch.Tensor | None = None) -> torch.Tensor:
+    """qkv slabs [S, Mpad, (H+2Hkv)D] (+ optional projection bias) -> rotated q
+    [Mpad, H*D] bf16; k/v to cache (``cos_sin`` None = no rotary embedding)."""
     S, Mpad, N = part.shape
     assert N == (n_heads + 2 * n_kv) * head_dim
     if not _gpu(part):
         return ref.slab_rope_append(part, positions, cos_sin, k_cache, v_cache, slots, n_heads,
-                                    n_kv, head_dim)
+                                    n_kv, head_dim, bias)
     assert slots.dtype == torch.int32 and slots.numel() == Mpad
     assert positions.dtype == torch.int32 and positions.numel() == Mpad
     assert k_cache.is_contiguous() and k_cache.shape[1] == n_kv and k_cache.shape[3] == head_dim
     q = torch.empty(Mpad, n_heads * head_dim, dtype=torch.bfloat16, device=part.device)
     check(kernels().loqa_slab_rope_append(ptr(part), S, Mpad, Mpad, ptr(positions), ptr(cos_sin),
                                           ptr(q), ptr(k_cache), ptr(v_cache), ptr(slots), n_heads,
-                                          n_kv, head_dim, k_cache.shape[2], stream_ptr(part)),
+                                          n_kv, head_dim, k_cache.shape[2], ptr(bias),
+                                          stream_ptr(part)),
           "slab_rope_append")
     return q
+
+
+def slab_layernorm(part: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+                   eps: float, bias: torch.Tensor | None = None,
+                   row_idx: torch.Tensor | None = None, write_residual: bool = True,
+                   out: torch.Tensor | None = None) -> torch.Tensor:
+    """residual[src] += bf16(sum_s part[s, src] + bias); y[i] = layernorm(residual[src])."""
+    S, Mpad, d = part.shape
+    rows = row_idx.numel() if row_idx is not None else Mpad
+    if not _gpu(part):
+        return ref.slab_layernorm(part, residual, w, b, eps, bias, row_idx, write_residual)
+    assert part.dtype == torch.float32 and part.is_contiguous()
+    _bf16_contig(residual, "residual")
+    assert residual.shape[-1] == d and residual.shape[0] >= Mpad
+    if row_idx is not None:
+        assert row_idx.dtype == torch.int64 and row_idx.is_contiguous()
+    if bias is not None:
+        _bf16_contig(bias, "bias")
+        assert bias.numel() == d
+    y = out if out is not None else torch.empty(rows, d, dtype=torch.bfloat16, device=part.device)
+    check(kernels().loqa_slab_layernorm(ptr(part), S, Mpad, ptr(row_idx), rows, ptr(bias),
+                                        ptr(residual), int(write_residual), ptr(w), ptr(b), ptr(y),
+                                        d, eps, stream_ptr(part)), "slab_layernorm")
+    return y
+
+
+def slab_bias_act(part: torch.Tensor, bias: torch.Tensor | None, act: str = "none") -> torch.Tensor:
+    """bf16(act(sum_s part + bias)) [Mpad, N]; act in {"none", "gelu"}."""
+    S, Mpad, N = part.shape
+    a = {"none": 0, "gelu": 1}[act]
+    if not _gpu(part):
+        return ref.slab_bias_act(part, bias, act)
+    if bias is not None:
+        _bf16_contig(bias, "bias")
+        assert bias.numel() == N
+    out = torch.empty(Mpad, N, dtype=torch.bfloat16, device=part.device)
+    check(kernels().loqa_slab_bias_act(ptr(part), S, Mpad, Mpad, N, ptr(bias), a, ptr(out),
+                                       stream_ptr(part)), "slab_bias_act")
+    return out
+
+
+def embed_pos(tokens: torch.Tensor, positions: torch.Tensor, tok_embed: torch.Tensor,
+              pos_embed: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16(tok_embed[tokens] + pos_embed[positions]) [rows, d]."""
+    rows, d = tokens.numel(), tok_embed.shape[1]
+    if not _gpu(tok_embed):
+        return (tok_embed[tokens.long()].float() + pos_embed[positions.long()].float()).to(
+            torch.bfloat16)
+    assert tokens.dtype == torch.int32 and positions.dtype == torch.int32
+    out = out if out is not None else torch.empty(rows, d, dtype=torch.bfloat16,
+                                                  device=tok_embed.device)
+    check(kernels().loqa_embed_pos(ptr(tokens), ptr(positions), ptr(tok_embed), ptr(pos_embed),
+                                   ptr(out), rows, d, stream_ptr(tok_embed)), "embed_pos")
+    return out
 
 
 def slab_silu_mul(part: torch.Tensor) -> torch.Tensor:

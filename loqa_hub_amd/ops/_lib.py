@@ -45,13 +45,18 @@ _KERNEL_SIGS = {
                        c_void_p],
     "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_ll, c_void_p, c_void_p,
-                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
-                         c_int, c_void_p, c_void_p, c_int, c_void_p],
+    "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
+                         c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "loqa_slab_rmsnorm": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                           c_void_p, c_int, c_float, c_void_p],
     "loqa_slab_rope_append": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+                              c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "loqa_slab_layernorm": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                            c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p],
+    "loqa_slab_bias_act": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                           c_void_p],
+    "loqa_embed_pos": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "loqa_slab_silu_mul": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }

@@ -298,10 +298,35 @@ def slab_rmsnorm(part, residual, w, eps, row_idx=None, write_residual=True):
     return y.to(residual.dtype)
 
 
-def slab_rope_append(part, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D):
-    qkv = part.sum(0).to(torch.bfloat16)
+def slab_rope_append(part, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D, bias=None):
+    tot = part.sum(0)
+    if bias is not None:
+        tot = tot + bias.float()
+    qkv = tot.to(torch.bfloat16)
     rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D)
     return qkv[:, : H * D].contiguous()
+
+
+def slab_layernorm(part, residual, w, b, eps, bias=None, row_idx=None, write_residual=True):
+    tot = part.sum(0)
+    if bias is not None:
+        tot = tot + bias.float()
+    tot = tot.to(torch.bfloat16).float()
+    idx = row_idx.long() if row_idx is not None else torch.arange(part.shape[1], device=part.device)
+    s = (tot[idx] + residual[idx].float()).to(residual.dtype)
+    if write_residual:
+        residual[idx] = s
+    return torch.nn.functional.layer_norm(s.float(), (s.shape[-1],), w.float(), b.float(),
+                                          eps).to(residual.dtype)
+
+
+def slab_bias_act(part, bias=None, act="none"):
+    tot = part.sum(0)
+    if bias is not None:
+        tot = tot + bias.float()
+    if act == "gelu":
+        tot = torch.nn.functional.gelu(tot.to(torch.bfloat16).float())
+    return tot.to(torch.bfloat16)
 
 
 def slab_silu_mul(part):

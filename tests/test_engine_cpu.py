@@ -205,3 +205,51 @@ def test_bench_cpu_smoke_dp2_gloo():
                 "--batch-per-gpu", "2"])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 4 and out["queue_success_rate"] == 1.0
+
+
+def test_whisper_fast_decode_matches_eager_cpu():
+    """The skinny-GEMM/slab decode path equals the eager reference decoder
+    (first step with the 4 SOT tokens and a follow-up 1-token step)."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    cfg = whisper_config("test-whisper")
+    utts = make_batch(1, 2, [1, 2])
+    engines = [STTEngine(cfg, torch.device("cpu"), seed=3, max_batch=4, fast_decode=f)
+               for f in (True, False)]
+    outs = []
+    for eng in engines:
+        reqs = [STTRequest(u.pcm) for u in utts]
+        audio, _ = eng.upload(reqs)
+        eng.cross_kv(eng.model.encode(audio))
+        for r in reqs:
+            r.seq_id = eng._next
+            eng._next += 1
+            eng.kv.pool.add_seq(r.seq_id, [])
+        feeds = [list(eng.sot) for _ in reqs]
+        live = [0, 1]
+        B_pad, T_pad = 2, 16
+        res = []
+        for step in range(2):
+            max_q, host = eng._host_meta(reqs, live, feeds, B_pad, T_pad)
+            dev = eng._dev(host)
+            if eng.fast_decode:
+                from loqa_hub_amd.models.whisper import decode_step_fast
+                lg = decode_step_fast(eng.model, dev["tokens"], dev["positions"], dev["slots"],
+                                      dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
+                                      eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"],
+                                      dev["enc_lens"], dev["logit_idx"], eng.ws, eng.self_splits)
+                lg = lg[:2, : cfg.vocab_size].float()
+            else:
+                T = int(host["cu_q"][2])
+                lg = eng.model.decode_step(
+                    dev["tokens"][:T], dev["positions"][:T], dev["slots"][:T], dev["cu_q"][:3],
+                    dev["ctx_lens"][:2], dev["block_tables"][:2], max_q, int(host["ctx_lens"].max()),
+                    eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"][:2], dev["enc_lens"][:2],
+                    dev["logit_idx"][:2], None).float()
+            res.append(lg)
+            feeds = [[11], [12]]
+        outs.append(res)
+    for a, b in zip(*outs):
+        err = (a - b).abs().max().item()
+        assert err <= 2e-2 * b.abs().max().item() + 1e-3, err

@@ -60,3 +60,56 @@ def test_stt_whisper_tiny_gpu():
     assert reqs[0].text == "turn on the lights"
     assert reqs[1].text == "hello there"
     assert reqs[0].rms > 0
+
+
+def _whisper_first_logits(eng, pcms):
+    from loqa_hub_amd.models.whisper import decode_step_fast
+    reqs = [STTRequest(p) for p in pcms]
+    audio, _ = eng.upload(reqs)
+    eng.cross_kv(eng.model.encode(audio))
+    for r in reqs:
+        r.seq_id = eng._next
+        eng._next += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+    feeds = [list(eng.sot) for _ in reqs]
+    live = list(range(len(reqs)))
+    max_q, host = eng._host_meta(reqs, live, feeds, 2, 16)
+    dev = eng._dev(host)
+    if eng.fast_decode:
+        lg = decode_step_fast(eng.model, dev["tokens"], dev["positions"], dev["slots"],
+                              dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q, eng.kv.k,
+                              eng.kv.v, eng.xkv, dev["enc_starts"], dev["enc_lens"],
+                              dev["logit_idx"], eng.ws, eng.self_splits)
+        return lg[:2, : eng.cfg.vocab_size].float()
+    T = int(host["cu_q"][2])
+    return eng.model.decode_step(
+        dev["tokens"][:T], dev["positions"][:T], dev["slots"][:T], dev["cu_q"][:3],
+        dev["ctx_lens"][:2], dev["block_tables"][:2], max_q, int(host["ctx_lens"].max()),
+        eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"][:2], dev["enc_lens"][:2],
+        dev["logit_idx"][:2], eng.ws).float()
+
+
+@pytest.mark.parametrize("name", ["whisper-tiny", "whisper-base"])
+def test_whisper_fast_decode_matches_eager_gpu(name):
+    cfg = whisper_config(name)
+    rng = np.random.default_rng(0)
+    pcms = [(rng.standard_normal(24000) * 3000).astype(np.int16),
+            (rng.standard_normal(40000) * 3000).astype(np.int16)]
+    fast = STTEngine(cfg, "cuda", seed=1, max_batch=4, fast_decode=True)
+    eager = STTEngine(cfg, "cuda", seed=1, max_batch=4, fast_decode=False)
+    a, b = _whisper_first_logits(fast, pcms), _whisper_first_logits(eager, pcms)
+    err = (a - b).abs().max().item()
+    assert err <= 2e-2 * b.abs().max().item() + 1e-3, err
+
+
+def test_whisper_graphs_match_eager_fast():
+    cfg = whisper_config("whisper-tiny")
+    rng = np.random.default_rng(1)
+    pcms = [(rng.standard_normal(n) * 3000).astype(np.int16) for n in (16000, 48000, 30000)]
+    outs = []
+    for graphs in (True, False):
+        e = STTEngine(cfg, "cuda", seed=2, max_batch=4, use_graphs=graphs)
+        reqs = [STTRequest(p, max_new_tokens=12) for p in pcms]
+        e.transcribe(reqs)
+        outs.append([r.tokens for r in reqs])
+    assert outs[0] == outs[1]

@@ -270,6 +270,62 @@ def test_slab_consumers():
     assert _rel(ops.slab_reduce(gu), gu.sum(0)) < 1e-5
 
 
+def test_whisper_slab_consumers():
+    """LayerNorm / bias+GELU / biased KV-append consumers and the embed kernel."""
+    Mpad, d, H, D = 16, 1280, 20, 64
+    part = torch.randn(5, Mpad, d, device=DEV)
+    bias = torch.randn(d, device=DEV).bfloat16()
+    res1 = torch.randn(Mpad, d, device=DEV, dtype=torch.bfloat16)
+    res2 = res1.clone()
+    w, b = torch.randn(d, device=DEV).bfloat16(), torch.randn(d, device=DEV).bfloat16()
+    y1 = ops.slab_layernorm(part, res1, w, b, 1e-5, bias=bias)
+    y2 = ref.slab_layernorm(part, res2, w, b, 1e-5, bias=bias)
+    assert _rel(y1, y2) < 1e-2 and _rel(res1, res2) < 1e-3
+    idx = torch.tensor([4, 2] + [0] * 14, dtype=torch.int64, device=DEV)
+    z1 = ops.slab_layernorm(part, res1, w, b, 1e-5, bias=bias, row_idx=idx, write_residual=False)
+    z2 = ref.slab_layernorm(part, res2, w, b, 1e-5, bias=bias, row_idx=idx, write_residual=False)
+    assert _rel(z1, z2) < 1e-2
+    f = torch.randn(2, Mpad, 5120, device=DEV)
+    fb = torch.randn(5120, device=DEV).bfloat16()
+    assert _rel(ops.slab_bias_act(f, fb, "gelu"), ref.slab_bias_act(f, fb, "gelu")) < 1e-2
+    assert _rel(ops.slab_bias_act(f, fb), ref.slab_bias_act(f, fb)) < 1e-2
+    qkv = torch.randn(2, Mpad, 3 * H * D, device=DEV)
+    qb = torch.randn(3 * H * D, device=DEV).bfloat16()
+    pos = torch.arange(Mpad, dtype=torch.int32, device=DEV)
+    slots = torch.arange(Mpad, dtype=torch.int32, device=DEV)
+    slots[-3:] = -1
+    kc1 = torch.zeros(2, H, 16, D, device=DEV, dtype=torch.bfloat16)
+    vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
+    q1 = ops.slab_rope_append(qkv, pos, None, kc1, vc1, slots, H, H, D, bias=qb)
+    q2 = ref.slab_rope_append(qkv, pos, None, kc2, vc2, slots, H, H, D, bias=qb)
+    assert _rel(q1, q2) < 1e-2 and _rel(kc1, kc2) < 1e-2 and _rel(vc1, vc2) < 1e-2
+    te = torch.randn(1000, d, device=DEV).bfloat16()
+    pe = torch.randn(448, d, device=DEV).bfloat16()
+    tk = torch.randint(0, 1000, (Mpad,), dtype=torch.int32, device=DEV)
+    e = ops.embed_pos(tk, pos, te, pe)
+    assert torch.equal(e, (te[tk.long()].float() + pe[pos.long()].float()).bfloat16())
+
+
+@pytest.mark.parametrize("qlens", [[1, 1, 1], [4, 4, 4]])
+def test_attn_decode_contiguous_cross(qlens):
+    """Split-key decode kernel on contiguous encoder rows (non-causal)."""
+    D, H, T = 64, 20, 1500
+    enc = torch.randn(4 * T, 2 * H * D, device=DEV, dtype=torch.bfloat16)
+    live = [3, 0, 2]
+    cu = torch.tensor(np.concatenate([[0], np.cumsum(qlens)]), dtype=torch.int32, device=DEV)
+    q = torch.randn(16, H * D, device=DEV, dtype=torch.bfloat16)
+    starts = torch.tensor([i * T for i in live], dtype=torch.int32, device=DEV)
+    lens = torch.full((3,), T, dtype=torch.int32, device=DEV)
+    ws = ops.AttnWorkspace(DEV, 64, H, D, 12)
+    o = ops.attention(q, enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D, causal=False,
+                      max_q=max(qlens), cu_k=starts, ctx_lens=lens, grouped=True, split_keys=128,
+                      num_splits=12, workspace=ws)
+    n = int(cu[-1])
+    orf = ref.attention(q[:n], enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D,
+                        causal=False, cu_k=starts, ctx_lens=lens)
+    assert _rel(o[:n], orf) < 2e-2
+
+
 def test_llama_decode_fast_path_matches_generic():
     """forward_decode (skinny GEMM + slab ops) == forward (hipBLASLt + generic ops)."""
     from loqa_hub_amd.engine.llm_engine import LLMEngine
