@@ -26,10 +26,15 @@ __device__ __forceinline__ float16v mfma32d(const bf16x8& a, const bf16x8& b, co
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// The V tiles are dead once the key loop ends, so the merge buffer aliases them:
+// 51 KB (D = 128) instead of 92 KB lets three workgroups share a CU, so a
+// 512-workgroup grid is resident in one round instead of two.
 template <int D>
 struct DecSmem {
-  bf16_t v[DEC_WAVES][DEC_TILE][D + 32];          // per-wave V tile (padded rows)
-  float o[DEC_WAVES - 1][D / 32][16][64];          // O^T partials of waves 1..3
+  union {
+    bf16_t v[DEC_WAVES][DEC_TILE][D + 32];        // per-wave V tile (padded rows)
+    float o[DEC_WAVES - 1][D / 32][16][64];        // O^T partials of waves 1..3
+  };
   float ml[DEC_WAVES][2][64];                      // (m, l) per wave per lane
 };
 
@@ -59,6 +64,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int qpos = klen - qlen + qi;
   const int kbeg = split * split_keys;
   const int kend = min(klen, kbeg + split_keys);
+  // splits past the context contribute nothing: leave before any load (the
+  // combine only reads the first ceil(klen / split_keys) splits). The grid is
+  // sized for the longest context a captured graph can see, so most of these
+  // workgroups would otherwise occupy a CU for a full pass.
+  if (split > 0 && kbeg >= klen) return;
   const bool paged = block_tables != nullptr;
   const int* bt = paged ? block_tables + (size_t)b * max_blocks : nullptr;
   const size_t kv0 = paged ? 0 : (size_t)kv_start[b];
@@ -181,7 +191,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     __builtin_amdgcn_wave_barrier();
   }
 
-  // ---- merge the 4 waves' online-softmax states through LDS
+  // ---- merge the 4 waves' online-softmax states through LDS (o aliases v: every
+  // wave must be done reading its V tile before any wave writes its O^T)
+  __syncthreads();
   sm.ml[wave][0][lane] = m_run;
   sm.ml[wave][1][lane] = l_run;
   if (wave > 0) {
@@ -229,12 +241,19 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 }
 
 // combine split partials (one workgroup of D threads per (token, head)); a
-// single split is a plain normalisation.
+// single split is a plain normalisation. Only the splits that hold keys of the
+// token's sequence were written (ceil(ctx / split_keys), at least one).
 __global__ void attn_decode_combine_kernel(const float* __restrict__ part_o,
                                            const float* __restrict__ part_ml, bf16_t* __restrict__ o,
                                            long long o_stride, int total_q, int Hq, int D,
-                                           int num_splits) {
+                                           int num_splits, const int* __restrict__ cu_q,
+                                           const int* __restrict__ ctx_lens, int B,
+                                           int split_keys) {
   const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
+  int b = 0;
+  while (b < B - 1 && cu_q[b + 1] <= tok) ++b;
+  if (tok >= cu_q[B]) return;  // padding row
+  num_splits = min(num_splits, max(1, (ctx_lens[b] + split_keys - 1) / split_keys));
   float mstar = -1e30f;
   for (int s = 0; s < num_splits; ++s)
     mstar = fmaxf(mstar, part_ml[(((size_t)s * total_q + tok) * Hq + head) * 2]);
@@ -278,6 +297,7 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(total_q, Hq), dim3(D), 0, s, part_o, part_ml,
-                     (bf16_t*)o, o_stride, total_q, Hq, D, num_splits);
+                     (bf16_t*)o, o_stride, total_q, Hq, D, num_splits, cu_q, ctx_lens, B,
+                     split_keys);
   return (int)hipGetLastError();
 }

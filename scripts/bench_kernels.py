@@ -36,6 +36,33 @@ def timeit(fn, reps=50, warm=5):
     return ts[len(ts) // 2]
 
 
+def gtime(fn, inner=20, reps=10):
+    """Per-call time of ``fn`` replayed from a captured HIP graph of ``inner``
+    back-to-back calls (in-graph cost: no host launch overhead)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(inner):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / inner)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def emit(**kw):
     print(json.dumps(kw), flush=True)
     fout.write(json.dumps(kw) + "\n")
@@ -85,6 +112,71 @@ def attn_bench():
                  TBps=round(gb / t * 1e3, 2))
 
 
+def attn2_bench():
+    """In-graph decode attention at the engine's shapes."""
+    H, Hkv, D, blk = 32, 8, 128, 16
+    for B, ctx, qlen in ((8, 500, 1), (8, 500, 4), (8, 900, 1)):
+        nb = (1024 + blk - 1) // blk
+        kc = torch.randn(B * nb, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(B * nb, dtype=torch.int32, device=dev).view(B, -1)
+        Tq = B * qlen
+        q = torch.randn(max(16, Tq), H * D, device=dev, dtype=torch.bfloat16)
+        cu = torch.arange(0, Tq + 1, qlen, dtype=torch.int32, device=dev)
+        cl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        ws = ops.AttnWorkspace(dev, 256, H, D, 32)
+        gb = 2 * B * ctx * Hkv * D * 2 / 1e9
+        for sk, ns in ((128, 8), (128, (ctx + 127) // 128), (256, 4), (64, 16)):
+            t = gtime(lambda: ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D,
+                                            causal=True, max_q=qlen, ctx_lens=cl, block_tables=bt,
+                                            grouped=True, split_keys=sk, num_splits=ns,
+                                            workspace=ws))
+            emit(kernel="decode_attn_graph", B=B, ctx=ctx, qlen=qlen, split_keys=sk, splits=ns,
+                 us=round(t, 2), TBps=round(gb / t * 1e3, 2))
+    # whisper-large cross-attention (contiguous encoder rows) and self-attention
+    Hw, Dw, T = 20, 64, 1500
+    B = 8
+    enc = torch.randn(B * T, 2 * Hw * Dw, device=dev, dtype=torch.bfloat16)
+    q = torch.randn(16, Hw * Dw, device=dev, dtype=torch.bfloat16)
+    cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
+    starts = torch.arange(0, B * T, T, dtype=torch.int32, device=dev)
+    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+    ws = ops.AttnWorkspace(dev, 256, Hw, Dw, 32)
+    for sk in (128, 256):
+        ns = (T + sk - 1) // sk
+        t = gtime(lambda: ops.attention(q, enc, enc[:, Hw * Dw:], cu, n_heads=Hw, n_kv=Hw,
+                                        head_dim=Dw, causal=False, max_q=1, cu_k=starts,
+                                        ctx_lens=lens, grouped=True, split_keys=sk, num_splits=ns,
+                                        workspace=ws))
+        emit(kernel="whisper_cross_graph", B=B, split_keys=sk, splits=ns, us=round(t, 2),
+             TBps=round(2 * B * T * Hw * Dw * 2 / 1e9 / t * 1e3, 2))
+
+
+def tiny_bench():
+    """Floor of a graph-replayed tiny kernel."""
+    x = torch.zeros(16, 4096, device=dev, dtype=torch.bfloat16)
+    emit(kernel="graph_tiny_add", us=round(gtime(lambda: x.add_(1)), 2))
+    part = torch.randn(8, 16, 4096, device=dev)
+    res = torch.randn(16, 4096, device=dev, dtype=torch.bfloat16)
+    w = torch.ones(4096, device=dev, dtype=torch.bfloat16)
+    emit(kernel="graph_slab_rmsnorm_S8", us=round(gtime(lambda: ops.slab_rmsnorm(part, res, w, 1e-5)), 2))
+    gu = torch.randn(8, 16, 2 * 14336, device=dev)
+    emit(kernel="graph_slab_silu_S8", us=round(gtime(lambda: ops.slab_silu_mul(gu)), 2))
+    for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096),
+                         "down": (4096, 14336)}.items():
+        wp = ops.shuffle_weight(torch.randn(N, K, device=dev, dtype=torch.bfloat16))
+        xx = torch.randn(16, K, device=dev, dtype=torch.bfloat16)
+        res = {"kernel": "graph_gemm", "shape": name}
+        for S in (1, 2, 4, 8):
+            if K % (S * 128):
+                continue
+            t = gtime(lambda: ops.skinny_gemm(xx, wp, S), inner=10)
+            res[f"S{S}_us"] = round(t, 2)
+            res[f"S{S}_TBps"] = round(N * K * 2 / 1e9 / t * 1e3, 2)
+        emit(**res)
+        del wp
+
+
 def slab_bench():
     for M, d, S in ((16, 4096, 4), (16, 4096, 2), (32, 4096, 4)):
         part = torch.randn(S, M, d, device=dev)
@@ -100,6 +192,10 @@ def slab_bench():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn", "slab"]
+    if "attn2" in which:
+        attn2_bench()
+    if "tiny" in which:
+        tiny_bench()
     if "gemm" in which:
         gemm_bench()
     if "attn" in which:
