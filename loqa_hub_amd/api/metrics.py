@@ -1,0 +1,49 @@
+"""``/api/metrics``: Prometheus text exposition of the hub's counters (audio
+service arbitration, GPU engines, skills, NATS). The reference exposes no
+metrics endpoint; this is additive."""
+from __future__ import annotations
+
+from aiohttp import web
+
+
+def _line(name: str, value, labels: dict | None = None, help_: str = "") -> str:
+    lab = ""
+    if labels:
+        lab = "{" + ",".join(f'{k}="{v}"' for k, v in sorted(labels.items())) + "}"
+    return f"{name}{lab} {float(value)}"
+
+
+class MetricsHandler:
+    def __init__(self, server):
+        self.server = server
+
+    def routes(self) -> list[web.RouteDef]:
+        return [web.get("/api/metrics", self.metrics)]
+
+    def collect(self) -> list[str]:
+        s = self.server
+        out = []
+        if s.audio_service is not None:
+            for k, v in s.audio_service.stats.items():
+                out.append(_line("loqa_audio_" + k + "_total", v))
+            out.append(_line("loqa_audio_active_streams", len(s.audio_service.active_streams)))
+        if s.skills is not None:
+            out.append(_line("loqa_skills_loaded", len(s.skills.skills)))
+        proc = getattr(s, "processor", None)
+        for k, v in (getattr(proc, "stats", None) or {}).items():
+            out.append(_line("loqa_processor_" + k + "_total", v))
+        pipe = getattr(proc, "pipeline", None)
+        if pipe is not None:
+            for k, v in pipe.llm.stats.items():
+                out.append(_line("loqa_llm_" + k, v))
+            for k, v in pipe.stt.stats.items():
+                out.append(_line("loqa_stt_" + k, v))
+        nats = s.nats.stats() if s.nats is not None and s.nats.conn is not None else None
+        if nats is not None:
+            for k, v in vars(nats).items():
+                out.append(_line("loqa_nats_" + k, v))
+        return out
+
+    async def metrics(self, req: web.Request) -> web.Response:
+        return web.Response(text="\n".join(self.collect()) + "\n",
+                            content_type="text/plain", charset="utf-8")

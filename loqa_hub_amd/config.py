@@ -213,6 +213,7 @@ class ArbitrationConfig:
     end_of_speech_wait: float = 5.0
     bridge_timeout: float = 2.0
     confirmation_enabled: bool = False
+    relay_groups: dict = field(default_factory=dict)  # relay id -> room/group
 
 
 @dataclass
@@ -251,6 +252,16 @@ class Config:
             raise ConfigError(f"invalid ARBITRATION_SCOPE: {self.arbitration.scope}")
         if self.gpu.tp < 1:
             raise ConfigError(f"HUB_TP must be >= 1: {self.gpu.tp}")
+
+
+def parse_relay_groups(s: str) -> dict:
+    """"relay-1=kitchen,relay-2=kitchen" -> {relay id: group}."""
+    out = {}
+    for part in filter(None, (p.strip() for p in s.split(","))):
+        k, sep, v = part.partition("=")
+        if sep and k.strip() and v.strip():
+            out[k.strip()] = v.strip()
+    return out
 
 
 class ConfigError(ValueError):
@@ -343,6 +354,7 @@ def load(env=None) -> Config:
             end_of_speech_wait=env_duration(e, 5.0, "ARBITRATION_EOS_WAIT"),
             bridge_timeout=env_duration(e, 2.0, "BRIDGE_TIMEOUT"),
             confirmation_enabled=env_bool(e, False, "CONFIRMATION_ENABLED"),
+            relay_groups=parse_relay_groups(env_str(e, "", "ARBITRATION_RELAY_GROUPS")),
         ),
     )
     try:

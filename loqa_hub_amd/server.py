@@ -1,0 +1,163 @@
+"""Hub composition root (``internal/server/server.go``).
+
+Builds: SQLite database -> voice-events store -> HTTP API; NATS service (and
+the embedded broker when ``NATS_URL`` is ``embedded``); skill manager with the
+builtin skills plus ``./skills`` auto-load; the voice processor (GPU pipeline
+or external services) behind the gRPC ``AudioService``; streaming components
+when enabled. Serves HTTP (``/health`` -> ``ok\\n`` (:137-142),
+``/api/voice-events[/…]``, ``/api/skills[/…]``, ``/api/streaming/*``,
+``/api/metrics``) and gRPC ``audio.AudioService/StreamAudio`` on
+``cfg.server.grpc_port`` (:98-125). Deliberate differences from the reference:
+the skills and streaming APIs are routed (the reference leaves them unrouted,
+SURVEY C11), and every service reads the one config object.
+
+GPU engines are built lazily by ``build_gpu_processor`` so a CPU-only hub
+(config 1) never imports the HIP path.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+
+from aiohttp import web
+
+from .api.metrics import MetricsHandler
+from .api.skills import SkillsHandler
+from .api.streaming import StreamingHandler
+from .api.voice_events import VoiceEventsHandler
+from .config import Config
+from .messaging.audio_stream_publisher import AudioStreamPublisher
+from .messaging.nats_service import NATSService
+from .skills import DefaultSkillLoader, SkillManager, SkillManagerConfig
+from .skills.builtin.lights import LightsSkill
+from .storage.database import Database
+from .storage.voice_events_store import VoiceEventsStore
+from .transport.audio_service import AudioService
+
+log = logging.getLogger("loqa.server")
+
+
+def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None):
+    """On-device STT -> constrained intent decode -> queue (one GPU)."""
+    from .engine.llm_engine import LLMEngine
+    from .engine.pipeline import VoicePipeline
+    from .engine.stt_engine import STTEngine
+    from .models.configs import llama_config, whisper_config
+    from .transport.voice_processor import GPUVoiceProcessor
+    g = cfg.gpu
+    stt = STTEngine(whisper_config(g.stt_model), device, seed=g.seed, max_batch=g.max_batch,
+                    use_graphs=g.use_graphs)
+    llm = LLMEngine(llama_config(g.llm_model), device, seed=g.seed, max_seqs=g.max_batch,
+                    max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs)
+    pipe = VoicePipeline(stt, llm, nats)
+    return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64))
+
+
+async def build_service_processor(cfg: Config, nats, tts=None):
+    """Reference path: external STT + Ollama parser (+ TTS)."""
+    from .llm.command_parser import CommandParser, OllamaBackend
+    from .llm.stt_client import STTClient
+    from .transport.voice_processor import ServiceVoiceProcessor
+    stt = STTClient(cfg.stt.url, cfg.stt.language)
+    parser = CommandParser(OllamaBackend(cfg.ollama.url, cfg.ollama.model))
+    return ServiceVoiceProcessor(stt, parser, nats=nats, tts=tts)
+
+
+class HubServer:
+    def __init__(self, cfg: Config, *, processor=None, nats: NATSService | None = None,
+                 streaming=None, skills_dir: str = "./skills",
+                 skills_config_store: str = "./data/skills"):
+        self.cfg = cfg
+        self.database = Database(cfg.server.db_path)
+        self.events = VoiceEventsStore(self.database)
+        self.nats = nats
+        self.processor = processor
+        self.streaming = streaming
+        self.skills = SkillManager(SkillManagerConfig(skills_dir=skills_dir,
+                                                      config_store=skills_config_store),
+                                   DefaultSkillLoader(skills_root=skills_dir))
+        self.audio_service: AudioService | None = None
+        self.grpc_server = None
+        self.http_runner: web.AppRunner | None = None
+        self.http_port = 0
+        self.grpc_port = 0
+        self._embedded_broker = None
+
+    # ------------------------------------------------------------------ wiring
+    def app(self) -> web.Application:
+        app = web.Application()
+        app.router.add_get("/health", self.handle_health)
+        app.add_routes(VoiceEventsHandler(self.events).routes())
+        app.add_routes(SkillsHandler(self.skills).routes())
+        app.add_routes(StreamingHandler(self.streaming).routes())
+        app.add_routes(MetricsHandler(self).routes())
+        return app
+
+    async def handle_health(self, req: web.Request) -> web.Response:
+        log.info("Health check received")
+        return web.Response(text="ok\n", content_type="text/plain")
+
+    async def _connect_nats(self) -> None:
+        url = self.cfg.nats.url
+        if self.nats is None:
+            if url == "embedded":
+                from .messaging.nats_server import NATSServer
+                self._embedded_broker = await NATSServer().start()
+                url = self._embedded_broker.url
+            self.nats = NATSService(url, self.cfg.nats.reconnect_wait)
+        if not self.nats.is_connected():
+            try:
+                await self.nats.connect()
+            except Exception as e:  # noqa: BLE001 - hub keeps serving without the bus
+                log.warning("Cannot connect to NATS: %s (events will not be published)", e)
+
+    async def start(self, host: str | None = None, http_port: int | None = None,
+                    grpc_port: int | None = None) -> None:
+        import grpc
+
+        from .transport.audio_proto import add_audio_service
+        await self._connect_nats()
+        await self.skills.register_plugin(LightsSkill())
+        await self.skills.start()
+        publisher = AudioStreamPublisher(self.nats.conn) if self.nats and self.nats.conn else None
+        a = self.cfg.arbitration
+        self.audio_service = AudioService(
+            self.processor, window_duration=a.window, scope=a.scope, relay_groups=a.relay_groups,
+            end_of_speech_wait=a.end_of_speech_wait, events_store=self.events,
+            audio_publisher=publisher, confirmation_enabled=a.confirmation_enabled)
+        host = host if host is not None else self.cfg.server.host
+        self.grpc_server = grpc.aio.server()
+        add_audio_service(self.grpc_server, self.audio_service)
+        gport = self.cfg.server.grpc_port if grpc_port is None else grpc_port
+        self.grpc_port = self.grpc_server.add_insecure_port(f"{host}:{gport}")
+        await self.grpc_server.start()
+        log.info("gRPC server listening on :%d", self.grpc_port)
+        self.http_runner = web.AppRunner(self.app())
+        await self.http_runner.setup()
+        site = web.TCPSite(self.http_runner, host,
+                           self.cfg.server.port if http_port is None else http_port)
+        await site.start()
+        self.http_port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        log.info("HTTP server listening on :%d", self.http_port)
+
+    async def stop(self) -> None:
+        if self.grpc_server is not None:
+            await self.grpc_server.stop(1.0)
+        if self.http_runner is not None:
+            await self.http_runner.cleanup()
+        await self.skills.stop()
+        if self.streaming is not None:
+            await self.streaming.shutdown()
+        if self.nats is not None:
+            await self.nats.close()
+        if self._embedded_broker is not None:
+            await self._embedded_broker.stop()
+        self.database.close()
+
+    async def serve_forever(self) -> None:
+        await self.start()
+        try:
+            while True:
+                await asyncio.sleep(3600)
+        finally:
+            await self.stop()
