@@ -1,0 +1,116 @@
+"""On-GPU text-to-speech engine (VITS) behind the ``TextToSpeech`` contract
+(``internal/llm/tts.go``), replacing the external OpenAI-compatible TTS.
+
+Concurrent ``synthesize`` calls (the progressive pipeline's phrase workers of
+every live session) are micro-batched into one padded VITS forward; each
+result is returned as a WAV (PCM16 mono, 22 050 Hz) or raw PCM. ``speed`` maps
+to the duration length scale (1 / speed), as in the reference's request body.
+"""
+from __future__ import annotations
+
+import asyncio
+import io
+import struct
+import threading
+
+import numpy as np
+import torch
+
+from ..llm.tts import TTSOptions, TTSResult
+from ..models.configs import VitsConfig
+from ..models.vits import VitsModel, VitsWeights, text_to_ids
+
+
+def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
+    data = np.ascontiguousarray(pcm, dtype="<i2").tobytes()
+    hdr = b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE"
+    hdr += b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, sample_rate, sample_rate * 2, 2, 16)
+    return hdr + b"data" + struct.pack("<I", len(data)) + data
+
+
+class VitsTTSEngine:
+    def __init__(self, cfg: VitsConfig, device, *, seed: int = 0, batch_window: float = 0.003,
+                 max_batch: int = 32):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.model = VitsModel(VitsWeights(cfg, self.device, seed=seed))
+        self.batch_window = batch_window
+        self.max_batch = max_batch
+        self._pending: list[tuple[str, float, asyncio.Future]] = []
+        self._flusher: asyncio.Task | None = None
+        self._gpu_lock = threading.Lock()
+        self._seed = seed
+        self.stats = {"batches": 0, "phrases": 0, "samples": 0}
+
+    # ---------------------------------------------------------------- batch
+    def synthesize_batch(self, texts: list[str], speeds: list[float] | None = None
+                         ) -> list[np.ndarray]:
+        """Synchronous batched synthesis -> PCM16 arrays."""
+        speeds = speeds or [1.0] * len(texts)
+        ids = [text_to_ids(t, self.cfg.n_symbols) for t in texts]
+        T = max(len(i) for i in ids)
+        arr = np.zeros((len(ids), T), np.int64)
+        for b, i in enumerate(ids):
+            arr[b, :len(i)] = i
+        lens = torch.tensor([len(i) for i in ids], dtype=torch.int32, device=self.device)
+        # one length scale per batch (the engine groups by speed upstream)
+        ls = 1.0 / max(1e-3, float(np.mean(speeds)))
+        with self._gpu_lock, torch.inference_mode():
+            self._seed += 1
+            pcm, n = self.model.synthesize(torch.from_numpy(arr).to(self.device), lens,
+                                           seed=self._seed, length_scale=ls)
+            pcm, n = pcm.cpu().numpy(), n.cpu().numpy()
+        self.stats["batches"] += 1
+        self.stats["phrases"] += len(texts)
+        self.stats["samples"] += int(n.sum())
+        return [pcm[b, : int(n[b])].copy() for b in range(len(texts))]
+
+    # ------------------------------------------------------ TextToSpeech API
+    async def synthesize(self, text: str, options: TTSOptions | None = None) -> TTSResult:
+        if not text:
+            raise ValueError("text cannot be empty")
+        speed = options.speed if options and options.speed > 0 else 1.0
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._pending.append((text, speed, fut))
+        if len(self._pending) >= self.max_batch or self._flusher is None or self._flusher.done():
+            self._flusher = loop.create_task(self._flush())
+        pcm = await fut
+        fmt = (options.response_format if options and options.response_format else "wav")
+        if fmt == "pcm":
+            data, ctype = pcm.astype("<i2").tobytes(), "audio/pcm"
+        else:
+            data, ctype = pcm16_to_wav(pcm, self.cfg.sample_rate), "audio/wav"
+        return TTSResult(data, ctype, len(data), self.cfg.sample_rate)
+
+    async def _flush(self) -> None:
+        await asyncio.sleep(self.batch_window)
+        while self._pending:
+            batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
+            try:
+                outs = await asyncio.get_running_loop().run_in_executor(
+                    None, self.synthesize_batch, [t for t, _, _ in batch], [s for _, s, _ in batch])
+            except Exception as e:  # noqa: BLE001
+                for *_, f in batch:
+                    if not f.done():
+                        f.set_exception(e)
+                continue
+            for (_, _, f), pcm in zip(batch, outs):
+                if not f.done():
+                    f.set_result(pcm)
+
+    async def get_available_voices(self) -> list[str]:
+        return [self.cfg.name]
+
+    async def close(self) -> None:
+        return None
+
+
+def wav_info(data: bytes) -> tuple[int, int]:
+    """(sample_rate, n_samples) of a PCM16 WAV produced by ``pcm16_to_wav``."""
+    f = io.BytesIO(data)
+    f.seek(24)
+    sr = struct.unpack("<I", f.read(4))[0]
+    f.seek(40)
+    n = struct.unpack("<I", f.read(4))[0] // 2
+    return sr, n

@@ -102,7 +102,7 @@ class VitsConfig:
 VITS_CONFIGS = {
     "vits-ljs": VitsConfig("vits-ljs"),
     "test-vits": VitsConfig("test-vits", hidden=64, filter_channels=128, enc_layers=2, flow_layers=2,
-                            wn_layers=2, inter_channels=64, upsample_initial=64),
+                            wn_layers=2, inter_channels=64, upsample_initial=256),
 }
 
 

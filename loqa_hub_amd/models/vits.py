@@ -1,0 +1,214 @@
+"""VITS text-to-speech (text encoder + duration predictor + reverse flow +
+HiFi-GAN generator) on the MI355X path, replacing the reference's external
+OpenAI-compatible TTS round trip (``openai_tts_client.go:101-224``).
+
+Layout: every activation is a channels-last bf16 [B, T, C] row tensor, so each
+convolution is the MFMA implicit-GEMM kernel of ``conv1d.hip`` with its fused
+epilogues:
+  text encoder   1x1 QKV conv -> windowed relative-position attention (tts.hip)
+                 -> 1x1 out conv (+residual) -> LayerNorm -> FFN (k3 convs,
+                 ReLU fused) (+residual) -> LayerNorm, x6; 1x1 projection to
+                 (m_p, logs_p)
+  durations      deterministic VITS duration predictor (k3 conv + ReLU + LN, x2,
+                 1x1 -> log w); random-init weights give arbitrary durations,
+                 so they are clamped to [1, 12] frames per symbol
+  prior sample   length regulation fused with z_p = m_p + eps exp(logs_p) * 0.667
+  flow (reverse) 4 mean-only coupling layers: 1x1 pre conv, WaveNet (k5 conv
+                 with the fused gate tanh(a)*sigmoid(b), 1x1 res/skip convs with
+                 fused residual / skip accumulation), 1x1 post conv fused with
+                 x1 <- x1 - m, channel flip
+  decoder        conv_pre k7 -> [leaky-ReLU + ConvTranspose1d (polyphase MFMA)
+                 -> MRF: 3 ResBlock1 (k 3/7/11, dilations 1/3/5; leaky-ReLU
+                 fused on the A operand, residual fused, the 1/3 average fused as
+                 scale+accumulate)] x4 (rates 8,8,2,2) -> leaky-ReLU + conv_post k7
+                 + tanh -> PCM16 written by the conv epilogue
+Sample rate 22 050 Hz, hop 256.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from .configs import VitsConfig
+
+SYMBOLS = ("_;:,.!?¡¿—…\"«»“” " + "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz"
+           + "ɑɐɒæɓʙβɔɕçɗɖðʤəɘɚɛɜɝɞɟʄɡɠɢʛɦɧħɥʜɨɪʝɭɬɫɮʟɱɯɰŋɳɲɴøɵɸθœɶʘɹɺɾɻʀʁɽʂʃʈʧʉʊʋⱱʌɣɤʍχʎʏʑʐʒʔʡʕʢǀǁǂǃˈˌːˑʼʴʰʱʲʷˠˤ˞↓↑→↗↘'̩'ᵻ")
+
+
+def text_to_ids(text: str, n_symbols: int) -> list[int]:
+    """Character-level symbol ids with VITS's blank interspersing (id 0)."""
+    table = {c: i for i, c in enumerate(SYMBOLS[:n_symbols])}
+    ids = [table.get(c, table[" "]) for c in text]
+    out = [0]
+    for i in ids:
+        out += [i, 0]
+    return out
+
+
+def _rnd(g, device, *shape, std=0.02):
+    t = torch.empty(*shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=g)
+    return t.to(torch.bfloat16)
+
+
+class VitsWeights:
+    def __init__(self, cfg: VitsConfig, device, seed: int = 0):
+        self.cfg = cfg
+        dev = torch.device(device)
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 7919 + 11)
+        H, F, C = cfg.hidden, cfg.filter_channels, cfg.inter_channels
+        zeros = lambda n: torch.zeros(n, dtype=torch.bfloat16, device=dev)  # noqa: E731
+        ones = lambda n: torch.ones(n, dtype=torch.bfloat16, device=dev)   # noqa: E731
+        # fan-in scaled random init keeps activations O(1) through the deep
+        # stacks (a fixed small std would make the random-init waveform vanish)
+        conv = lambda co, ci, k, std=None, gated=False: ops.ConvWeight(  # noqa: E731
+            _rnd(g, dev, co, ci, k, std=(ci * k) ** -0.5 if std is None else std), zeros(co),
+            gated=gated)
+        self.emb = _rnd(g, dev, cfg.n_symbols, H, std=H ** -0.5)
+        dh = H // cfg.n_heads
+        self.enc = []
+        for _ in range(cfg.enc_layers):
+            self.enc.append({
+                "qkv": conv(3 * H, H, 1), "o": conv(H, H, 1),
+                "emb_k": _rnd(g, dev, 2 * cfg.window + 1, dh, std=dh ** -0.5),
+                "emb_v": _rnd(g, dev, 2 * cfg.window + 1, dh, std=dh ** -0.5),
+                "ln1_w": ones(H), "ln1_b": zeros(H),
+                "ffn1": conv(F, H, cfg.kernel_size), "ffn2": conv(H, F, cfg.kernel_size),
+                "ln2_w": ones(H), "ln2_b": zeros(H)})
+        self.proj = conv(2 * C, H, 1)
+        Fd = 256 if H >= 192 else H
+        self.dp = {"c1": conv(Fd, H, 3), "ln1_w": ones(Fd), "ln1_b": zeros(Fd),
+                   "c2": conv(Fd, Fd, 3), "ln2_w": ones(Fd), "ln2_b": zeros(Fd),
+                   "proj": conv(1, Fd, 1)}
+        half = C // 2
+        self.flows = []
+        for _ in range(cfg.flow_layers):
+            wn = []
+            for i in range(cfg.wn_layers):
+                last = i == cfg.wn_layers - 1
+                wn.append({"in": conv(2 * H, H, 5, gated=True),
+                           "res": None if last else conv(H, H, 1),
+                           "skip": conv(H, H, 1)})
+            self.flows.append({"pre": conv(H, half, 1), "wn": wn,
+                               "post": conv(half, H, 1, std=0.0)})   # VITS zero-inits post
+        U = cfg.upsample_initial
+        self.conv_pre = conv(U, C, 7)
+        self.ups, self.res = [], []
+        ch = U
+        for i, r in enumerate(cfg.upsample_rates):
+            k = 2 * r if r > 2 else 4
+            co = ch // 2
+            self.ups.append(ops.ConvTransposeWeight(_rnd(g, dev, ch, co, k, std=(ch * k / r) ** -0.5),
+                                                    zeros(co),
+                                                    r, (k - r) // 2))
+            blocks = []
+            for ks, dils in zip(cfg.resblock_kernels, cfg.resblock_dilations):
+                blocks.append([(conv(co, co, ks), conv(co, co, ks), d) for d in dils])
+            self.res.append(blocks)
+            ch = co
+        self.conv_post = ops.ConvWeight(_rnd(g, dev, 1, ch, 7, std=(ch * 7) ** -0.5), None)
+        self.last_channels = ch
+
+
+class VitsModel:
+    NOISE_SCALE = 0.667
+    MAX_FRAMES_PER_SYMBOL = 12
+
+    def __init__(self, w: VitsWeights):
+        self.w = w
+        self.cfg = w.cfg
+
+    # ------------------------------------------------------------------ text
+    def encode_text(self, ids: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        """ids [B, T] int64 -> stats [B, T, 2C] (m_p | logs_p)."""
+        cfg, w = self.cfg, self.w
+        H = cfg.hidden
+        dh = H // cfg.n_heads
+        x = (w.emb[ids].float() * math.sqrt(H)).to(torch.bfloat16)
+        T = ids.shape[1]
+        mask = (torch.arange(T, device=ids.device)[None, :] < lens[:, None].long())[..., None]
+        x = (x * mask).contiguous()
+        for L in w.enc:
+            qkv = ops.conv1d(x, L["qkv"], lens=lens)
+            a = ops.relpos_attention(qkv, L["emb_k"], L["emb_v"], lens, cfg.n_heads, dh,
+                                     cfg.window)
+            y = ops.conv1d(a, L["o"], res=x, lens=lens)                       # x + attn
+            x = ops.layernorm(y.view(-1, H), L["ln1_w"], L["ln1_b"], 1e-5).view_as(y)
+            f = ops.conv1d(x, L["ffn1"], act="relu", lens=lens)
+            y = ops.conv1d(f, L["ffn2"], res=x, lens=lens)
+            x = ops.layernorm(y.view(-1, H), L["ln2_w"], L["ln2_b"], 1e-5).view_as(y)
+            x = (x * mask).contiguous()
+        return ops.conv1d(x, w.proj, lens=lens), x
+
+    def durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale: float = 1.0
+                  ) -> torch.Tensor:
+        d = self.w.dp
+        Fd = d["c1"].Cout
+        h = ops.conv1d(x, d["c1"], act="relu", lens=lens)
+        h = ops.layernorm(h.view(-1, Fd), d["ln1_w"], d["ln1_b"], 1e-5).view_as(h)
+        h = ops.conv1d(h, d["c2"], act="relu", lens=lens)
+        h = ops.layernorm(h.view(-1, Fd), d["ln2_w"], d["ln2_b"], 1e-5).view_as(h)
+        logw = ops.conv1d(h, d["proj"], lens=lens)[..., 0].float()
+        dur = torch.ceil(torch.exp(logw) * length_scale)
+        dur = dur.clamp(1, self.MAX_FRAMES_PER_SYMBOL)
+        T = x.shape[1]
+        valid = torch.arange(T, device=x.device)[None, :] < lens[:, None].long()
+        return (dur * valid).to(torch.int32)
+
+    # ------------------------------------------------------------------ flow
+    def flow_reverse(self, z: torch.Tensor, flen: torch.Tensor) -> torch.Tensor:
+        cfg, w = self.cfg, self.w
+        half = cfg.inter_channels // 2
+        for fl in reversed(w.flows):
+            z = z.flip(-1).contiguous()          # Flip (its own inverse)
+            x0, x1 = z[..., :half], z[..., half:]
+            h = ops.conv1d(x0, fl["pre"], lens=flen)
+            skip = None
+            for layer in fl["wn"]:
+                acts = ops.conv1d(h, layer["in"], act="gated", lens=flen)
+                skip = ops.conv1d(acts, layer["skip"], acc=skip, lens=flen)   # skip += conv
+                if layer["res"] is not None:
+                    h = ops.conv1d(acts, layer["res"], res=h, lens=flen)      # h += conv
+            # mean-only coupling, reverse: x1 <- x1 - post(skip), written in place
+            ops.conv1d(skip, fl["post"], alpha=-1.0, acc=x1, out=x1, lens=flen)
+        return z
+
+    # --------------------------------------------------------------- decoder
+    def decode(self, z: torch.Tensor, pcm_lens: torch.Tensor | None = None) -> torch.Tensor:
+        """z [B, F, C] -> PCM16 [B, F * hop]."""
+        w, cfg = self.w, self.cfg
+        x = ops.conv1d(z, w.conv_pre)
+        for i, ct in enumerate(w.ups):
+            x = ops.conv_transpose1d(x, ct, pre_slope=0.1)
+            xs = None
+            nb = len(w.res[i])
+            for blocks in w.res[i]:
+                xb = x
+                for j, (c1, c2, d) in enumerate(blocks):
+                    t = ops.conv1d(xb, c1, dil=d, pre_slope=0.1)
+                    if j < len(blocks) - 1:
+                        xb = ops.conv1d(t, c2, pre_slope=0.1, res=xb)
+                    else:  # last pair of the block: xs += (conv + xb) / nb
+                        xs = ops.conv1d(t, c2, pre_slope=0.1, res=xb, alpha=1.0 / nb, acc=xs,
+                                        out=xs)
+            x = xs
+        pcm = ops.conv1d(x, w.conv_post, pre_slope=0.01, act="tanh", pcm16=True, lens=pcm_lens)
+        return pcm[..., 0]
+
+    # ---------------------------------------------------------------- full
+    def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
+                   length_scale: float = 1.0) -> tuple[torch.Tensor, torch.Tensor]:
+        """ids [B, T] -> (PCM16 [B, S], samples per utterance [B])."""
+        stats, x = self.encode_text(ids, lens)
+        dur = self.durations(x, lens, length_scale)
+        cum = torch.cumsum(dur, dim=1, dtype=torch.int32)
+        flen = cum[:, -1].contiguous()
+        F = int(flen.max().item())
+        z = ops.expand_sample(stats, cum.contiguous(), flen, F, self.NOISE_SCALE, seed)
+        z = self.flow_reverse(z, flen)
+        hop = int(math.prod(self.cfg.upsample_rates))
+        pcm = self.decode(z, (flen * hop).to(torch.int32))
+        return pcm, flen * hop

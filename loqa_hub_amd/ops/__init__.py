@@ -523,3 +523,171 @@ def slab_reduce(part: torch.Tensor) -> torch.Tensor:
     check(kernels().loqa_slab_reduce(ptr(part), S, Mpad, Mpad, N, ptr(out), stream_ptr(part)),
           "slab_reduce")
     return out
+
+
+# ------------------------------------------------------------- VITS / HiFi-GAN
+class ConvWeight:
+    """A conv1d weight prepared for the MFMA implicit-GEMM kernel: [Cout_pad, K,
+    Cin] bf16 (Cout padded to 32; gated convs interleave the tanh / sigmoid
+    halves in 16-channel blocks). Keeps the torch-layout copy for the CPU path."""
+
+    def __init__(self, w: torch.Tensor, bias: torch.Tensor | None = None, gated: bool = False):
+        self.w, self.bias, self.gated = w, bias, gated      # w [Cout, Cin, K]
+        Cout, Cin, K = w.shape
+        self.Cout, self.Cin, self.K = Cout, Cin, K
+        assert Cin % 16 == 0, "input channels must be a multiple of 16"
+        perm = torch.arange(Cout, device=w.device)
+        if gated:
+            Hh = Cout // 2
+            assert Hh % 16 == 0
+            blocks = []
+            for q in range(Hh // 16):
+                blocks += [torch.arange(16 * q, 16 * q + 16), torch.arange(Hh + 16 * q, Hh + 16 * q + 16)]
+            perm = torch.cat(blocks).to(w.device)
+        cpad = (Cout + 31) // 32 * 32
+        wp = torch.zeros(cpad, K, Cin, dtype=torch.bfloat16, device=w.device)
+        wp[:Cout] = w[perm].permute(0, 2, 1).to(torch.bfloat16)
+        self.wp = wp.contiguous()
+        self.bp = None
+        if bias is not None:
+            bp = torch.zeros(cpad, dtype=torch.bfloat16, device=w.device)
+            bp[:Cout] = bias[perm].to(torch.bfloat16)
+            self.bp = bp
+        self.cpad = cpad
+
+    @property
+    def out_channels(self) -> int:
+        return self.Cout // 2 if self.gated else self.Cout
+
+
+def conv1d(x: torch.Tensor, cw: ConvWeight, *, dil: int = 1, pad: int | None = None,
+           stride: int = 1, pre_slope: float | None = None, act: str | None = None,
+           res: torch.Tensor | None = None, alpha: float = 1.0, acc: torch.Tensor | None = None,
+           lens: torch.Tensor | None = None, out: torch.Tensor | None = None,
+           pcm16: bool = False, Tout: int | None = None, ostride: int = 1, ophase: int = 0,
+           Tq: int | None = None) -> torch.Tensor:
+    """Channels-last conv1d [B, Tin, Cin] -> [B, Tout, Cout'] with fused
+    pre-activation (leaky ReLU), bias, act (relu / tanh / gated), residual add,
+    scale, accumulate and length mask (see conv1d.hip). ``pad`` defaults to
+    'same'. ``res``/``acc``/``out`` may be strided views; ``acc`` may alias ``out``."""
+    B, Tin, Cin = x.shape
+    assert Cin == cw.Cin
+    if pad is None:
+        pad = dil * (cw.K - 1) // 2
+    if Tq is None:
+        Tq = (Tin + 2 * pad - dil * (cw.K - 1) - 1) // stride + 1
+    T_out = Tout if Tout is not None else Tq * ostride + ophase
+    Co = cw.out_channels
+    act_id = {None: 0, "relu": 1, "tanh": 2, "gated": 3}[act]
+    assert (act == "gated") == cw.gated
+    if not _gpu(x):
+        y = ref.conv1d(x, cw.w, cw.bias, dil=dil, pad=pad, stride=stride, pre_slope=pre_slope,
+                       act=act, res=res, alpha=alpha, acc=acc, lens=lens, Tout=T_out,
+                       ostride=ostride, ophase=ophase, Tq=Tq)
+        if pcm16:
+            y = (y.clamp(-1, 1) * 32767).round().to(torch.int16)
+        else:
+            y = y.to(torch.bfloat16)
+        if out is not None:
+            if ostride == 1 and ophase == 0 and Tq == T_out:
+                out.copy_(y)
+            else:  # polyphase: only this phase's rows
+                q = torch.arange(Tq, device=x.device) * ostride + ophase
+                q = q[(q >= 0) & (q < T_out)]
+                out[:, q] = y[:, q]
+            return out
+        return y
+    assert x.dtype == torch.bfloat16 and x.stride(-1) == 1
+    dt = torch.int16 if pcm16 else torch.bfloat16
+    if out is None:
+        out = torch.empty(B, T_out, Co, dtype=dt, device=x.device)
+    assert out.dtype == dt and out.stride(-1) == 1 and out.shape[1] == T_out
+
+    def bs(t):
+        return (0, 0) if t is None else (t.stride(0), t.stride(1))
+    for t in (res, acc):
+        if t is not None:
+            assert t.dtype == torch.bfloat16 and t.stride(-1) == 1 and t.shape[1] >= T_out
+    if lens is not None:
+        assert lens.dtype == torch.int32 and lens.numel() == B
+    check(kernels().loqa_conv1d(
+        ptr(x), x.stride(0), x.stride(1), ptr(cw.wp), ptr(cw.bp), ptr(out), out.stride(0),
+        out.stride(1), ptr(res), *bs(res), ptr(acc), *bs(acc), ptr(lens), B, Tin, Cin, Tq,
+        cw.cpad, cw.K, dil, pad, stride, ostride, ophase, T_out,
+        0 if pre_slope is None else 1, float(pre_slope or 0.0), act_id, float(alpha), int(pcm16),
+        Co, stream_ptr(x)), "conv1d")
+    return out
+
+
+class ConvTransposeWeight:
+    """ConvTranspose1d(kernel Kt = 2s-style, stride s) as s polyphase convs:
+    y[q*s + r - p] = sum_j x[q - j] w[:, :, r + j*s]."""
+
+    def __init__(self, w: torch.Tensor, bias: torch.Tensor | None, stride: int, padding: int):
+        Cin, Cout, Kt = w.shape
+        assert Kt % stride == 0
+        self.w, self.bias, self.stride, self.padding = w, bias, stride, padding
+        self.taps = Kt // stride
+        self.phases = []
+        for r in range(stride):
+            # tap kk of the regular conv reads x[q - (taps-1) + kk] with weight w[r + (taps-1-kk)*s]
+            ks = [r + (self.taps - 1 - kk) * stride for kk in range(self.taps)]
+            wr = w[:, :, ks].permute(1, 0, 2).contiguous()  # [Cout, Cin, taps]
+            self.phases.append(ConvWeight(wr, bias))
+        self.Cout = Cout
+
+    def out_len(self, Tin: int) -> int:
+        return (Tin - 1) * self.stride - 2 * self.padding + self.taps * self.stride
+
+
+def conv_transpose1d(x: torch.Tensor, ct: ConvTransposeWeight, *,
+                     pre_slope: float | None = None, polyphase: bool | None = None) -> torch.Tensor:
+    """ConvTranspose1d on channels-last rows; on the GPU always as polyphase
+    MFMA convolutions (``polyphase=True`` forces that decomposition on the CPU
+    too, for testing)."""
+    B, Tin, _ = x.shape
+    T_out = ct.out_len(Tin)
+    s, p = ct.stride, ct.padding
+    if not _gpu(x) and not polyphase:
+        return ref.conv_transpose1d(x, ct.w, ct.bias, stride=s, padding=p,
+                                    pre_slope=pre_slope).to(torch.bfloat16)
+    out = torch.zeros(B, T_out, ct.Cout, dtype=torch.bfloat16, device=x.device)
+    for r, cw in enumerate(ct.phases):
+        Tq = (T_out - r + p + s - 1) // s
+        conv1d(x, cw, dil=1, pad=ct.taps - 1, stride=1, pre_slope=pre_slope, out=out, Tout=T_out,
+               ostride=s, ophase=r - p, Tq=Tq)
+    return out
+
+
+def relpos_attention(qkv: torch.Tensor, emb_k: torch.Tensor, emb_v: torch.Tensor,
+                     lens: torch.Tensor | None, n_heads: int, head_dim: int, window: int,
+                     scale: float | None = None) -> torch.Tensor:
+    """VITS windowed relative-position self-attention over q|k|v rows [B, T, 3C]."""
+    B, T, _ = qkv.shape
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    if not _gpu(qkv):
+        return ref.relpos_attention(qkv, emb_k, emb_v, lens, n_heads, head_dim, window,
+                                    scale).to(torch.bfloat16)
+    assert qkv.dtype == torch.bfloat16 and qkv.stride(-1) == 1
+    out = torch.empty(B, T, n_heads * head_dim, dtype=torch.bfloat16, device=qkv.device)
+    check(kernels().loqa_relpos_attention(ptr(qkv), qkv.stride(1), ptr(emb_k), ptr(emb_v),
+                                          ptr(lens), ptr(out), out.stride(1), B, T, n_heads,
+                                          head_dim, window, scale, stream_ptr(qkv)),
+          "relpos_attention")
+    return out
+
+
+def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F: int,
+                  noise_scale: float, seed: int = 0) -> torch.Tensor:
+    """Length regulation + prior sampling: [B, T, 2C] stats -> z_p [B, F, C] bf16."""
+    B, T, C2 = stats.shape
+    if not _gpu(stats):
+        g = torch.Generator().manual_seed(seed)
+        noise = torch.randn(B, F, C2 // 2, generator=g)
+        return ref.expand_sample(stats, cum, flen, F, noise_scale, noise).to(torch.bfloat16)
+    assert cum.dtype == torch.int32 and flen.dtype == torch.int32
+    z = torch.empty(B, F, C2 // 2, dtype=torch.bfloat16, device=stats.device)
+    check(kernels().loqa_expand_sample(ptr(stats), stats.stride(1), ptr(cum), B, T, ptr(flen),
+                                       ptr(z), F, C2 // 2, float(noise_scale), seed & 0xFFFFFFFF,
+                                       stream_ptr(stats)), "expand_sample")
+    return z

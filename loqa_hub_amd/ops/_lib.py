@@ -57,6 +57,14 @@ _KERNEL_SIGS = {
     "loqa_slab_bias_act": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                            c_void_p],
     "loqa_embed_pos": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "loqa_conv1d": [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p,
+                    c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
+                    c_float, c_int, c_int, c_void_p],
+    "loqa_relpos_attention": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                              c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "loqa_expand_sample": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                           c_int, c_float, ctypes.c_uint, c_void_p],
     "loqa_slab_silu_mul": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }

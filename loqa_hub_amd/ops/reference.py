@@ -331,3 +331,102 @@ def slab_bias_act(part, bias=None, act="none"):
 
 def slab_silu_mul(part):
     return silu_mul(part.sum(0).to(torch.bfloat16))
+
+
+# ------------------------------------------------------------------ VITS / HiFi-GAN
+def conv1d(x, w, bias=None, *, dil=1, pad=0, stride=1, pre_slope=None, act=None, res=None,
+           alpha=1.0, acc=None, lens=None, Tout=None, ostride=1, ophase=0, Tq=None):
+    """Reference of loqa_conv1d: x [B, Tin, Cin] (channels-last), w [Cout, Cin, K]
+    (torch layout) -> y [B, Tout, Cout'] following the kernel's epilogue order.
+    Returns float32 (callers round)."""
+    B, Tin, Cin = x.shape
+    xf = x.float()
+    if pre_slope is not None:
+        xf = torch.nn.functional.leaky_relu(xf, pre_slope)
+    xf = xf.to(torch.bfloat16).float()  # the kernel feeds bf16 operands to the MFMA
+    y = torch.nn.functional.conv1d(xf.transpose(1, 2), w.float(), None, stride=stride, padding=pad,
+                                   dilation=dil).transpose(1, 2)
+    if Tq is not None:
+        y = y[:, :Tq]
+    if bias is not None:
+        y = y + bias.float()
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "tanh":
+        y = torch.tanh(y)
+    elif act == "gated":
+        Hh = y.shape[-1] // 2
+        a, g = y[..., :Hh].to(torch.bfloat16).float(), y[..., Hh:].to(torch.bfloat16).float()
+        y = torch.tanh(a) * torch.sigmoid(g)
+    T_out = Tout if Tout is not None else y.shape[1] * ostride + ophase
+    full = torch.zeros(B, T_out, y.shape[-1], dtype=torch.float32, device=x.device)
+    q = torch.arange(y.shape[1], device=x.device)
+    oi = q * ostride + ophase
+    ok = (oi >= 0) & (oi < T_out)
+    full[:, oi[ok]] = y[:, q[ok]]
+    idx = oi[ok]
+    if res is not None:
+        full[:, idx] += res[:, idx].float()
+    full[:, idx] *= alpha
+    if acc is not None:
+        full[:, idx] += acc[:, idx].float()
+    if lens is not None:
+        t = torch.arange(T_out, device=x.device)
+        full = full * (t[None, :] < lens[:, None].to(x.device)).float()[..., None]
+    return full
+
+
+def conv_transpose1d(x, w, bias=None, *, stride, padding, pre_slope=None):
+    """torch ConvTranspose1d on channels-last x; w [Cin, Cout, K] torch layout."""
+    xf = x.float()
+    if pre_slope is not None:
+        xf = torch.nn.functional.leaky_relu(xf, pre_slope)
+    xf = xf.to(torch.bfloat16).float()
+    y = torch.nn.functional.conv_transpose1d(xf.transpose(1, 2), w.float(),
+                                             None if bias is None else bias.float(),
+                                             stride=stride, padding=padding)
+    return y.transpose(1, 2)
+
+
+def relpos_attention(qkv, emb_k, emb_v, lens, H, D, window, scale):
+    B, T, _ = qkv.shape
+    C = H * D
+    q = qkv[..., :C].float().view(B, T, H, D).transpose(1, 2) * scale
+    k = qkv[..., C:2 * C].float().view(B, T, H, D).transpose(1, 2)
+    v = qkv[..., 2 * C:3 * C].float().view(B, T, H, D).transpose(1, 2)
+    s = q @ k.transpose(-1, -2)
+    idx = torch.arange(T, device=qkv.device)
+    rel = idx[None, :] - idx[:, None]
+    inwin = rel.abs() <= window
+    ek = emb_k.float()
+    rl = torch.einsum("bhid,rd->bhir", q, ek)  # [B,H,T,2w+1]
+    ridx = (rel + window).clamp(0, 2 * window)
+    s = s + torch.where(inwin, rl.gather(-1, ridx[None, None].expand(B, H, T, T)),
+                        torch.zeros((), device=qkv.device))
+    L = lens.to(qkv.device) if lens is not None else torch.full((B,), T, device=qkv.device)
+    valid = idx[None, :] < L[:, None]
+    m = valid[:, None, :, None] & valid[:, None, None, :]
+    s = s.masked_fill(~m, -1e4)
+    p = torch.softmax(s, -1)
+    o = p @ v
+    pw = torch.where(inwin, p, torch.zeros((), device=qkv.device))
+    pr = torch.zeros(B, H, T, 2 * window + 1, device=qkv.device)
+    pr.scatter_add_(-1, ridx[None, None].expand(B, H, T, T), pw)
+    o = o + pr @ emb_v.float()
+    o = o * valid[:, None, :, None]
+    return o.transpose(1, 2).reshape(B, T, C)
+
+
+def expand_sample(stats, cum, flen, F, noise_scale, noise=None):
+    """z[b, f] = m[i(f)] + noise * exp(logs[i(f)]) * noise_scale."""
+    B, T, C2 = stats.shape
+    C = C2 // 2
+    z = torch.zeros(B, F, C, device=stats.device)
+    for b in range(B):
+        n = int(flen[b])
+        f = torch.arange(n, device=stats.device)
+        i = torch.searchsorted(cum[b].to(stats.device), f, right=True)
+        m, lg = stats[b, i, :C].float(), stats[b, i, C:].float()
+        e = noise[b, :n].float() if noise is not None else torch.zeros_like(m)
+        z[b, :n] = m + e * torch.exp(lg) * noise_scale
+    return z

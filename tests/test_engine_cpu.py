@@ -253,3 +253,35 @@ def test_whisper_fast_decode_matches_eager_cpu():
     for a, b in zip(*outs):
         err = (a - b).abs().max().item()
         assert err <= 2e-2 * b.abs().max().item() + 1e-3, err
+
+
+def test_vits_tts_cpu():
+    import asyncio
+    from loqa_hub_amd.engine.tts_engine import VitsTTSEngine, wav_info
+    from loqa_hub_amd.llm.tts import TTSOptions
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    e = VitsTTSEngine(VITS_CONFIGS["test-vits"], "cpu")
+    outs = e.synthesize_batch(["Turning on the lights.", "Hi!"])
+    assert outs[0].size % 256 == 0 and outs[0].size > outs[1].size
+    assert np.abs(outs[0].astype(np.float32)).mean() > 100
+
+    async def go():
+        r1, r2 = await asyncio.gather(e.synthesize("hello"), e.synthesize("world", TTSOptions(
+            speed=2.0, response_format="pcm")))
+        assert r1.content_type == "audio/wav" and wav_info(r1.audio)[0] == 22050
+        assert r2.content_type == "audio/pcm" and len(r2.audio) % 2 == 0
+    asyncio.run(go())
+    assert e.stats["batches"] >= 2
+
+
+def test_conv_transpose_polyphase_cpu():
+    from loqa_hub_amd import ops
+    torch.manual_seed(0)
+    for Cin, Cout, K, s in ((64, 32, 16, 8), (32, 32, 4, 2)):
+        p = (K - s) // 2
+        w, b = torch.randn(Cin, Cout, K) * 0.1, torch.randn(Cout) * 0.1
+        x = torch.randn(2, 13, Cin).bfloat16()
+        ct = ops.ConvTransposeWeight(w, b, s, p)
+        y1 = ops.conv_transpose1d(x, ct, pre_slope=0.1, polyphase=True).float()
+        y2 = R.conv_transpose1d(x, w, b, stride=s, padding=p, pre_slope=0.1)
+        assert y1.shape == y2.shape and (y1 - y2).abs().max() <= 0.02 * y2.abs().max()

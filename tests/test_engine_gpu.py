@@ -113,3 +113,13 @@ def test_whisper_graphs_match_eager_fast():
         e.transcribe(reqs)
         outs.append([r.tokens for r in reqs])
     assert outs[0] == outs[1]
+
+
+def test_vits_tts_gpu():
+    from loqa_hub_amd.engine.tts_engine import VitsTTSEngine
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    e = VitsTTSEngine(VITS_CONFIGS["vits-ljs"], "cuda")
+    outs = e.synthesize_batch(["Turning on the kitchen lights.", "Done."])
+    assert len(outs) == 2 and outs[0].dtype == np.int16
+    assert outs[0].size % 256 == 0 and outs[0].size > outs[1].size > 0
+    assert np.abs(outs[0].astype(np.float32)).mean() > 100

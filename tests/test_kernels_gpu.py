@@ -354,3 +354,68 @@ def test_llama_decode_fast_path_matches_generic():
             lg = eng.model.logits(eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws))
         outs.append(lg.float())
     assert _rel(outs[0], outs[1]) < 3e-2
+
+
+# ------------------------------------------------------------------ VITS kernels
+@pytest.mark.parametrize("Cin,Cout,K,dil,act,pre", [(192, 192, 5, 1, None, None), (64, 32, 7, 3, "relu", 0.1),
+                                                   (512, 256, 3, 1, "tanh", None), (32, 1, 7, 1, "tanh", 0.01),
+                                                   (192, 384, 5, 1, "gated", None)])
+def test_conv1d_mfma(Cin, Cout, K, dil, act, pre):
+    B, T = 2, 300
+    w = torch.randn(Cout, Cin, K, device=DEV) * (Cin * K) ** -0.5
+    b = torch.randn(Cout, device=DEV) * 0.1
+    cw = ops.ConvWeight(w, b, gated=act == "gated")
+    x = torch.randn(B, T, Cin, device=DEV).bfloat16()
+    res = torch.randn(B, T, cw.out_channels, device=DEV).bfloat16()
+    lens = torch.tensor([T, 211], dtype=torch.int32, device=DEV)
+    y = ops.conv1d(x, cw, dil=dil, pre_slope=pre, act=act, res=res, alpha=0.5, lens=lens)
+    yr = ref.conv1d(x, w, b, dil=dil, pad=dil * (K - 1) // 2, pre_slope=pre, act=act, res=res,
+                    alpha=0.5, lens=lens)
+    assert _rel(y, yr) < 1e-2
+
+
+def test_conv1d_accumulate_inplace_and_pcm16():
+    B, T, C = 1, 513, 64
+    cw = ops.ConvWeight(torch.randn(C, C, 3, device=DEV) * 0.1, torch.zeros(C, device=DEV))
+    x = torch.randn(B, T, C, device=DEV).bfloat16()
+    acc = torch.randn(B, T, C, device=DEV).bfloat16()
+    expect = ref.conv1d(x, cw.w, cw.bias, pad=1, alpha=1 / 3, acc=acc)
+    out = ops.conv1d(x, cw, alpha=1 / 3, acc=acc, out=acc)
+    assert out.data_ptr() == acc.data_ptr() and _rel(acc, expect) < 1e-2
+    post = ops.ConvWeight(torch.randn(1, C, 7, device=DEV) * 0.05, None)
+    pcm = ops.conv1d(x, post, pre_slope=0.01, act="tanh", pcm16=True)
+    pr = ref.conv1d(x, post.w, None, pad=3, pre_slope=0.01, act="tanh")
+    assert pcm.dtype == torch.int16
+    assert (pcm.float() - (pr.clamp(-1, 1) * 32767).round()).abs().max() <= 400
+
+
+@pytest.mark.parametrize("Cin,Cout,K,s", [(512, 256, 16, 8), (64, 32, 4, 2)])
+def test_conv_transpose_polyphase(Cin, Cout, K, s):
+    w = torch.randn(Cin, Cout, K, device=DEV) * (Cin * K / s) ** -0.5
+    b = torch.randn(Cout, device=DEV) * 0.1
+    ct = ops.ConvTransposeWeight(w, b, s, (K - s) // 2)
+    x = torch.randn(2, 57, Cin, device=DEV).bfloat16()
+    y = ops.conv_transpose1d(x, ct, pre_slope=0.1)
+    yr = ref.conv_transpose1d(x, w, b, stride=s, padding=(K - s) // 2, pre_slope=0.1)
+    assert y.shape == yr.shape and _rel(y, yr) < 1e-2
+
+
+def test_relpos_attention_and_expand():
+    B, T, H, D, W = 2, 77, 2, 96, 4
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV).bfloat16()
+    ek = torch.randn(2 * W + 1, D, device=DEV).bfloat16() * 0.1
+    ev = torch.randn(2 * W + 1, D, device=DEV).bfloat16() * 0.1
+    lens = torch.tensor([T, 50], dtype=torch.int32, device=DEV)
+    o = ops.relpos_attention(qkv, ek, ev, lens, H, D, W)
+    orf = ref.relpos_attention(qkv, ek, ev, lens, H, D, W, 1 / math.sqrt(D))
+    assert _rel(o, orf) < 1e-2
+    stats = torch.randn(B, T, 2 * 64, device=DEV).bfloat16() * 0.5
+    dur = torch.randint(1, 6, (B, T), device=DEV, dtype=torch.int32)
+    dur[1, 50:] = 0
+    cum = torch.cumsum(dur, 1, dtype=torch.int32)
+    flen = cum[:, -1].contiguous()
+    F = int(flen.max())
+    z = ops.expand_sample(stats, cum, flen, F, 0.0)
+    assert _rel(z, ref.expand_sample(stats, cum, flen, F, 0.0)) < 1e-2
+    zn = ops.expand_sample(torch.zeros_like(stats), cum, flen, F, 1.0, seed=7)[0].float()
+    assert abs(zn.mean().item()) < 0.05 and abs(zn.std().item() - 1.0) < 0.05
