@@ -64,11 +64,12 @@ class LLMEngine:
 
     def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
-                 tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192):
+                 tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192,
+                 weights: LlamaWeights | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.tp = tp or TPGroup()
-        self.weights = LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
+        self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
         self.model = LlamaModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
         self.grammar = GrammarTables(self.tok, self.device)

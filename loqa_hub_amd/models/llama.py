@@ -107,6 +107,43 @@ class LlamaWeights:
                 ops.tune_skinny_splits(self.decode_layers[0][k])
             ops.tune_skinny_splits(self.lm_head_p)
 
+    @classmethod
+    def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":
+        """Tensor-parallel shard ``tp.rank`` of an unsharded model (Megatron
+        split: column-parallel QKV / gate|up / vocab, row-parallel O / down), so
+        a TP group computes exactly what the single-GPU model computes."""
+        cfg = full.cfg
+        assert full.tp.world == 1
+        self = cls.__new__(cls)
+        self.cfg, self.tp = cfg, tp
+        self.h, self.hkv = cfg.n_heads // tp.world, cfg.n_kv_heads // tp.world
+        self.f, self.v = cfg.ffn_dim // tp.world, cfg.vocab_size // tp.world
+        r, D = tp.rank, cfg.head_dim
+        H, Hkv, F = cfg.n_heads, cfg.n_kv_heads, cfg.ffn_dim
+        qs, ks = slice(r * self.h * D, (r + 1) * self.h * D), slice(r * self.hkv * D, (r + 1) * self.hkv * D)
+        fs, vs = slice(r * self.f, (r + 1) * self.f), slice(r * self.v, (r + 1) * self.v)
+        self.embed = full.embed[vs].contiguous()
+        self.layers = []
+        for L in full.layers:
+            w = L["wqkv"]
+            q, k, v = w[: H * D], w[H * D:(H + Hkv) * D], w[(H + Hkv) * D:]
+            gu = L["w_gate_up"]
+            self.layers.append({
+                "attn_norm": L["attn_norm"],
+                "wqkv": torch.cat([q[qs], k[ks], v[ks]]).contiguous(),
+                "wo": L["wo"][:, qs].contiguous(),
+                "mlp_norm": L["mlp_norm"],
+                "w_gate_up": torch.cat([gu[:F][fs], gu[F:][fs]]).contiguous(),
+                "w_down": L["w_down"][:, fs].contiguous()})
+        self.final_norm = full.final_norm
+        self.lm_head = self.embed if cfg.tie_embeddings else full.lm_head[vs].contiguous()
+        self.cos_sin = full.cos_sin
+        self.decode_layers = [{k: ops.shuffle_weight(L[k])
+                               for k in ("wqkv", "wo", "w_gate_up", "w_down")}
+                              for L in self.layers]
+        self.lm_head_p = ops.shuffle_weight(self.lm_head)
+        return self
+
     def nbytes(self) -> int:
         n = self.embed.numel() + (0 if self.cfg.tie_embeddings else self.lm_head.numel())
         for L in self.layers:

@@ -69,6 +69,17 @@ _KERNEL_SIGS = {
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
 }
 
+# (argtypes, restype) of the custom all-reduce entry points (in the kernels library)
+_CAR_SIGS = {
+    "loqa_car_create": ([c_int, c_int, c_ll], c_void_p),
+    "loqa_car_handle": ([c_void_p, c_void_p], c_int),
+    "loqa_car_handle_size": ([], c_int),
+    "loqa_car_open": ([c_void_p, c_void_p], c_int),
+    "loqa_car_allreduce": ([c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p], c_int),
+    "loqa_car_error": ([c_void_p], c_int),
+    "loqa_car_destroy": ([c_void_p], None),
+}
+
 _RUNTIME_SIGS = {
     "loqa_stager_create": ([c_int, c_ll], c_void_p),
     "loqa_stager_destroy": ([c_void_p], None),
@@ -112,6 +123,10 @@ def kernels() -> ctypes.CDLL:
                     f = getattr(lib, fn)
                     f.argtypes = sig
                     f.restype = c_int
+                for fn, (args, res) in _CAR_SIGS.items():
+                    f = getattr(lib, fn)
+                    f.argtypes = args
+                    f.restype = res
                 _kernels = lib
     return _kernels
 

@@ -1,0 +1,91 @@
+"""Tensor parallelism on the CPU over gloo: a TP=2 group built
+from shards of one model computes the same logits and the same constrained
+decode as the single-process model (column-parallel QKV / gate|up / vocab,
+row-parallel O / down with all-reduce, vocab-parallel masked argmax)."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _prompt_reqs(eng):
+    from loqa_hub_amd.engine.grammar import multi_command_schema
+    from loqa_hub_amd.engine.llm_engine import GenRequest
+    return [GenRequest(eng.tok.encode(f"voice command {i}: turn on the lights", bos=True),
+                       multi_command_schema(n, min_response_tokens=2)) for i, n in enumerate((1, 2))]
+
+
+def _logits(eng):
+    """One prefill forward over a fixed token batch -> full-vocab logits."""
+    import numpy as np
+
+    from loqa_hub_amd.engine.llm_engine import GenRequest
+    reqs = [GenRequest(list(range(5, 25)), []), GenRequest(list(range(40, 52)), [])]
+    for r in reqs:
+        r.seq_id = eng._next_id
+        eng._next_id += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+    feeds = [r.prompt for r in reqs]
+    max_q, max_ctx, host = eng._meta(reqs, feeds, decode=False)
+    dev = eng._to_device(host)
+    meta = eng._build_meta(dev, max_q, max_ctx, False)
+    hid = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws)
+    local = eng.model.logits(hid).float()
+    if eng.tp.world == 1:
+        return local
+    parts = [torch.empty_like(local) for _ in range(eng.tp.world)]
+    dist.all_gather(parts, local, group=eng.tp.group)
+    return torch.cat(parts, dim=1)
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from loqa_hub_amd.engine.llm_engine import LLMEngine
+        from loqa_hub_amd.models.configs import llama_config
+        from loqa_hub_amd.models.llama import LlamaWeights, TPGroup
+        cfg = llama_config("test-tiny")
+        full = LlamaWeights(cfg, "cpu", seed=5)
+        tp = TPGroup(rank, world, dist.group.WORLD)
+        eng = LLMEngine(cfg, "cpu", max_seqs=4, max_seq_len=256, tp=tp,
+                        weights=LlamaWeights.shard(full, tp))
+        lg = _logits(eng)
+        outs = [r.output for r in eng.generate(_prompt_reqs(eng))]
+        if rank == 0:
+            torch.save(lg, os.path.join(out_dir, "tp_logits.pt"))
+            with open(os.path.join(out_dir, "tp_out.json"), "w") as f:
+                json.dump(outs, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_tp_matches_single(tmp_path, world):
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import LlamaWeights
+    cfg = llama_config("test-tiny")
+    single = LLMEngine(cfg, "cpu", max_seqs=4, max_seq_len=256,
+                       weights=LlamaWeights(cfg, "cpu", seed=5))
+    ref_logits = _logits(single)
+    ref_out = [r.output for r in single.generate(_prompt_reqs(single))]
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    tp_logits = torch.load(tmp_path / "tp_logits.pt", weights_only=True)
+    err = (tp_logits - ref_logits).abs().max().item()
+    assert err <= 0.03 * ref_logits.abs().max().item() + 1e-3, err
+    assert (tp_logits.argmax(-1) == ref_logits.argmax(-1)).float().mean() >= 0.9
+    tp_out = json.load(open(tmp_path / "tp_out.json"))
+    for a, b in zip(tp_out, ref_out):
+        assert len(json.loads(a)["commands"]) == len(json.loads(b)["commands"])
