@@ -47,6 +47,18 @@ class TPGroup:
         self.rank, self.world, self.group = rank, world, group
         self._allreduce = allreduce
 
+    @classmethod
+    def create(cls, rank: int, world: int, group=None, device=None,
+               custom_allreduce: bool = True) -> "TPGroup":
+        """TP group; on GPUs the decode/prefill all-reduces use the one-shot IPC
+        kernel (parallel/custom_allreduce.py) with RCCL as the fallback."""
+        ar = None
+        if world > 1 and custom_allreduce and device is not None and \
+                torch.device(device).type == "cuda":
+            from ..parallel.custom_allreduce import CustomAllReduce
+            ar = CustomAllReduce(group)
+        return cls(rank, world, group, ar)
+
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return x
