@@ -100,18 +100,28 @@ class LLMEngine:
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
-              B_pad: int | None = None, T_pad: int | None = None) -> tuple[StepMeta, dict]:
+              B_pad: int | None = None, T_pad: int | None = None,
+              out: dict | None = None) -> tuple[StepMeta, dict]:
+        """Host metadata of one step; ``out`` = preallocated (pinned) numpy views
+        to fill in place (the graph path: one H2D copy per step, no allocation)."""
         B = len(seqs)
         T = sum(len(f) for f in feeds)
         B_pad = B_pad or B
         T_pad = T_pad or T
-        tokens = np.zeros(T_pad, np.int32)
-        positions = np.zeros(T_pad, np.int32)
-        slots = np.full(T_pad, -1, np.int32)
-        cu = np.zeros(B_pad + 1, np.int32)
-        ctx = np.zeros(B_pad, np.int32)
-        bt = np.zeros((B_pad, self.max_blocks), np.int32)
-        lidx = np.zeros(max(16, B_pad) if decode else B_pad, np.int64)
+        if out is not None:
+            tokens, positions, slots = out["tokens"], out["positions"], out["slots"]
+            cu, ctx, bt, lidx = out["cu_q"], out["ctx_lens"], out["block_tables"], out["logit_idx"]
+            for a in (tokens, positions, cu, ctx, bt, lidx):
+                a.fill(0)
+            slots.fill(-1)
+        else:
+            tokens = np.zeros(T_pad, np.int32)
+            positions = np.zeros(T_pad, np.int32)
+            slots = np.full(T_pad, -1, np.int32)
+            cu = np.zeros(B_pad + 1, np.int32)
+            ctx = np.zeros(B_pad, np.int32)
+            bt = np.zeros((B_pad, self.max_blocks), np.int32)
+            lidx = np.zeros(max(16, B_pad) if decode else B_pad, np.int64)
         off = 0
         max_q = 1
         max_ctx = 1
@@ -191,16 +201,26 @@ class LLMEngine:
         g = self._graphs.get(key)
         if g is not None:
             return g
-        dev = {
-            "tokens": torch.zeros(T_pad, dtype=torch.int32, device=self.device),
-            "positions": torch.zeros(T_pad, dtype=torch.int32, device=self.device),
-            "slots": torch.full((T_pad,), -1, dtype=torch.int32, device=self.device),
-            "cu_q": torch.zeros(B_pad + 1, dtype=torch.int32, device=self.device),
-            "ctx_lens": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
-            "block_tables": torch.zeros(B_pad, self.max_blocks, dtype=torch.int32, device=self.device),
-            "logit_idx": torch.zeros(max(16, B_pad), dtype=torch.int64, device=self.device),
-            "mask_rows": torch.zeros(B_pad, dtype=torch.int32, device=self.device),
-        }
+        # all int32 metadata lives in ONE device buffer (one H2D copy per step)
+        # mirrored by ONE pinned host buffer; logit_idx (int64) has its own pair
+        shapes = {"tokens": (T_pad,), "positions": (T_pad,), "slots": (T_pad,),
+                  "cu_q": (B_pad + 1,), "ctx_lens": (B_pad,),
+                  "block_tables": (B_pad, self.max_blocks), "mask_rows": (B_pad,)}
+        n32 = sum(int(np.prod(v)) for v in shapes.values())
+        L = max(16, B_pad)
+        d32 = torch.zeros(n32, dtype=torch.int32, device=self.device)
+        h32 = torch.zeros(n32, dtype=torch.int32).pin_memory()
+        d64 = torch.zeros(L, dtype=torch.int64, device=self.device)
+        h64 = torch.zeros(L, dtype=torch.int64).pin_memory()
+        dev, host, off = {}, {}, 0
+        hn = h32.numpy()
+        for k, shp in shapes.items():
+            n = int(np.prod(shp))
+            dev[k] = d32[off:off + n].view(*shp)
+            host[k] = hn[off:off + n].reshape(shp)
+            off += n
+        dev["slots"].fill_(-1)
+        dev["logit_idx"], host["logit_idx"] = d64, h64.numpy()
         meta = self._build_meta(dev, self.max_decode_q, self.max_seq_len, True)
         # warm up (allocator + kernels) on a side stream, then capture
         s = torch.cuda.Stream(self.device)
@@ -211,7 +231,8 @@ class LLMEngine:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = self._forward_sample(meta, dev["mask_rows"])
-        g = {"graph": graph, "dev": dev, "out": out}
+        g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
+             "h64": h64, "d64": d64}
         self._graphs[key] = g
         return g
 
@@ -296,11 +317,12 @@ class LLMEngine:
             B_pad = _bucket(B, self.SEQ_BUCKETS)
             T_pad = ops.mpad_for(T)
             g = self._decode_graph(B_pad, T_pad)
-            max_q, max_ctx, host = self._meta(live, feeds, True, B_pad, T_pad)
-            mr = np.zeros(B_pad, np.int32)
-            mr[:B] = rows
-            host["mask_rows"] = mr
-            self._to_device(host, g["dev"])
+            hb = g["host"]
+            self._meta(live, feeds, True, B_pad, T_pad, out=hb)
+            hb["mask_rows"].fill(0)
+            hb["mask_rows"][:B] = rows
+            g["d32"].copy_(g["h32"], non_blocking=True)
+            g["d64"].copy_(g["h64"], non_blocking=True)
             g["graph"].replay()
             nxt = g["out"][:B].cpu().numpy()
         else:

@@ -125,17 +125,26 @@ class STTEngine:
             torch.addmm(L["xkv_b"], enc, L["xkv"].t(), out=buf[:rows])
         return self.xkv
 
-    def _host_meta(self, reqs, live, feeds, B_pad: int, T_pad: int) -> tuple[int, dict]:
+    def _host_meta(self, reqs, live, feeds, B_pad: int, T_pad: int,
+                   out: dict | None = None) -> tuple[int, dict]:
         T_enc = self.cfg.n_audio_ctx
-        tokens = np.zeros(T_pad, np.int32)
-        positions = np.zeros(T_pad, np.int32)
-        slots = np.full(T_pad, -1, np.int32)
-        cu = np.zeros(B_pad + 1, np.int32)
-        ctx = np.zeros(B_pad, np.int32)
-        bt = np.zeros((B_pad, self.max_blocks), np.int32)
-        enc_starts = np.zeros(B_pad, np.int32)
-        enc_lens = np.zeros(B_pad, np.int32)
-        lidx = np.zeros(max(16, ops.mpad_for(B_pad)), np.int64)
+        L = max(16, ops.mpad_for(B_pad))
+        if out is not None:  # preallocated pinned views (graph path)
+            for k, a in out.items():
+                a.fill(-1 if k == "slots" else 0)
+            tokens, positions, slots = out["tokens"], out["positions"], out["slots"]
+            cu, ctx, bt = out["cu_q"], out["ctx_lens"], out["block_tables"]
+            enc_starts, enc_lens, lidx = out["enc_starts"], out["enc_lens"], out["logit_idx"]
+        else:
+            tokens = np.zeros(T_pad, np.int32)
+            positions = np.zeros(T_pad, np.int32)
+            slots = np.full(T_pad, -1, np.int32)
+            cu = np.zeros(B_pad + 1, np.int32)
+            ctx = np.zeros(B_pad, np.int32)
+            bt = np.zeros((B_pad, self.max_blocks), np.int32)
+            enc_starts = np.zeros(B_pad, np.int32)
+            enc_lens = np.zeros(B_pad, np.int32)
+            lidx = np.zeros(L, np.int64)
         off, max_q = 0, 1
         pool = self.kv.pool
         for j, i in enumerate(live):
@@ -188,12 +197,25 @@ class STTEngine:
         g = self._graphs.get(key)
         if g is not None:
             return g
-        z = lambda *shape, dt=torch.int32: torch.zeros(*shape, dtype=dt, device=self.device)
-        dev = {"tokens": z(T_pad), "positions": z(T_pad),
-               "slots": torch.full((T_pad,), -1, dtype=torch.int32, device=self.device),
-               "cu_q": z(B_pad + 1), "ctx_lens": z(B_pad),
-               "block_tables": z(B_pad, self.max_blocks), "enc_starts": z(B_pad),
-               "enc_lens": z(B_pad), "logit_idx": z(max(16, ops.mpad_for(B_pad)), dt=torch.int64)}
+        shapes = {"tokens": (T_pad,), "positions": (T_pad,), "slots": (T_pad,),
+                  "cu_q": (B_pad + 1,), "ctx_lens": (B_pad,),
+                  "block_tables": (B_pad, self.max_blocks), "enc_starts": (B_pad,),
+                  "enc_lens": (B_pad,)}
+        n32 = sum(int(np.prod(v)) for v in shapes.values())
+        L = max(16, ops.mpad_for(B_pad))
+        d32 = torch.zeros(n32, dtype=torch.int32, device=self.device)
+        h32 = torch.zeros(n32, dtype=torch.int32).pin_memory()
+        d64 = torch.zeros(L, dtype=torch.int64, device=self.device)
+        h64 = torch.zeros(L, dtype=torch.int64).pin_memory()
+        dev, host, off = {}, {}, 0
+        hn = h32.numpy()
+        for k, shp in shapes.items():
+            n = int(np.prod(shp))
+            dev[k] = d32[off:off + n].view(*shp)
+            host[k] = hn[off:off + n].reshape(shp)
+            off += n
+        dev["slots"].fill_(-1)
+        dev["logit_idx"], host["logit_idx"] = d64, h64.numpy()
         max_q = max(1, min(len(self.sot), T_pad))
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -203,7 +225,8 @@ class STTEngine:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = self._fast_forward(dev, max_q, B_pad)
-        g = {"graph": graph, "dev": dev, "out": out}
+        g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
+             "h64": h64, "d64": d64}
         self._graphs[key] = g
         return g
 
@@ -215,8 +238,9 @@ class STTEngine:
             T_pad = ops.mpad_for(T)
             if self.use_graphs:
                 g = self._graph(B_pad, T_pad)
-                _, host = self._host_meta(reqs, live, feeds, B_pad, T_pad)
-                self._dev(host, g["dev"])
+                self._host_meta(reqs, live, feeds, B_pad, T_pad, out=g["host"])
+                g["d32"].copy_(g["h32"], non_blocking=True)
+                g["d64"].copy_(g["h64"], non_blocking=True)
                 g["graph"].replay()
                 return g["out"][:B].cpu().numpy()
             max_q, host = self._host_meta(reqs, live, feeds, B_pad, T_pad)
