@@ -191,3 +191,321 @@ extern "C" int loqa_shuffle_weight(const void* W, void* Wp, int N, int K, hipStr
                      (const bf16_t*)W, (bf16_t*)Wp, N, K, tv);
   return (int)hipGetLastError();
 }
+
+// ============================================================================
+// Fused decode GEMMs: the skinny GEMM above with its follow-on op moved into
+// the epilogue and the preceding RMSNorm moved into the operand load, so a
+// Llama decode layer is 5 launches instead of 10:
+//   qkv     : prologue rmsnorm(attn_norm) | epilogue RoPE + paged KV append + q
+//   o       : epilogue residual add + per-tile row sum of squares
+//   gate|up : prologue rmsnorm(mlp_norm)  | epilogue silu(gate) * up -> bf16
+//   down    : epilogue residual add + per-tile row sum of squares
+// Split-K (S > 1) partials are reduced inside the launch by the last arriving
+// workgroup of each 32-row tile (guide §5 "in-launch split-K reduction":
+// write-through sc1 slab stores -> vmcnt(0) -> barrier -> relaxed agent ticket;
+// the reducer takes an agent acquire and sums the S slabs in fixed order, so
+// results are bitwise identical to the launch-boundary reduce). The RMSNorm
+// scale of a row is rebuilt in every consumer workgroup from the producer's
+// per-tile partial sums of squares in a fixed order (deterministic, no atomics).
+// Weight rows are permuted at load time so one 32-row tile holds (gate, up)
+// feature pairs, or the (c, c + D/2) RoPE pairs of one head.
+enum { EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3 };
+
+struct FusedArgs {
+  const bf16_t* x; long long ldx; const bf16_t* Wp; float* part; int N, K, S, Mpad;
+  int* counters;
+  const float* rowsq_in; int rowsq_tiles; const bf16_t* norm_w; float eps;   // NORM prologue
+  bf16_t* silu_out; int F;                                                    // EPI_SILU
+  bf16_t* residual; float* rowsq_out;                                         // EPI_RESID
+  const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
+  const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
+};
+
+__device__ __forceinline__ void store_sc1_f4(float* p, float4v_ v) {
+  // write-through (sc1) 8-byte stores: visible to an agent-scope acquire on any XCD
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     *reinterpret_cast<unsigned long long*>(&v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  float2 hi = make_float2(v[2], v[3]);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p + 2),
+                     *reinterpret_cast<unsigned long long*>(&hi), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MT, int U, bool NORM>
+__device__ __forceinline__ void load_frag_n(Frag<2, MT, U>& f, const bf16_t* wp, size_t tile_stride,
+                                            const bf16_t* xp, long long ldx_, int ks,
+                                            const bf16_t* nw, const float (&sc)[MT], int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) f.a[u][i] = ldw(wp + (size_t)i * tile_stride + (size_t)(ks + u) * 512);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float wv[8];
+    if constexpr (NORM) unpack8(*reinterpret_cast<const uint4*>(nw + (ks + u) * 32 + 8 * (lane >> 4)), wv);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const bf16_t* p = xp + (size_t)j * 16 * ldx_ + (size_t)(ks + u) * 32;
+      if constexpr (NORM) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const uint4*>(p), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = xv[e] * sc[j] * wv[e];
+        uint4 q = pack8(xv);
+        f.b[u][j] = *reinterpret_cast<bf16x8*>(&q);
+      } else {
+        f.b[u][j] = ldx(p);
+      }
+    }
+  }
+}
+
+template <int MT, int U, int MODE, bool NORM>
+__global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
+  __shared__ float4v_ red[3][2 * MT][64];
+  float* sred = reinterpret_cast<float*>(&red[0][0][0]);   // aliases: prologue / ticket
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x;                   // 32-row output tile
+  const int s = blockIdx.y;
+  const int KS = a.K >> 5;
+  const int kw = KS / (a.S * 4);
+  const int ks0 = (s * 4 + wave) * kw;
+  const size_t tile_stride = (size_t)KS * 512;
+  const bf16_t* wp = a.Wp + (size_t)(tile * 2) * tile_stride + (size_t)lane * 8;
+  const bf16_t* xp = a.x + (size_t)(lane & 15) * a.ldx + 8 * (lane >> 4);
+
+  float sc[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j) sc[j] = 1.f;
+  if constexpr (NORM) {
+    // row scale = rsqrt(mean of squares) from the producer's per-tile partial sums
+    const int Mp = a.Mpad, G = 256 / Mp;
+    const int m = threadIdx.x % Mp, g = threadIdx.x / Mp;
+    float acc = 0.f;
+    for (int t = g; t < a.rowsq_tiles; t += G) acc += a.rowsq_in[(size_t)t * Mp + m];
+    sred[g * Mp + m] = acc;
+    __syncthreads();
+    if (threadIdx.x < Mp) {
+      float tot = 0.f;
+      for (int q = 0; q < G; ++q) tot += sred[q * Mp + threadIdx.x];
+      sred[256 + threadIdx.x] = rsqrtf(tot / (float)a.K + a.eps);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT; ++j) sc[j] = sred[256 + j * 16 + (lane & 15)];
+    __syncthreads();
+  }
+
+  float4v_ acc[2][MT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
+  const int ng = kw / U;
+  Frag<2, MT, U> f0, f1;
+  load_frag_n<MT, U, NORM>(f0, wp, tile_stride, xp, a.ldx, ks0, a.norm_w, sc, lane);
+  int g = 0;
+  for (; g + 2 <= ng; g += 2) {
+    load_frag_n<MT, U, NORM>(f1, wp, tile_stride, xp, a.ldx, ks0 + (g + 1) * U, a.norm_w, sc, lane);
+    mma_frag(f0, acc);
+    if (g + 2 < ng) load_frag_n<MT, U, NORM>(f0, wp, tile_stride, xp, a.ldx, ks0 + (g + 2) * U, a.norm_w, sc, lane);
+    mma_frag(f1, acc);
+  }
+  if (g < ng) mma_frag(f0, acc);
+
+  if (wave > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) red[wave - 1][i * MT + j][lane] = acc[i][j];
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+        acc[i][j] = acc[i][j] + red[0][i * MT + j][lane] + red[1][i * MT + j][lane] +
+                    red[2][i * MT + j][lane];
+  }
+  if (a.S > 1) {
+    // publish this split's partial, take a ticket; the last arriver reduces
+    if (wave == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+          const int m = j * 16 + (lane & 15);
+          const int n = tile * 32 + i * 16 + 4 * (lane >> 4);
+          store_sc1_f4(a.part + ((size_t)s * a.Mpad + m) * a.N + n, acc[i][j]);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int t = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      sred[0] = (float)t;
+    }
+    __syncthreads();
+    if ((int)sred[0] != a.S - 1) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int m = j * 16 + (lane & 15);
+        const int n = tile * 32 + i * 16 + 4 * (lane >> 4);
+        float4v_ v = *reinterpret_cast<const float4v_*>(a.part + (size_t)m * a.N + n);
+        for (int q = 1; q < a.S; ++q)
+          v += *reinterpret_cast<const float4v_*>(a.part + ((size_t)q * a.Mpad + m) * a.N + n);
+        acc[i][j] = v;
+      }
+  } else if (wave != 0) {
+    return;
+  }
+
+  // ---- epilogue (wave 0): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
+  const int nq = 4 * (lane >> 4);
+  if constexpr (MODE == EPI_SILU) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 16 + (lane & 15);
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gg = bf2f(f2bf(acc[0][j][r])), uu = bf2f(f2bf(acc[1][j][r]));
+        o[r] = gg / (1.f + __expf(-gg)) * uu;
+      }
+      uint2 w2;
+      w2.x = pack_bf16x2(o[0], o[1]);
+      w2.y = pack_bf16x2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(a.silu_out + (size_t)m * a.F + tile * 16 + nq) = w2;
+    }
+  } else if constexpr (MODE == EPI_RESID) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 16 + (lane & 15);
+      float sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        bf16_t* rp = a.residual + (size_t)m * a.N + tile * 32 + i * 16 + nq;
+        uint2 rv = *reinterpret_cast<const uint2*>(rp);
+        const float r0 = bf2f(rv.x & 0xffff), r1 = bf2f(rv.x >> 16);
+        const float r2 = bf2f(rv.y & 0xffff), r3 = bf2f(rv.y >> 16);
+        const float h0 = bf2f(f2bf(acc[i][j][0] + r0)), h1 = bf2f(f2bf(acc[i][j][1] + r1));
+        const float h2 = bf2f(f2bf(acc[i][j][2] + r2)), h3 = bf2f(f2bf(acc[i][j][3] + r3));
+        uint2 w2;
+        w2.x = pack_bf16x2(h0, h1);
+        w2.y = pack_bf16x2(h2, h3);
+        *reinterpret_cast<uint2*>(rp) = w2;
+        sq += h0 * h0 + h1 * h1 + h2 * h2 + h3 * h3;
+      }
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 16) a.rowsq_out[(size_t)tile * a.Mpad + m] = sq;
+    }
+  } else if constexpr (MODE == EPI_ROPE) {
+    const int D = a.D, half = D >> 1, tph = D / 32;
+    const int nq_t = a.H * tph, nk_t = a.Hkv * tph;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 16 + (lane & 15);
+      const int slot = a.slots[m];
+      if (tile < nq_t + nk_t) {
+        const bool isk = tile >= nq_t;
+        const int tt = isk ? tile - nq_t : tile;
+        const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
+        const float2* e = a.cs + (size_t)a.positions[m] * half + c;
+        float ra[4], rb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x0 = bf2f(f2bf(acc[0][j][r])), x1 = bf2f(f2bf(acc[1][j][r]));
+          const float2 cs = e[r];
+          ra[r] = x0 * cs.x - x1 * cs.y;
+          rb[r] = x1 * cs.x + x0 * cs.y;
+        }
+        uint2 lo, hi;
+        lo.x = pack_bf16x2(ra[0], ra[1]); lo.y = pack_bf16x2(ra[2], ra[3]);
+        hi.x = pack_bf16x2(rb[0], rb[1]); hi.y = pack_bf16x2(rb[2], rb[3]);
+        bf16_t* dst;
+        if (!isk) {
+          dst = a.q_out + (size_t)m * a.H * D + head * D;
+        } else {
+          if (slot < 0) continue;
+          const int bb = slot / a.blk, o = slot - bb * a.blk;
+          dst = a.kc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D;
+        }
+        *reinterpret_cast<uint2*>(dst + c) = lo;
+        *reinterpret_cast<uint2*>(dst + c + half) = hi;
+      } else {
+        if (slot < 0) continue;
+        const int bb = slot / a.blk, o = slot - bb * a.blk;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = (tile - nq_t - nk_t) * 32 + i * 16 + nq;
+          const int head = row / D, c = row - head * D;
+          uint2 w2;
+          w2.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+          w2.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(a.vc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c) = w2;
+        }
+      }
+    }
+  }
+}
+
+template <int MT, int MODE, bool NORM>
+static int launch_fused(const FusedArgs& a, hipStream_t st) {
+  dim3 grid(a.N / 32, a.S);
+  const int kw = a.K / 32 / (a.S * 4);
+  if (kw % 4 == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<MT, 4, MODE, NORM>), grid, dim3(256), 0, st, a);
+  else if (kw % 2 == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<MT, 2, MODE, NORM>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((skinny_fused_kernel<MT, 1, MODE, NORM>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, bool NORM>
+static int dispatch_fused(const FusedArgs& a, hipStream_t st) {
+  return a.Mpad == 16 ? launch_fused<1, MODE, NORM>(a, st) : launch_fused<2, MODE, NORM>(a, st);
+}
+
+// mode: 1 silu (out [Mpad, N/2]), 2 residual+rowsq, 3 rope+append. norm: x is
+// the bf16 residual, normalised in the operand load with (rowsq_in, norm_w).
+// part: [S, Mpad, N] f32 scratch (S > 1); counters: >= N/32 zeroed ints.
+extern "C" int loqa_skinny_fused(const void* x, long long ldx_, const void* Wp, float* part,
+                                 int* counters, int Mpad, int N, int K, int S, int mode, int norm,
+                                 const float* rowsq_in, int rowsq_tiles, const void* norm_w,
+                                 float eps, void* silu_out, void* residual, float* rowsq_out,
+                                 const int* positions, const void* cs, void* q_out, void* kc,
+                                 void* vc, const int* slots, int H, int Hkv, int D, int blk,
+                                 hipStream_t st) {
+  if (S < 1 || K % (S * 128) || ldx_ % 8 || N % 32 || (Mpad != 16 && Mpad != 32))
+    return (int)hipErrorInvalidValue;
+  if (S > 1 && (!part || !counters)) return (int)hipErrorInvalidValue;
+  if (norm && (!rowsq_in || !norm_w || rowsq_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (mode == EPI_ROPE && (D % 32 || N != (H + 2 * Hkv) * D)) return (int)hipErrorInvalidValue;
+  FusedArgs a{(const bf16_t*)x, ldx_, (const bf16_t*)Wp, part, N, K, S, Mpad, counters,
+              rowsq_in, rowsq_tiles, (const bf16_t*)norm_w, eps, (bf16_t*)silu_out, N / 2,
+              (bf16_t*)residual, rowsq_out, positions, (const float2*)cs, (bf16_t*)q_out,
+              (bf16_t*)kc, (bf16_t*)vc, slots, H, Hkv, D, blk};
+  switch (mode * 2 + (norm ? 1 : 0)) {
+    case EPI_SILU * 2: return dispatch_fused<EPI_SILU, false>(a, st);
+    case EPI_SILU * 2 + 1: return dispatch_fused<EPI_SILU, true>(a, st);
+    case EPI_RESID * 2: return dispatch_fused<EPI_RESID, false>(a, st);
+    case EPI_RESID * 2 + 1: return dispatch_fused<EPI_RESID, true>(a, st);
+    case EPI_ROPE * 2: return dispatch_fused<EPI_ROPE, false>(a, st);
+    case EPI_ROPE * 2 + 1: return dispatch_fused<EPI_ROPE, true>(a, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -65,7 +65,7 @@ class LLMEngine:
     def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
                  tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192,
-                 weights: LlamaWeights | None = None):
+                 weights: LlamaWeights | None = None, fused_decode: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.tp = tp or TPGroup()
@@ -90,6 +90,9 @@ class LLMEngine:
         self.attn_ws = ops.AttnWorkspace(self.device, 128, self.weights.h, cfg.head_dim,
                                          (max_seq_len + 127) // 128) if self.is_gpu else None
         self.use_graphs = use_graphs and self.is_gpu
+        # fused-epilogue decode GEMMs (single GPU, <= 32 tokens per step)
+        self.fused_decode = fused_decode and self.weights.fused
+        self.scratch = ops.FusedScratch(self.device)
         self.prefill_chunk = prefill_chunk
         self._graphs: dict[tuple[int, int], dict] = {}
         self._next_id = 1
@@ -164,7 +167,11 @@ class LLMEngine:
     # ------------------------------------------------------------ forward
     def _forward_sample(self, meta: StepMeta, mask_rows: torch.Tensor) -> torch.Tensor:
         if meta.decode:
-            logits = self.model.forward_decode(meta, self.kv.k, self.kv.v, self.attn_ws)
+            if self.fused_decode and meta.tokens.numel() <= 32:
+                logits = self.model.forward_decode_fused(meta, self.kv.k, self.kv.v, self.attn_ws,
+                                                         self.scratch)
+            else:
+                logits = self.model.forward_decode(meta, self.kv.k, self.kv.v, self.attn_ws)
             logits = logits[: mask_rows.numel()]
         else:
             hid = self.model.forward(meta, self.kv.k, self.kv.v, self.attn_ws)

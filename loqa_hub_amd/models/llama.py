@@ -114,10 +114,24 @@ class LlamaWeights:
                                for k in ("wqkv", "wo", "w_gate_up", "w_down")}
                               for L in self.layers]
         self.lm_head_p = ops.shuffle_weight(self.lm_head)
+        self._add_fused_copies()
         if torch.device(device).type == "cuda":
             for k in ("wqkv", "wo", "w_gate_up", "w_down"):
                 ops.tune_skinny_splits(self.decode_layers[0][k])
             ops.tune_skinny_splits(self.lm_head_p)
+
+    def _add_fused_copies(self) -> None:
+        """Row-permuted decode copies for the fused-epilogue GEMMs (RoPE pairs /
+        gate-up pairs share a 32-row tile); single-GPU only."""
+        self.fused = self.tp.world == 1
+        if not self.fused:
+            return
+        from ..ops import reference as _ref
+        pq = _ref.perm_rope_qkv(self.h, self.hkv, self.cfg.head_dim).to(self.embed.device)
+        pg = _ref.perm_gate_up(self.f).to(self.embed.device)
+        for L, P in zip(self.layers, self.decode_layers):
+            P["wqkv_f"] = ops.shuffle_weight(L["wqkv"][pq].contiguous())
+            P["w_gate_up_f"] = ops.shuffle_weight(L["w_gate_up"][pg].contiguous())
 
     @classmethod
     def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":
@@ -154,6 +168,7 @@ class LlamaWeights:
                                for k in ("wqkv", "wo", "w_gate_up", "w_down")}
                               for L in self.layers]
         self.lm_head_p = ops.shuffle_weight(self.lm_head)
+        self._add_fused_copies()
         return self
 
     def nbytes(self) -> int:
@@ -247,6 +262,48 @@ class LlamaModel:
             tp.all_reduce_(down)
         hf = ops.slab_rmsnorm(down, residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx,
                               write_residual=False)
+        return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
+
+    def forward_decode_fused(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                             attn_ws: ops.AttnWorkspace | None, scratch: ops.FusedScratch,
+                             split_keys: int = 128) -> torch.Tensor:
+        """Decode step with the fused-epilogue GEMMs (5 launches per layer):
+        qkv (RMSNorm prologue, RoPE + KV append epilogue) -> attention ->
+        o (residual + row sum-of-squares epilogue) -> gate|up (RMSNorm prologue,
+        SwiGLU epilogue) -> down (residual + row sum-of-squares). Single GPU,
+        Mpad 16 / 32. Same numerics as ``forward_decode``."""
+        cfg, w = self.cfg, self.w
+        H, Hkv, D, d = w.h, w.hkv, cfg.head_dim, cfg.d_model
+        Mpad = meta.tokens.numel()
+        residual = self.embed(meta.tokens).contiguous()
+        h = ops.rmsnorm(residual, w.layers[0]["attn_norm"], cfg.norm_eps)
+        num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
+        q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
+        tiles = d // 32
+        for li, L in enumerate(w.layers):
+            P = w.decode_layers[li]
+            if li == 0:
+                ops.skinny_fused(h, P["wqkv_f"], "rope", scratch, positions=meta.positions,
+                                 cos_sin=w.cos_sin, q_out=q, k_cache=k_cache[li],
+                                 v_cache=v_cache[li], slots=meta.slots, n_heads=H, n_kv=Hkv,
+                                 head_dim=D)
+            else:
+                ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm_w=L["attn_norm"],
+                                 eps=cfg.norm_eps, rowsq_tiles=tiles, positions=meta.positions,
+                                 cos_sin=w.cos_sin, q_out=q, k_cache=k_cache[li],
+                                 v_cache=v_cache[li], slots=meta.slots, n_heads=H, n_kv=Hkv,
+                                 head_dim=D)
+            attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
+                                 block_tables=meta.block_tables, grouped=True,
+                                 split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
+                                 max_k=meta.max_ctx)
+            ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
+            a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch,
+                                 norm_w=L["mlp_norm"], eps=cfg.norm_eps, rowsq_tiles=tiles)
+            ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
+        sel = residual.index_select(0, meta.logit_idx).contiguous()
+        hf = ops.rmsnorm(sel, w.final_norm, cfg.norm_eps)
         return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

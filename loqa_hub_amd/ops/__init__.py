@@ -691,3 +691,83 @@ def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F:
                                        ptr(z), F, C2 // 2, float(noise_scale), seed & 0xFFFFFFFF,
                                        stream_ptr(stats)), "expand_sample")
     return z
+
+
+# ------------------------------------------------------------ fused decode GEMMs
+class FusedScratch:
+    """Device state shared by the fused decode GEMMs of one engine: split-K
+    ticket counters (zeroed once; each reducer resets its own) and the row
+    sum-of-squares partials handed from the residual epilogues to the next
+    GEMM's RMSNorm prologue."""
+
+    def __init__(self, device, max_tiles: int = 8192, max_rows: int = 32):
+        self.counters = torch.zeros(max_tiles, dtype=torch.int32, device=device)
+        self.rowsq = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
+
+
+_FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3}
+
+
+def skinny_fused(x: torch.Tensor, wp: torch.Tensor, mode: str, scratch: FusedScratch, *,
+                 splits: int | None = None, norm_w: torch.Tensor | None = None,
+                 eps: float = 1e-5, rowsq_tiles: int = 0, residual: torch.Tensor | None = None,
+                 positions=None, cos_sin=None, q_out=None, k_cache=None, v_cache=None, slots=None,
+                 n_heads: int = 0, n_kv: int = 0, head_dim: int = 0, out=None) -> torch.Tensor:
+    """Skinny GEMM with a fused epilogue (and optional RMSNorm prologue, ``norm_w``
+    with ``rowsq_tiles`` partial sums in ``scratch.rowsq``); Mpad 16 or 32.
+    mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
+    "resid": residual += x W^T in place, writes per-tile row sums of squares;
+    "rope": q -> q_out, RoPE'd k and v -> paged caches (``perm_rope_qkv`` order)."""
+    Mpad, K = x.shape
+    N = wp.shape[0] * 16
+    S = splits or choose_splits(N, K, Mpad)
+    m = _FUSED_MODES[mode]
+    ntiles = N // 32
+    if not _gpu(x):
+        return _skinny_fused_ref(x, wp, mode, scratch, norm_w, eps, rowsq_tiles, residual,
+                                 positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
+                                 n_kv, head_dim, out)
+    assert Mpad in (16, 32) and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert ntiles <= scratch.counters.numel()
+    part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device) if S > 1 else None
+    if mode == "silu":
+        out = out if out is not None else torch.empty(Mpad, N // 2, dtype=torch.bfloat16,
+                                                      device=x.device)
+    rs_in = scratch.rowsq if norm_w is not None else None
+    blk = k_cache.shape[2] if k_cache is not None else 0
+    check(kernels().loqa_skinny_fused(
+        ptr(x), x.stride(0), ptr(wp), ptr(part), ptr(scratch.counters), Mpad, N, K, S, m,
+        int(norm_w is not None), ptr(rs_in), rowsq_tiles, ptr(norm_w), eps, ptr(out),
+        ptr(residual), ptr(scratch.rowsq) if mode == "resid" else None, ptr(positions),
+        ptr(cos_sin), ptr(q_out), ptr(k_cache), ptr(v_cache), ptr(slots), n_heads, n_kv,
+        head_dim, blk, stream_ptr(x)), "skinny_fused")
+    return out if mode == "silu" else (q_out if mode == "rope" else residual)
+
+
+def _skinny_fused_ref(x, wp, mode, scratch, norm_w, eps, rowsq_tiles, residual, positions,
+                      cos_sin, q_out, k_cache, v_cache, slots, H, Hkv, D, out):
+    Mpad, K = x.shape
+    N = wp.shape[0] * 16
+    rs = scratch.rowsq[: rowsq_tiles * Mpad].view(rowsq_tiles, Mpad) if norm_w is not None else None
+    xe = ref.fused_prologue(x, rs, norm_w, eps, K)
+    y = xe @ ref.unshuffle_weight(wp).float().t()  # [Mpad, N] in permuted row order
+    if mode == "silu":
+        F = N // 2
+        inv = torch.argsort(ref.perm_gate_up(F))
+        y = y[:, inv]
+        res = ref.silu_mul(y.to(torch.bfloat16))
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+    if mode == "resid":
+        h = (y + residual.float()).to(torch.bfloat16)
+        residual.copy_(h)
+        sq = h.float().pow(2).view(Mpad, N // 32, 32).sum(-1).t().contiguous()  # [tiles, Mpad]
+        scratch.rowsq[: sq.numel()] = sq.flatten()
+        return residual
+    inv = torch.argsort(ref.perm_rope_qkv(H, Hkv, D))
+    qkv = y[:, inv].to(torch.bfloat16)
+    ref.rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D)
+    q_out.copy_(qkv[:, : H * D])
+    return q_out

@@ -430,3 +430,35 @@ def expand_sample(stats, cum, flen, F, noise_scale, noise=None):
         e = noise[b, :n].float() if noise is not None else torch.zeros_like(m)
         z[b, :n] = m + e * torch.exp(lg) * noise_scale
     return z
+
+
+# ------------------------------------------------------------ fused decode GEMMs
+def perm_rope_qkv(H, Hkv, D):
+    """Row order of the fused qkv weight: per q / k head, 32-row tiles holding
+    16 first-half rows c0.. and their RoPE partners c0 + D/2; v rows unchanged."""
+    half = D // 2
+    rows = []
+    for base, n in ((0, H), (H * D, Hkv)):
+        for h in range(n):
+            for s in range(D // 32):
+                c0 = 16 * s
+                rows += list(range(base + h * D + c0, base + h * D + c0 + 16))
+                rows += list(range(base + h * D + half + c0, base + h * D + half + c0 + 16))
+    rows += list(range((H + Hkv) * D, (H + 2 * Hkv) * D))
+    return torch.tensor(rows, dtype=torch.long)
+
+
+def perm_gate_up(F):
+    """Row order of the fused gate|up weight: 32-row tiles of (16 gate, 16 up)."""
+    rows = []
+    for t in range(F // 16):
+        rows += list(range(16 * t, 16 * t + 16)) + list(range(F + 16 * t, F + 16 * t + 16))
+    return torch.tensor(rows, dtype=torch.long)
+
+
+def fused_prologue(x, rowsq_in, norm_w, eps, K):
+    if rowsq_in is None:
+        return x.float()
+    tot = rowsq_in.float().sum(0)  # [Mpad]
+    scale = torch.rsqrt(tot / K + eps)
+    return (x.float() * scale[:, None] * norm_w.float()[None, :]).to(torch.bfloat16).float()

@@ -1,0 +1,105 @@
+"""Fused-epilogue decode GEMMs (RMSNorm prologue; RoPE+KV-append / residual +
+row-sumsq / SwiGLU epilogues; in-launch split-K reduce) against the unfused
+skinny-GEMM + slab-consumer path, on the CPU (reference semantics of the
+weight permutations) and on the GPU (the HIP kernels)."""
+import numpy as np
+import pytest
+import torch
+
+from loqa_hub_amd import ops
+
+
+def _decode_logits(eng, fused: bool, seq_base: int, tok, Mpad: int):
+    from loqa_hub_amd.engine.llm_engine import GenRequest
+    pool = eng.kv.pool
+    seqs = []
+    for i in range(len(tok)):
+        r = GenRequest([], [])
+        r.seq_id = seq_base + i
+        pool.add_seq(r.seq_id, [])
+        seqs.append(r)
+    outs = []
+    feeds = [t[:5] for t in tok]
+    for step in range(3):  # a 5-token step then single-token steps (cache grows)
+        max_q, max_ctx, host = eng._meta(seqs, feeds, True, len(tok), Mpad)
+        dev = eng._to_device(host)
+        meta = eng._build_meta(dev, max_q, max_ctx, True)
+        if fused:
+            lg = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+        else:
+            lg = eng.model.forward_decode(meta, eng.kv.k, eng.kv.v, eng.attn_ws)
+        outs.append(lg[: len(tok)].float().cpu())
+        feeds = [[t[5 + step]] for t in tok]
+    return outs
+
+
+def _compare(device, splits=None):
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), device, max_seqs=8, use_graphs=False)
+    if splits is not None:  # force split-K (exercises the in-launch reducer)
+        for key in list(ops._SPLITS):
+            del ops._SPLITS[key]
+        d = eng.cfg.d_model
+        for N, K in ((eng.weights.h * 64 + 2 * eng.weights.hkv * 64, d), (d, eng.weights.h * 64),
+                     (2 * eng.weights.f, d), (d, eng.weights.f)):
+            for Mpad in (16, 32):
+                s = max(x for x in ops.SPLIT_CANDIDATES if x <= splits and K % (x * 128) == 0)
+                ops._SPLITS[(N, K, Mpad)] = s
+    g = torch.Generator().manual_seed(3)
+    tok = torch.randint(10, 4000, (3, 12), generator=g).tolist()
+    a = _decode_logits(eng, True, 100, tok, 16)
+    b = _decode_logits(eng, False, 200, tok, 16)
+    for x, y in zip(a, b):
+        rel = float((x - y).norm() / (y.norm() + 1e-12))
+        assert rel < 2e-2, rel
+    ops._SPLITS.clear()
+
+
+def test_fused_decode_matches_unfused_cpu():
+    _compare("cpu")
+
+
+def test_permutations_are_bijections():
+    from loqa_hub_amd.ops import reference as ref
+    p = ref.perm_rope_qkv(32, 8, 128)
+    assert sorted(p.tolist()) == list(range((32 + 16) * 128))
+    g = ref.perm_gate_up(14336)
+    assert sorted(g.tolist()) == list(range(2 * 14336))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("splits", [None, 1, 2])
+def test_fused_decode_matches_unfused_gpu(splits):
+    _compare("cuda", splits)
+
+
+@pytest.mark.gpu
+def test_fused_resid_rowsq_and_silu_gpu():
+    """Kernel-level: residual epilogue + row sum-of-squares, then the RMSNorm
+    prologue of a SwiGLU GEMM, against the reference chain."""
+    from loqa_hub_amd.ops import reference as ref
+    dev = "cuda"
+    torch.manual_seed(0)
+    Mpad, d, F = 16, 1024, 2048
+    scr = ops.FusedScratch(dev)
+    x = torch.randn(Mpad, 512, device=dev).bfloat16()
+    wo = ops.shuffle_weight((torch.randn(d, 512, device=dev) * 0.05).bfloat16())
+    res1 = torch.randn(Mpad, d, device=dev).bfloat16()
+    res2 = res1.clone()
+    for S in (1, 4):
+        ops.skinny_fused(x, wo, "resid", scr, splits=S, residual=res1)
+        part = ops.skinny_gemm(x, wo, S)
+        ops.slab_rmsnorm(part, res2, torch.ones(d, device=dev).bfloat16(), 1e-5)
+        assert torch.equal(res1, res2)
+    sq = scr.rowsq[: (d // 32) * Mpad].view(d // 32, Mpad).sum(0)
+    assert torch.allclose(sq, res1.float().pow(2).sum(1), rtol=1e-3)
+    wgu = (torch.randn(2 * F, d, device=dev) * 0.03).bfloat16()
+    wn = torch.rand(d, device=dev).bfloat16() + 0.5
+    wp = ops.shuffle_weight(wgu[ref.perm_gate_up(F).to(dev)].contiguous())
+    for S in (1, 2):
+        a = ops.skinny_fused(res1, wp, "silu", scr, splits=S, norm_w=wn, eps=1e-5,
+                             rowsq_tiles=d // 32)
+        h = ref.rmsnorm(res1, wn, 1e-5)
+        expect = ref.silu_mul((h.float() @ wgu.float().t()).bfloat16())
+        assert float((a.float() - expect.float()).norm() / expect.float().norm()) < 1e-2
