@@ -197,6 +197,9 @@ extern "C" int loqa_shuffle_weight(const void* W, void* Wp, int N, int K, hipStr
 // the epilogue and the preceding RMSNorm moved into the operand load, so a
 // Llama decode layer is 5 launches instead of 10:
 //   qkv     : prologue rmsnorm(attn_norm) | epilogue RoPE + paged KV append + q
+// (RMSNorm: the norm weight is folded into the weight rows at load time and the
+//  per-row 1/rms scale, a property of the row, is applied to the accumulator,
+//  so the operand stream stays the plain prefetch pipeline)
 //   o       : epilogue residual add + per-tile row sum of squares
 //   gate|up : prologue rmsnorm(mlp_norm)  | epilogue silu(gate) * up -> bf16
 //   down    : epilogue residual add + per-tile row sum of squares
@@ -209,57 +212,18 @@ extern "C" int loqa_shuffle_weight(const void* W, void* Wp, int N, int K, hipStr
 // per-tile partial sums of squares in a fixed order (deterministic, no atomics).
 // Weight rows are permuted at load time so one 32-row tile holds (gate, up)
 // feature pairs, or the (c, c + D/2) RoPE pairs of one head.
+typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
 enum { EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3 };
 
 struct FusedArgs {
   const bf16_t* x; long long ldx; const bf16_t* Wp; float* part; int N, K, S, Mpad;
   int* counters;
-  const float* rowsq_in; int rowsq_tiles; const bf16_t* norm_w; float eps;   // NORM prologue
+  const float* rowsq_in; int rowsq_tiles; float eps;   // NORM row scale
   bf16_t* silu_out; int F;                                                    // EPI_SILU
   bf16_t* residual; float* rowsq_out;                                         // EPI_RESID
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
 };
-
-__device__ __forceinline__ void store_sc1_f4(float* p, float4v_ v) {
-  // write-through (sc1) 8-byte stores: visible to an agent-scope acquire on any XCD
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                     *reinterpret_cast<unsigned long long*>(&v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  float2 hi = make_float2(v[2], v[3]);
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p + 2),
-                     *reinterpret_cast<unsigned long long*>(&hi), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int MT, int U, bool NORM>
-__device__ __forceinline__ void load_frag_n(Frag<2, MT, U>& f, const bf16_t* wp, size_t tile_stride,
-                                            const bf16_t* xp, long long ldx_, int ks,
-                                            const bf16_t* nw, const float (&sc)[MT], int lane) {
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) f.a[u][i] = ldw(wp + (size_t)i * tile_stride + (size_t)(ks + u) * 512);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    float wv[8];
-    if constexpr (NORM) unpack8(*reinterpret_cast<const uint4*>(nw + (ks + u) * 32 + 8 * (lane >> 4)), wv);
-#pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const bf16_t* p = xp + (size_t)j * 16 * ldx_ + (size_t)(ks + u) * 32;
-      if constexpr (NORM) {
-        float xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(p), xv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[e] = xv[e] * sc[j] * wv[e];
-        uint4 q = pack8(xv);
-        f.b[u][j] = *reinterpret_cast<bf16x8*>(&q);
-      } else {
-        f.b[u][j] = ldx(p);
-      }
-    }
-  }
-}
 
 template <int MT, int U, int MODE, bool NORM>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
@@ -304,12 +268,12 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
   const int ng = kw / U;
   Frag<2, MT, U> f0, f1;
-  load_frag_n<MT, U, NORM>(f0, wp, tile_stride, xp, a.ldx, ks0, a.norm_w, sc, lane);
+  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0);
   int g = 0;
   for (; g + 2 <= ng; g += 2) {
-    load_frag_n<MT, U, NORM>(f1, wp, tile_stride, xp, a.ldx, ks0 + (g + 1) * U, a.norm_w, sc, lane);
+    load_frag(f1, wp, tile_stride, xp, a.ldx, ks0 + (g + 1) * U);
     mma_frag(f0, acc);
-    if (g + 2 < ng) load_frag_n<MT, U, NORM>(f0, wp, tile_stride, xp, a.ldx, ks0 + (g + 2) * U, a.norm_w, sc, lane);
+    if (g + 2 < ng) load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + (g + 2) * U);
     mma_frag(f1, acc);
   }
   if (g < ng) mma_frag(f0, acc);
@@ -330,48 +294,64 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
                     red[2][i * MT + j][lane];
   }
   if (a.S > 1) {
-    // publish this split's partial, take a ticket; the last arriver reduces
+    // publish this split's partial (tile-contiguous slab, sc1 write-through),
+    // take a ticket; the last arriver reduces with sc1 loads (no acquire fence:
+    // every handed-off byte is stored and loaded sc1, guide §6 Guideline 16)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.part, 0, (int)((size_t)gridDim.x * a.S * 2 * MT * 64 * 16), 0x00020000);
+    const int slab0 = tile * a.S * 2 * MT;
     if (wave == 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j) {
-          const int m = j * 16 + (lane & 15);
-          const int n = tile * 32 + i * 16 + 4 * (lane >> 4);
-          store_sc1_f4(a.part + ((size_t)s * a.Mpad + m) * a.N + n, acc[i][j]);
-        }
+        for (int j = 0; j < MT; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4_, acc[i][j]), rsrc,
+              (((slab0 + s * 2 * MT) + i * MT + j) * 64 + lane) * 16, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       const int t = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (t == a.S - 1)
+        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sred[0] = (float)t;
     }
     __syncthreads();
-    if ((int)sred[0] != a.S - 1) return;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (wave != 0) return;
+    if ((int)sred[0] != a.S - 1 || wave != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // fixed summation order (split 0..S-1) whichever block arrives last
+    float4v_ tot[2][MT];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int m = j * 16 + (lane & 15);
-        const int n = tile * 32 + i * 16 + 4 * (lane >> 4);
-        float4v_ v = *reinterpret_cast<const float4v_*>(a.part + (size_t)m * a.N + n);
-        for (int q = 1; q < a.S; ++q)
-          v += *reinterpret_cast<const float4v_*>(a.part + ((size_t)q * a.Mpad + m) * a.N + n);
-        acc[i][j] = v;
-      }
+      for (int j = 0; j < MT; ++j) tot[i][j] = float4v_{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < a.S; ++q) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j)
+          tot[i][j] += __builtin_bit_cast(
+              float4v_, __builtin_amdgcn_raw_buffer_load_b128(
+                            rsrc, (((slab0 + q * 2 * MT) + i * MT + j) * 64 + lane) * 16, 0, 16));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) acc[i][j] = tot[i][j];
   } else if (wave != 0) {
     return;
   }
 
+  // RMSNorm: the norm weight is folded into W at load time, so the row scale
+  // factors out of the k-sum and is applied once here
+  if constexpr (NORM) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) acc[i][j] *= sc[j];
+  }
   // ---- epilogue (wave 0): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
   const int nq = 4 * (lane >> 4);
   if constexpr (MODE == EPI_SILU) {
@@ -481,11 +461,12 @@ static int dispatch_fused(const FusedArgs& a, hipStream_t st) {
 }
 
 // mode: 1 silu (out [Mpad, N/2]), 2 residual+rowsq, 3 rope+append. norm: x is
-// the bf16 residual, normalised in the operand load with (rowsq_in, norm_w).
-// part: [S, Mpad, N] f32 scratch (S > 1); counters: >= N/32 zeroed ints.
+// the bf16 residual, Wp has the norm weight folded in, and the accumulator is
+// scaled by rsqrt(sum(rowsq_in over tiles) / K + eps) per row.
+// part: S * Mpad * N f32 scratch (S > 1, tile-contiguous slabs); counters: >= N/32 zeroed ints.
 extern "C" int loqa_skinny_fused(const void* x, long long ldx_, const void* Wp, float* part,
                                  int* counters, int Mpad, int N, int K, int S, int mode, int norm,
-                                 const float* rowsq_in, int rowsq_tiles, const void* norm_w,
+                                 const float* rowsq_in, int rowsq_tiles,
                                  float eps, void* silu_out, void* residual, float* rowsq_out,
                                  const int* positions, const void* cs, void* q_out, void* kc,
                                  void* vc, const int* slots, int H, int Hkv, int D, int blk,
@@ -493,10 +474,10 @@ extern "C" int loqa_skinny_fused(const void* x, long long ldx_, const void* Wp, 
   if (S < 1 || K % (S * 128) || ldx_ % 8 || N % 32 || (Mpad != 16 && Mpad != 32))
     return (int)hipErrorInvalidValue;
   if (S > 1 && (!part || !counters)) return (int)hipErrorInvalidValue;
-  if (norm && (!rowsq_in || !norm_w || rowsq_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (norm && (!rowsq_in || rowsq_tiles < 1)) return (int)hipErrorInvalidValue;
   if (mode == EPI_ROPE && (D % 32 || N != (H + 2 * Hkv) * D)) return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)x, ldx_, (const bf16_t*)Wp, part, N, K, S, Mpad, counters,
-              rowsq_in, rowsq_tiles, (const bf16_t*)norm_w, eps, (bf16_t*)silu_out, N / 2,
+              rowsq_in, rowsq_tiles, eps, (bf16_t*)silu_out, N / 2,
               (bf16_t*)residual, rowsq_out, positions, (const float2*)cs, (bf16_t*)q_out,
               (bf16_t*)kc, (bf16_t*)vc, slots, H, Hkv, D, blk};
   switch (mode * 2 + (norm ? 1 : 0)) {

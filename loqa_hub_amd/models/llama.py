@@ -130,8 +130,44 @@ class LlamaWeights:
         pq = _ref.perm_rope_qkv(self.h, self.hkv, self.cfg.head_dim).to(self.embed.device)
         pg = _ref.perm_gate_up(self.f).to(self.embed.device)
         for L, P in zip(self.layers, self.decode_layers):
-            P["wqkv_f"] = ops.shuffle_weight(L["wqkv"][pq].contiguous())
-            P["w_gate_up_f"] = ops.shuffle_weight(L["w_gate_up"][pg].contiguous())
+            P["wqkv_f"] = ops.shuffle_weight(ops.fold_norm(L["wqkv"], L["attn_norm"])[pq].contiguous())
+            P["w_gate_up_f"] = ops.shuffle_weight(
+                ops.fold_norm(L["w_gate_up"], L["mlp_norm"])[pg].contiguous())
+        if self.embed.device.type == "cuda":
+            self._tune_fused()
+
+    def _tune_fused(self) -> None:
+        """Measure the split-K of each fused decode GEMM (layer-0 weights, dummy
+        activations / caches) for Mpad 16 and 32; before any graph capture."""
+        dev, D, d = self.embed.device, self.cfg.head_dim, self.cfg.d_model
+        P = self.decode_layers[0]
+        scr = ops.FusedScratch(dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        blk = 16
+        kc = torch.zeros(4, self.hkv, blk, D, **bf)
+        vc = torch.zeros_like(kc)
+        for Mpad in (16, 32):
+            scr.rowsq[: d // 32 * Mpad].fill_(float(d) / (d // 32))
+            res = torch.randn(Mpad, d, **bf)
+            pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
+            q = torch.empty(Mpad, self.h * D, **bf)
+            a = torch.randn(Mpad, self.h * D, **bf)
+            f = torch.randn(Mpad, self.f, **bf)
+            jobs = {
+                "rope": (P["wqkv_f"], lambda s, w: ops.skinny_fused(
+                    res, w, "rope", scr, splits=s, norm=True, rowsq_tiles=d // 32, positions=pos,
+                    cos_sin=self.cos_sin, q_out=q, k_cache=kc, v_cache=vc, slots=pos,
+                    n_heads=self.h, n_kv=self.hkv, head_dim=D)),
+                "silu": (P["w_gate_up_f"], lambda s, w: ops.skinny_fused(
+                    res, w, "silu", scr, splits=s, norm=True, rowsq_tiles=d // 32)),
+                "resid_o": (P["wo"], lambda s, w: ops.skinny_fused(
+                    a, w, "resid", scr, splits=s, residual=res.clone())),
+                "resid_down": (P["w_down"], lambda s, w: ops.skinny_fused(
+                    f, w, "resid", scr, splits=s, residual=res.clone())),
+            }
+            for name, (w, run) in jobs.items():
+                N, K = w.shape[0] * 16, w.shape[1] * 32
+                ops.tune_fused_splits((name.split("_")[0], N, K, Mpad), lambda s: run(s, w), K)
 
     @classmethod
     def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":
@@ -276,31 +312,26 @@ class LlamaModel:
         H, Hkv, D, d = w.h, w.hkv, cfg.head_dim, cfg.d_model
         Mpad = meta.tokens.numel()
         residual = self.embed(meta.tokens).contiguous()
-        h = ops.rmsnorm(residual, w.layers[0]["attn_norm"], cfg.norm_eps)
+        # layer 0's RMSNorm row scale: one partial sum of squares per row
+        torch.sum(residual.float().square(), 1, out=scratch.rowsq[:Mpad])
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
         q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
         tiles = d // 32
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
-            if li == 0:
-                ops.skinny_fused(h, P["wqkv_f"], "rope", scratch, positions=meta.positions,
-                                 cos_sin=w.cos_sin, q_out=q, k_cache=k_cache[li],
-                                 v_cache=v_cache[li], slots=meta.slots, n_heads=H, n_kv=Hkv,
-                                 head_dim=D)
-            else:
-                ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm_w=L["attn_norm"],
-                                 eps=cfg.norm_eps, rowsq_tiles=tiles, positions=meta.positions,
-                                 cos_sin=w.cos_sin, q_out=q, k_cache=k_cache[li],
-                                 v_cache=v_cache[li], slots=meta.slots, n_heads=H, n_kv=Hkv,
-                                 head_dim=D)
+            ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True,
+                             eps=cfg.norm_eps, rowsq_tiles=1 if li == 0 else tiles,
+                             positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
+                             k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
+                             n_heads=H, n_kv=Hkv, head_dim=D)
             attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
                                  head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
                                  block_tables=meta.block_tables, grouped=True,
                                  split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
                                  max_k=meta.max_ctx)
             ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
-            a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch,
-                                 norm_w=L["mlp_norm"], eps=cfg.norm_eps, rowsq_tiles=tiles)
+            a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
+                                 eps=cfg.norm_eps, rowsq_tiles=tiles)
             ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
         sel = residual.index_select(0, meta.logit_idx).contiguous()
         hf = ops.rmsnorm(sel, w.final_norm, cfg.norm_eps)

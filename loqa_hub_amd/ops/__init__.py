@@ -357,6 +357,35 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
     return out
 
 
+_FSPLITS: dict = {}
+
+
+def tune_fused_splits(key: tuple, run, K: int, reps: int = 8) -> int:
+    """Split-K for a fused-epilogue GEMM, measured: ``run(s)`` launches it at
+    split ``s``. The in-launch reduce adds a store-drain + ticket round trip to
+    every workgroup's tail, so the best split is lower than the plain GEMM's
+    and is tuned separately (``key`` = (mode, N, K, Mpad))."""
+    if key in _FSPLITS:
+        return _FSPLITS[key]
+    best, best_t = 1, float("inf")
+    for s in SPLIT_CANDIDATES:
+        if K % (s * 128):
+            continue
+        for _ in range(2):
+            run(s)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            run(s)
+        b.record()
+        b.synchronize()
+        t = a.elapsed_time(b)
+        if t < best_t * 0.98:
+            best, best_t = s, t
+    _FSPLITS[key] = best
+    return best
+
+
 def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
     """Split-K factor: the tuned value if available, else enough splits for
     >= ~2 workgroups per CU (256 CUs)."""
@@ -709,22 +738,24 @@ _FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3}
 
 
 def skinny_fused(x: torch.Tensor, wp: torch.Tensor, mode: str, scratch: FusedScratch, *,
-                 splits: int | None = None, norm_w: torch.Tensor | None = None,
+                 splits: int | None = None, norm: bool = False,
                  eps: float = 1e-5, rowsq_tiles: int = 0, residual: torch.Tensor | None = None,
                  positions=None, cos_sin=None, q_out=None, k_cache=None, v_cache=None, slots=None,
                  n_heads: int = 0, n_kv: int = 0, head_dim: int = 0, out=None) -> torch.Tensor:
-    """Skinny GEMM with a fused epilogue (and optional RMSNorm prologue, ``norm_w``
-    with ``rowsq_tiles`` partial sums in ``scratch.rowsq``); Mpad 16 or 32.
+    """Skinny GEMM with a fused epilogue and optional RMSNorm (``norm``: the row
+    scale comes from ``rowsq_tiles`` partial sums of squares in ``scratch.rowsq``;
+    the norm weight must already be folded into ``wp``, see ``fold_norm``);
+    Mpad 16 or 32.
     mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
     "resid": residual += x W^T in place, writes per-tile row sums of squares;
     "rope": q -> q_out, RoPE'd k and v -> paged caches (``perm_rope_qkv`` order)."""
     Mpad, K = x.shape
     N = wp.shape[0] * 16
-    S = splits or choose_splits(N, K, Mpad)
+    S = splits or _FSPLITS.get((mode, N, K, Mpad)) or choose_splits(N, K, Mpad)
     m = _FUSED_MODES[mode]
     ntiles = N // 32
     if not _gpu(x):
-        return _skinny_fused_ref(x, wp, mode, scratch, norm_w, eps, rowsq_tiles, residual,
+        return _skinny_fused_ref(x, wp, mode, scratch, norm, eps, rowsq_tiles, residual,
                                  positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
                                  n_kv, head_dim, out)
     assert Mpad in (16, 32) and x.dtype == torch.bfloat16 and x.stride(1) == 1
@@ -733,24 +764,31 @@ def skinny_fused(x: torch.Tensor, wp: torch.Tensor, mode: str, scratch: FusedScr
     if mode == "silu":
         out = out if out is not None else torch.empty(Mpad, N // 2, dtype=torch.bfloat16,
                                                       device=x.device)
-    rs_in = scratch.rowsq if norm_w is not None else None
+    rs_in = scratch.rowsq if norm else None
     blk = k_cache.shape[2] if k_cache is not None else 0
     check(kernels().loqa_skinny_fused(
         ptr(x), x.stride(0), ptr(wp), ptr(part), ptr(scratch.counters), Mpad, N, K, S, m,
-        int(norm_w is not None), ptr(rs_in), rowsq_tiles, ptr(norm_w), eps, ptr(out),
+        int(norm), ptr(rs_in), rowsq_tiles, eps, ptr(out),
         ptr(residual), ptr(scratch.rowsq) if mode == "resid" else None, ptr(positions),
         ptr(cos_sin), ptr(q_out), ptr(k_cache), ptr(v_cache), ptr(slots), n_heads, n_kv,
         head_dim, blk, stream_ptr(x)), "skinny_fused")
     return out if mode == "silu" else (q_out if mode == "rope" else residual)
 
 
-def _skinny_fused_ref(x, wp, mode, scratch, norm_w, eps, rowsq_tiles, residual, positions,
+def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+    """Weight rows with an RMSNorm weight folded in (W * diag(g)), the operand
+    of a ``norm=True`` fused GEMM: rmsnorm(x) W^T = s(x) * (x (W diag(g))^T)."""
+    return (w.float() * norm_w.float()[None, :]).to(w.dtype)
+
+
+def _skinny_fused_ref(x, wp, mode, scratch, norm, eps, rowsq_tiles, residual, positions,
                       cos_sin, q_out, k_cache, v_cache, slots, H, Hkv, D, out):
     Mpad, K = x.shape
     N = wp.shape[0] * 16
-    rs = scratch.rowsq[: rowsq_tiles * Mpad].view(rowsq_tiles, Mpad) if norm_w is not None else None
-    xe = ref.fused_prologue(x, rs, norm_w, eps, K)
-    y = xe @ ref.unshuffle_weight(wp).float().t()  # [Mpad, N] in permuted row order
+    y = x.float() @ ref.unshuffle_weight(wp).float().t()  # [Mpad, N] in permuted row order
+    if norm:
+        rs = scratch.rowsq[: rowsq_tiles * Mpad].view(rowsq_tiles, Mpad)
+        y = y * ref.fused_row_scale(rs, eps, K)[:, None]
     if mode == "silu":
         F = N // 2
         inv = torch.argsort(ref.perm_gate_up(F))

@@ -46,7 +46,7 @@ _KERNEL_SIGS = {
     "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "loqa_skinny_fused": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                          c_int, c_int, c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p,
+                          c_int, c_int, c_void_p, c_int, c_float, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,

@@ -456,9 +456,7 @@ def perm_gate_up(F):
     return torch.tensor(rows, dtype=torch.long)
 
 
-def fused_prologue(x, rowsq_in, norm_w, eps, K):
-    if rowsq_in is None:
-        return x.float()
+def fused_row_scale(rowsq_in, eps, K):
+    """RMSNorm row scale 1/rms from per-tile partial sums of squares [tiles, Mpad]."""
     tot = rowsq_in.float().sum(0)  # [Mpad]
-    scale = torch.rsqrt(tot / K + eps)
-    return (x.float() * scale[:, None] * norm_w.float()[None, :]).to(torch.bfloat16).float()
+    return torch.rsqrt(tot / K + eps)

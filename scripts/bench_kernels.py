@@ -177,6 +177,41 @@ def tiny_bench():
         del wp
 
 
+def fused_bench():
+    """Fused-epilogue decode GEMMs vs plain skinny GEMM at each split (graph-timed)."""
+    scr = ops.FusedScratch(dev)
+    M, d, H, Hkv, D, blk = 16, 4096, 32, 8, 128, 16
+    res_ = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
+    scr.rowsq[: 128 * M].fill_(float(d) / 128)
+    pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
+    cs = torch.randn(4096, D // 2, 2, device=dev)
+    kc = torch.zeros(64, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slots = torch.arange(M, dtype=torch.int32, device=dev)
+    q = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
+    for name, (N, K), mode in (("qkv", (6144, 4096), "rope"), ("o", (4096, 4096), "resid"),
+                               ("gate_up", (28672, 4096), "silu"), ("down", (4096, 14336), "resid")):
+        wp = ops.shuffle_weight(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02)
+        xx = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        res = {"kernel": "graph_fused", "shape": name, "mode": mode}
+        for S in (1, 2, 4, 8):
+            if K % (S * 128):
+                continue
+            kw = dict(splits=S)
+            if mode == "rope":
+                kw.update(norm=True, rowsq_tiles=128, positions=pos, cos_sin=cs, q_out=q,
+                          k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv, head_dim=D)
+            elif mode == "silu":
+                kw.update(norm=True, rowsq_tiles=128)
+            else:
+                kw.update(residual=res_)
+            t = gtime(lambda: ops.skinny_fused(xx, wp, mode, scr, **kw), inner=10)
+            res[f"fusedS{S}_us"] = round(t, 2)
+            res[f"plainS{S}_us"] = round(gtime(lambda: ops.skinny_gemm(xx, wp, S), inner=10), 2)
+        emit(**res)
+        del wp
+
+
 def slab_bench():
     for M, d, S in ((16, 4096, 4), (16, 4096, 2), (32, 4096, 4)):
         part = torch.randn(S, M, d, device=dev)
@@ -196,6 +231,8 @@ if __name__ == "__main__":
         attn2_bench()
     if "tiny" in which:
         tiny_bench()
+    if "fused" in which:
+        fused_bench()
     if "gemm" in which:
         gemm_bench()
     if "attn" in which:

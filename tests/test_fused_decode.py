@@ -96,9 +96,9 @@ def test_fused_resid_rowsq_and_silu_gpu():
     assert torch.allclose(sq, res1.float().pow(2).sum(1), rtol=1e-3)
     wgu = (torch.randn(2 * F, d, device=dev) * 0.03).bfloat16()
     wn = torch.rand(d, device=dev).bfloat16() + 0.5
-    wp = ops.shuffle_weight(wgu[ref.perm_gate_up(F).to(dev)].contiguous())
+    wp = ops.shuffle_weight(ops.fold_norm(wgu, wn)[ref.perm_gate_up(F).to(dev)].contiguous())
     for S in (1, 2):
-        a = ops.skinny_fused(res1, wp, "silu", scr, splits=S, norm_w=wn, eps=1e-5,
+        a = ops.skinny_fused(res1, wp, "silu", scr, splits=S, norm=True, eps=1e-5,
                              rowsq_tiles=d // 32)
         h = ref.rmsnorm(res1, wn, 1e-5)
         expect = ref.silu_mul((h.float() @ wgu.float().t()).bfloat16())
