@@ -12,15 +12,25 @@
 //   O^T += V^T P^T : V goes through the wave's private LDS tile and is read with
 //                    ds_read_b64_tr_b16 (guide T10); P^T is the exp2'ed S^T
 //                    accumulator repacked to bf16 in registers.
-//   merge          : the 4 waves' (m, l, O^T) are merged through LDS by wave 0,
-//                    which writes one split partial; attn_decode_combine merges
-//                    the splits (sequences longer than split_keys).
+//   merge          : the 4 waves' (m, l, O^T) are merged through LDS by wave 0.
+//   split combine  : a sequence that fits one split is normalised and written
+//                    directly; otherwise wave 0 publishes its split partial
+//                    (sc1 write-through stores), takes a ticket on the
+//                    (sequence, kv head) counter, and the last arriving split
+//                    merges all partials (sc1 loads, fixed split order) and
+//                    writes the bf16 output - no second launch (guide §5
+//                    "In-launch split-K reduction", §6 Guideline 16).
+// Paged block-table entries are wave-uniform per 32-key tile (tiles are
+// 32-aligned, blk is a power of two >= 16), so they are scalar loads and the
+// K/V addresses need no per-lane dependent lookup.
 #include "common.h"
 
 #define DEC_TILE 32
 #define DEC_WAVES 4
 
 typedef short v4s_ __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float16v mfma32d(const bf16x8& a, const bf16x8& b, const float16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -48,11 +58,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     const int* __restrict__ block_tables, int max_blocks, int blk, int Hq, int Hkv,
     float scale_log2, int causal, int split_keys, int num_splits, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int total_q) {
+    float* __restrict__ part_ml, int total_q, int* __restrict__ counters, bf16_t* __restrict__ out,
+    long long o_stride) {
   constexpr int NS = D / 16, NDT = D / 32, CH = D / 8;
   constexpr int VPL = DEC_TILE * CH / 64;  // 16-byte V chunks per lane per tile
   __shared__ __attribute__((aligned(16))) DecSmem<D> sm;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar tile math
   const int h = lane >> 5, r = lane & 31;
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int G = Hq / Hkv;
@@ -93,17 +105,24 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     // issue K (-> registers) and V (-> registers -> LDS) loads of this wave's tile
     uint4 kraw[NS], vraw[VPL];
     {
+      // the tile's (at most two) cache blocks: wave-uniform scalar lookups
+      int base0 = 0, base1 = 0, bi0 = 0;
+      if (paged) {
+        bi0 = kt / blk;
+        base0 = bt[bi0];
+        base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? bt[bi0 + 1] : base0;
+      }
+      auto row_off = [&](int key) -> size_t {
+        if (paged) {
+          const int local = key - bi0 * blk;
+          const int bid = local >= blk ? base1 : base0;
+          return (((size_t)bid * Hkv + kvh) * blk + (local & (blk - 1))) * D;
+        }
+        return (kv0 + key) * (size_t)kv_stride + (size_t)kvh * D;
+      };
       const int key = kt + r;
       const bool ok = key < kend;
-      size_t off = 0;
-      if (ok) {
-        if (paged) {
-          const int bi = key / blk, bo = key - bi * blk;
-          off = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
-        } else {
-          off = (kv0 + key) * (size_t)kv_stride + (size_t)kvh * D;
-        }
-      }
+      const size_t off = row_off(ok ? key : kt);
 #pragma unroll
       for (int s = 0; s < NS; ++s)
         kraw[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
@@ -112,18 +131,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         const int c = lane + 64 * i;
         const int kr = c / CH, cc = (c - kr * CH) * 8;
         const int k2 = kt + kr;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (k2 < kend) {
-          size_t voff;
-          if (paged) {
-            const int bi = k2 / blk, bo = k2 - bi * blk;
-            voff = (((size_t)bt[bi] * Hkv + kvh) * blk + bo) * D;
-          } else {
-            voff = (kv0 + k2) * (size_t)kv_stride + (size_t)kvh * D;
-          }
-          v = *reinterpret_cast<const uint4*>(vc + voff + cc);
-        }
-        vraw[i] = v;
+        vraw[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + row_off(k2) + cc)
+                            : make_uint4(0, 0, 0, 0);
       }
     }
     // S^T = K Q^T
@@ -222,65 +231,108 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[dt][j] += sw * sm.o[w - 1][dt][j][lane];
   }
-  if (!row_valid) return;
   const size_t tok = (size_t)(q0 + qi);
-  float* po = part_o + (((size_t)split * total_q + tok) * Hq + head) * D;
+  const int nsplit = min(num_splits, max(1, (klen + split_keys - 1) / split_keys));
+  bf16_t* orow = out + tok * (size_t)o_stride + (size_t)head * D;
+  if (nsplit == 1) {
+    if (!row_valid) return;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
+                      acc[dt][4 * g4 + 3] * inv};
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+      }
+    return;
+  }
+  // publish this split's partial write-through, then take a ticket
+  const auto ro = __builtin_amdgcn_make_buffer_rsrc(
+      part_o, 0, (int)((size_t)num_splits * total_q * Hq * D * 4), 0x00020000);
+  const auto rm = __builtin_amdgcn_make_buffer_rsrc(
+      part_ml, 0, (int)((size_t)num_splits * total_q * Hq * 2 * 4), 0x00020000);
+  const int row = (int)tok * Hq + head;
+  if (row_valid) {
+    const int ob = (split * total_q * Hq + row) * D * 4;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4v v = {acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), ro,
+                                               ob + (32 * dt + 8 * g4 + 4 * h) * 4, 0, 16);
+      }
+    if (h == 0) {
+      const float2 ml = make_float2(mstar, l);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, ml), rm,
+                                            (split * total_q * Hq + row) * 8, 0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int* cnt = counters + (size_t)b * Hkv + kvh;
+  int t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != nsplit - 1) return;
+  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!row_valid) return;
+  // last split: merge every split's partial in split order (sc1 loads only)
+  float msx = -1e30f;
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const float2 ml = __builtin_bit_cast(
+        float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (sp * total_q * Hq + row) * 8, 0, 16));
+    msx = fmaxf(msx, ml.x);
+  }
+  float L = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[dt][j] = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const float2 ml = __builtin_bit_cast(
+        float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (sp * total_q * Hq + row) * 8, 0, 16));
+    const float w = exp2f(ml.x - msx);
+    L += w * ml.y;
+    const int ob = (sp * total_q * Hq + row) * D * 4;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4v v = __builtin_bit_cast(
+            float4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + (32 * dt + 8 * g4 + 4 * h) * 4, 0, 16));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[dt][4 * g4 + e] += w * v[e];
+      }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const int d0 = 32 * dt + 8 * g4 + 4 * h;
-      *reinterpret_cast<float4*>(po + d0) =
-          make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+      float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
+                    acc[dt][4 * g4 + 3] * inv};
+      *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
     }
-  if (h == 0) {
-    float* pm = part_ml + (((size_t)split * total_q + tok) * Hq + head) * 2;
-    pm[0] = mstar;
-    pm[1] = l;
-  }
-}
-
-// combine split partials (one workgroup of D threads per (token, head)); a
-// single split is a plain normalisation. Only the splits that hold keys of the
-// token's sequence were written (ceil(ctx / split_keys), at least one).
-__global__ void attn_decode_combine_kernel(const float* __restrict__ part_o,
-                                           const float* __restrict__ part_ml, bf16_t* __restrict__ o,
-                                           long long o_stride, int total_q, int Hq, int D,
-                                           int num_splits, const int* __restrict__ cu_q,
-                                           const int* __restrict__ ctx_lens, int B,
-                                           int split_keys) {
-  const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
-  int b = 0;
-  while (b < B - 1 && cu_q[b + 1] <= tok) ++b;
-  if (tok >= cu_q[B]) return;  // padding row
-  num_splits = min(num_splits, max(1, (ctx_lens[b] + split_keys - 1) / split_keys));
-  float mstar = -1e30f;
-  for (int s = 0; s < num_splits; ++s)
-    mstar = fmaxf(mstar, part_ml[(((size_t)s * total_q + tok) * Hq + head) * 2]);
-  float l = 0.f, acc = 0.f;
-  for (int s = 0; s < num_splits; ++s) {
-    const size_t idx = ((size_t)s * total_q + tok) * Hq + head;
-    const float w = exp2f(part_ml[idx * 2] - mstar);
-    l += w * part_ml[idx * 2 + 1];
-    acc += w * part_o[idx * D + d];
-  }
-  o[(size_t)tok * o_stride + (size_t)head * D + d] = f2bf(l > 0.f ? acc / l : 0.f);
 }
 
 // q: [Tq, >=Hq*D] bf16; K/V paged caches [nb, Hkv, blk, D] (block_tables) or
 // contiguous rows (kv_stride, kv_start); out [Tq, Hq*D] bf16.
-// Requires G * max_q <= 32 and split_keys % 32 == 0.
+// Requires G * max_q <= 32 and split_keys % 32 == 0; counters: >= B * Hkv zeroed ints
+// (left zeroed); paged blk a power of two >= 16.
 extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* kc, const void* vc,
                                 long long kv_stride, const int* kv_start, void* o,
                                 long long o_stride, const int* cu_q, const int* ctx_lens,
                                 const int* block_tables, int max_blocks, int blk, int B, int max_q,
                                 int Hq, int Hkv, int D, float scale, int causal, int split_keys,
                                 int num_splits, float* part_o, float* part_ml, int total_q,
-                                hipStream_t s) {
+                                int* counters, hipStream_t s) {
   if (B <= 0 || total_q <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv || (Hq / Hkv) * max_q > 32 || split_keys % DEC_TILE || num_splits < 1 ||
-      (D != 64 && D != 128) || !part_o || !part_ml)
+      (D != 64 && D != 128) || !part_o || !part_ml || !counters)
     return (int)hipErrorInvalidValue;
+  if (block_tables && (blk < 16 || (blk & (blk - 1)))) return (int)hipErrorInvalidValue;
   if (!block_tables && (!kv_start || kv_stride % 8)) return (int)hipErrorInvalidValue;
   dim3 grid(num_splits, Hkv, B);
   const float sl2 = scale * 1.4426950408889634f;
@@ -288,16 +340,11 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
     hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
                        block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
-                       part_o, part_ml, total_q);
+                       part_o, part_ml, total_q, counters, (bf16_t*)o, o_stride);
   else
     hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
                        block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
-                       part_o, part_ml, total_q);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(total_q, Hq), dim3(D), 0, s, part_o, part_ml,
-                     (bf16_t*)o, o_stride, total_q, Hq, D, num_splits, cu_q, ctx_lens, B,
-                     split_keys);
+                       part_o, part_ml, total_q, counters, (bf16_t*)o, o_stride);
   return (int)hipGetLastError();
 }

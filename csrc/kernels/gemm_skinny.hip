@@ -213,19 +213,33 @@ extern "C" int loqa_shuffle_weight(const void* W, void* Wp, int N, int K, hipStr
 // Weight rows are permuted at load time so one 32-row tile holds (gate, up)
 // feature pairs, or the (c, c + D/2) RoPE pairs of one head.
 typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-enum { EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3 };
+enum { EPI_SILU = 1, EPI_RESID = 2, EPI_ROPE = 3, EPI_ACT = 4 };
+enum { NORM_NONE = 0, NORM_RMS = 1, NORM_LN = 2 };
+
+// Host-side parameter block (mirrored by a ctypes.Structure in ops/_lib.py).
+struct FusedParams {
+  const void* x; long long ldx; const void* Wp; float* part; int* counters;
+  int Mpad, N, K, S, mode, norm;
+  const float* rowsq_in; const float* rowsum_in; int rowstat_tiles; float eps;
+  const float* colsum; const float* bias;
+  void* out; long long ldo; int act;
+  void* residual; float* rowsq_out; float* rowsum_out;
+  const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
+  int H, Hkv, D, blk;
+};
 
 struct FusedArgs {
   const bf16_t* x; long long ldx; const bf16_t* Wp; float* part; int N, K, S, Mpad;
   int* counters;
-  const float* rowsq_in; int rowsq_tiles; float eps;   // NORM row scale
-  bf16_t* silu_out; int F;                                                    // EPI_SILU
-  bf16_t* residual; float* rowsq_out;                                         // EPI_RESID
+  const float* rowsq_in; const float* rowsum_in; int rowstat_tiles; float eps;  // norm row stats
+  const float* colsum; const float* bias;   // LayerNorm mean correction, output bias (per row of W)
+  bf16_t* out; long long ldo; int act;                                        // EPI_SILU / EPI_ACT
+  bf16_t* residual; float* rowsq_out; float* rowsum_out;                      // EPI_RESID
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
 };
 
-template <int MT, int U, int MODE, bool NORM>
+template <int MT, int U, int MODE, int NORM>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   __shared__ float4v_ red[3][2 * MT][64];
   float* sred = reinterpret_cast<float*>(&red[0][0][0]);   // aliases: prologue / ticket
@@ -239,25 +253,50 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   const bf16_t* wp = a.Wp + (size_t)(tile * 2) * tile_stride + (size_t)lane * 8;
   const bf16_t* xp = a.x + (size_t)(lane & 15) * a.ldx + 8 * (lane >> 4);
 
-  float sc[MT];
+  float sc[MT], mu[MT];
 #pragma unroll
-  for (int j = 0; j < MT; ++j) sc[j] = 1.f;
-  if constexpr (NORM) {
-    // row scale = rsqrt(mean of squares) from the producer's per-tile partial sums
+  for (int j = 0; j < MT; ++j) sc[j] = 1.f, mu[j] = 0.f;
+  if constexpr (NORM != NORM_NONE) {
+    // row statistics from the producer's per-tile partial sums (fixed order):
+    // RMSNorm scale rsqrt(E[x^2] + eps); LayerNorm also the mean
     const int Mp = a.Mpad, G = 256 / Mp;
     const int m = threadIdx.x % Mp, g = threadIdx.x / Mp;
-    float acc = 0.f;
-    for (int t = g; t < a.rowsq_tiles; t += G) acc += a.rowsq_in[(size_t)t * Mp + m];
-    sred[g * Mp + m] = acc;
+    // every load issued before any add (a dependent loop would serialise
+    // up to 16 memory latencies); host guarantees rowstat_tiles * Mpad <= 4096
+    float vq[16], vs[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int t = g + i * G;
+      const bool ok = t < a.rowstat_tiles;
+      vq[i] = ok ? a.rowsq_in[(size_t)t * Mp + m] : 0.f;
+      if constexpr (NORM == NORM_LN) vs[i] = ok ? a.rowsum_in[(size_t)t * Mp + m] : 0.f;
+    }
+    float aq = 0.f, as = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      aq += vq[i];
+      if constexpr (NORM == NORM_LN) as += vs[i];
+    }
+    sred[g * Mp + m] = aq;
+    if constexpr (NORM == NORM_LN) sred[512 + g * Mp + m] = as;
     __syncthreads();
     if (threadIdx.x < Mp) {
-      float tot = 0.f;
-      for (int q = 0; q < G; ++q) tot += sred[q * Mp + threadIdx.x];
-      sred[256 + threadIdx.x] = rsqrtf(tot / (float)a.K + a.eps);
+      float tq = 0.f, ts = 0.f;
+      for (int q = 0; q < G; ++q) {
+        tq += sred[q * Mp + threadIdx.x];
+        if constexpr (NORM == NORM_LN) ts += sred[512 + q * Mp + threadIdx.x];
+      }
+      const float mean = ts / (float)a.K;
+      const float var = fmaxf(tq / (float)a.K - mean * mean, 0.f);
+      sred[256 + threadIdx.x] = rsqrtf(var + a.eps);
+      sred[256 + 64 + threadIdx.x] = mean;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < MT; ++j) sc[j] = sred[256 + j * 16 + (lane & 15)];
+    for (int j = 0; j < MT; ++j) {
+      sc[j] = sred[256 + j * 16 + (lane & 15)];
+      mu[j] = sred[256 + 64 + j * 16 + (lane & 15)];
+    }
     __syncthreads();
   }
 
@@ -344,16 +383,40 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     return;
   }
 
-  // RMSNorm: the norm weight is folded into W at load time, so the row scale
-  // factors out of the k-sum and is applied once here
-  if constexpr (NORM) {
+  // ---- epilogue (wave 0): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
+  const int nq = 4 * (lane >> 4);
+  // Norms: the norm weight g is folded into W at load time, so the row scale
+  // factors out of the k-sum: RMSNorm  y = s * (W g) x;  LayerNorm
+  // y = s * ((W g) x - mean * colsum) with colsum[n] = sum_k (W g)[n][k]; the
+  // LayerNorm shift (W b) is folded into the bias.
+  if constexpr (NORM == NORM_RMS) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] *= sc[j];
+  } else if constexpr (NORM == NORM_LN) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4 cv = *reinterpret_cast<const float4*>(a.colsum + tile * 32 + i * 16 + nq);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        acc[i][j][0] = sc[j] * (acc[i][j][0] - mu[j] * cv.x);
+        acc[i][j][1] = sc[j] * (acc[i][j][1] - mu[j] * cv.y);
+        acc[i][j][2] = sc[j] * (acc[i][j][2] - mu[j] * cv.z);
+        acc[i][j][3] = sc[j] * (acc[i][j][3] - mu[j] * cv.w);
+      }
+    }
   }
-  // ---- epilogue (wave 0): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
-  const int nq = 4 * (lane >> 4);
+  if (a.bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4 bv = *reinterpret_cast<const float4*>(a.bias + tile * 32 + i * 16 + nq);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        acc[i][j][0] += bv.x; acc[i][j][1] += bv.y; acc[i][j][2] += bv.z; acc[i][j][3] += bv.w;
+      }
+    }
+  }
   if constexpr (MODE == EPI_SILU) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
@@ -367,13 +430,13 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       uint2 w2;
       w2.x = pack_bf16x2(o[0], o[1]);
       w2.y = pack_bf16x2(o[2], o[3]);
-      *reinterpret_cast<uint2*>(a.silu_out + (size_t)m * a.F + tile * 16 + nq) = w2;
+      *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * 16 + nq) = w2;
     }
   } else if constexpr (MODE == EPI_RESID) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       const int m = j * 16 + (lane & 15);
-      float sq = 0.f;
+      float sq = 0.f, sm = 0.f;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         bf16_t* rp = a.residual + (size_t)m * a.N + tile * 32 + i * 16 + nq;
@@ -387,10 +450,16 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         w2.y = pack_bf16x2(h2, h3);
         *reinterpret_cast<uint2*>(rp) = w2;
         sq += h0 * h0 + h1 * h1 + h2 * h2 + h3 * h3;
+        sm += h0 + h1 + h2 + h3;
       }
       sq += __shfl_xor(sq, 16, 64);
       sq += __shfl_xor(sq, 32, 64);
-      if (lane < 16) a.rowsq_out[(size_t)tile * a.Mpad + m] = sq;
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      if (lane < 16) {
+        a.rowsq_out[(size_t)tile * a.Mpad + m] = sq;
+        if (a.rowsum_out) a.rowsum_out[(size_t)tile * a.Mpad + m] = sm;
+      }
     }
   } else if constexpr (MODE == EPI_ROPE) {
     const int D = a.D, half = D >> 1, tph = D / 32;
@@ -403,14 +472,19 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         const bool isk = tile >= nq_t;
         const int tt = isk ? tile - nq_t : tile;
         const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
-        const float2* e = a.cs + (size_t)a.positions[m] * half + c;
         float ra[4], rb[4];
+        if (a.cs) {
+          const float2* e = a.cs + (size_t)a.positions[m] * half + c;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x0 = bf2f(f2bf(acc[0][j][r])), x1 = bf2f(f2bf(acc[1][j][r]));
-          const float2 cs = e[r];
-          ra[r] = x0 * cs.x - x1 * cs.y;
-          rb[r] = x1 * cs.x + x0 * cs.y;
+          for (int r = 0; r < 4; ++r) {
+            const float x0 = bf2f(f2bf(acc[0][j][r])), x1 = bf2f(f2bf(acc[1][j][r]));
+            const float2 cs = e[r];
+            ra[r] = x0 * cs.x - x1 * cs.y;
+            rb[r] = x1 * cs.x + x0 * cs.y;
+          }
+        } else {  // no rotary embedding (Whisper): plain q / k halves
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ra[r] = acc[0][j][r], rb[r] = acc[1][j][r];
         }
         uint2 lo, hi;
         lo.x = pack_bf16x2(ra[0], ra[1]); lo.y = pack_bf16x2(ra[2], ra[3]);
@@ -439,10 +513,28 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         }
       }
     }
+  } else if constexpr (MODE == EPI_ACT) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = bf2f(f2bf(acc[i][j][r]));
+          o[r] = a.act == 1 ? 0.5f * x * (1.f + erff(x * 0.70710678118654752f)) : x;
+        }
+        uint2 w2;
+        w2.x = pack_bf16x2(o[0], o[1]);
+        w2.y = pack_bf16x2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * 32 + i * 16 + nq) = w2;
+      }
+    }
   }
 }
 
-template <int MT, int MODE, bool NORM>
+template <int MT, int MODE, int NORM>
 static int launch_fused(const FusedArgs& a, hipStream_t st) {
   dim3 grid(a.N / 32, a.S);
   const int kw = a.K / 32 / (a.S * 4);
@@ -455,38 +547,50 @@ static int launch_fused(const FusedArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <int MODE, bool NORM>
+template <int MODE, int NORM>
 static int dispatch_fused(const FusedArgs& a, hipStream_t st) {
   return a.Mpad == 16 ? launch_fused<1, MODE, NORM>(a, st) : launch_fused<2, MODE, NORM>(a, st);
 }
 
-// mode: 1 silu (out [Mpad, N/2]), 2 residual+rowsq, 3 rope+append. norm: x is
-// the bf16 residual, Wp has the norm weight folded in, and the accumulator is
-// scaled by rsqrt(sum(rowsq_in over tiles) / K + eps) per row.
-// part: S * Mpad * N f32 scratch (S > 1, tile-contiguous slabs); counters: >= N/32 zeroed ints.
-extern "C" int loqa_skinny_fused(const void* x, long long ldx_, const void* Wp, float* part,
-                                 int* counters, int Mpad, int N, int K, int S, int mode, int norm,
-                                 const float* rowsq_in, int rowsq_tiles,
-                                 float eps, void* silu_out, void* residual, float* rowsq_out,
-                                 const int* positions, const void* cs, void* q_out, void* kc,
-                                 void* vc, const int* slots, int H, int Hkv, int D, int blk,
-                                 hipStream_t st) {
-  if (S < 1 || K % (S * 128) || ldx_ % 8 || N % 32 || (Mpad != 16 && Mpad != 32))
+template <int MODE>
+static int dispatch_norm(const FusedArgs& a, int norm, hipStream_t st) {
+  switch (norm) {
+    case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, st);
+    case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, st);
+    case NORM_LN: return dispatch_fused<MODE, NORM_LN>(a, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// mode: 1 silu (out [Mpad, ldo >= N/2]), 2 residual (+bias) + row sum-of-squares
+// (+ row sums), 3 (RoPE if cs) + paged KV append + q, 4 act(bias + x W^T) -> out
+// (act 0 identity, 1 GELU-erf). norm: 1 RMSNorm / 2 LayerNorm of x (the bf16
+// residual) with the norm weight folded into Wp; the row statistics come from
+// rowstat_tiles partial sums. part: S * Mpad * N f32 scratch (S > 1,
+// tile-contiguous slabs); counters: >= N/32 zeroed ints.
+extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
+  const int Mpad = p->Mpad, N = p->N, K = p->K, S = p->S;
+  if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 || (Mpad != 16 && Mpad != 32))
     return (int)hipErrorInvalidValue;
-  if (S > 1 && (!part || !counters)) return (int)hipErrorInvalidValue;
-  if (norm && (!rowsq_in || rowsq_tiles < 1)) return (int)hipErrorInvalidValue;
-  if (mode == EPI_ROPE && (D % 32 || N != (H + 2 * Hkv) * D)) return (int)hipErrorInvalidValue;
-  FusedArgs a{(const bf16_t*)x, ldx_, (const bf16_t*)Wp, part, N, K, S, Mpad, counters,
-              rowsq_in, rowsq_tiles, eps, (bf16_t*)silu_out, N / 2,
-              (bf16_t*)residual, rowsq_out, positions, (const float2*)cs, (bf16_t*)q_out,
-              (bf16_t*)kc, (bf16_t*)vc, slots, H, Hkv, D, blk};
-  switch (mode * 2 + (norm ? 1 : 0)) {
-    case EPI_SILU * 2: return dispatch_fused<EPI_SILU, false>(a, st);
-    case EPI_SILU * 2 + 1: return dispatch_fused<EPI_SILU, true>(a, st);
-    case EPI_RESID * 2: return dispatch_fused<EPI_RESID, false>(a, st);
-    case EPI_RESID * 2 + 1: return dispatch_fused<EPI_RESID, true>(a, st);
-    case EPI_ROPE * 2: return dispatch_fused<EPI_ROPE, false>(a, st);
-    case EPI_ROPE * 2 + 1: return dispatch_fused<EPI_ROPE, true>(a, st);
+  if (S > 1 && (!p->part || !p->counters)) return (int)hipErrorInvalidValue;
+  if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1 || p->rowstat_tiles * Mpad > 4096))
+    return (int)hipErrorInvalidValue;
+  if (p->norm == NORM_LN && (!p->rowsum_in || !p->colsum)) return (int)hipErrorInvalidValue;
+  if (p->mode == EPI_ROPE && (p->D % 32 || N != (p->H + 2 * p->Hkv) * p->D))
+    return (int)hipErrorInvalidValue;
+  if ((p->mode == EPI_SILU || p->mode == EPI_ACT) && (!p->out || p->ldo % 4))
+    return (int)hipErrorInvalidValue;
+  if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
+  FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
+              p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,
+              p->bias, (bf16_t*)p->out, p->ldo, p->act, (bf16_t*)p->residual, p->rowsq_out,
+              p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
+              (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
+  switch (p->mode) {
+    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, st);
+    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, st);
+    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, st);
+    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

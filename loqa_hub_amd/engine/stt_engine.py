@@ -19,7 +19,7 @@ import torch
 
 from .. import ops
 from ..models.configs import WhisperConfig
-from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast
+from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
@@ -45,7 +45,8 @@ class STTEngine:
     SPLIT_KEYS = 128
 
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
-                 block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True):
+                 block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
+                 fused: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.weights = WhisperWeights(cfg, self.device, seed=seed)
@@ -66,6 +67,9 @@ class STTEngine:
         self.stats = {"utterances": 0, "decode_steps": 0}
         self.max_batch = max_batch
         self.fast_decode = fast_decode
+        # fused-epilogue decoder GEMMs (8 launches per layer) for Mpad <= 32
+        self.fused = fused and fast_decode
+        self.scratch = ops.FusedScratch(self.device) if self.fused else None
         self.use_graphs = use_graphs and self.is_gpu and fast_decode
         self.self_splits = (cfg.n_text_ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS
         if fast_decode and self.is_gpu:
@@ -185,6 +189,13 @@ class STTEngine:
         return out
 
     def _fast_forward(self, dev: dict, max_q: int, B_pad: int) -> torch.Tensor:
+        if self.fused and dev["tokens"].numel() <= 32:
+            logits = decode_step_fused(self.model, dev["tokens"], dev["positions"], dev["slots"],
+                                       dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
+                                       self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
+                                       dev["enc_lens"], dev["logit_idx"], self.ws, self.scratch,
+                                       self.self_splits, self.SPLIT_KEYS)
+            return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
         logits = decode_step_fast(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                   dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
                                   self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],

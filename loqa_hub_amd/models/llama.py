@@ -137,37 +137,13 @@ class LlamaWeights:
             self._tune_fused()
 
     def _tune_fused(self) -> None:
-        """Measure the split-K of each fused decode GEMM (layer-0 weights, dummy
-        activations / caches) for Mpad 16 and 32; before any graph capture."""
-        dev, D, d = self.embed.device, self.cfg.head_dim, self.cfg.d_model
-        P = self.decode_layers[0]
-        scr = ops.FusedScratch(dev)
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        blk = 16
-        kc = torch.zeros(4, self.hkv, blk, D, **bf)
-        vc = torch.zeros_like(kc)
-        for Mpad in (16, 32):
-            scr.rowsq[: d // 32 * Mpad].fill_(float(d) / (d // 32))
-            res = torch.randn(Mpad, d, **bf)
-            pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
-            q = torch.empty(Mpad, self.h * D, **bf)
-            a = torch.randn(Mpad, self.h * D, **bf)
-            f = torch.randn(Mpad, self.f, **bf)
-            jobs = {
-                "rope": (P["wqkv_f"], lambda s, w: ops.skinny_fused(
-                    res, w, "rope", scr, splits=s, norm=True, rowsq_tiles=d // 32, positions=pos,
-                    cos_sin=self.cos_sin, q_out=q, k_cache=kc, v_cache=vc, slots=pos,
-                    n_heads=self.h, n_kv=self.hkv, head_dim=D)),
-                "silu": (P["w_gate_up_f"], lambda s, w: ops.skinny_fused(
-                    res, w, "silu", scr, splits=s, norm=True, rowsq_tiles=d // 32)),
-                "resid_o": (P["wo"], lambda s, w: ops.skinny_fused(
-                    a, w, "resid", scr, splits=s, residual=res.clone())),
-                "resid_down": (P["w_down"], lambda s, w: ops.skinny_fused(
-                    f, w, "resid", scr, splits=s, residual=res.clone())),
-            }
-            for name, (w, run) in jobs.items():
-                N, K = w.shape[0] * 16, w.shape[1] * 32
-                ops.tune_fused_splits((name.split("_")[0], N, K, Mpad), lambda s: run(s, w), K)
+        """Measure the split-K of each fused decode GEMM shape (layer-0 weights)."""
+        P, D = self.decode_layers[0], self.cfg.head_dim
+        ops.tune_fused(P["wqkv_f"], "rope", norm="rms", heads=(self.h, self.hkv, D),
+                       cos_sin=self.cos_sin)
+        ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms")
+        ops.tune_fused(P["wo"], "resid")
+        ops.tune_fused(P["w_down"], "resid")
 
     @classmethod
     def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":

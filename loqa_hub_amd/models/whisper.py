@@ -73,10 +73,34 @@ class WhisperWeights:
         self.lm_head_p = ops.shuffle_weight(lm)
         del lm
         self.dec_p = [{k: ops.shuffle_weight(L[k]) for k in DEC_PROJ} for L in self.dec]
+        # fused-epilogue copies: LayerNorm weight folded into qkv / xq / fc1 rows,
+        # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
+        # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)
+        self.dec_f = [self._fused_layer(L) for L in self.dec]
         if torch.device(device).type == "cuda":
             for k in DEC_PROJ:
                 ops.tune_skinny_splits(self.dec_p[0][k], mpads=(16, 32))
             ops.tune_skinny_splits(self.lm_head_p, mpads=(16, 32))
+            F = self.dec_f[0]
+            ops.tune_fused(F["qkv"], "rope", heads=(cfg.n_heads, cfg.n_heads, cfg.head_dim))
+            ops.tune_fused(F["o"], "resid")
+            ops.tune_fused(F["xq"], "act")
+            ops.tune_fused(F["fc1"], "act", act="gelu")
+            ops.tune_fused(F["fc2"], "resid")
+
+    def _fused_layer(self, L: dict) -> dict:
+        H, D = self.cfg.n_heads, self.cfg.head_dim
+        perm = ops.reference.perm_rope_qkv(H, H, D).to(L["wqkv"].device)
+        FL = ops.FusedLinear
+        return {
+            "qkv": FL(L["wqkv"], norm="ln", norm_w=L["ln1_w"], norm_b=L["ln1_b"], bias=L["bqkv"],
+                      perm=perm),
+            "o": FL(L["wo"], bias=L["bo"]),
+            "xq": FL(L["xq"], norm="ln", norm_w=L["lnx_w"], norm_b=L["lnx_b"], bias=L["xq_b"]),
+            "xo": FL(L["xo"], bias=L["xo_b"]),
+            "fc1": FL(L["fc1"], norm="ln", norm_w=L["ln2_w"], norm_b=L["ln2_b"], bias=L["fc1_b"]),
+            "fc2": FL(L["fc2"], bias=L["fc2_b"]),
+        }
 
     @staticmethod
     def _block(rnd, zeros, ones, d, f, cross: bool) -> dict:
@@ -234,6 +258,55 @@ def decode_step_fast(model: "WhisperModel", tokens: torch.Tensor, positions: tor
         part = ops.skinny_gemm(m, P["fc2"])
     hf = ops.slab_layernorm(part, residual, w.dec_ln_w, w.dec_ln_b, 1e-5,
                             bias=w.dec[-1]["fc2_b"], row_idx=logit_idx, write_residual=False)
+    return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
+
+
+def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: torch.Tensor,
+                      slots: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor,
+                      block_tables: torch.Tensor, max_q: int, k_cache: torch.Tensor,
+                      v_cache: torch.Tensor, xkv: list[torch.Tensor], enc_starts: torch.Tensor,
+                      enc_lens: torch.Tensor, logit_idx: torch.Tensor, ws, scratch,
+                      self_splits: int, split_keys: int = 128,
+                      cross_split_keys: int = 512) -> torch.Tensor:
+    """Decoder step on the fused-epilogue GEMMs: 8 launches per layer.
+
+    qkv   (LayerNorm ln1 prologue | bias + q / paged K,V append epilogue) ->
+    self-attention -> o (bias + residual + row sum / sum-of-squares) ->
+    xq    (LayerNorm lnx | bias) -> cross-attention over the encoder rows ->
+    xo    (bias + residual + row stats) -> fc1 (LayerNorm ln2 | bias + GELU) ->
+    fc2   (bias + residual + row stats).
+    The LayerNorm statistics of a row come from the previous residual
+    epilogue's per-tile partial sums, so no separate norm launch exists. Same
+    contract as ``decode_step_fast``; Mpad (tokens rows) 16 or 32."""
+    cfg, w = model.cfg, model.w
+    d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
+    enc_splits = (cfg.n_audio_ctx + cross_split_keys - 1) // cross_split_keys
+    Mpad = tokens.numel()
+    residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
+    scratch.seed_stats(residual)
+    tiles = d // 32
+    q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
+    for i, F in enumerate(w.dec_f):
+        ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5,
+                         rowsq_tiles=1 if i == 0 else tiles, positions=positions, q_out=q,
+                         k_cache=k_cache[i], v_cache=v_cache[i], slots=slots, n_heads=H, n_kv=H,
+                         head_dim=D)
+        a = ops.attention(q, k_cache[i], v_cache[i], cu_q, n_heads=H, n_kv=H, head_dim=D,
+                          causal=True, max_q=max_q, ctx_lens=ctx_lens, block_tables=block_tables,
+                          grouped=True, split_keys=split_keys, num_splits=self_splits,
+                          workspace=ws)
+        ops.skinny_fused(a, F["o"], "resid", scratch, residual=residual, row_sums=True)
+        xq = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5, rowsq_tiles=tiles)
+        kv = xkv[i]
+        a = ops.attention(xq, kv, kv[:, d:], cu_q, n_heads=H, n_kv=H, head_dim=D, causal=False,
+                          max_q=max_q, cu_k=enc_starts, ctx_lens=enc_lens, grouped=True,
+                          split_keys=cross_split_keys, num_splits=enc_splits, workspace=ws)
+        ops.skinny_fused(a, F["xo"], "resid", scratch, residual=residual, row_sums=True)
+        m = ops.skinny_fused(residual, F["fc1"], "act", scratch, act="gelu", eps=1e-5,
+                             rowsq_tiles=tiles)
+        ops.skinny_fused(m, F["fc2"], "resid", scratch, residual=residual, row_sums=True)
+    sel = residual.index_select(0, logit_idx).contiguous()
+    hf = ops.layernorm(sel, w.dec_ln_w, w.dec_ln_b, 1e-5)
     return ops.skinny_gemm(hf, w.lm_head_p, 1)[0]
 
 

@@ -14,12 +14,13 @@ elementwise/normalisation/attention/audio op around them is ours.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
 
 from . import reference as ref
-from ._lib import check, kernels, ptr, stream_ptr
+from ._lib import FusedParams, check, kernels, ptr, stream_ptr
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -141,6 +142,9 @@ class AttnWorkspace:
                                   device=device)
         self.part_ml = torch.empty(max_splits * max_tokens * n_heads * 2, dtype=torch.float32,
                                    device=device)
+        # split-arrival tickets of the decode kernel's in-launch combine, one per
+        # (sequence, kv head); the last arriving split resets its counter
+        self.counters = torch.zeros(max_tokens * n_heads, dtype=torch.int32, device=device)
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Tensor, *,
@@ -196,14 +200,15 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Ten
         # split-key decode kernel (attn_decode.hip): paged cache, or contiguous
         # rows at per-sequence starts cu_k[b] with lengths ctx_lens[b]
         assert workspace is not None and workspace.max_splits >= num_splits
-        assert workspace.max_tokens >= Tq
+        assert workspace.max_tokens >= Tq and B * n_kv <= workspace.counters.numel()
+        assert not paged or (blk >= 16 and blk & (blk - 1) == 0)
         kv_stride = 0 if paged else k.stride(0)
         check(kernels().loqa_attn_decode(
             ptr(q), q.stride(0), ptr(k), ptr(v), kv_stride, None if paged else ptr(cu_k),
             ptr(out), out.stride(0), ptr(cu_q), ptr(ctx_lens),
             ptr(block_tables) if paged else None, max_blocks, blk, B, max_q, n_heads, n_kv,
             head_dim, scale, int(causal), split_keys, num_splits, ptr(workspace.part_o),
-            ptr(workspace.part_ml), Tq, stream_ptr(q)),
+            ptr(workspace.part_ml), Tq, ptr(workspace.counters), stream_ptr(q)),
             "attn_decode")
         return out
     if grouped:
@@ -725,54 +730,97 @@ def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F:
 # ------------------------------------------------------------ fused decode GEMMs
 class FusedScratch:
     """Device state shared by the fused decode GEMMs of one engine: split-K
-    ticket counters (zeroed once; each reducer resets its own) and the row
-    sum-of-squares partials handed from the residual epilogues to the next
-    GEMM's RMSNorm prologue."""
+    ticket counters (zeroed once; each reducer resets its own) and the per-tile
+    row statistics (sums of squares, sums) handed from the residual epilogues to
+    the next GEMM's norm prologue."""
 
     def __init__(self, device, max_tiles: int = 8192, max_rows: int = 32):
         self.counters = torch.zeros(max_tiles, dtype=torch.int32, device=device)
         self.rowsq = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
+        self.rowsum = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
+
+    def seed_stats(self, x: torch.Tensor) -> None:
+        """Row statistics of ``x`` as ONE partial tile (layer 0's norm input)."""
+        M = x.shape[0]
+        xf = x.float()
+        torch.sum(xf.square(), 1, out=self.rowsq[:M])
+        torch.sum(xf, 1, out=self.rowsum[:M])
 
 
-_FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3}
+_FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3, "act": 4}
+_NORMS = {None: 0, False: 0, True: 1, "rms": 1, "ln": 2}
+_ACTS = {"none": 0, "gelu": 1}
 
 
-def skinny_fused(x: torch.Tensor, wp: torch.Tensor, mode: str, scratch: FusedScratch, *,
-                 splits: int | None = None, norm: bool = False,
-                 eps: float = 1e-5, rowsq_tiles: int = 0, residual: torch.Tensor | None = None,
-                 positions=None, cos_sin=None, q_out=None, k_cache=None, v_cache=None, slots=None,
-                 n_heads: int = 0, n_kv: int = 0, head_dim: int = 0, out=None) -> torch.Tensor:
-    """Skinny GEMM with a fused epilogue and optional RMSNorm (``norm``: the row
-    scale comes from ``rowsq_tiles`` partial sums of squares in ``scratch.rowsq``;
-    the norm weight must already be folded into ``wp``, see ``fold_norm``);
-    Mpad 16 or 32.
-    mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
-    "resid": residual += x W^T in place, writes per-tile row sums of squares;
-    "rope": q -> q_out, RoPE'd k and v -> paged caches (``perm_rope_qkv`` order)."""
-    Mpad, K = x.shape
-    N = wp.shape[0] * 16
-    S = splits or _FSPLITS.get((mode, N, K, Mpad)) or choose_splits(N, K, Mpad)
-    m = _FUSED_MODES[mode]
-    ntiles = N // 32
-    if not _gpu(x):
-        return _skinny_fused_ref(x, wp, mode, scratch, norm, eps, rowsq_tiles, residual,
-                                 positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
-                                 n_kv, head_dim, out)
-    assert Mpad in (16, 32) and x.dtype == torch.bfloat16 and x.stride(1) == 1
-    assert ntiles <= scratch.counters.numel()
-    part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device) if S > 1 else None
-    if mode == "silu":
-        out = out if out is not None else torch.empty(Mpad, N // 2, dtype=torch.bfloat16,
-                                                      device=x.device)
-    rs_in = scratch.rowsq if norm else None
-    blk = k_cache.shape[2] if k_cache is not None else 0
-    check(kernels().loqa_skinny_fused(
-        ptr(x), x.stride(0), ptr(wp), ptr(part), ptr(scratch.counters), Mpad, N, K, S, m,
-        int(norm), ptr(rs_in), rowsq_tiles, eps, ptr(out),
-        ptr(residual), ptr(scratch.rowsq) if mode == "resid" else None, ptr(positions),
-        ptr(cos_sin), ptr(q_out), ptr(k_cache), ptr(v_cache), ptr(slots), n_heads, n_kv,
-        head_dim, blk, stream_ptr(x)), "skinny_fused")
-    return out if mode == "silu" else (q_out if mode == "rope" else residual)
+class FusedLinear:
+    """A decode projection prepared for the fused GEMM: the pre-shuffled weight
+    (rows optionally permuted), with the input norm's weight folded into it and
+    the norm's shift / the linear bias folded into one f32 output bias.
+
+    norm "rms": rmsnorm(x; g) W^T            -> s * (W g) x
+    norm "ln" : layernorm(x; g, b) W^T + c   -> s * ((W g) x - mean * colsum) + (W b + c)
+    """
+
+    def __init__(self, w: torch.Tensor, *, norm: str | None = None, norm_w=None, norm_b=None,
+                 bias=None, perm: torch.Tensor | None = None):
+        wf = w.float()
+        self.norm = norm
+        if norm is not None:
+            wf = wf * norm_w.float()[None, :]
+        wb = wf.to(torch.bfloat16)
+        b = torch.zeros(w.shape[0], dtype=torch.float32, device=w.device)
+        if bias is not None:
+            b = b + bias.float()
+        if norm == "ln" and norm_b is not None:
+            b = b + w.float() @ norm_b.float()
+        self.colsum = wb.float().sum(1) if norm == "ln" else None
+        self.has_bias = bias is not None or (norm == "ln" and norm_b is not None)
+        if perm is not None:
+            wb = wb[perm]
+            b = b[perm]
+            if self.colsum is not None:
+                self.colsum = self.colsum[perm].contiguous()
+        self.bias = b.contiguous() if self.has_bias else None
+        self.wp = shuffle_weight(wb.contiguous())
+        self.N, self.K = w.shape
+
+
+def tune_fused(wp, mode: str, *, mpads=(16, 32), norm=None, act: str = "none",
+               heads: tuple | None = None, cos_sin=None) -> None:
+    """Measure the split-K of one fused decode GEMM shape on dummy operands
+    (``heads`` = (H, Hkv, D) for "rope"); before any graph capture."""
+    lin = wp if isinstance(wp, FusedLinear) else None
+    w = lin.wp if lin is not None else wp
+    if not _gpu(w):
+        return
+    dev = w.device
+    N, K = w.shape[0] * 16, w.shape[1] * 32
+    scr = FusedScratch(dev)
+    bf = dict(dtype=torch.bfloat16, device=dev)
+    nrm = norm if norm is not None else (lin.norm if lin is not None else None)
+    for Mpad in mpads:
+        key = (mode, N, K, Mpad)
+        if key in _FSPLITS:
+            continue
+        x = torch.randn(Mpad, K, **bf)
+        kw: dict = {}
+        if nrm:
+            tiles = max(1, K // 32)
+            scr.rowsq[: tiles * Mpad].fill_(float(K) / tiles)
+            kw.update(rowsq_tiles=tiles)
+        if mode == "resid":
+            kw.update(residual=torch.zeros(Mpad, N, **bf))
+        elif mode == "act":
+            kw.update(act=act)
+        elif mode == "rope":
+            H, Hkv, D = heads
+            kc = torch.zeros(4, Hkv, 16, D, **bf)
+            pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
+            kw.update(positions=pos, cos_sin=cos_sin, q_out=torch.empty(Mpad, H * D, **bf),
+                      k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
+                      head_dim=D)
+        tune_fused_splits(key, lambda sp: skinny_fused(x, wp, mode, scr, splits=sp, norm=nrm,
+                                                       **kw), K)
 
 
 def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
@@ -781,28 +829,109 @@ def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
     return (w.float() * norm_w.float()[None, :]).to(w.dtype)
 
 
-def _skinny_fused_ref(x, wp, mode, scratch, norm, eps, rowsq_tiles, residual, positions,
-                      cos_sin, q_out, k_cache, v_cache, slots, H, Hkv, D, out):
+def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
+                 splits: int | None = None, norm=None, eps: float = 1e-5, rowsq_tiles: int = 0,
+                 residual: torch.Tensor | None = None, positions=None, cos_sin=None, q_out=None,
+                 k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
+                 head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
+                 row_sums: bool = False) -> torch.Tensor:
+    """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16 or 32.
+
+    ``wp`` is a shuffled weight or a ``FusedLinear`` (which supplies the norm
+    kind unless ``norm`` is given, the folded bias and the LayerNorm column
+    sums). ``norm`` True/"rms":
+    RMSNorm, "ln": LayerNorm; the row statistics come from ``rowsq_tiles``
+    partial tiles in ``scratch`` (the norm weight is folded into the weight).
+    mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
+    "resid": residual += x W^T (+ bias) in place, writes per-tile row sums of
+    squares (and row sums with ``row_sums``);
+    "rope": q -> q_out, k (RoPE'd when ``cos_sin``) and v -> paged caches
+    (``perm_rope_qkv`` order); "act": returns act(x W^T + bias) bf16 [Mpad, N]."""
+    if isinstance(wp, FusedLinear):
+        lin = wp
+        wp = lin.wp
+        norm = lin.norm if norm is None else norm
+        bias = lin.bias if bias is None else bias
+        colsum = lin.colsum if colsum is None else colsum
+    Mpad, K = x.shape
+    N = wp.shape[0] * 16
+    nrm = _NORMS[norm]
+    S = splits or _FSPLITS.get((mode, N, K, Mpad)) or choose_splits(N, K, Mpad)
+    m = _FUSED_MODES[mode]
+    ntiles = N // 32
+    if mode == "silu" and out is None:
+        out = torch.empty(Mpad, N // 2, dtype=torch.bfloat16, device=x.device)
+    elif mode == "act" and out is None:
+        out = torch.empty(Mpad, N, dtype=torch.bfloat16, device=x.device)
+    if not _gpu(x):
+        return _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual,
+                                 positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
+                                 n_kv, head_dim, out, act, bias, colsum, row_sums)
+    assert Mpad in (16, 32) and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert ntiles <= scratch.counters.numel()
+    if nrm == 2:
+        assert colsum is not None and colsum.numel() == N
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.numel() == N and bias.is_contiguous()
+    part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device) if S > 1 else None
+    blk = k_cache.shape[2] if k_cache is not None else 0
+    p = FusedParams()
+    p.x, p.ldx, p.Wp, p.part, p.counters = ptr(x), x.stride(0), ptr(wp), ptr(part), \
+        ptr(scratch.counters)
+    p.Mpad, p.N, p.K, p.S, p.mode, p.norm = Mpad, N, K, S, m, nrm
+    if nrm:
+        p.rowsq_in, p.rowsum_in = ptr(scratch.rowsq), ptr(scratch.rowsum)
+    p.rowstat_tiles, p.eps = rowsq_tiles, eps
+    p.colsum, p.bias = ptr(colsum), ptr(bias)
+    p.out, p.ldo, p.act = ptr(out), (out.stride(0) if out is not None else 0), _ACTS[act]
+    if mode == "resid":
+        p.residual, p.rowsq_out = ptr(residual), ptr(scratch.rowsq)
+        p.rowsum_out = ptr(scratch.rowsum) if row_sums else None
+    p.positions, p.cs, p.q_out = ptr(positions), ptr(cos_sin), ptr(q_out)
+    p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
+    p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
+    check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
+    if mode in ("silu", "act"):
+        return out
+    return q_out if mode == "rope" else residual
+
+
+def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, positions,
+                      cos_sin, q_out, k_cache, v_cache, slots, H, Hkv, D, out, act, bias, colsum,
+                      row_sums):
     Mpad, K = x.shape
     N = wp.shape[0] * 16
     y = x.float() @ ref.unshuffle_weight(wp).float().t()  # [Mpad, N] in permuted row order
-    if norm:
+    if nrm:
         rs = scratch.rowsq[: rowsq_tiles * Mpad].view(rowsq_tiles, Mpad)
-        y = y * ref.fused_row_scale(rs, eps, K)[:, None]
+        if nrm == 1:
+            y = y * ref.fused_row_scale(rs, eps, K)[:, None]
+        else:
+            sm = scratch.rowsum[: rowsq_tiles * Mpad].view(rowsq_tiles, Mpad)
+            mean, rstd = ref.fused_ln_stats(rs, sm, eps, K)
+            y = rstd[:, None] * (y - mean[:, None] * colsum.float()[None, :])
+    if bias is not None:
+        y = y + bias.float()[None, :]
     if mode == "silu":
         F = N // 2
         inv = torch.argsort(ref.perm_gate_up(F))
         y = y[:, inv]
-        res = ref.silu_mul(y.to(torch.bfloat16))
-        if out is not None:
-            out.copy_(res)
-            return out
-        return res
+        out.copy_(ref.silu_mul(y.to(torch.bfloat16)))
+        return out
+    if mode == "act":
+        yb = y.to(torch.bfloat16)
+        if act == "gelu":
+            yb = torch.nn.functional.gelu(yb.float()).to(torch.bfloat16)
+        out.copy_(yb)
+        return out
     if mode == "resid":
         h = (y + residual.float()).to(torch.bfloat16)
         residual.copy_(h)
         sq = h.float().pow(2).view(Mpad, N // 32, 32).sum(-1).t().contiguous()  # [tiles, Mpad]
         scratch.rowsq[: sq.numel()] = sq.flatten()
+        if row_sums:
+            sm = h.float().view(Mpad, N // 32, 32).sum(-1).t().contiguous()
+            scratch.rowsum[: sm.numel()] = sm.flatten()
         return residual
     inv = torch.argsort(ref.perm_rope_qkv(H, Hkv, D))
     qkv = y[:, inv].to(torch.bfloat16)

@@ -24,6 +24,24 @@ c_int = ctypes.c_int
 c_ll = ctypes.c_longlong
 c_float = ctypes.c_float
 
+class FusedParams(ctypes.Structure):
+    """Mirror of ``FusedParams`` in csrc/kernels/gemm_skinny.hip."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_ll), ("Wp", c_void_p), ("part", c_void_p),
+        ("counters", c_void_p),
+        ("Mpad", c_int), ("N", c_int), ("K", c_int), ("S", c_int), ("mode", c_int),
+        ("norm", c_int),
+        ("rowsq_in", c_void_p), ("rowsum_in", c_void_p), ("rowstat_tiles", c_int),
+        ("eps", c_float),
+        ("colsum", c_void_p), ("bias", c_void_p),
+        ("out", c_void_p), ("ldo", c_ll), ("act", c_int),
+        ("residual", c_void_p), ("rowsq_out", c_void_p), ("rowsum_out", c_void_p),
+        ("positions", c_void_p), ("cs", c_void_p), ("q_out", c_void_p), ("kc", c_void_p),
+        ("vc", c_void_p), ("slots", c_void_p),
+        ("H", c_int), ("Hkv", c_int), ("D", c_int), ("blk", c_int),
+    ]
+
+
 _KERNEL_SIGS = {
     "loqa_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "loqa_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
@@ -45,13 +63,11 @@ _KERNEL_SIGS = {
                        c_void_p],
     "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "loqa_skinny_fused": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                          c_int, c_int, c_void_p, c_int, c_float, c_void_p, c_void_p,
-                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_int, c_int, c_int, c_int, c_void_p],
+    "loqa_skinny_fused": [c_void_p, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                         c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
+                         c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                         c_void_p],
     "loqa_slab_rmsnorm": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                           c_void_p, c_int, c_float, c_void_p],
     "loqa_slab_rope_append": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -456,6 +456,13 @@ def perm_gate_up(F):
     return torch.tensor(rows, dtype=torch.long)
 
 
+def fused_ln_stats(rowsq_in, rowsum_in, eps, K):
+    """LayerNorm (mean, 1/std) per row from per-tile partial sums [tiles, Mpad]."""
+    mean = rowsum_in.float().sum(0) / K
+    var = (rowsq_in.float().sum(0) / K - mean * mean).clamp_min(0.0)
+    return mean, torch.rsqrt(var + eps)
+
+
 def fused_row_scale(rowsq_in, eps, K):
     """RMSNorm row scale 1/rms from per-tile partial sums of squares [tiles, Mpad]."""
     tot = rowsq_in.float().sum(0)  # [Mpad]

@@ -142,7 +142,7 @@ def attn2_bench():
     starts = torch.arange(0, B * T, T, dtype=torch.int32, device=dev)
     lens = torch.full((B,), T, dtype=torch.int32, device=dev)
     ws = ops.AttnWorkspace(dev, 256, Hw, Dw, 32)
-    for sk in (128, 256):
+    for sk in (128, 256, 384, 512):
         ns = (T + sk - 1) // sk
         t = gtime(lambda: ops.attention(q, enc, enc[:, Hw * Dw:], cu, n_heads=Hw, n_kv=Hw,
                                         head_dim=Dw, causal=False, max_q=1, cu_k=starts,

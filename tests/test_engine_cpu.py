@@ -215,10 +215,11 @@ def test_whisper_fast_decode_matches_eager_cpu():
     from loqa_hub_amd.models.configs import whisper_config
     cfg = whisper_config("test-whisper")
     utts = make_batch(1, 2, [1, 2])
-    engines = [STTEngine(cfg, torch.device("cpu"), seed=3, max_batch=4, fast_decode=f)
-               for f in (True, False)]
+    modes = ("fused", "fast", "eager")
+    engines = [STTEngine(cfg, torch.device("cpu"), seed=3, max_batch=4, fast_decode=m != "eager")
+               for m in modes]
     outs = []
-    for eng in engines:
+    for mode, eng in zip(modes, engines):
         reqs = [STTRequest(u.pcm) for u in utts]
         audio, _ = eng.upload(reqs)
         eng.cross_kv(eng.model.encode(audio))
@@ -233,7 +234,15 @@ def test_whisper_fast_decode_matches_eager_cpu():
         for step in range(2):
             max_q, host = eng._host_meta(reqs, live, feeds, B_pad, T_pad)
             dev = eng._dev(host)
-            if eng.fast_decode:
+            if mode == "fused":
+                from loqa_hub_amd.models.whisper import decode_step_fused
+                lg = decode_step_fused(eng.model, dev["tokens"], dev["positions"], dev["slots"],
+                                       dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
+                                       eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"],
+                                       dev["enc_lens"], dev["logit_idx"], eng.ws, eng.scratch,
+                                       eng.self_splits)
+                lg = lg[:2, : cfg.vocab_size].float()
+            elif mode == "fast":
                 from loqa_hub_amd.models.whisper import decode_step_fast
                 lg = decode_step_fast(eng.model, dev["tokens"], dev["positions"], dev["slots"],
                                       dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
@@ -250,9 +259,10 @@ def test_whisper_fast_decode_matches_eager_cpu():
             res.append(lg)
             feeds = [[11], [12]]
         outs.append(res)
-    for a, b in zip(*outs):
-        err = (a - b).abs().max().item()
-        assert err <= 2e-2 * b.abs().max().item() + 1e-3, err
+    for other in outs[:2]:
+        for a, b in zip(other, outs[2]):
+            err = (a - b).abs().max().item()
+            assert err <= 2e-2 * b.abs().max().item() + 1e-3, err
 
 
 def test_vits_tts_cpu():

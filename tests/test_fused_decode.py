@@ -103,3 +103,83 @@ def test_fused_resid_rowsq_and_silu_gpu():
         h = ref.rmsnorm(res1, wn, 1e-5)
         expect = ref.silu_mul((h.float() @ wgu.float().t()).bfloat16())
         assert float((a.float() - expect.float()).norm() / expect.float().norm()) < 1e-2
+
+
+def _ln_case(dev, S=None):
+    """LayerNorm-prologue GEMM (folded weight / shift / bias) with a GELU
+    epilogue, against layernorm -> linear -> gelu in fp32."""
+    torch.manual_seed(1)
+    Mpad, K, N = 16, 512, 768
+    x = (torch.randn(Mpad, K, device=dev) * 2 + 0.5).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+    g = (torch.rand(K, device=dev) + 0.5).bfloat16()
+    b = (torch.randn(K, device=dev) * 0.1).bfloat16()
+    bias = (torch.randn(N, device=dev) * 0.1).bfloat16()
+    lin = ops.FusedLinear(w, norm="ln", norm_w=g, norm_b=b, bias=bias)
+    scr = ops.FusedScratch(dev)
+    scr.seed_stats(x)
+    y = ops.skinny_fused(x, lin, "act", scr, splits=S, act="gelu", eps=1e-5, rowsq_tiles=1)
+    h = torch.nn.functional.layer_norm(x.float(), (K,), g.float(), b.float(), 1e-5)
+    expect = torch.nn.functional.gelu(h @ w.float().t() + bias.float())
+    rel = float((y.float() - expect).norm() / expect.norm())
+    assert rel < 2e-2, rel
+    # residual epilogue with row sums feeds the next LayerNorm prologue
+    res = x.clone()
+    a = (torch.randn(Mpad, N, device=dev) * 0.5).bfloat16()
+    wo = (torch.randn(K, N, device=dev) * 0.05).bfloat16()
+    ops.skinny_fused(a, ops.FusedLinear(wo, bias=bias[:K]), "resid", scr,
+                     splits=S, residual=res, row_sums=True)
+    tiles = K // 32
+    sm = scr.rowsum[: tiles * Mpad].view(tiles, Mpad).sum(0)
+    sq = scr.rowsq[: tiles * Mpad].view(tiles, Mpad).sum(0)
+    assert torch.allclose(sm, res.float().sum(1), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sq, res.float().pow(2).sum(1), rtol=1e-3)
+
+
+def test_fused_layernorm_act_cpu():
+    _ln_case("cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 2])
+def test_fused_layernorm_act_gpu(S):
+    _ln_case("cuda", S)
+
+
+@pytest.mark.gpu
+def test_whisper_fused_decode_matches_fast_gpu():
+    """Whisper decoder step: fused-epilogue path vs the skinny-GEMM + slab path."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    from loqa_hub_amd.models.whisper import decode_step_fast, decode_step_fused
+    cfg = whisper_config("test-whisper")
+    utts = make_batch(1, 3, [1, 2, 3])
+    eng = STTEngine(cfg, torch.device("cuda"), seed=3, max_batch=4, use_graphs=False)
+    outs = {}
+    for mode in ("fused", "fast"):
+        reqs = [STTRequest(u.pcm) for u in utts]
+        audio, _ = eng.upload(reqs)
+        eng.cross_kv(eng.model.encode(audio))
+        for r in reqs:
+            r.seq_id = eng._next
+            eng._next += 1
+            eng.kv.pool.add_seq(r.seq_id, [])
+        feeds = [list(eng.sot) for _ in reqs]
+        res = []
+        for step in range(3):
+            max_q, host = eng._host_meta(reqs, [0, 1, 2], feeds, 4, 16)
+            dev = eng._dev(host)
+            args = (eng.model, dev["tokens"], dev["positions"], dev["slots"], dev["cu_q"],
+                    dev["ctx_lens"], dev["block_tables"], max_q, eng.kv.k, eng.kv.v, eng.xkv,
+                    dev["enc_starts"], dev["enc_lens"], dev["logit_idx"], eng.ws)
+            if mode == "fused":
+                lg = decode_step_fused(*args, eng.scratch, eng.self_splits)
+            else:
+                lg = decode_step_fast(*args, eng.self_splits)
+            res.append(lg[:3, : cfg.vocab_size].float().cpu())
+            feeds = [[11 + step], [12 + step], [13 + step]]
+        outs[mode] = res
+    for a, b in zip(outs["fused"], outs["fast"]):
+        rel = float((a - b).norm() / b.norm())
+        assert rel < 2e-2, rel

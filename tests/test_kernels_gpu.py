@@ -155,12 +155,19 @@ def test_attention_grouped_paged(qlens, G, splits):
     cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
     ws = ops.AttnWorkspace(DEV, 64, H, D, 4)
     split_keys = 256
-    o = ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, max_q=max(qlens),
-                      ctx_lens=cl, block_tables=bt, grouped=True, split_keys=split_keys,
-                      num_splits=max(splits, math.ceil(max(ctx) / split_keys)), workspace=ws)
+
+    def run():
+        return ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True,
+                             max_q=max(qlens), ctx_lens=cl, block_tables=bt, grouped=True,
+                             split_keys=split_keys,
+                             num_splits=max(splits, math.ceil(max(ctx) / split_keys)), workspace=ws)
+    o = run()
     orf = ref.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, ctx_lens=cl,
                         block_tables=bt)
     assert _rel(o, orf) < 2e-2
+    # the in-launch split combine leaves its tickets reset: a replay is bitwise equal
+    assert torch.equal(run(), o)
+    assert int(ws.counters.abs().sum()) == 0
 
 
 def test_attention_grouped_cross_starts():
