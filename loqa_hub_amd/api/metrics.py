@@ -32,6 +32,18 @@ class MetricsHandler:
         proc = getattr(s, "processor", None)
         for k, v in (getattr(proc, "stats", None) or {}).items():
             out.append(_line("loqa_processor_" + k + "_total", v))
+        dpm = proc.metrics() if hasattr(proc, "metrics") else None
+        if dpm is not None:  # data-parallel workers (one per GPU)
+            out.append(_line("loqa_gpu_workers_healthy", dpm["healthy"]))
+            out.append(_line("loqa_gpu_worker_failures_total", len(dpm["failures"])))
+            for w in dpm["workers"]:
+                lab = {"rank": w["rank"]}
+                out.append(_line("loqa_gpu_worker_healthy", int(w["healthy"]), lab))
+                out.append(_line("loqa_gpu_worker_queue_depth", w["queued"], lab))
+                out.append(_line("loqa_gpu_worker_utterances_total", w["done"], lab))
+                for k, v in w["stats"].items():
+                    if isinstance(v, (int, float)):
+                        out.append(_line("loqa_gpu_worker_" + k + "_total", v, lab))
         pipe = getattr(proc, "pipeline", None)
         if pipe is not None:
             for k, v in pipe.llm.stats.items():

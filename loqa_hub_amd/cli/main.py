@@ -5,8 +5,9 @@
 Backends follow ``HUB_*``: with a visible GPU and ``HUB_LLM_BACKEND=gpu``
 (default) the on-device pipeline serves STT + intent parsing on ``cuda:0``;
 otherwise the reference's external services (STT_URL, OLLAMA_URL, TTS_URL).
-One hub process drives one GPU; scale-out runs one process per GPU behind the
-relay fan-out (gRPC) with the DP router (``parallel/dp_router.py``).
+With ``HUB_NUM_GPUS`` (or ``HUB_DP``) > 1 the hub front-end stays in this
+process and spawns one worker process per GPU behind the least-loaded router
+with crash / hang re-routing (``parallel/dp_serving.py``).
 """
 from __future__ import annotations
 
@@ -21,14 +22,19 @@ log = logging.getLogger("loqa.main")
 
 
 async def run(cfg) -> None:
-    from ..server import HubServer, build_gpu_processor, build_service_processor
+    from ..server import (HubServer, build_dp_processor, build_gpu_processor,
+                          build_service_processor)
     server = HubServer(cfg)
     await server._connect_nats()
     processor = None
     use_gpu = cfg.gpu.llm_backend == "gpu" and cfg.gpu.stt_backend == "gpu"
     if use_gpu:
         import torch
-        if torch.cuda.device_count() > 0:
+        n = torch.cuda.device_count()
+        want = cfg.gpu.dp or cfg.gpu.num_gpus or 1
+        if n > 1 and want > 1:
+            processor = await build_dp_processor(cfg, min(n, want))
+        elif n > 0:
             processor = build_gpu_processor(cfg, server.nats)
         else:
             log.warning("no GPU visible; using the external STT/LLM services")

@@ -24,6 +24,7 @@ from ..llm.commands import (Command, MultiCommand, ParseError, detect_compound_u
 from ..llm.prompts import build_multi_command_prompt, build_prompt
 from ..llm.transcriber import TranscriptionResult, to_transcription_result
 from ..transport.device_commands import ExecutionContext, NATSCommandExecutor
+from ..utils.faults import faults
 from .grammar import multi_command_schema, single_command_schema
 from .llm_engine import GenRequest, LLMEngine
 from .stt_engine import STTEngine, STTRequest
@@ -44,6 +45,7 @@ class PipelineJob:
     llm_output: str = ""
     queue: ExecutionResult | None = None
     error: str = ""
+    stt_failed: bool = False
     t: dict = field(default_factory=dict)   # stage timestamps (perf_counter)
 
     @property
@@ -68,13 +70,23 @@ class VoicePipeline:
         reqs = [STTRequest(j.pcm, transcript=j.transcript_hint) for j in jobs]
         self.stt.transcribe(reqs, device_pcm)
         now = time.perf_counter()
+        fi = faults()
         for j, r in zip(jobs, reqs):
             j.raw_text, j.rms = r.text, r.rms
-            j.transcription = to_transcription_result(r.text)
             j.t["stt_done"] = now
+            if fi and fi.active("stt_error"):
+                j.stt_failed, j.error = True, "stt: injected fault"
+                continue
+            j.transcription = to_transcription_result(r.text)
 
     def build_request(self, j: PipelineJob) -> GenRequest | None:
+        if j.stt_failed:
+            return None
         text = j.transcription.text if j.transcription else ""
+        fi = faults()
+        if text and fi and fi.active("llm_timeout"):
+            j.error = "llm: injected timeout"   # -> parse-failed reply, no commands
+            return None
         if not text:
             j.multi = MultiCommand([], False, text, "I didn't hear anything.")
             return None

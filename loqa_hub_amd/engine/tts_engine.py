@@ -19,6 +19,7 @@ import torch
 from ..llm.tts import TTSOptions, TTSResult
 from ..models.configs import VitsConfig
 from ..models.vits import VitsModel, VitsWeights, text_to_ids
+from ..utils.faults import faults
 
 
 def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
@@ -69,6 +70,7 @@ class VitsTTSEngine:
     async def synthesize(self, text: str, options: TTSOptions | None = None) -> TTSResult:
         if not text:
             raise ValueError("text cannot be empty")
+        faults().check("tts_error")
         speed = options.speed if options and options.speed > 0 else 1.0
         loop = asyncio.get_running_loop()
         fut = loop.create_future()

@@ -21,6 +21,7 @@ from dataclasses import dataclass
 from typing import Protocol
 
 from .http import AiohttpClient, HTTPClient
+from ..utils.faults import faults
 
 
 @dataclass
@@ -93,6 +94,7 @@ class OpenAITTSClient:
     async def synthesize(self, text: str, options: TTSOptions | None = None) -> TTSResult:
         if not text:
             raise ValueError("text cannot be empty")
+        faults().check("tts_error")
         try:
             await asyncio.wait_for(self._sem.acquire(), self.QUEUE_WAIT_S)
         except asyncio.TimeoutError:

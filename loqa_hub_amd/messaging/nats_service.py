@@ -11,6 +11,7 @@ import time
 from dataclasses import dataclass, field
 
 from ..utils import gojson
+from ..utils.faults import faults
 from .nats_client import Msg, NATSClient, NATSError
 
 log = logging.getLogger("loqa.messaging")
@@ -116,6 +117,8 @@ class NATSService:
         return self.conn is not None and self.conn.is_connected()
 
     def _require(self) -> NATSClient:
+        if faults().active("nats_down"):
+            raise NATSError("NATS connection not established (injected fault: nats_down)")
         if self.conn is None:
             raise NATSError("NATS connection not established")
         return self.conn

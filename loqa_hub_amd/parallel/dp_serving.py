@@ -1,0 +1,305 @@
+"""Data-parallel serving over the GPUs of one node.
+
+The hub front-end (gRPC relays, arbitration, HTTP, NATS) stays on the CPU in
+one process; every GPU gets ONE worker process (spawned, pinned to
+``cuda:<rank>``) that owns a full on-device pipeline (``GPUVoiceProcessor``:
+batched Whisper -> constrained multi-command decode -> command queue / NATS).
+Arbitration winners are routed to the least-loaded healthy worker
+(``LeastLoadedRouter``: fewest queued utterances, ties -> lowest rank); each
+worker micro-batches whatever it receives, so continuous batching happens per
+GPU. The reference serialises every relay behind one global arbitration
+window and one HTTP STT/Ollama service (``audio_service.go:89,435``); it has no
+multi-GPU anything.
+
+Failure handling (reference: none beyond service retries):
+
+* crash  - a worker process that exits is detected by the monitor;
+* hang   - every worker heartbeats (its own thread) with the age of its last
+           completed utterance while it has work in flight: no progress for
+           ``watchdog_s`` with work queued = a hung GPU;
+* either way the router marks it unhealthy, the process is killed (exact PID,
+  it is our child), and its queued utterances are re-dispatched to the
+  surviving workers; with no survivor they complete with the STT-failed
+  reply. ``FAULT_INJECT=gpu_kill:<rank>[@n]`` drives this path.
+
+``metrics()`` aggregates per-worker counters (D3) for ``/api/metrics``.
+"""
+from __future__ import annotations
+
+import asyncio
+import dataclasses
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import queue
+import threading
+import time
+
+import numpy as np
+
+from ..transport.audio_service import MSG_STT_FAILED, UtteranceResult
+from .dp_router import LeastLoadedRouter
+
+log = logging.getLogger("loqa.dp")
+
+
+# --------------------------------------------------------------- worker side
+def _build_worker_processor(spec: dict, device: str):
+    """The per-GPU pipeline (same composition as ``server.build_gpu_processor``)."""
+    from ..engine.llm_engine import LLMEngine
+    from ..engine.pipeline import VoicePipeline
+    from ..engine.stt_engine import STTEngine
+    from ..models.configs import llama_config, whisper_config
+    from ..transport.voice_processor import GPUVoiceProcessor
+    stt = STTEngine(whisper_config(spec["stt_model"]), device, seed=spec.get("seed", 0),
+                    max_batch=spec.get("max_batch", 8), use_graphs=spec.get("use_graphs", True))
+    llm = LLMEngine(llama_config(spec["llm_model"]), device, seed=spec.get("seed", 0),
+                    max_seqs=spec.get("max_batch", 8), max_seq_len=spec.get("max_seq_len", 1024),
+                    use_graphs=spec.get("use_graphs", True))
+    pipe = VoicePipeline(stt, llm, None, min_response_tokens=spec.get("min_response_tokens", 8))
+    return GPUVoiceProcessor(pipe, max_batch=spec.get("max_batch", 8),
+                             batch_window=spec.get("batch_window", 0.005))
+
+
+def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
+    from ..utils.faults import set_faults
+    spec = dict(spec, rank=rank)
+    fi = set_faults(spec.get("fault_inject"))
+    kill_after = fi.gpu_kill_after(rank)
+    device = spec.get("device", "cuda")
+    if device == "cuda":
+        import torch
+        device = f"cuda:{rank % max(1, torch.cuda.device_count())}"
+        torch.cuda.set_device(device)
+    factory = spec.get("factory") or _build_worker_processor
+    proc = factory(spec, device)
+    loop = asyncio.new_event_loop()
+    asyncio.set_event_loop(loop)
+    state = {"inflight": 0, "last_progress": time.monotonic(), "done": 0, "stop": False}
+    lock = threading.Lock()
+
+    def heartbeat() -> None:
+        while not state["stop"]:
+            with lock:
+                age = time.monotonic() - state["last_progress"]
+                hb = {"inflight": state["inflight"], "since_progress": age,
+                      "done": state["done"], "stats": dict(getattr(proc, "stats", {}))}
+            resp_q.put(("hb", rank, hb))
+            time.sleep(spec.get("heartbeat_s", 0.5))
+
+    async def handle(item) -> None:
+        rid, relay_id, request_id, pcm16, sr = item
+        try:
+            res = await proc.process(relay_id, request_id, pcm16.astype(np.float32) / 32767.0, sr)
+            out = dataclasses.asdict(res)
+        except Exception as e:  # noqa: BLE001
+            out = dataclasses.asdict(UtteranceResult(success=False, command="error",
+                                                     response_text=MSG_STT_FAILED, error=str(e)))
+        with lock:
+            state["inflight"] -= 1
+            state["done"] += 1
+            state["last_progress"] = time.monotonic()
+        resp_q.put(("res", rank, (rid, out)))
+
+    def reader() -> None:
+        received = 0
+        while True:
+            item = req_q.get()
+            if item is None:
+                loop.call_soon_threadsafe(loop.stop)
+                return
+            received += 1
+            if kill_after is not None and received >= kill_after:
+                os._exit(17)  # injected GPU-worker crash (FAULT_INJECT=gpu_kill)
+            with lock:
+                if state["inflight"] == 0:
+                    state["last_progress"] = time.monotonic()
+                state["inflight"] += 1
+            asyncio.run_coroutine_threadsafe(handle(item), loop)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+    threading.Thread(target=reader, daemon=True).start()
+    resp_q.put(("ready", rank, None))
+    try:
+        loop.run_forever()
+    finally:
+        state["stop"] = True
+
+
+# --------------------------------------------------------------- front side
+@dataclasses.dataclass
+class _Req:
+    args: tuple
+    fut: asyncio.Future
+    worker: int = -1
+    attempts: int = 0
+
+
+class DPVoiceProcessor:
+    """``VoiceProcessor`` over one worker process per GPU."""
+
+    def __init__(self, spec: dict, n_workers: int, *, watchdog_s: float = 60.0,
+                 ready_timeout: float = 900.0, max_attempts: int = 3):
+        self.spec = dict(spec)
+        self.n = n_workers
+        self.watchdog_s = watchdog_s
+        self.ready_timeout = ready_timeout
+        self.max_attempts = max_attempts
+        self.router = LeastLoadedRouter(n_workers)
+        self._ids = itertools.count()
+        self._reqs: dict[int, _Req] = {}
+        self._pending: list[set[int]] = [set() for _ in range(n_workers)]
+        self._hb: list[dict] = [{} for _ in range(n_workers)]
+        self._last_hb = [0.0] * n_workers
+        self._ready = [False] * n_workers
+        self.failures: list[dict] = []
+        self._running = False
+
+    # lifecycle
+    async def start(self) -> None:
+        ctx = mp.get_context("spawn")
+        self._req_qs = [ctx.Queue() for _ in range(self.n)]
+        self._resp_q = ctx.Queue()
+        self._procs = [ctx.Process(target=_worker_main, args=(r, self.spec, self._req_qs[r],
+                                                              self._resp_q), daemon=True)
+                       for r in range(self.n)]
+        for p in self._procs:
+            p.start()
+        self._loop = asyncio.get_running_loop()
+        self._running = True
+        self._reader = threading.Thread(target=self._read, daemon=True)
+        self._reader.start()
+        t0 = time.monotonic()
+        while not all(self._ready[r] or not self._procs[r].is_alive() for r in range(self.n)):
+            if time.monotonic() - t0 > self.ready_timeout:
+                raise TimeoutError("DP workers did not become ready")
+            await asyncio.sleep(0.05)
+        for r in range(self.n):
+            if not self._ready[r]:
+                self._fail_worker(r, "died during start-up")
+        now = time.monotonic()
+        self._last_hb = [now] * self.n
+        self._monitor = asyncio.ensure_future(self._watch())
+
+    async def close(self) -> None:
+        self._running = False
+        if getattr(self, "_monitor", None):
+            self._monitor.cancel()
+        for r, p in enumerate(self._procs):
+            if p.is_alive():
+                self._req_qs[r].put(None)
+        for p in self._procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=5)
+
+    # routing
+    async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
+                      sample_rate: int) -> UtteranceResult:
+        pcm16 = np.clip(np.round(np.asarray(audio, np.float32) * 32767.0), -32768,
+                        32767).astype(np.int16)
+        rid = next(self._ids)
+        req = _Req((relay_id, request_id, pcm16, sample_rate), self._loop.create_future())
+        self._reqs[rid] = req
+        self._dispatch(rid)
+        return await req.fut
+
+    def _dispatch(self, rid: int) -> None:
+        req = self._reqs[rid]
+        req.attempts += 1
+        try:
+            w = self.router.pick()
+        except RuntimeError:
+            self._finish(rid, UtteranceResult(success=False, command="error",
+                                              response_text=MSG_STT_FAILED,
+                                              error="no healthy GPU workers"))
+            return
+        req.worker = w
+        self._pending[w].add(rid)
+        self._req_qs[w].put((rid,) + req.args)
+
+    def _finish(self, rid: int, res: UtteranceResult) -> None:
+        req = self._reqs.pop(rid, None)
+        if req is not None and not req.fut.done():
+            req.fut.set_result(res)
+
+    # worker -> front messages (reader thread -> event loop)
+    def _read(self) -> None:
+        while self._running:
+            try:
+                msg = self._resp_q.get(timeout=0.2)
+            except queue.Empty:
+                continue
+            except (EOFError, OSError):
+                return
+            self._loop.call_soon_threadsafe(self._on_msg, msg)
+
+    def _on_msg(self, msg) -> None:
+        kind, w, payload = msg
+        if kind == "ready":
+            self._ready[w] = True
+            self._last_hb[w] = time.monotonic()
+        elif kind == "hb":
+            self._hb[w] = payload
+            self._last_hb[w] = time.monotonic()
+        elif kind == "res":
+            rid, d = payload
+            if rid in self._pending[w]:
+                self._pending[w].discard(rid)
+                self.router.done(w)
+            self._finish(rid, UtteranceResult(**d))
+
+    # health
+    async def _watch(self) -> None:
+        period = max(0.05, self.spec.get("heartbeat_s", 0.5))
+        while self._running:
+            await asyncio.sleep(period)
+            now = time.monotonic()
+            for w in range(self.n):
+                if not self.router.healthy[w]:
+                    continue
+                p = self._procs[w]
+                hb = self._hb[w]
+                if not p.is_alive():
+                    self._fail_worker(w, f"process exited (code {p.exitcode})")
+                elif now - self._last_hb[w] > self.watchdog_s:
+                    self._fail_worker(w, "heartbeat lost")
+                elif self._pending[w] and hb.get("inflight", 0) > 0 and \
+                        hb.get("since_progress", 0.0) > self.watchdog_s:
+                    self._fail_worker(w, "no progress (GPU hang)")
+
+    def _fail_worker(self, w: int, why: str) -> None:
+        if not self.router.healthy[w] and not self._pending[w]:
+            return
+        log.error("GPU worker %d unhealthy: %s; re-routing %d utterances", w, why,
+                  len(self._pending[w]))
+        self.failures.append({"worker": w, "reason": why, "rerouted": len(self._pending[w]),
+                              "t": time.time()})
+        self.router.mark_unhealthy(w)
+        p = self._procs[w]
+        if p.is_alive():
+            p.kill()
+        orphans, self._pending[w] = self._pending[w], set()
+        for rid in sorted(orphans):
+            req = self._reqs.get(rid)
+            if req is None:
+                continue
+            if req.attempts >= self.max_attempts:
+                self._finish(rid, UtteranceResult(success=False, command="error",
+                                                  response_text=MSG_STT_FAILED,
+                                                  error=f"worker failures: {why}"))
+            else:
+                self._dispatch(rid)
+
+    def metrics(self) -> dict:
+        """Per-worker counters aggregated on the front-end (D3)."""
+        workers = []
+        for w in range(self.n):
+            hb = self._hb[w]
+            workers.append({"rank": w, "healthy": self.router.healthy[w],
+                            "queued": len(self._pending[w]), "done": hb.get("done", 0),
+                            "stats": hb.get("stats", {})})
+        return {"workers": workers, "healthy": sum(self.router.healthy),
+                "utterances": sum(x["done"] for x in workers), "failures": list(self.failures)}

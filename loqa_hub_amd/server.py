@@ -53,6 +53,18 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None):
     return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64))
 
 
+async def build_dp_processor(cfg: Config, n_gpus: int):
+    """One worker process per GPU behind the least-loaded router (D1)."""
+    from .parallel.dp_serving import DPVoiceProcessor
+    g = cfg.gpu
+    spec = {"device": "cuda", "stt_model": g.stt_model, "llm_model": g.llm_model,
+            "max_batch": min(g.max_batch, 64), "max_seq_len": g.max_seq_len,
+            "use_graphs": g.use_graphs, "seed": g.seed}
+    dp = DPVoiceProcessor(spec, n_gpus)
+    await dp.start()
+    return dp
+
+
 async def build_service_processor(cfg: Config, nats, tts=None):
     """Reference path: external STT + Ollama parser (+ TTS)."""
     from .llm.command_parser import CommandParser, OllamaBackend

@@ -27,6 +27,7 @@ from ..llm.commands import MultiCommand
 from ..llm.transcriber import TranscriptionResult
 from .audio_service import (MSG_NO_COMMANDS, MSG_NO_SPEECH, MSG_PARSE_FAILED, MSG_STT_FAILED,
                             UtteranceResult)
+from ..utils.faults import faults
 from .device_commands import ExecutionContext, NATSCommandExecutor
 
 log = logging.getLogger("loqa.processor")
@@ -71,11 +72,14 @@ class GPUVoiceProcessor:
         self.stats = {"batches": 0, "utterances": 0}
 
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
-                      sample_rate: int) -> UtteranceResult:
+                      sample_rate: int, transcript_hint: str | None = None) -> UtteranceResult:
+        """``transcript_hint``: synthetic-traffic ground truth that teacher-forces
+        the (random-init) Whisper decoder; real relays never pass it."""
         from ..engine.pipeline import PipelineJob
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        self._pending.append((PipelineJob(relay_id, request_id, float_to_pcm16(audio)), fut))
+        self._pending.append((PipelineJob(relay_id, request_id, float_to_pcm16(audio),
+                                          transcript_hint), fut))
         if len(self._pending) >= self.max_batch or self._flusher is None or self._flusher.done():
             self._flusher = loop.create_task(self._flush())
         return await fut
@@ -102,6 +106,10 @@ class GPUVoiceProcessor:
         self.stats["utterances"] += len(jobs)
         results = []
         for j in jobs:
+            if j.stt_failed:
+                results.append(UtteranceResult(success=False, command="error",
+                                               response_text=MSG_STT_FAILED, error=j.error))
+                continue
             text = j.transcription.text if j.transcription else ""
             ok = None if j.queue is None else j.queue.success
             results.append(_result_from(text, j.multi, ok, j.transcription))
@@ -143,6 +151,7 @@ class ServiceVoiceProcessor:
                       sample_rate: int) -> UtteranceResult:
         t0 = time.perf_counter()
         try:
+            faults().check("stt_error")
             tr = await self.transcriber.transcribe_with_confidence(audio, sample_rate)
         except Exception as e:  # noqa: BLE001
             return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
@@ -163,6 +172,7 @@ class ServiceVoiceProcessor:
             except Exception as e:  # noqa: BLE001
                 log.info("bridge fallback: %s", e)
         try:
+            faults().check("llm_timeout")
             mc = await self.parser.parse_multi_command(tr.text)
         except Exception as e:  # noqa: BLE001
             log.warning("command parsing failed: %s", e)

@@ -1,0 +1,85 @@
+"""Data-parallel serving: one worker process per device
+behind the least-loaded router, crash / hang detection and re-routing, and
+FAULT_INJECT-driven failures. Workers run on the CPU here (spawned processes,
+same code path as one process per GPU)."""
+import asyncio
+import time
+
+import numpy as np
+import pytest
+
+from loqa_hub_amd.parallel.dp_serving import DPVoiceProcessor
+from loqa_hub_amd.transport.audio_service import UtteranceResult
+
+
+class _EchoProcessor:
+    def __init__(self, spec):
+        self.rank = spec["rank"]
+        self.hang = spec.get("hang_rank") == self.rank
+        self.stats = {"utterances": 0}
+
+    async def process(self, relay_id, request_id, audio, sr):
+        if self.hang:
+            time.sleep(3600)  # a wedged GPU: the worker's loop never comes back
+        await asyncio.sleep(0.02)
+        self.stats["utterances"] += 1
+        return UtteranceResult(transcription=f"w{self.rank}:{request_id}:{len(audio)}",
+                               response_text="ok")
+
+
+def echo_factory(spec, device):
+    return _EchoProcessor(spec)
+
+
+def _run(spec, n_workers, n_req, **kw):
+    async def main():
+        dp = DPVoiceProcessor(dict(spec, device="cpu", factory=echo_factory, heartbeat_s=0.1),
+                              n_workers, **kw)
+        await dp.start()
+        try:
+            audio = np.zeros(1600, np.float32)
+            res = await asyncio.wait_for(asyncio.gather(*[
+                dp.process(f"relay-{i}", f"req-{i}", audio, 16000) for i in range(n_req)]), 60)
+            return res, dp.metrics()
+        finally:
+            await dp.close()
+    return asyncio.run(main())
+
+
+def test_dp_routes_to_all_workers():
+    res, m = _run({}, 2, 8)
+    assert all(r.success for r in res)
+    owners = {r.transcription.split(":")[0] for r in res}
+    assert owners == {"w0", "w1"}
+    assert [r.transcription.split(":")[1] for r in res] == [f"req-{i}" for i in range(8)]
+    assert m["healthy"] == 2 and not m["failures"]
+
+
+def test_dp_worker_crash_is_rerouted():
+    res, m = _run({"fault_inject": "gpu_kill:1@2"}, 2, 8)
+    assert all(r.success for r in res), [r.error for r in res]
+    assert all(r.transcription.startswith("w0:") or r.transcription.startswith("w1:") for r in res)
+    assert m["healthy"] == 1
+    assert m["failures"] and m["failures"][0]["worker"] == 1
+    assert "exited" in m["failures"][0]["reason"]
+
+
+def test_dp_gpu_hang_is_detected():
+    res, m = _run({"hang_rank": 0}, 2, 4, watchdog_s=1.0)
+    assert all(r.success and r.transcription.startswith("w1:") for r in res)
+    assert m["failures"][0]["worker"] == 0
+
+
+def test_dp_all_workers_dead_fail_cleanly():
+    res, m = _run({"fault_inject": "gpu_kill:0@1"}, 1, 3)
+    assert all(not r.success and r.command == "error" for r in res)
+    assert m["healthy"] == 0
+
+
+@pytest.mark.parametrize("spec", ["stt_error", "llm_timeout,nats_down", "gpu_kill:3@2%0.5"])
+def test_fault_spec_parsing(spec):
+    from loqa_hub_amd.utils.faults import FaultInjector
+    fi = FaultInjector(spec)
+    assert bool(fi)
+    with pytest.raises(ValueError):
+        FaultInjector("disk_full")
