@@ -203,6 +203,8 @@ class GPUConfig:
     tts_backend: str = "gpu"          # gpu | http | none
     use_graphs: bool = True
     seed: int = 0
+    stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
+    llm_checkpoint: str = ""
 
 
 @dataclass
@@ -346,6 +348,8 @@ def load(env=None) -> Config:
             tts_backend=env_str(e, "gpu", "HUB_TTS_BACKEND"),
             use_graphs=env_bool(e, True, "HUB_USE_GRAPHS"),
             seed=env_int(e, 0, "HUB_SEED"),
+            stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
+            llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
         ),
         arbitration=ArbitrationConfig(
             window=env_duration(e, 0.300, "ARBITRATION_WINDOW_DURATION"),

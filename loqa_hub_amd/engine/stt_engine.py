@@ -46,10 +46,10 @@ class STTEngine:
 
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
                  block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
-                 fused: bool = True):
+                 fused: bool = True, weights: WhisperWeights | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
-        self.weights = WhisperWeights(cfg, self.device, seed=seed)
+        self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
         self.model = WhisperModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
         self.sot = [self.tok.token_id(s) for s in

@@ -107,6 +107,10 @@ class LlamaWeights:
         self.final_norm = ones(d)
         self.lm_head = self.embed if cfg.tie_embeddings else rnd(self.v, d)
         self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
+        self._finalize()
+
+    def _finalize(self) -> None:
+        """Derived decode copies + split-K tuning (after the base tensors exist)."""
         # decode copies in MFMA-fragment order for the weight-streaming skinny GEMM
         # (prefill keeps the row-major copies for hipBLASLt; 288 GB of HBM makes
         # the duplicate affordable and each path gets its ideal layout)
@@ -115,10 +119,30 @@ class LlamaWeights:
                               for L in self.layers]
         self.lm_head_p = ops.shuffle_weight(self.lm_head)
         self._add_fused_copies()
-        if torch.device(device).type == "cuda":
+        if self.embed.device.type == "cuda":
             for k in ("wqkv", "wo", "w_gate_up", "w_down"):
                 ops.tune_skinny_splits(self.decode_layers[0][k])
             ops.tune_skinny_splits(self.lm_head_p)
+
+    @classmethod
+    def from_tensors(cls, cfg: LlamaConfig, device, *, embed, layers: list[dict], final_norm,
+                     lm_head=None, tp: TPGroup | None = None) -> "LlamaWeights":
+        """Weights from explicit tensors (checkpoint loaders): ``layers`` hold
+        attn_norm / wqkv (q|k|v rows) / wo / mlp_norm / w_gate_up (gate|up rows)
+        / w_down. Unsharded tensors; ``tp`` > 1 shards them (Megatron split)."""
+        self = cls.__new__(cls)
+        self.cfg, self.tp = cfg, TPGroup()
+        self.h, self.hkv, self.f, self.v = cfg.n_heads, cfg.n_kv_heads, cfg.ffn_dim, cfg.vocab_size
+        self.embed = embed
+        self.layers = layers
+        self.final_norm = final_norm
+        self.lm_head = self.embed if (cfg.tie_embeddings or lm_head is None) else lm_head
+        self.cos_sin = rope_cos_sin(cfg.head_dim, cfg.max_positions, cfg.rope_theta, device=device)
+        if tp is not None and tp.world > 1:
+            self.decode_layers, self.lm_head_p = [], None
+            return cls.shard(self, tp)
+        self._finalize()
+        return self
 
     def _add_fused_copies(self) -> None:
         """Row-permuted decode copies for the fused-epilogue GEMMs (RoPE pairs /
@@ -176,11 +200,7 @@ class LlamaWeights:
         self.final_norm = full.final_norm
         self.lm_head = self.embed if cfg.tie_embeddings else full.lm_head[vs].contiguous()
         self.cos_sin = full.cos_sin
-        self.decode_layers = [{k: ops.shuffle_weight(L[k])
-                               for k in ("wqkv", "wo", "w_gate_up", "w_down")}
-                              for L in self.layers]
-        self.lm_head_p = ops.shuffle_weight(self.lm_head)
-        self._add_fused_copies()
+        self._finalize()
         return self
 
     def nbytes(self) -> int:

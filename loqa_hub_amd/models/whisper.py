@@ -65,6 +65,12 @@ class WhisperWeights:
         for _ in range(cfg.dec_layers):
             self.dec.append(self._block(rnd, zeros, ones, d, f, cross=True))
         self.dec_ln_w, self.dec_ln_b = ones(d), zeros(d)
+        self._finalize()
+
+    def _finalize(self) -> None:
+        """Derived decode copies + split-K tuning (after the base tensors exist)."""
+        cfg, d = self.cfg, self.cfg.d_model
+        device, dtype = self.tok_embed.device, self.tok_embed.dtype
         # decode-path copies in MFMA fragment order for the weight-streaming
         # skinny GEMM; the vocab is zero-padded to a multiple of 32 rows
         self.vocab_pad = (cfg.vocab_size + 31) // 32 * 32
@@ -77,7 +83,7 @@ class WhisperWeights:
         # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
         # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)
         self.dec_f = [self._fused_layer(L) for L in self.dec]
-        if torch.device(device).type == "cuda":
+        if device.type == "cuda":
             for k in DEC_PROJ:
                 ops.tune_skinny_splits(self.dec_p[0][k], mpads=(16, 32))
             ops.tune_skinny_splits(self.lm_head_p, mpads=(16, 32))
@@ -87,6 +93,21 @@ class WhisperWeights:
             ops.tune_fused(F["xq"], "act")
             ops.tune_fused(F["fc1"], "act", act="gelu")
             ops.tune_fused(F["fc2"], "resid")
+
+    @classmethod
+    def from_tensors(cls, cfg: WhisperConfig, *, conv1_w, conv1_b, conv2_w, conv2_b, pos_enc, enc,
+                     enc_ln_w, enc_ln_b, tok_embed, dec_pos, dec, dec_ln_w,
+                     dec_ln_b) -> "WhisperWeights":
+        """Weights from explicit tensors (checkpoint loaders); block dicts use
+        the ``_block`` names (wqkv = q|k|v rows, xkv = k|v rows)."""
+        self = cls.__new__(cls)
+        self.cfg = cfg
+        self.conv1_w, self.conv1_b, self.conv2_w, self.conv2_b = conv1_w, conv1_b, conv2_w, conv2_b
+        self.pos_enc, self.enc, self.enc_ln_w, self.enc_ln_b = pos_enc, enc, enc_ln_w, enc_ln_b
+        self.tok_embed, self.dec_pos, self.dec = tok_embed, dec_pos, dec
+        self.dec_ln_w, self.dec_ln_b = dec_ln_w, dec_ln_b
+        self._finalize()
+        return self
 
     def _fused_layer(self, L: dict) -> dict:
         H, D = self.cfg.n_heads, self.cfg.head_dim

@@ -45,9 +45,15 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None):
     from .models.configs import llama_config, whisper_config
     from .transport.voice_processor import GPUVoiceProcessor
     g = cfg.gpu
-    stt = STTEngine(whisper_config(g.stt_model), device, seed=g.seed, max_batch=g.max_batch,
-                    use_graphs=g.use_graphs)
-    llm = LLMEngine(llama_config(g.llm_model), device, seed=g.seed, max_seqs=g.max_batch,
+    scfg, lcfg = whisper_config(g.stt_model), llama_config(g.llm_model)
+    sw = lw = None
+    if g.stt_checkpoint or g.llm_checkpoint:
+        from .models import loader
+        sw = loader.load_whisper(scfg, g.stt_checkpoint, device) if g.stt_checkpoint else None
+        lw = loader.load_llama(lcfg, g.llm_checkpoint, device) if g.llm_checkpoint else None
+    stt = STTEngine(scfg, device, seed=g.seed, max_batch=g.max_batch, use_graphs=g.use_graphs,
+                    weights=sw)
+    llm = LLMEngine(lcfg, device, seed=g.seed, max_seqs=g.max_batch, weights=lw,
                     max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs)
     pipe = VoicePipeline(stt, llm, nats)
     return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64))
