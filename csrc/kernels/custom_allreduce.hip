@@ -24,9 +24,12 @@
 #define CAR_BLOCKS 32
 #define CAR_SPIN_LIMIT (1 << 26)
 
+#define CAR_TWOSHOT_MIN_BYTES (512 << 10)
+
 struct CarSignals {
   unsigned start[CAR_BLOCKS][CAR_MAX_WORLD];
   unsigned end[CAR_BLOCKS][CAR_MAX_WORLD];
+  unsigned mid[CAR_BLOCKS][CAR_MAX_WORLD];     // two-shot: reduce-scatter -> all-gather
   unsigned epoch;
   unsigned done;
   unsigned error;
@@ -52,13 +55,14 @@ __device__ bool car_barrier(CarPeers peers, int rank, int world, int which, int 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope release
     for (int q = 0; q < world; ++q) {
       CarSignals* s = reinterpret_cast<CarSignals*>(peers.base[q]);
-      st_sys(which ? &s->end[blk][rank] : &s->start[blk][rank], e);
+      st_sys(which == 0 ? &s->start[blk][rank] : which == 1 ? &s->end[blk][rank] : &s->mid[blk][rank], e);
     }
   }
   bool ok = true;
   if (threadIdx.x < world) {
     CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
-    const unsigned* f = which ? &me->end[blk][threadIdx.x] : &me->start[blk][threadIdx.x];
+    const unsigned* f = which == 0 ? &me->start[blk][threadIdx.x]
+                        : which == 1 ? &me->end[blk][threadIdx.x] : &me->mid[blk][threadIdx.x];
     unsigned spins = 0;
     while (ld_sys(f) != e) {
       if (++spins > CAR_SPIN_LIMIT) {
@@ -71,6 +75,29 @@ __device__ bool car_barrier(CarPeers peers, int rank, int world, int which, int 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   return __syncthreads_and(ok);
+}
+
+// 16-byte vector sum over the peers' slots at vector index v (fixed peer order)
+template <bool F32>
+__device__ __forceinline__ uint4 car_sum16(const CarPeers& peers, size_t slot_off, int world,
+                                           long long v) {
+  if constexpr (F32) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < world; ++q) {
+      const float4 x = reinterpret_cast<const float4*>(peers.base[q] + slot_off)[v];
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    return *reinterpret_cast<uint4*>(&acc);
+  } else {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < world; ++q) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(peers.base[q] + slot_off)[v], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    return pack8(acc);
+  }
 }
 
 // element type: bf16 (8 per 16-byte vector) or f32 (4 per vector, the decode
@@ -91,29 +118,60 @@ __global__ __launch_bounds__(256) void car_oneshot_kernel(CarPeers peers, const 
   for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) mine[v] = src[v];
   if (car_barrier(peers, rank, world, 0, blk, e)) {
     uint4* dst = reinterpret_cast<uint4*>(out);
-    for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-      if constexpr (F32) {
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int q = 0; q < world; ++q) {  // fixed order: bitwise identical on every rank
-          const float4 x = reinterpret_cast<const float4*>(peers.base[q] + slot_off)[v];
-          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
-        }
-        reinterpret_cast<float4*>(dst)[v] = acc;
-      } else {
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int q = 0; q < world; ++q) {
-          const uint4 x = reinterpret_cast<const uint4*>(peers.base[q] + slot_off)[v];
-          float f[8];
-          unpack8(x, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += f[j];
-        }
-        dst[v] = pack8(acc);
-      }
-    }
+    // fixed peer order: bitwise identical on every rank
+    for (long long v = v0 + threadIdx.x; v < v1; v += blockDim.x)
+      dst[v] = car_sum16<F32>(peers, slot_off, world, v);
     car_barrier(peers, rank, world, 1, blk, e);
   }
   // the last block to finish publishes the epoch for the next call
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned d = __hip_atomic_fetch_add(&me->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == CAR_BLOCKS - 1) {
+      st_sys(&me->done, 0u);
+      st_sys(&me->epoch, e);
+    }
+  }
+}
+
+// Two-shot (bandwidth-bound sizes, e.g. prefill activations): rank r owns
+// slice r of the tensor. Block b (of every rank) stages chunk b of every slice
+// -> start barrier -> sums chunk b of ITS slice over all peers (each link
+// carries 1/world of the tensor) and writes it back into its own slot and the
+// output -> mid barrier -> gathers chunk b of every other slice from its owner
+// -> end barrier. Per rank ~2N bytes cross the links instead of world * N.
+template <bool F32>
+__global__ __launch_bounds__(256) void car_twoshot_kernel(CarPeers peers, const void* __restrict__ in,
+                                                          void* __restrict__ out, long long nbytes,
+                                                          int rank, int world, long long slot_bytes) {
+  CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
+  const unsigned e = ld_sys(&me->epoch) + 1;
+  const int blk = blockIdx.x;
+  const long long sv = (nbytes >> 4) / world;                 // vectors per slice
+  const long long per = (sv + CAR_BLOCKS - 1) / CAR_BLOCKS;
+  const long long c0 = blk * per, c1 = c0 + per < sv ? c0 + per : sv;
+  const size_t slot_off = sizeof(CarSignals) + (size_t)(e & 1) * slot_bytes;
+  uint4* mine = reinterpret_cast<uint4*>(peers.base[rank] + slot_off);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  uint4* dst = reinterpret_cast<uint4*>(out);
+  for (int q = 0; q < world; ++q)
+    for (long long v = c0 + threadIdx.x; v < c1; v += blockDim.x) mine[q * sv + v] = src[q * sv + v];
+  if (car_barrier(peers, rank, world, 0, blk, e)) {
+    for (long long v = c0 + threadIdx.x; v < c1; v += blockDim.x) {
+      const long long i = rank * sv + v;
+      const uint4 r = car_sum16<F32>(peers, slot_off, world, i);
+      mine[i] = r;
+      dst[i] = r;
+    }
+    if (car_barrier(peers, rank, world, 2, blk, e)) {
+      for (int q = 0; q < world; ++q) {
+        if (q == rank) continue;
+        const uint4* theirs = reinterpret_cast<const uint4*>(peers.base[q] + slot_off);
+        for (long long v = c0 + threadIdx.x; v < c1; v += blockDim.x) dst[q * sv + v] = theirs[q * sv + v];
+      }
+      car_barrier(peers, rank, world, 1, blk, e);
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned d = __hip_atomic_fetch_add(&me->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -177,7 +235,8 @@ extern "C" int loqa_car_open(void* hp, const void* handles) {
   return 0;
 }
 
-// n elements of bf16 (is_f32 = 0) or f32 (is_f32 = 1); n * size % 16 == 0
+// n elements of bf16 (is_f32 = 0) or f32 (is_f32 = 1); n * size % 16 == 0.
+// One-shot below CAR_TWOSHOT_MIN_BYTES (latency-bound decode), two-shot above.
 extern "C" int loqa_car_allreduce(void* hp, const void* in, void* out, long long n, int is_f32,
                                   hipStream_t s) {
   CarHandle* h = static_cast<CarHandle*>(hp);
@@ -186,12 +245,11 @@ extern "C" int loqa_car_allreduce(void* hp, const void* in, void* out, long long
   if (nbytes % 16 || (size_t)nbytes > h->slot_bytes) return (int)hipErrorInvalidValue;
   for (int q = 0; q < h->world; ++q)
     if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
-  if (is_f32)
-    hipLaunchKernelGGL(car_oneshot_kernel<true>, dim3(CAR_BLOCKS), dim3(256), 0, s, h->peers, in,
-                       out, nbytes, h->rank, h->world, (long long)h->slot_bytes);
-  else
-    hipLaunchKernelGGL(car_oneshot_kernel<false>, dim3(CAR_BLOCKS), dim3(256), 0, s, h->peers, in,
-                       out, nbytes, h->rank, h->world, (long long)h->slot_bytes);
+  const bool two = h->world > 1 && nbytes >= CAR_TWOSHOT_MIN_BYTES && nbytes % (16LL * h->world) == 0;
+  auto k = two ? (is_f32 ? car_twoshot_kernel<true> : car_twoshot_kernel<false>)
+               : (is_f32 ? car_oneshot_kernel<true> : car_oneshot_kernel<false>);
+  hipLaunchKernelGGL(k, dim3(CAR_BLOCKS), dim3(256), 0, s, h->peers, in, out, nbytes, h->rank,
+                     h->world, (long long)h->slot_bytes);
   return (int)hipGetLastError();
 }
 

@@ -18,7 +18,7 @@ class MetricsHandler:
         self.server = server
 
     def routes(self) -> list[web.RouteDef]:
-        return [web.get("/api/metrics", self.metrics)]
+        return [web.get("/api/metrics", self.metrics), web.get("/api/trace", self.trace)]
 
     def collect(self) -> list[str]:
         s = self.server
@@ -50,11 +50,22 @@ class MetricsHandler:
                 out.append(_line("loqa_llm_" + k, v))
             for k, v in pipe.stt.stats.items():
                 out.append(_line("loqa_stt_" + k, v))
+        from ..utils.tracing import tracer
+        for stage, st in tracer().summary().items():
+            lab = {"stage": stage}
+            out.append(_line("loqa_stage_count", st["count"], lab))
+            out.append(_line("loqa_stage_p50_ms", st["p50_ms"], lab))
+            out.append(_line("loqa_stage_p99_ms", st["p99_ms"], lab))
         nats = s.nats.stats() if s.nats is not None and s.nats.conn is not None else None
         if nats is not None:
             for k, v in vars(nats).items():
                 out.append(_line("loqa_nats_" + k, v))
         return out
+
+    async def trace(self, req: web.Request) -> web.Response:
+        """Chrome-trace JSON of the recent per-stage spans (load in Perfetto)."""
+        from ..utils.tracing import tracer
+        return web.Response(text=tracer().chrome_trace(), content_type="application/json")
 
     async def metrics(self, req: web.Request) -> web.Response:
         return web.Response(text="\n".join(self.collect()) + "\n",

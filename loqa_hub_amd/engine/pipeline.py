@@ -25,6 +25,7 @@ from ..llm.prompts import build_multi_command_prompt, build_prompt
 from ..llm.transcriber import TranscriptionResult, to_transcription_result
 from ..transport.device_commands import ExecutionContext, NATSCommandExecutor
 from ..utils.faults import faults
+from ..utils.tracing import tracer
 from .grammar import multi_command_schema, single_command_schema
 from .llm_engine import GenRequest, LLMEngine
 from .stt_engine import STTEngine, STTRequest
@@ -124,7 +125,8 @@ class VoicePipeline:
             return
         ctx = ExecutionContext(j.relay_id, j.request_id, "", j.transcription.text)
         q = CommandQueue(j.multi.commands, self.queue_max_duration, self.rollback)
-        j.queue = await q.execute(NATSCommandExecutor(self.nats, ctx))
+        with tracer().span("queue", request=j.request_id, commands=len(j.multi.commands)):
+            j.queue = await q.execute(NATSCommandExecutor(self.nats, ctx))
         j.t["queue_done"] = time.perf_counter()
 
     # ------------------------------------------------------------- batch run
@@ -161,14 +163,17 @@ class VoicePipeline:
             j = owner_of[id(r)]
             j.t["llm_first"] = r.t_first
             j.t["llm_done"] = r.t_done
-            self.parse(j, r)
+            with tracer().span("parse", request=j.request_id):
+                self.parse(j, r)
             tasks.append(asyncio.ensure_future(self.execute(j)))
 
         def on_done(r: GenRequest) -> None:  # called on the GPU worker thread
             loop.call_soon_threadsafe(start_queue, r)
 
         if reqs:
+            t_llm = time.monotonic()
             await loop.run_in_executor(ex, self.llm.generate, reqs, on_done)
+            tracer().record("llm", t_llm, time.monotonic(), batch=len(reqs))
         await asyncio.sleep(0)  # let the last call_soon_threadsafe callbacks run
         while len(tasks) < len(reqs):
             await asyncio.sleep(0.0005)

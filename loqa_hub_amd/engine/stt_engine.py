@@ -20,6 +20,7 @@ import torch
 from .. import ops
 from ..models.configs import WhisperConfig
 from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused
+from ..utils.tracing import tracer
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
@@ -293,9 +294,14 @@ class STTEngine:
         if not reqs:
             return reqs
         assert len(reqs) <= self.max_batch, "batch exceeds max_batch"
-        audio, sumsq = self.upload(reqs, device_pcm)
-        enc = self.model.encode(audio)
-        self.cross_kv(enc)
+        tr = tracer()
+        dev = self.device if self.is_gpu else None
+        with tr.span("h2d", dev, batch=len(reqs)):
+            audio, sumsq = self.upload(reqs, device_pcm)
+        with tr.span("encode", dev, batch=len(reqs)):
+            enc = self.model.encode(audio)
+            self.cross_kv(enc)
+        t_dec = time.monotonic()
         B = len(reqs)
         targets = []
         for r in reqs:
@@ -325,6 +331,7 @@ class STTEngine:
                 still.append(i)
             live = still
             step += 1
+        tr.record("stt_decode", t_dec, time.monotonic(), steps=step, batch=B)
         ss = sumsq.cpu().numpy()
         for i, r in enumerate(reqs):
             n = max(1, min(len(r.pcm), N_SAMPLES))

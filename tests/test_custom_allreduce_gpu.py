@@ -1,4 +1,4 @@
-"""Custom IPC one-shot all-reduce (K17). The round-end box has one GPU, so the
+"""Custom IPC one-shot / two-shot all-reduce (K17). The round-end box has one GPU, so the
 ranks share cuda:0: the IPC mapping, the signal protocol, the epoch double
 buffering and graph replay are exercised; the cross-GPU xGMI reads are the
 same code path with different physical links. Handles are exchanged over gloo."""
@@ -25,9 +25,11 @@ def _worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
         from loqa_hub_amd.parallel.custom_allreduce import CustomAllReduce
-        car = CustomAllReduce(dist.group.WORLD, slot_bytes=1 << 20)
+        car = CustomAllReduce(dist.group.WORLD, slot_bytes=4 << 20)
         ok = True
-        for dt, n in ((torch.bfloat16, 16 * 8192), (torch.float32, 16 * 4096), (torch.bfloat16, 8)):
+        # one-shot (small, decode) and two-shot (>= 512 KB, prefill) sizes
+        for dt, n in ((torch.bfloat16, 16 * 8192), (torch.float32, 16 * 4096), (torch.bfloat16, 8),
+                      (torch.bfloat16, 1 << 20), (torch.float32, 3 << 18)):
             xs = [torch.randn(n, generator=torch.Generator().manual_seed(100 * r + n)).to(dt)
                   for r in range(world)]
             expect = torch.zeros(n)

@@ -87,3 +87,16 @@ def test_tts_error_degrades_to_text(engines):
             raise AssertionError("unreachable")
     res = _process(engines, "tts_error", nats=True, tts=FakeTTS())
     assert all(r.success and r.response_text and not r.audio for r in res)
+
+
+def test_tracing_spans_recorded(engines):
+    import json
+
+    from loqa_hub_amd.utils.tracing import tracer
+    tracer().clear()
+    _process(engines, "", nats=True)
+    summ = tracer().summary()
+    for stage in ("h2d", "encode", "stt_decode", "llm", "parse", "queue"):
+        assert stage in summ and summ[stage]["count"] >= 1, (stage, summ.keys())
+    ev = json.loads(tracer().chrome_trace())["traceEvents"]
+    assert any(e["name"] == "queue" for e in ev)
