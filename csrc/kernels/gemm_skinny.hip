@@ -261,21 +261,23 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     // RMSNorm scale rsqrt(E[x^2] + eps); LayerNorm also the mean
     const int Mp = a.Mpad, G = 256 / Mp;
     const int m = threadIdx.x % Mp, g = threadIdx.x / Mp;
-    // every load issued before any add (a dependent loop would serialise
-    // up to 16 memory latencies); host guarantees rowstat_tiles * Mpad <= 4096
-    float vq[16], vs[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int t = g + i * G;
-      const bool ok = t < a.rowstat_tiles;
-      vq[i] = ok ? a.rowsq_in[(size_t)t * Mp + m] : 0.f;
-      if constexpr (NORM == NORM_LN) vs[i] = ok ? a.rowsum_in[(size_t)t * Mp + m] : 0.f;
-    }
+    // loads issued 16 at a time before any add (a dependent loop would
+    // serialise one memory latency per tile)
     float aq = 0.f, as = 0.f;
+    for (int base = 0; base < a.rowstat_tiles; base += 16 * G) {
+      float vq[16], vs[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      aq += vq[i];
-      if constexpr (NORM == NORM_LN) as += vs[i];
+      for (int i = 0; i < 16; ++i) {
+        const int t = base + g + i * G;
+        const bool ok = t < a.rowstat_tiles;
+        vq[i] = ok ? a.rowsq_in[(size_t)t * Mp + m] : 0.f;
+        if constexpr (NORM == NORM_LN) vs[i] = ok ? a.rowsum_in[(size_t)t * Mp + m] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        aq += vq[i];
+        if constexpr (NORM == NORM_LN) as += vs[i];
+      }
     }
     sred[g * Mp + m] = aq;
     if constexpr (NORM == NORM_LN) sred[512 + g * Mp + m] = as;
@@ -538,8 +540,8 @@ template <int MT, int MODE, int NORM>
 static int launch_fused(const FusedArgs& a, hipStream_t st) {
   dim3 grid(a.N / 32, a.S);
   const int kw = a.K / 32 / (a.S * 4);
-  if (kw % 4 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<MT, 4, MODE, NORM>), grid, dim3(256), 0, st, a);
+  if (MT <= 2 && kw % 4 == 0)   // Mpad 64: at most 2 k-steps per prefetch group (VGPRs)
+    hipLaunchKernelGGL((skinny_fused_kernel<MT, (MT <= 2 ? 4 : 2), MODE, NORM>), grid, dim3(256), 0, st, a);
   else if (kw % 2 == 0)
     hipLaunchKernelGGL((skinny_fused_kernel<MT, 2, MODE, NORM>), grid, dim3(256), 0, st, a);
   else
@@ -549,7 +551,11 @@ static int launch_fused(const FusedArgs& a, hipStream_t st) {
 
 template <int MODE, int NORM>
 static int dispatch_fused(const FusedArgs& a, hipStream_t st) {
-  return a.Mpad == 16 ? launch_fused<1, MODE, NORM>(a, st) : launch_fused<2, MODE, NORM>(a, st);
+  switch (a.Mpad) {
+    case 16: return launch_fused<1, MODE, NORM>(a, st);
+    case 32: return launch_fused<2, MODE, NORM>(a, st);
+    default: return launch_fused<4, MODE, NORM>(a, st);
+  }
 }
 
 template <int MODE>
@@ -570,11 +576,10 @@ static int dispatch_norm(const FusedArgs& a, int norm, hipStream_t st) {
 // tile-contiguous slabs); counters: >= N/32 zeroed ints.
 extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   const int Mpad = p->Mpad, N = p->N, K = p->K, S = p->S;
-  if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 || (Mpad != 16 && Mpad != 32))
+  if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 || (Mpad != 16 && Mpad != 32 && Mpad != 64))
     return (int)hipErrorInvalidValue;
   if (S > 1 && (!p->part || !p->counters)) return (int)hipErrorInvalidValue;
-  if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1 || p->rowstat_tiles * Mpad > 4096))
-    return (int)hipErrorInvalidValue;
+  if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1)) return (int)hipErrorInvalidValue;
   if (p->norm == NORM_LN && (!p->rowsum_in || !p->colsum)) return (int)hipErrorInvalidValue;
   if (p->mode == EPI_ROPE && (p->D % 32 || N != (p->H + 2 * p->Hkv) * p->D))
     return (int)hipErrorInvalidValue;

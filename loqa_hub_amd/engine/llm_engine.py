@@ -167,7 +167,7 @@ class LLMEngine:
     # ------------------------------------------------------------ forward
     def _forward_sample(self, meta: StepMeta, mask_rows: torch.Tensor) -> torch.Tensor:
         if meta.decode:
-            if self.fused_decode and meta.tokens.numel() <= 32:
+            if self.fused_decode and meta.tokens.numel() <= 64:
                 logits = self.model.forward_decode_fused(meta, self.kv.k, self.kv.v, self.attn_ws,
                                                          self.scratch)
             else:
@@ -203,8 +203,13 @@ class LLMEngine:
                         cu_q=dev["cu_q"], ctx_lens=dev["ctx_lens"], block_tables=dev["block_tables"],
                         logit_idx=dev["logit_idx"], max_q=max_q, max_ctx=max_ctx, decode=decode)
 
-    def _decode_graph(self, B_pad: int, T_pad: int) -> dict:
-        key = (B_pad, T_pad)
+    CTX_BUCKET = 256
+
+    def _decode_graph(self, B_pad: int, T_pad: int, ctx: int | None = None) -> dict:
+        """Captured decode step per (sequence, token, context) bucket; the
+        context bucket sizes the attention split grid (no empty splits)."""
+        ctx = ctx or self.max_seq_len
+        key = (B_pad, T_pad, ctx)
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -228,7 +233,7 @@ class LLMEngine:
             off += n
         dev["slots"].fill_(-1)
         dev["logit_idx"], host["logit_idx"] = d64, h64.numpy()
-        meta = self._build_meta(dev, self.max_decode_q, self.max_seq_len, True)
+        meta = self._build_meta(dev, self.max_decode_q, ctx, True)
         # warm up (allocator + kernels) on a side stream, then capture
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -323,7 +328,9 @@ class LLMEngine:
         if self.use_graphs:
             B_pad = _bucket(B, self.SEQ_BUCKETS)
             T_pad = ops.mpad_for(T)
-            g = self._decode_graph(B_pad, T_pad)
+            ctx = max(self.kv.pool.seq_len(r.seq_id) + len(f) for r, f in zip(live, feeds))
+            C = min(self.max_seq_len, -(-ctx // self.CTX_BUCKET) * self.CTX_BUCKET)
+            g = self._decode_graph(B_pad, T_pad, C)
             hb = g["host"]
             self._meta(live, feeds, True, B_pad, T_pad, out=hb)
             hb["mask_rows"].fill(0)

@@ -68,7 +68,7 @@ class STTEngine:
         self.stats = {"utterances": 0, "decode_steps": 0}
         self.max_batch = max_batch
         self.fast_decode = fast_decode
-        # fused-epilogue decoder GEMMs (8 launches per layer) for Mpad <= 32
+        # fused-epilogue decoder GEMMs (8 launches per layer) for Mpad <= 64
         self.fused = fused and fast_decode
         self.scratch = ops.FusedScratch(self.device) if self.fused else None
         self.use_graphs = use_graphs and self.is_gpu and fast_decode
@@ -189,23 +189,33 @@ class STTEngine:
                 out[k] = t.to(self.device, non_blocking=True)
         return out
 
-    def _fast_forward(self, dev: dict, max_q: int, B_pad: int) -> torch.Tensor:
-        if self.fused and dev["tokens"].numel() <= 32:
+    def _self_splits(self, ctx: int | None) -> int:
+        """Self-attention key splits for a context bound (graph bucket)."""
+        if ctx is None:
+            return self.self_splits
+        return max(1, min(self.self_splits, (ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS))
+
+    def _fast_forward(self, dev: dict, max_q: int, B_pad: int, ctx: int | None = None) -> torch.Tensor:
+        ns = self._self_splits(ctx)
+        if self.fused and dev["tokens"].numel() <= 64:
             logits = decode_step_fused(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                        dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
                                        self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
                                        dev["enc_lens"], dev["logit_idx"], self.ws, self.scratch,
-                                       self.self_splits, self.SPLIT_KEYS)
+                                       ns, self.SPLIT_KEYS)
             return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
         logits = decode_step_fast(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                   dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
                                   self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
-                                  dev["enc_lens"], dev["logit_idx"], self.ws, self.self_splits,
+                                  dev["enc_lens"], dev["logit_idx"], self.ws, ns,
                                   self.SPLIT_KEYS)
         return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
 
-    def _graph(self, B_pad: int, T_pad: int) -> dict:
-        key = (B_pad, T_pad)
+    def _graph(self, B_pad: int, T_pad: int, ctx: int) -> dict:
+        """Captured decode step for (sequence bucket, token bucket, context
+        bucket): the attention grid is sized for the bucket's context, so no
+        workgroups are spent on splits past the longest sequence."""
+        key = (B_pad, T_pad, ctx)
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -232,11 +242,11 @@ class STTEngine:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            self._fast_forward(dev, max_q, B_pad)
+            self._fast_forward(dev, max_q, B_pad, ctx)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            out = self._fast_forward(dev, max_q, B_pad)
+            out = self._fast_forward(dev, max_q, B_pad, ctx)
         g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
              "h64": h64, "d64": d64}
         self._graphs[key] = g
@@ -249,7 +259,9 @@ class STTEngine:
             B_pad = next((b for b in self.SEQ_BUCKETS if b >= B), B)
             T_pad = ops.mpad_for(T)
             if self.use_graphs:
-                g = self._graph(B_pad, T_pad)
+                ctx = max(self.kv.pool.seq_len(reqs[i].seq_id) + len(feeds[i]) for i in live)
+                C = min(self.cfg.n_text_ctx, -(-ctx // self.SPLIT_KEYS) * self.SPLIT_KEYS)
+                g = self._graph(B_pad, T_pad, C)
                 self._host_meta(reqs, live, feeds, B_pad, T_pad, out=g["host"])
                 g["d32"].copy_(g["h32"], non_blocking=True)
                 g["d64"].copy_(g["h64"], non_blocking=True)

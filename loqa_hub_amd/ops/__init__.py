@@ -785,7 +785,7 @@ class FusedLinear:
         self.N, self.K = w.shape
 
 
-def tune_fused(wp, mode: str, *, mpads=(16, 32), norm=None, act: str = "none",
+def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none",
                heads: tuple | None = None, cos_sin=None) -> None:
     """Measure the split-K of one fused decode GEMM shape on dummy operands
     (``heads`` = (H, Hkv, D) for "rope"); before any graph capture."""
@@ -835,7 +835,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
                  row_sums: bool = False) -> torch.Tensor:
-    """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16 or 32.
+    """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32 or 64.
 
     ``wp`` is a shuffled weight or a ``FusedLinear`` (which supplies the norm
     kind unless ``norm`` is given, the folded bias and the LayerNorm column
@@ -867,8 +867,8 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
         return _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual,
                                  positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
                                  n_kv, head_dim, out, act, bias, colsum, row_sums)
-    assert Mpad in (16, 32) and x.dtype == torch.bfloat16 and x.stride(1) == 1
-    assert ntiles <= scratch.counters.numel()
+    assert Mpad in (16, 32, 64) and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert ntiles <= scratch.counters.numel() and ntiles * Mpad <= scratch.rowsq.numel()
     if nrm == 2:
         assert colsum is not None and colsum.numel() == N
     if bias is not None:

@@ -33,7 +33,7 @@ def _decode_logits(eng, fused: bool, seq_base: int, tok, Mpad: int):
     return outs
 
 
-def _compare(device, splits=None):
+def _compare(device, splits=None, Mpad=16):
     from loqa_hub_amd.engine.llm_engine import LLMEngine
     from loqa_hub_amd.models.configs import llama_config
     eng = LLMEngine(llama_config("test-tiny"), device, max_seqs=8, use_graphs=False)
@@ -43,17 +43,21 @@ def _compare(device, splits=None):
         d = eng.cfg.d_model
         for N, K in ((eng.weights.h * 64 + 2 * eng.weights.hkv * 64, d), (d, eng.weights.h * 64),
                      (2 * eng.weights.f, d), (d, eng.weights.f)):
-            for Mpad in (16, 32):
+            for mp in (16, 32, 64):
                 s = max(x for x in ops.SPLIT_CANDIDATES if x <= splits and K % (x * 128) == 0)
-                ops._SPLITS[(N, K, Mpad)] = s
+                ops._SPLITS[(N, K, mp)] = s
+        saved = dict(ops._FSPLITS)
+        ops._FSPLITS.clear()
     g = torch.Generator().manual_seed(3)
     tok = torch.randint(10, 4000, (3, 12), generator=g).tolist()
-    a = _decode_logits(eng, True, 100, tok, 16)
-    b = _decode_logits(eng, False, 200, tok, 16)
+    a = _decode_logits(eng, True, 100, tok, Mpad)
+    b = _decode_logits(eng, False, 200, tok, Mpad)
     for x, y in zip(a, b):
         rel = float((x - y).norm() / (y.norm() + 1e-12))
         assert rel < 2e-2, rel
     ops._SPLITS.clear()
+    if splits is not None:
+        ops._FSPLITS.update(saved)
 
 
 def test_fused_decode_matches_unfused_cpu():
@@ -69,9 +73,9 @@ def test_permutations_are_bijections():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("splits", [None, 1, 2])
-def test_fused_decode_matches_unfused_gpu(splits):
-    _compare("cuda", splits)
+@pytest.mark.parametrize("splits,Mpad", [(None, 16), (1, 16), (2, 16), (None, 64), (2, 64)])
+def test_fused_decode_matches_unfused_gpu(splits, Mpad):
+    _compare("cuda", splits, Mpad)
 
 
 @pytest.mark.gpu
@@ -105,11 +109,11 @@ def test_fused_resid_rowsq_and_silu_gpu():
         assert float((a.float() - expect.float()).norm() / expect.float().norm()) < 1e-2
 
 
-def _ln_case(dev, S=None):
+def _ln_case(dev, S=None, Mpad=16):
     """LayerNorm-prologue GEMM (folded weight / shift / bias) with a GELU
     epilogue, against layernorm -> linear -> gelu in fp32."""
     torch.manual_seed(1)
-    Mpad, K, N = 16, 512, 768
+    K, N = 512, 768
     x = (torch.randn(Mpad, K, device=dev) * 2 + 0.5).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
     g = (torch.rand(K, device=dev) + 0.5).bfloat16()
@@ -141,9 +145,9 @@ def test_fused_layernorm_act_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S", [1, 2])
-def test_fused_layernorm_act_gpu(S):
-    _ln_case("cuda", S)
+@pytest.mark.parametrize("S,Mpad", [(1, 16), (2, 16), (1, 64), (2, 32)])
+def test_fused_layernorm_act_gpu(S, Mpad):
+    _ln_case("cuda", S, Mpad)
 
 
 @pytest.mark.gpu
