@@ -92,11 +92,37 @@ def build(force: bool = False, debug: bool = False) -> list[str]:
     ]
 
 
+def build_sanitized(kind: str = "address,undefined", out_dir: str | None = None) -> str:
+    """Host-only sanitizer build of the C++ runtime + its stress test
+    (GPU sanitizers are not available on the target pool).
+    ``kind``: "address,undefined" or "thread". Returns the executable path."""
+    out_dir = out_dir or os.path.join(HERE, "build", "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "pool_stress_" + kind.replace(",", "_"))
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        raise RuntimeError("no host C++ compiler")
+    cmd = [cxx, "-std=c++17", "-O1", "-g", f"-fsanitize={kind}", "-fno-omit-frame-pointer",
+           "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-Wno-unused-result",
+           os.path.join(CSRC, "runtime", "runtime.cpp"),
+           os.path.join(CSRC, "runtime", "tests", "pool_stress.cpp"),
+           "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath,/opt/rocm/lib", "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"sanitizer build failed: {' '.join(cmd)}\n{r.stderr[-3000:]}")
+    return exe
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--sanitize", choices=["address,undefined", "thread"],
+                    help="build + run the host runtime stress test under a sanitizer")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        exe = build_sanitized(a.sanitize)
+        return subprocess.run([exe]).returncode
     for p in build(force=a.force, debug=a.debug):
         print(p)
     return 0
