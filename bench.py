@@ -72,6 +72,8 @@ def main(argv=None) -> int:
     ap.add_argument("--mix", default="1,2,3,4", help="commands per utterance, cycled")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (2: STT of the next batch overlaps the LLM decode)")
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
     args = ap.parse_args(argv)
 
@@ -109,11 +111,13 @@ def main(argv=None) -> int:
     slot = slot_len_for(per_rank)
     all_jobs: list[PipelineJob] = []
 
-    def step(record: bool) -> None:
+    async def step(record: bool, prev: asyncio.Future | None) -> None:
         dpcm = scatter_pcm(info, per_rank if info.rank == 0 else None, slot)
         jobs = [PipelineJob(u.relay_id, f"req-{info.rank}-{i}", u.pcm, transcript_hint=u.text)
                 for i, u in enumerate(mine)]
-        loop.run_until_complete(pipe.process(jobs, device_pcm=dpcm))
+        await pipe.process(jobs, device_pcm=dpcm)
+        if prev is not None:
+            await prev  # collectives stay in step order on every rank
         rec = torch.tensor([[j.n_commands, j.n_expected, float(j.queue is not None and j.queue.success),
                              (j.t.get("queue_done", j.t["start"]) - j.t["start"]) * 1e3]
                             for j in jobs], dtype=torch.float64)
@@ -123,15 +127,26 @@ def main(argv=None) -> int:
             step.records.append(gathered.cpu())
 
     step.records = []
-    for _ in range(args.warmup):
-        step(False)
+
+    async def run(n: int, record: bool) -> None:
+        """n batches with up to ``--inflight`` in flight: batch k+1's STT (its
+        own worker thread + stream) overlaps batch k's LLM decode."""
+        sem = asyncio.Semaphore(max(1, args.inflight))
+        tasks: list[asyncio.Future] = []
+        for _ in range(n):
+            await sem.acquire()
+            t = asyncio.ensure_future(step(record, tasks[-1] if tasks else None))
+            t.add_done_callback(lambda _t: sem.release())
+            tasks.append(t)
+        await asyncio.gather(*tasks)
+
+    loop.run_until_complete(run(args.warmup, False))
     pdist.barrier(info)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     s0 = dict(llm.stats)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    loop.run_until_complete(run(args.steps, True))
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     pdist.barrier(info)
@@ -170,7 +185,7 @@ def main(argv=None) -> int:
             "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT, grammar-constrained LLM)",
             "config": {"model": f"{args.stt} + {args.llm}", "global_batch": info.world * B,
                        "seq_len": 1500, "parallelism": f"dp{info.world}",
-                       "commands_mix": mix, "baseline_config": 4},
+                       "commands_mix": mix, "baseline_config": 4, "inflight": args.inflight},
             "ms_per_added_command_e2e_marginal": None if e2e < 0 else round(e2e, 3),
             "ms_per_added_command_ref_equiv": None if ref < 0 else round(ref, 4),
             "baseline_ms_per_added_command": BASELINE_MS_PER_ADDED_COMMAND,

@@ -241,7 +241,8 @@ class LLMEngine:
             out = self._forward_sample(meta, dev["mask_rows"])
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture: the other GPU worker thread keeps running
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             out = self._forward_sample(meta, dev["mask_rows"])
         g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
              "h64": h64, "d64": d64}

@@ -57,17 +57,26 @@ class PipelineJob:
 class VoicePipeline:
     def __init__(self, stt: STTEngine, llm: LLMEngine, nats=None, *, min_response_tokens: int = 8,
                  queue_max_duration: float = 0.0, rollback: bool = True, tts=None,
-                 response_audio: bool = False):
+                 response_audio: bool = False, overlap: bool = True):
         self.stt, self.llm, self.nats = stt, llm, nats
         self.min_response_tokens = min_response_tokens
         self.queue_max_duration = queue_max_duration
         self.rollback = rollback
         self.tts = tts
         self.response_audio = response_audio
+        # overlap: STT and the LLM decode run on their own worker threads and
+        # HIP streams, so batch k+1's (compute-bound) encoder overlaps batch k's
+        # (HBM-bound) decode when several batches are in flight
+        self.overlap = overlap and llm.device.type == "cuda"
         self._pool: ThreadPoolExecutor | None = None
+        self._stt_pool: ThreadPoolExecutor | None = None
 
     # --------------------------------------------------------------- stages
     def transcribe(self, jobs: list[PipelineJob], device_pcm=None) -> None:
+        if device_pcm is not None and device_pcm.is_cuda:
+            # the samples were produced on the default stream (e.g. an RCCL scatter)
+            cur = torch.cuda.current_stream(device_pcm.device)
+            cur.wait_stream(torch.cuda.default_stream(device_pcm.device))
         reqs = [STTRequest(j.pcm, transcript=j.transcript_hint) for j in jobs]
         self.stt.transcribe(reqs, device_pcm)
         now = time.perf_counter()
@@ -130,15 +139,27 @@ class VoicePipeline:
         j.t["queue_done"] = time.perf_counter()
 
     # ------------------------------------------------------------- batch run
+    def _worker(self, name: str, own_stream: bool) -> ThreadPoolExecutor:
+        dev = self.llm.device
+
+        def init():
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
+                if own_stream:
+                    torch.cuda.set_stream(torch.cuda.Stream(dev))
+        return ThreadPoolExecutor(1, thread_name_prefix=name, initializer=init)
+
     def _gpu_executor(self) -> ThreadPoolExecutor:
         if self._pool is None:
-            dev = self.llm.device
-
-            def init():
-                if dev.type == "cuda":
-                    torch.cuda.set_device(dev)
-            self._pool = ThreadPoolExecutor(1, thread_name_prefix="gpu-worker", initializer=init)
+            self._pool = self._worker("gpu-worker", self.overlap)
         return self._pool
+
+    def _stt_executor(self) -> ThreadPoolExecutor:
+        if not self.overlap:
+            return self._gpu_executor()
+        if self._stt_pool is None:
+            self._stt_pool = self._worker("stt-worker", True)
+        return self._stt_pool
 
     async def process(self, jobs: list[PipelineJob], device_pcm=None) -> list[PipelineJob]:
         """GPU stages run on a dedicated worker thread; each utterance's command
@@ -149,7 +170,7 @@ class VoicePipeline:
         t0 = time.perf_counter()
         for j in jobs:
             j.t["start"] = t0
-        await loop.run_in_executor(ex, self.transcribe, jobs, device_pcm)
+        await loop.run_in_executor(self._stt_executor(), self.transcribe, jobs, device_pcm)
         reqs, owners = [], []
         for j in jobs:
             r = self.build_request(j)
