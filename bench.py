@@ -72,8 +72,11 @@ def main(argv=None) -> int:
     ap.add_argument("--mix", default="1,2,3,4", help="commands per utterance, cycled")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--mode", choices=["closed", "batch"], default="closed",
+                    help="closed: B concurrent closed-loop streams per GPU (continuous batching); "
+                         "batch: lockstep batches of B")
     ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight (2: STT of the next batch overlaps the LLM decode)")
+                    help="--mode batch: batches in flight (2: next batch's STT overlaps the decode)")
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
     args = ap.parse_args(argv)
 
@@ -100,7 +103,7 @@ def main(argv=None) -> int:
     stt = STTEngine(whisper_config(args.stt), dev, seed=args.seed, max_batch=max(B, 8))
     llm = LLMEngine(llama_config(args.llm), dev, seed=args.seed, max_seqs=max(B, 8), max_seq_len=1024,
                     use_graphs=not args.no_graphs)
-    pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8)
+    pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=B)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t_init = time.perf_counter() - t_init
@@ -128,9 +131,9 @@ def main(argv=None) -> int:
 
     step.records = []
 
-    async def run(n: int, record: bool) -> None:
-        """n batches with up to ``--inflight`` in flight: batch k+1's STT (its
-        own worker thread + stream) overlaps batch k's LLM decode."""
+    async def run_batches(n: int, record: bool) -> None:
+        """--mode batch: n lockstep batches of B utterances, up to
+        ``--inflight`` batches in flight."""
         sem = asyncio.Semaphore(max(1, args.inflight))
         tasks: list[asyncio.Future] = []
         for _ in range(n):
@@ -139,6 +142,29 @@ def main(argv=None) -> int:
             t.add_done_callback(lambda _t: sem.release())
             tasks.append(t)
         await asyncio.gather(*tasks)
+
+    async def run_closed(n: int, record: bool) -> None:
+        """--mode closed (default): B concurrent relay streams per GPU, each a
+        closed loop (its next utterance is sent when the previous one's reply
+        is back); n utterances per stream. Arrivals are micro-batched for STT
+        and join the running LLM decode batch (continuous batching)."""
+        async def client(ci: int) -> None:
+            for k in range(n):
+                u = mine[(ci + k) % len(mine)]
+                j = PipelineJob(u.relay_id, f"req-{info.rank}-{ci}-{k}", u.pcm,
+                                transcript_hint=u.text)
+                await pipe.submit(j)
+                if record:
+                    all_jobs.append(j)
+                    recs_local.append([j.n_commands, j.n_expected,
+                                       float(j.queue is not None and j.queue.success),
+                                       (j.t.get("queue_done", j.t["start"]) - j.t["start"]) * 1e3])
+        await asyncio.gather(*[client(ci) for ci in range(B)])
+
+    recs_local: list[list[float]] = []
+
+    def run(n: int, record: bool):
+        return run_closed(n, record) if args.mode == "closed" else run_batches(n, record)
 
     loop.run_until_complete(run(args.warmup, False))
     pdist.barrier(info)
@@ -152,6 +178,8 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
 
+    if args.mode == "closed" and recs_local:
+        step.records.append(gather_records(info, torch.tensor(recs_local, dtype=torch.float64)).cpu())
     stats = added_command_stats(all_jobs)
     phase_ms = {
         "stt": round(float(np.mean([(j.t["stt_done"] - j.t["start"]) for j in all_jobs])) * 1e3, 2)
@@ -185,7 +213,9 @@ def main(argv=None) -> int:
             "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT, grammar-constrained LLM)",
             "config": {"model": f"{args.stt} + {args.llm}", "global_batch": info.world * B,
                        "seq_len": 1500, "parallelism": f"dp{info.world}",
-                       "commands_mix": mix, "baseline_config": 4, "inflight": args.inflight},
+                       "commands_mix": mix, "baseline_config": 4, "mode": args.mode,
+                       "concurrent_streams_per_gpu": B,
+                       "inflight": args.inflight if args.mode == "batch" else None},
             "ms_per_added_command_e2e_marginal": None if e2e < 0 else round(e2e, 3),
             "ms_per_added_command_ref_equiv": None if ref < 0 else round(ref, 4),
             "baseline_ms_per_added_command": BASELINE_MS_PER_ADDED_COMMAND,

@@ -226,6 +226,7 @@ struct FusedParams {
   void* residual; float* rowsq_out; float* rowsum_out;
   const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
   int H, Hkv, D, blk;
+  int rt;                 // output tile rows / 16 (1: residual / act modes only)
 };
 
 struct FusedArgs {
@@ -239,18 +240,19 @@ struct FusedArgs {
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
 };
 
-template <int MT, int U, int MODE, int NORM>
+template <int RT, int MT, int U, int MODE, int NORM>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
-  __shared__ float4v_ red[3][2 * MT][64];
+  static_assert(RT == 2 || (MODE != EPI_SILU && MODE != EPI_ROPE), "paired epilogues need 32-row tiles");
+  __shared__ float4v_ red[3][RT * MT][64];
   float* sred = reinterpret_cast<float*>(&red[0][0][0]);   // aliases: prologue / ticket
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x;                   // 32-row output tile
+  const int tile = blockIdx.x;                   // (16 * RT)-row output tile
   const int s = blockIdx.y;
   const int KS = a.K >> 5;
   const int kw = KS / (a.S * 4);
   const int ks0 = (s * 4 + wave) * kw;
   const size_t tile_stride = (size_t)KS * 512;
-  const bf16_t* wp = a.Wp + (size_t)(tile * 2) * tile_stride + (size_t)lane * 8;
+  const bf16_t* wp = a.Wp + (size_t)(tile * RT) * tile_stride + (size_t)lane * 8;
   const bf16_t* xp = a.x + (size_t)(lane & 15) * a.ldx + 8 * (lane >> 4);
 
   float sc[MT], mu[MT];
@@ -302,13 +304,13 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     __syncthreads();
   }
 
-  float4v_ acc[2][MT];
+  float4v_ acc[RT][MT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
   const int ng = kw / U;
-  Frag<2, MT, U> f0, f1;
+  Frag<RT, MT, U> f0, f1;
   load_frag(f0, wp, tile_stride, xp, a.ldx, ks0);
   int g = 0;
   for (; g + 2 <= ng; g += 2) {
@@ -321,14 +323,14 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
 
   if (wave > 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) red[wave - 1][i * MT + j][lane] = acc[i][j];
   }
   __syncthreads();
   if (wave == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j)
         acc[i][j] = acc[i][j] + red[0][i * MT + j][lane] + red[1][i * MT + j][lane] +
@@ -339,16 +341,16 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     // take a ticket; the last arriver reduces with sc1 loads (no acquire fence:
     // every handed-off byte is stored and loaded sc1, guide §6 Guideline 16)
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.part, 0, (int)((size_t)gridDim.x * a.S * 2 * MT * 64 * 16), 0x00020000);
-    const int slab0 = tile * a.S * 2 * MT;
+        a.part, 0, (int)((size_t)gridDim.x * a.S * RT * MT * 64 * 16), 0x00020000);
+    const int slab0 = tile * a.S * RT * MT;
     if (wave == 0) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < MT; ++j)
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u32x4_, acc[i][j]), rsrc,
-              (((slab0 + s * 2 * MT) + i * MT + j) * 64 + lane) * 16, 0, 16);
+              (((slab0 + s * RT * MT) + i * MT + j) * 64 + lane) * 16, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -363,22 +365,22 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     if ((int)sred[0] != a.S - 1 || wave != 0) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // fixed summation order (split 0..S-1) whichever block arrives last
-    float4v_ tot[2][MT];
+    float4v_ tot[RT][MT];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) tot[i][j] = float4v_{0.f, 0.f, 0.f, 0.f};
     for (int q = 0; q < a.S; ++q) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int j = 0; j < MT; ++j)
           tot[i][j] += __builtin_bit_cast(
               float4v_, __builtin_amdgcn_raw_buffer_load_b128(
-                            rsrc, (((slab0 + q * 2 * MT) + i * MT + j) * 64 + lane) * 16, 0, 16));
+                            rsrc, (((slab0 + q * RT * MT) + i * MT + j) * 64 + lane) * 16, 0, 16));
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = tot[i][j];
   } else if (wave != 0) {
@@ -393,13 +395,13 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   // LayerNorm shift (W b) is folded into the bias.
   if constexpr (NORM == NORM_RMS) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] *= sc[j];
   } else if constexpr (NORM == NORM_LN) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float4 cv = *reinterpret_cast<const float4*>(a.colsum + tile * 32 + i * 16 + nq);
+    for (int i = 0; i < RT; ++i) {
+      const float4 cv = *reinterpret_cast<const float4*>(a.colsum + tile * (16 * RT) + i * 16 + nq);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         acc[i][j][0] = sc[j] * (acc[i][j][0] - mu[j] * cv.x);
@@ -411,8 +413,8 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   }
   if (a.bias) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.bias + tile * 32 + i * 16 + nq);
+    for (int i = 0; i < RT; ++i) {
+      const float4 bv = *reinterpret_cast<const float4*>(a.bias + tile * (16 * RT) + i * 16 + nq);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         acc[i][j][0] += bv.x; acc[i][j][1] += bv.y; acc[i][j][2] += bv.z; acc[i][j][3] += bv.w;
@@ -440,8 +442,8 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       const int m = j * 16 + (lane & 15);
       float sq = 0.f, sm = 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        bf16_t* rp = a.residual + (size_t)m * a.N + tile * 32 + i * 16 + nq;
+      for (int i = 0; i < RT; ++i) {
+        bf16_t* rp = a.residual + (size_t)m * a.N + tile * (16 * RT) + i * 16 + nq;
         uint2 rv = *reinterpret_cast<const uint2*>(rp);
         const float r0 = bf2f(rv.x & 0xffff), r1 = bf2f(rv.x >> 16);
         const float r2 = bf2f(rv.y & 0xffff), r3 = bf2f(rv.y >> 16);
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         if (slot < 0) continue;
         const int bb = slot / a.blk, o = slot - bb * a.blk;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < RT; ++i) {
           const int row = (tile - nq_t - nk_t) * 32 + i * 16 + nq;
           const int head = row / D, c = row - head * D;
           uint2 w2;
@@ -520,7 +522,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     for (int j = 0; j < MT; ++j) {
       const int m = j * 16 + (lane & 15);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < RT; ++i) {
         float o[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -530,40 +532,51 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         uint2 w2;
         w2.x = pack_bf16x2(o[0], o[1]);
         w2.y = pack_bf16x2(o[2], o[3]);
-        *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * 32 + i * 16 + nq) = w2;
+        *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq) = w2;
       }
     }
   }
 }
 
-template <int MT, int MODE, int NORM>
+template <int RT, int MT, int MODE, int NORM>
 static int launch_fused(const FusedArgs& a, hipStream_t st) {
-  dim3 grid(a.N / 32, a.S);
+  dim3 grid(a.N / (16 * RT), a.S);
   const int kw = a.K / 32 / (a.S * 4);
   if (MT <= 2 && kw % 4 == 0)   // Mpad 64: at most 2 k-steps per prefetch group (VGPRs)
-    hipLaunchKernelGGL((skinny_fused_kernel<MT, (MT <= 2 ? 4 : 2), MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), MODE, NORM>), grid, dim3(256), 0, st, a);
   else if (kw % 2 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<MT, 2, MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, MODE, NORM>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((skinny_fused_kernel<MT, 1, MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, MODE, NORM>), grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
-template <int MODE, int NORM>
-static int dispatch_fused(const FusedArgs& a, hipStream_t st) {
+template <int RT, int MODE, int NORM>
+static int dispatch_mt(const FusedArgs& a, hipStream_t st) {
   switch (a.Mpad) {
-    case 16: return launch_fused<1, MODE, NORM>(a, st);
-    case 32: return launch_fused<2, MODE, NORM>(a, st);
-    default: return launch_fused<4, MODE, NORM>(a, st);
+    case 16: return launch_fused<RT, 1, MODE, NORM>(a, st);
+    case 32: return launch_fused<RT, 2, MODE, NORM>(a, st);
+    default: return launch_fused<RT, 4, MODE, NORM>(a, st);
   }
 }
 
+// rt: rows per output tile / 16. The paired epilogues (SwiGLU gate|up, RoPE
+// halves) need 32-row tiles; residual / activation epilogues may use 16-row
+// tiles (twice the workgroups without a K split: no split-K reduction tail).
+template <int MODE, int NORM>
+static int dispatch_fused(const FusedArgs& a, int rt, hipStream_t st) {
+  if constexpr (MODE == EPI_RESID || MODE == EPI_ACT) {
+    if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, st);
+  }
+  return dispatch_mt<2, MODE, NORM>(a, st);
+}
+
 template <int MODE>
-static int dispatch_norm(const FusedArgs& a, int norm, hipStream_t st) {
+static int dispatch_norm(const FusedArgs& a, int norm, int rt, hipStream_t st) {
   switch (norm) {
-    case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, st);
-    case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, st);
-    case NORM_LN: return dispatch_fused<MODE, NORM_LN>(a, st);
+    case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, rt, st);
+    case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, rt, st);
+    case NORM_LN: return dispatch_fused<MODE, NORM_LN>(a, rt, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -573,7 +586,8 @@ static int dispatch_norm(const FusedArgs& a, int norm, hipStream_t st) {
 // (act 0 identity, 1 GELU-erf). norm: 1 RMSNorm / 2 LayerNorm of x (the bf16
 // residual) with the norm weight folded into Wp; the row statistics come from
 // rowstat_tiles partial sums. part: S * Mpad * N f32 scratch (S > 1,
-// tile-contiguous slabs); counters: >= N/32 zeroed ints.
+// tile-contiguous slabs); counters: >= N/(16*rt) zeroed ints. Row statistics of
+// the residual epilogue are written per (16*rt)-row tile.
 extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   const int Mpad = p->Mpad, N = p->N, K = p->K, S = p->S;
   if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 || (Mpad != 16 && Mpad != 32 && Mpad != 64))
@@ -585,6 +599,8 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if ((p->mode == EPI_SILU || p->mode == EPI_ACT) && (!p->out || p->ldo % 4))
     return (int)hipErrorInvalidValue;
+  if ((p->rt != 1 && p->rt != 2) || ((p->mode == EPI_SILU || p->mode == EPI_ROPE) && p->rt != 2))
+    return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
               p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,
@@ -592,10 +608,10 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   switch (p->mode) {
-    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, st);
-    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, st);
-    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, st);
-    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, st);
+    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, st);
+    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, st);
+    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, p->rt, st);
+    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, p->rt, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

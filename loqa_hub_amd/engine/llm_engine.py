@@ -18,7 +18,10 @@ sequence) plus one small pinned H2D copy of the step metadata.
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
+from concurrent.futures import Future
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -50,6 +53,8 @@ class GenRequest:
     # optional streaming hook: called from the engine thread with each step's
     # newly emitted token ids (sampled token + jump-forward literal)
     on_tokens: object = None
+    # optional completion hook (continuous-batching scheduler), engine thread
+    on_done: object = None
 
 
 def _bucket(n: int, buckets: list[int]) -> int:
@@ -286,7 +291,9 @@ class LLMEngine:
                 r.t_done = now
                 r.output = r.grammar.text()
                 r.feed = []
-                if self._on_done is not None:
+                if r.on_done is not None:
+                    r.on_done(r)
+                elif self._on_done is not None:
                     self._on_done(r)
             else:
                 r.feed = [int(t)] + forced
@@ -349,6 +356,96 @@ class LLMEngine:
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += T
         self._sample_and_advance(live, nxt, time.perf_counter(), carry)
+
+    # --------------------------------------------- continuous batching
+    def start(self, stream_priority: int = 0) -> None:
+        """Start the scheduler thread: requests submitted with ``submit_batch``
+        join the running decode batch at the next step boundary (their prompts
+        are prefilled first), so utterances arriving while others decode share
+        every weight read of the decode steps."""
+        if getattr(self, "_sched", None) is not None:
+            return
+        self._inbox: queue.Queue = queue.Queue()
+        self._running = True
+        self._sched = threading.Thread(target=self._schedule, args=(stream_priority,),
+                                       name="llm-scheduler", daemon=True)
+        self._sched.start()
+
+    def stop(self) -> None:
+        if getattr(self, "_sched", None) is None:
+            return
+        self._running = False
+        self._inbox.put(None)
+        self._sched.join(timeout=60)
+        self._sched = None
+
+    def submit_batch(self, reqs: list[GenRequest], on_done=None) -> Future:
+        """Queue requests for the scheduler; ``on_done(req)`` fires on the
+        engine thread as each finishes; the returned future resolves with
+        ``reqs`` when all of them are done."""
+        self.start()
+        fut: Future = Future()
+        self._inbox.put((reqs, on_done, fut))
+        return fut
+
+    def _schedule(self, stream_priority: int) -> None:
+        if self.is_gpu:
+            torch.cuda.set_device(self.device)
+            torch.cuda.set_stream(torch.cuda.Stream(self.device, priority=stream_priority))
+        live: list[GenRequest] = []
+        cells: dict[int, list] = {}   # id(cell) -> [remaining, future, reqs]
+        while self._running:
+            items = [self._inbox.get()] if not live else []   # idle: block for work
+            while True:
+                try:
+                    items.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            new: list[GenRequest] = []
+            for it in items:
+                if it is None:
+                    continue
+                reqs, cb, fut = it
+                if not reqs:
+                    fut.set_result(reqs)
+                    continue
+                cell = [len(reqs), fut, reqs]
+                cells[id(cell)] = cell
+                for r in reqs:
+                    r.on_done = self._completion(cb, cell, cells)
+                    self.submit(r)
+                new += reqs
+            try:
+                if new:
+                    t0 = time.perf_counter()
+                    self.prefill(new)
+                    self.stats["prefill_s"] += time.perf_counter() - t0
+                    live += [r for r in new if not r.done]
+                if live:
+                    t0 = time.perf_counter()
+                    self.decode_step(live)
+                    self.stats["decode_s"] += time.perf_counter() - t0
+                    live = [r for r in live if not r.done]
+            except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
+                for cell in list(cells.values()):
+                    if not cell[1].done():
+                        cell[1].set_exception(e)
+                    for r in cell[2]:
+                        if not r.done:
+                            self.kv.pool.free_seq(r.seq_id)
+                live, cells = [], {}
+
+    def _completion(self, cb, cell, cells):
+        def done(r: GenRequest) -> None:
+            self.kv.pool.free_seq(r.seq_id)
+            if cb is not None:
+                cb(r)
+            cell[0] -= 1
+            if cell[0] == 0:
+                cells.pop(id(cell), None)
+                if not cell[1].done():
+                    cell[1].set_result(cell[2])
+        return done
 
     def generate(self, reqs: list[GenRequest], on_done=None) -> list[GenRequest]:
         """Run the requests to completion. ``on_done(req)`` fires as soon as each

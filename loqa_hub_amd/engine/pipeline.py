@@ -57,7 +57,9 @@ class PipelineJob:
 class VoicePipeline:
     def __init__(self, stt: STTEngine, llm: LLMEngine, nats=None, *, min_response_tokens: int = 8,
                  queue_max_duration: float = 0.0, rollback: bool = True, tts=None,
-                 response_audio: bool = False, overlap: bool = True):
+                 response_audio: bool = False, overlap: bool = True,
+                 continuous: bool | None = None, batch_window: float = 0.002,
+                 max_batch: int = 8):
         self.stt, self.llm, self.nats = stt, llm, nats
         self.min_response_tokens = min_response_tokens
         self.queue_max_duration = queue_max_duration
@@ -68,8 +70,16 @@ class VoicePipeline:
         # HIP streams, so batch k+1's (compute-bound) encoder overlaps batch k's
         # (HBM-bound) decode when several batches are in flight
         self.overlap = overlap and llm.device.type == "cuda"
+        # continuous: utterances join the LLM engine's running decode batch
+        # (scheduler thread) instead of decoding batch by batch
+        self.continuous = self.overlap if continuous is None else continuous
+        self.batch_window, self.max_batch = batch_window, max_batch
         self._pool: ThreadPoolExecutor | None = None
         self._stt_pool: ThreadPoolExecutor | None = None
+        self._pending: list[tuple[PipelineJob, asyncio.Future]] = []
+        self._batcher: asyncio.Task | None = None
+        self._stt_lock: asyncio.Lock | None = None
+        self.stats = {"stt_batches": 0, "utterances": 0}
 
     # --------------------------------------------------------------- stages
     def transcribe(self, jobs: list[PipelineJob], device_pcm=None) -> None:
@@ -161,22 +171,83 @@ class VoicePipeline:
             self._stt_pool = self._worker("stt-worker", True)
         return self._stt_pool
 
-    async def process(self, jobs: list[PipelineJob], device_pcm=None) -> list[PipelineJob]:
-        """GPU stages run on a dedicated worker thread; each utterance's command
-        queue is scheduled on the event loop the moment its own decode finishes,
-        so command execution/NATS publishing overlaps the remaining decode."""
+    # ------------------------------------------------------------ serving
+    async def submit(self, job: PipelineJob) -> PipelineJob:
+        """Serve one utterance. Arrivals are micro-batched for the STT stage
+        (every utterance that arrived while the previous STT batch ran, up to
+        ``max_batch``); their parses then join the LLM engine's running decode
+        batch, and each command queue starts as soon as its own decode ends."""
         loop = asyncio.get_running_loop()
-        ex = self._gpu_executor()
+        fut = loop.create_future()
+        self._pending.append((job, fut))
+        if self._batcher is None or self._batcher.done():
+            self._batcher = loop.create_task(self._batch_loop())
+        return await fut
+
+    async def _batch_loop(self) -> None:
+        if self._stt_lock is None:
+            self._stt_lock = asyncio.Lock()
+        while self._pending:
+            await asyncio.sleep(self.batch_window)
+            async with self._stt_lock:
+                batch = self._pending[: self.max_batch]
+                self._pending = self._pending[self.max_batch:]
+                jobs = [j for j, _ in batch]
+                try:
+                    await self._stt_stage(jobs)
+                except Exception as e:  # noqa: BLE001
+                    for j, f in batch:
+                        if not f.done():
+                            f.set_exception(e)
+                    continue
+            asyncio.ensure_future(self._finish(batch))
+
+    async def _finish(self, batch) -> None:
+        futs = {id(j): f for j, f in batch}
+
+        def job_done(j: PipelineJob) -> None:  # each reply as soon as ITS queue is done
+            f = futs.get(id(j))
+            if f is not None and not f.done():
+                f.set_result(j)
+        try:
+            await self._llm_stage([j for j, _ in batch], job_done)
+        except Exception as e:  # noqa: BLE001
+            for _, f in batch:
+                if not f.done():
+                    f.set_exception(e)
+            return
+        for j, f in batch:
+            if not f.done():
+                f.set_result(j)
+
+    async def process(self, jobs: list[PipelineJob], device_pcm=None) -> list[PipelineJob]:
+        """One batch end to end: STT on the STT worker thread, then the LLM
+        stage; each utterance's command queue is scheduled on the event loop
+        the moment its own decode finishes, so command execution / NATS
+        publishing overlaps the remaining decode."""
+        await self._stt_stage(jobs, device_pcm)
+        await self._llm_stage(jobs)
+        return jobs
+
+    async def _stt_stage(self, jobs: list[PipelineJob], device_pcm=None) -> None:
+        loop = asyncio.get_running_loop()
         t0 = time.perf_counter()
         for j in jobs:
-            j.t["start"] = t0
+            j.t["start"] = j.t.get("start", t0)
         await loop.run_in_executor(self._stt_executor(), self.transcribe, jobs, device_pcm)
+        self.stats["stt_batches"] += 1
+        self.stats["utterances"] += len(jobs)
+
+    async def _llm_stage(self, jobs: list[PipelineJob], job_done=None) -> None:
+        loop = asyncio.get_running_loop()
         reqs, owners = [], []
         for j in jobs:
             r = self.build_request(j)
             if r is not None:
                 reqs.append(r)
                 owners.append(j)
+            elif job_done is not None:
+                job_done(j)
         owner_of = {id(r): j for r, j in zip(reqs, owners)}
         tasks: list[asyncio.Future] = []
 
@@ -186,20 +257,25 @@ class VoicePipeline:
             j.t["llm_done"] = r.t_done
             with tracer().span("parse", request=j.request_id):
                 self.parse(j, r)
-            tasks.append(asyncio.ensure_future(self.execute(j)))
+            t = asyncio.ensure_future(self.execute(j))
+            if job_done is not None:
+                t.add_done_callback(lambda _t, j=j: job_done(j))
+            tasks.append(t)
 
         def on_done(r: GenRequest) -> None:  # called on the GPU worker thread
             loop.call_soon_threadsafe(start_queue, r)
 
         if reqs:
             t_llm = time.monotonic()
-            await loop.run_in_executor(ex, self.llm.generate, reqs, on_done)
+            if self.continuous:
+                await asyncio.wrap_future(self.llm.submit_batch(reqs, on_done))
+            else:
+                await loop.run_in_executor(self._gpu_executor(), self.llm.generate, reqs, on_done)
             tracer().record("llm", t_llm, time.monotonic(), batch=len(reqs))
         await asyncio.sleep(0)  # let the last call_soon_threadsafe callbacks run
         while len(tasks) < len(reqs):
             await asyncio.sleep(0.0005)
         await asyncio.gather(*tasks)
-        return jobs
 
 
 def added_command_stats(jobs: list[PipelineJob]) -> dict:

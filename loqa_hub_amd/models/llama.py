@@ -309,14 +309,13 @@ class LlamaModel:
         Mpad = meta.tokens.numel()
         residual = self.embed(meta.tokens).contiguous()
         # layer 0's RMSNorm row scale: one partial sum of squares per row
-        torch.sum(residual.float().square(), 1, out=scratch.rowsq[:Mpad])
+        scratch.seed_stats(residual, sums=False)
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
         q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
-        tiles = d // 32
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
             ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True,
-                             eps=cfg.norm_eps, rowsq_tiles=1 if li == 0 else tiles,
+                             eps=cfg.norm_eps,
                              positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
                              k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
                              n_heads=H, n_kv=Hkv, head_dim=D)
@@ -327,7 +326,7 @@ class LlamaModel:
                                  max_k=meta.max_ctx)
             ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
             a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
-                                 eps=cfg.norm_eps, rowsq_tiles=tiles)
+                                 eps=cfg.norm_eps)
             ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
         sel = residual.index_select(0, meta.logit_idx).contiguous()
         hf = ops.rmsnorm(sel, w.final_norm, cfg.norm_eps)

@@ -305,11 +305,9 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
     Mpad = tokens.numel()
     residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
     scratch.seed_stats(residual)
-    tiles = d // 32
     q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
     for i, F in enumerate(w.dec_f):
-        ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5,
-                         rowsq_tiles=1 if i == 0 else tiles, positions=positions, q_out=q,
+        ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5, positions=positions, q_out=q,
                          k_cache=k_cache[i], v_cache=v_cache[i], slots=slots, n_heads=H, n_kv=H,
                          head_dim=D)
         a = ops.attention(q, k_cache[i], v_cache[i], cu_q, n_heads=H, n_kv=H, head_dim=D,
@@ -317,14 +315,13 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
                           grouped=True, split_keys=split_keys, num_splits=self_splits,
                           workspace=ws)
         ops.skinny_fused(a, F["o"], "resid", scratch, residual=residual, row_sums=True)
-        xq = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5, rowsq_tiles=tiles)
+        xq = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5)
         kv = xkv[i]
         a = ops.attention(xq, kv, kv[:, d:], cu_q, n_heads=H, n_kv=H, head_dim=D, causal=False,
                           max_q=max_q, cu_k=enc_starts, ctx_lens=enc_lens, grouped=True,
                           split_keys=cross_split_keys, num_splits=enc_splits, workspace=ws)
         ops.skinny_fused(a, F["xo"], "resid", scratch, residual=residual, row_sums=True)
-        m = ops.skinny_fused(residual, F["fc1"], "act", scratch, act="gelu", eps=1e-5,
-                             rowsq_tiles=tiles)
+        m = ops.skinny_fused(residual, F["fc1"], "act", scratch, act="gelu", eps=1e-5)
         ops.skinny_fused(m, F["fc2"], "resid", scratch, residual=residual, row_sums=True)
     sel = residual.index_select(0, logit_idx).contiguous()
     hf = ops.layernorm(sel, w.dec_ln_w, w.dec_ln_b, 1e-5)

@@ -346,15 +346,7 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
         for s in SPLIT_CANDIDATES:
             if K % (s * 128):
                 continue
-            for _ in range(2):
-                skinny_gemm(x, wp, s)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(reps):
-                skinny_gemm(x, wp, s)
-            b.record()
-            b.synchronize()
-            t = a.elapsed_time(b)
+            t = graph_time(lambda: skinny_gemm(x, wp, s), reps)
             if t < best_t * 0.98:
                 best, best_t = s, t
         _SPLITS[key] = best
@@ -365,29 +357,51 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 _FSPLITS: dict = {}
 
 
-def tune_fused_splits(key: tuple, run, K: int, reps: int = 8) -> int:
-    """Split-K for a fused-epilogue GEMM, measured: ``run(s)`` launches it at
-    split ``s``. The in-launch reduce adds a store-drain + ticket round trip to
-    every workgroup's tail, so the best split is lower than the plain GEMM's
-    and is tuned separately (``key`` = (mode, N, K, Mpad))."""
+def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,)) -> tuple[int, int]:
+    """(split-K, tile rows / 16) for a fused-epilogue GEMM, measured:
+    ``run(s, rt)`` launches it. The in-launch reduce adds a store-drain +
+    ticket round trip to every workgroup's tail, so the best split is lower
+    than the plain GEMM's; 16-row tiles (rt=1, residual / act epilogues only)
+    double the workgroups without any reduction. ``key`` = (mode, N, K, Mpad)."""
     if key in _FSPLITS:
         return _FSPLITS[key]
-    best, best_t = 1, float("inf")
-    for s in SPLIT_CANDIDATES:
-        if K % (s * 128):
-            continue
+    best, best_t = (1, rts[-1]), float("inf")
+    for rt in rts:
+        for s in SPLIT_CANDIDATES:
+            if K % (s * 128):
+                continue
+            t = graph_time(lambda: run(s, rt), reps)
+            if t < best_t * 0.98:
+                best, best_t = (s, rt), t
+    _FSPLITS[key] = best
+    return best
+
+
+def graph_time(fn, reps: int = 8, trials: int = 3) -> float:
+    """Device time (ms) of ``reps`` back-to-back calls of ``fn`` replayed from
+    a captured HIP graph (no host launch overhead in the measurement: a few-µs
+    kernel is otherwise hidden behind its own launch cost); min over trials."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
         for _ in range(2):
-            run(s)
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(trials):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(reps):
-            run(s)
+        g.replay()
         b.record()
         b.synchronize()
-        t = a.elapsed_time(b)
-        if t < best_t * 0.98:
-            best, best_t = s, t
-    _FSPLITS[key] = best
+        best = min(best, a.elapsed_time(b))
+    del g
     return best
 
 
@@ -738,13 +752,16 @@ class FusedScratch:
         self.counters = torch.zeros(max_tiles, dtype=torch.int32, device=device)
         self.rowsq = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
         self.rowsum = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
+        self.stat_tiles = 0   # partial tiles written by the last residual epilogue
 
-    def seed_stats(self, x: torch.Tensor) -> None:
+    def seed_stats(self, x: torch.Tensor, sums: bool = True) -> None:
         """Row statistics of ``x`` as ONE partial tile (layer 0's norm input)."""
         M = x.shape[0]
         xf = x.float()
         torch.sum(xf.square(), 1, out=self.rowsq[:M])
-        torch.sum(xf, 1, out=self.rowsum[:M])
+        if sums:
+            torch.sum(xf, 1, out=self.rowsum[:M])
+        self.stat_tiles = 1
 
 
 _FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3, "act": 4}
@@ -819,8 +836,9 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
             kw.update(positions=pos, cos_sin=cos_sin, q_out=torch.empty(Mpad, H * D, **bf),
                       k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
                       head_dim=D)
-        tune_fused_splits(key, lambda sp: skinny_fused(x, wp, mode, scr, splits=sp, norm=nrm,
-                                                       **kw), K)
+        rts = (1, 2) if mode in ("resid", "act") else (2,)
+        tune_fused_splits(key, lambda sp, rt: skinny_fused(x, wp, mode, scr, splits=sp, rt=rt,
+                                                           norm=nrm, **kw), K, rts=rts)
 
 
 def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
@@ -830,7 +848,8 @@ def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
 
 
 def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
-                 splits: int | None = None, norm=None, eps: float = 1e-5, rowsq_tiles: int = 0,
+                 splits: int | None = None, norm=None, eps: float = 1e-5,
+                 rowsq_tiles: int | None = None, rt: int | None = None,
                  residual: torch.Tensor | None = None, positions=None, cos_sin=None, q_out=None,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
@@ -841,7 +860,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     kind unless ``norm`` is given, the folded bias and the LayerNorm column
     sums). ``norm`` True/"rms":
     RMSNorm, "ln": LayerNorm; the row statistics come from ``rowsq_tiles``
-    partial tiles in ``scratch`` (the norm weight is folded into the weight).
+    partial tiles in ``scratch`` (default: what the last residual epilogue wrote) (the norm weight is folded into the weight).
     mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
     "resid": residual += x W^T (+ bias) in place, writes per-tile row sums of
     squares (and row sums with ``row_sums``);
@@ -856,9 +875,17 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     Mpad, K = x.shape
     N = wp.shape[0] * 16
     nrm = _NORMS[norm]
-    S = splits or _FSPLITS.get((mode, N, K, Mpad)) or choose_splits(N, K, Mpad)
+    tuned = _FSPLITS.get((mode, N, K, Mpad))
+    S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
+    rt = rt or (tuned[1] if tuned else 2)
+    if mode in ("silu", "rope"):
+        rt = 2
+    if rowsq_tiles is None:
+        rowsq_tiles = scratch.stat_tiles
     m = _FUSED_MODES[mode]
-    ntiles = N // 32
+    ntiles = N // (16 * rt)
+    if mode == "resid":
+        scratch.stat_tiles = ntiles
     if mode == "silu" and out is None:
         out = torch.empty(Mpad, N // 2, dtype=torch.bfloat16, device=x.device)
     elif mode == "act" and out is None:
@@ -866,7 +893,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     if not _gpu(x):
         return _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual,
                                  positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
-                                 n_kv, head_dim, out, act, bias, colsum, row_sums)
+                                 n_kv, head_dim, out, act, bias, colsum, row_sums, rt)
     assert Mpad in (16, 32, 64) and x.dtype == torch.bfloat16 and x.stride(1) == 1
     assert ntiles <= scratch.counters.numel() and ntiles * Mpad <= scratch.rowsq.numel()
     if nrm == 2:
@@ -890,6 +917,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.positions, p.cs, p.q_out = ptr(positions), ptr(cos_sin), ptr(q_out)
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
+    p.rt = rt
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out
@@ -898,7 +926,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
 
 def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, positions,
                       cos_sin, q_out, k_cache, v_cache, slots, H, Hkv, D, out, act, bias, colsum,
-                      row_sums):
+                      row_sums, rt=2):
     Mpad, K = x.shape
     N = wp.shape[0] * 16
     y = x.float() @ ref.unshuffle_weight(wp).float().t()  # [Mpad, N] in permuted row order
@@ -927,10 +955,11 @@ def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, pos
     if mode == "resid":
         h = (y + residual.float()).to(torch.bfloat16)
         residual.copy_(h)
-        sq = h.float().pow(2).view(Mpad, N // 32, 32).sum(-1).t().contiguous()  # [tiles, Mpad]
+        R = 16 * rt
+        sq = h.float().pow(2).view(Mpad, N // R, R).sum(-1).t().contiguous()  # [tiles, Mpad]
         scratch.rowsq[: sq.numel()] = sq.flatten()
         if row_sums:
-            sm = h.float().view(Mpad, N // 32, 32).sum(-1).t().contiguous()
+            sm = h.float().view(Mpad, N // R, R).sum(-1).t().contiguous()
             scratch.rowsum[: sm.numel()] = sm.flatten()
         return residual
     inv = torch.argsort(ref.perm_rope_qkv(H, Hkv, D))

@@ -63,61 +63,34 @@ class GPUVoiceProcessor:
                  tts_format: str = "wav"):
         self.pipeline = pipeline
         self.tts = tts
-        self.batch_window = batch_window
-        self.max_batch = max_batch
         self.tts_format = tts_format
-        self._pending: list[tuple[object, asyncio.Future]] = []
-        self._flusher: asyncio.Task | None = None
-        self._lock = asyncio.Lock()
-        self.stats = {"batches": 0, "utterances": 0}
+        pipeline.batch_window, pipeline.max_batch = batch_window, max_batch
+        self.stats = {"utterances": 0, "errors": 0}
 
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
                       sample_rate: int, transcript_hint: str | None = None) -> UtteranceResult:
         """``transcript_hint``: synthetic-traffic ground truth that teacher-forces
-        the (random-init) Whisper decoder; real relays never pass it."""
+        the (random-init) Whisper decoder; real relays never pass it. Concurrent
+        calls are micro-batched by the pipeline (STT batch, continuous LLM batch)."""
         from ..engine.pipeline import PipelineJob
-        loop = asyncio.get_running_loop()
-        fut = loop.create_future()
-        self._pending.append((PipelineJob(relay_id, request_id, float_to_pcm16(audio),
-                                          transcript_hint), fut))
-        if len(self._pending) >= self.max_batch or self._flusher is None or self._flusher.done():
-            self._flusher = loop.create_task(self._flush())
-        return await fut
-
-    async def _flush(self) -> None:
-        await asyncio.sleep(self.batch_window)
-        async with self._lock:  # one GPU batch at a time
-            while self._pending:
-                batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
-                await self._run(batch)
-
-    async def _run(self, batch) -> None:
-        jobs = [j for j, _ in batch]
+        j = PipelineJob(relay_id, request_id, float_to_pcm16(audio), transcript_hint)
         try:
-            await self.pipeline.process(jobs)
+            await self.pipeline.submit(j)
         except Exception as e:  # noqa: BLE001
             log.exception("GPU pipeline failed")
-            for _, f in batch:
-                if not f.done():
-                    f.set_result(UtteranceResult(success=False, command="error",
-                                                 response_text=MSG_STT_FAILED, error=str(e)))
-            return
-        self.stats["batches"] += 1
-        self.stats["utterances"] += len(jobs)
-        results = []
-        for j in jobs:
-            if j.stt_failed:
-                results.append(UtteranceResult(success=False, command="error",
-                                               response_text=MSG_STT_FAILED, error=j.error))
-                continue
-            text = j.transcription.text if j.transcription else ""
-            ok = None if j.queue is None else j.queue.success
-            results.append(_result_from(text, j.multi, ok, j.transcription))
+            self.stats["errors"] += 1
+            return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
+                                   error=str(e))
+        self.stats["utterances"] += 1
+        if j.stt_failed:
+            return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
+                                   error=j.error)
+        text = j.transcription.text if j.transcription else ""
+        ok = None if j.queue is None else j.queue.success
+        r = _result_from(text, j.multi, ok, j.transcription)
         if self.tts is not None:
-            await self._speak(results)
-        for (_, f), r in zip(batch, results):
-            if not f.done():
-                f.set_result(r)
+            await self._speak([r])
+        return r
 
     async def _speak(self, results: list[UtteranceResult]) -> None:
         from ..llm.tts import TTSOptions

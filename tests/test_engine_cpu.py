@@ -295,3 +295,52 @@ def test_conv_transpose_polyphase_cpu():
         y1 = ops.conv_transpose1d(x, ct, pre_slope=0.1, polyphase=True).float()
         y2 = R.conv_transpose1d(x, w, b, stride=s, padding=p, pre_slope=0.1)
         assert y1.shape == y2.shape and (y1 - y2).abs().max() <= 0.02 * y2.abs().max()
+
+
+def test_llm_continuous_batching_scheduler_cpu():
+    """Requests submitted while others decode join the running batch; every
+    request completes with its schema's command count and KV blocks are freed."""
+    import time as _t
+
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=8,
+                    max_seq_len=512, use_graphs=False)
+    free0 = eng.kv.pool.free_blocks()
+    mk = lambda ns: [GenRequest(eng.tok.encode(f"turn on the lights {n}", bos=True),
+                                multi_command_schema(n, min_response_tokens=2)) for n in ns]
+    seen = []
+    a = eng.submit_batch(mk((1, 3)), on_done=lambda r: seen.append(r.seq_id))
+    _t.sleep(0.05)
+    b = eng.submit_batch(mk((2, 4)))
+    ra, rb = a.result(timeout=120), b.result(timeout=120)
+    for n, r in zip((1, 3, 2, 4), ra + rb):
+        assert len(parse_multi_command_response(r.output, "x").commands) == n
+    assert sorted(seen) == sorted(r.seq_id for r in ra)
+    eng.stop()
+    assert eng.kv.pool.free_blocks() == free0
+
+
+def test_pipeline_submit_continuous_cpu():
+    import asyncio
+
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline
+    from loqa_hub_amd.engine.stt_engine import STTEngine
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import llama_config, whisper_config
+    stt = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4)
+    llm = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=8,
+                    max_seq_len=1024, use_graphs=False)
+    pipe = VoicePipeline(stt, llm, None, min_response_tokens=2, continuous=True, max_batch=4)
+    utts = make_batch(1, 4, [1, 2, 3, 4])
+
+    async def go():
+        async def one(i, u, delay):
+            await asyncio.sleep(delay)
+            return await pipe.submit(PipelineJob(u.relay_id, f"r{i}", u.pcm, transcript_hint=u.text))
+        return await asyncio.gather(*[one(i, u, 0.03 * i) for i, u in enumerate(utts)])
+    jobs = asyncio.run(go())
+    llm.stop()
+    assert [j.n_commands for j in jobs] == [j.n_expected for j in jobs] == [1, 2, 3, 4]
+    assert pipe.stats["utterances"] == 4

@@ -109,7 +109,7 @@ def test_fused_resid_rowsq_and_silu_gpu():
         assert float((a.float() - expect.float()).norm() / expect.float().norm()) < 1e-2
 
 
-def _ln_case(dev, S=None, Mpad=16):
+def _ln_case(dev, S=None, Mpad=16, rt=2):
     """LayerNorm-prologue GEMM (folded weight / shift / bias) with a GELU
     epilogue, against layernorm -> linear -> gelu in fp32."""
     torch.manual_seed(1)
@@ -122,7 +122,7 @@ def _ln_case(dev, S=None, Mpad=16):
     lin = ops.FusedLinear(w, norm="ln", norm_w=g, norm_b=b, bias=bias)
     scr = ops.FusedScratch(dev)
     scr.seed_stats(x)
-    y = ops.skinny_fused(x, lin, "act", scr, splits=S, act="gelu", eps=1e-5, rowsq_tiles=1)
+    y = ops.skinny_fused(x, lin, "act", scr, splits=S, act="gelu", eps=1e-5, rowsq_tiles=1, rt=rt)
     h = torch.nn.functional.layer_norm(x.float(), (K,), g.float(), b.float(), 1e-5)
     expect = torch.nn.functional.gelu(h @ w.float().t() + bias.float())
     rel = float((y.float() - expect).norm() / expect.norm())
@@ -132,8 +132,9 @@ def _ln_case(dev, S=None, Mpad=16):
     a = (torch.randn(Mpad, N, device=dev) * 0.5).bfloat16()
     wo = (torch.randn(K, N, device=dev) * 0.05).bfloat16()
     ops.skinny_fused(a, ops.FusedLinear(wo, bias=bias[:K]), "resid", scr,
-                     splits=S, residual=res, row_sums=True)
-    tiles = K // 32
+                     splits=S, residual=res, row_sums=True, rt=rt)
+    tiles = K // (16 * rt)
+    assert scr.stat_tiles == tiles
     sm = scr.rowsum[: tiles * Mpad].view(tiles, Mpad).sum(0)
     sq = scr.rowsq[: tiles * Mpad].view(tiles, Mpad).sum(0)
     assert torch.allclose(sm, res.float().sum(1), rtol=1e-3, atol=1e-2)
@@ -145,9 +146,10 @@ def test_fused_layernorm_act_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,Mpad", [(1, 16), (2, 16), (1, 64), (2, 32)])
-def test_fused_layernorm_act_gpu(S, Mpad):
-    _ln_case("cuda", S, Mpad)
+@pytest.mark.parametrize("S,Mpad,rt", [(1, 16, 2), (2, 16, 2), (1, 64, 2), (2, 32, 2),
+                                       (1, 16, 1), (2, 32, 1), (2, 64, 1)])
+def test_fused_layernorm_act_gpu(S, Mpad, rt):
+    _ln_case("cuda", S, Mpad, rt)
 
 
 @pytest.mark.gpu

@@ -175,7 +175,8 @@ def test_gpu_voice_processor_batches_on_cpu(tmp_path):
         audios = [rng.standard_normal(16000).astype(np.float32) * 0.1 for _ in range(3)]
         res = await asyncio.gather(*[proc.process(f"r{i}", f"q{i}", a, 16000)
                                      for i, a in enumerate(audios)])
-        assert proc.stats == {"batches": 1, "utterances": 3}
+        assert proc.stats["utterances"] == 3
+        assert proc.pipeline.stats == {"stt_batches": 1, "utterances": 3}
         assert all(r.command in ("voice_command_success", "no_speech", "error",
                                  "confirmation_needed") for r in res)
     asyncio.run(go())
