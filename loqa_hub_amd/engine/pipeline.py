@@ -251,8 +251,13 @@ class VoicePipeline:
         owner_of = {id(r): j for r, j in zip(reqs, owners)}
         tasks: list[asyncio.Future] = []
 
+        t_llm = time.monotonic()
+
         def start_queue(r: GenRequest) -> None:
             j = owner_of[id(r)]
+            # per-utterance LLM span (submit -> its own decode done): replies go
+            # out per utterance, so a batch-level span could outlive the caller
+            tracer().record("llm", t_llm, time.monotonic(), request=j.request_id)
             j.t["llm_first"] = r.t_first
             j.t["llm_done"] = r.t_done
             with tracer().span("parse", request=j.request_id):
@@ -266,12 +271,10 @@ class VoicePipeline:
             loop.call_soon_threadsafe(start_queue, r)
 
         if reqs:
-            t_llm = time.monotonic()
             if self.continuous:
                 await asyncio.wrap_future(self.llm.submit_batch(reqs, on_done))
             else:
                 await loop.run_in_executor(self._gpu_executor(), self.llm.generate, reqs, on_done)
-            tracer().record("llm", t_llm, time.monotonic(), batch=len(reqs))
         await asyncio.sleep(0)  # let the last call_soon_threadsafe callbacks run
         while len(tasks) < len(reqs):
             await asyncio.sleep(0.0005)
