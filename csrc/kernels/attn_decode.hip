@@ -52,7 +52,7 @@ struct DecSmem {
 // == nullptr) contiguous rows kc/vc[(kv_start[b] + key) * kv_stride + kvh * D]
 // (Whisper cross-attention over the encoder output, read in place).
 template <int D>
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, long long q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, long long kv_stride, const int* __restrict__ kv_start,
     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
@@ -212,109 +212,148 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       for (int j = 0; j < 16; ++j) sm.o[wave - 1][dt][j][lane] = acc[dt][j];
   }
   __syncthreads();
-  if (wave != 0) return;
-  float mstar = m_run;
-#pragma unroll
-  for (int w = 1; w < DEC_WAVES; ++w) mstar = fmaxf(mstar, sm.ml[w][0][lane]);
-  const float s0 = exp2f(m_run - mstar);
-  float l = l_run * s0;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[dt][j] *= s0;
-#pragma unroll
-  for (int w = 1; w < DEC_WAVES; ++w) {
-    const float sw = exp2f(sm.ml[w][0][lane] - mstar);
-    l += sm.ml[w][1][lane] * sw;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[dt][j] += sw * sm.o[w - 1][dt][j][lane];
-  }
-  const size_t tok = (size_t)(q0 + qi);
   const int nsplit = min(num_splits, max(1, (klen + split_keys - 1) / split_keys));
-  bf16_t* orow = out + tok * (size_t)o_stride + (size_t)head * D;
-  if (nsplit == 1) {
-    if (!row_valid) return;
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (wave == 0) {
+    float mstar = m_run;
+#pragma unroll
+    for (int w = 1; w < DEC_WAVES; ++w) mstar = fmaxf(mstar, sm.ml[w][0][lane]);
+    const float s0 = exp2f(m_run - mstar);
+    float l = l_run * s0;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
-                      acc[dt][4 * g4 + 3] * inv};
-        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
-      }
-    return;
-  }
-  // publish this split's partial write-through, then take a ticket
-  const auto ro = __builtin_amdgcn_make_buffer_rsrc(
-      part_o, 0, (int)((size_t)num_splits * total_q * Hq * D * 4), 0x00020000);
-  const auto rm = __builtin_amdgcn_make_buffer_rsrc(
-      part_ml, 0, (int)((size_t)num_splits * total_q * Hq * 2 * 4), 0x00020000);
-  const int row = (int)tok * Hq + head;
-  if (row_valid) {
-    const int ob = (split * total_q * Hq + row) * D * 4;
+      for (int j = 0; j < 16; ++j) acc[dt][j] *= s0;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
+    for (int w = 1; w < DEC_WAVES; ++w) {
+      const float sw = exp2f(sm.ml[w][0][lane] - mstar);
+      l += sm.ml[w][1][lane] * sw;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4v v = {acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), ro,
-                                               ob + (32 * dt + 8 * g4 + 4 * h) * 4, 0, 16);
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[dt][j] += sw * sm.o[w - 1][dt][j][lane];
+    }
+    const size_t tok = (size_t)(q0 + qi);
+    if (nsplit == 1) {
+      if (!row_valid) return;
+      bf16_t* orow = out + tok * (size_t)o_stride + (size_t)head * D;
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
+                        acc[dt][4 * g4 + 3] * inv};
+          *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+        }
+      return;
+    }
+    // publish this split's partial write-through, then take a ticket
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(
+        part_o, 0, (int)((size_t)num_splits * total_q * Hq * D * 4), 0x00020000);
+    const auto rm = __builtin_amdgcn_make_buffer_rsrc(
+        part_ml, 0, (int)((size_t)num_splits * total_q * Hq * 2 * 4), 0x00020000);
+    const int row = (int)tok * Hq + head;
+    if (row_valid) {
+      const int ob = (split * total_q * Hq + row) * D * 4;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4v v = {acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), ro,
+                                                 ob + (32 * dt + 8 * g4 + 4 * h) * 4, 0, 16);
+        }
+      if (h == 0) {
+        const float2 ml = make_float2(mstar, l);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, ml), rm,
+                                              (split * total_q * Hq + row) * 8, 0, 16);
       }
-    if (h == 0) {
-      const float2 ml = make_float2(mstar, l);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_, ml), rm,
-                                            (split * total_q * Hq + row) * 8, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* cnt = counters + (size_t)b * Hkv + kvh;
+    if (lane == 0) {
+      const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == nsplit - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm.ml[0][0][0] = __int_as_float(t);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int* cnt = counters + (size_t)b * Hkv + kvh;
-  int t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __shfl(t, 0, 64);
-  if (t != nsplit - 1) return;
-  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (!row_valid) return;
-  // last split: merge every split's partial in split order (sc1 loads only)
-  float msx = -1e30f;
-  for (int sp = 0; sp < nsplit; ++sp) {
-    const float2 ml = __builtin_bit_cast(
-        float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (sp * total_q * Hq + row) * 8, 0, 16));
-    msx = fmaxf(msx, ml.x);
-  }
-  float L = 0.f;
+  if (nsplit == 1) return;
+  __syncthreads();
+  if (__float_as_int(sm.ml[0][0][0]) != nsplit - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // Last split: the WHOLE workgroup merges every split's partial (split
+  // order fixed, sc1 loads only). Thread t owns row t / 8 of the 32-row tile
+  // and D / 8 of its columns; each batch's loads are all issued before any is
+  // consumed (a rolled loop pays one L2 round trip per split).
+  {
+    constexpr int CW = D / 8, NV = CW / 4;     // columns / float4 per thread
+    constexpr int MLB = 16, OB = 16 / NV;      // (m, l) pairs / partials per batch
+    const int rr = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * CW;
+    const int qr = rr / G;
+    if (!(qr < qlen && rr < (32 / G) * G)) return;
+    const int hr = kvh * G + (rr - qr * G);
+    const size_t tokr = (size_t)(q0 + qr);
+    const int row = (int)tokr * Hq + hr;
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(
+        part_o, 0, (int)((size_t)num_splits * total_q * Hq * D * 4), 0x00020000);
+    const auto rm = __builtin_amdgcn_make_buffer_rsrc(
+        part_ml, 0, (int)((size_t)num_splits * total_q * Hq * 2 * 4), 0x00020000);
+    float msx = -1e30f;
+    float2 mlr[MLB];
+    for (int sp0 = 0; sp0 < nsplit; sp0 += MLB) {
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
+      for (int i = 0; i < MLB; ++i)
+        mlr[i] = sp0 + i < nsplit
+                     ? __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      rm, ((sp0 + i) * total_q * Hq + row) * 8, 0, 16))
+                     : make_float2(-1e30f, 0.f);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[dt][j] = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) {
-    const float2 ml = __builtin_bit_cast(
-        float2, __builtin_amdgcn_raw_buffer_load_b64(rm, (sp * total_q * Hq + row) * 8, 0, 16));
-    const float w = exp2f(ml.x - msx);
-    L += w * ml.y;
-    const int ob = (sp * total_q * Hq + row) * D * 4;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4v v = __builtin_bit_cast(
-            float4v, __builtin_amdgcn_raw_buffer_load_b128(ro, ob + (32 * dt + 8 * g4 + 4 * h) * 4, 0, 16));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[dt][4 * g4 + e] += w * v[e];
-      }
-  }
-  const float inv = L > 0.f ? 1.f / L : 0.f;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
-                    acc[dt][4 * g4 + 3] * inv};
-      *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+      for (int i = 0; i < MLB; ++i) msx = fmaxf(msx, mlr[i].x);
     }
+    const bool ml_cached = nsplit <= MLB;
+    float o[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) o[c] = 0.f;
+    float L = 0.f;
+    for (int sp0 = 0; sp0 < nsplit; sp0 += OB) {
+      float4v v[OB][NV];
+#pragma unroll
+      for (int i = 0; i < OB; ++i) {
+        const int sp = sp0 + i < nsplit ? sp0 + i : 0;
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          v[i][k] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    ro, ((sp * total_q * Hq + row) * D + c0 + 4 * k) * 4, 0, 16));
+      }
+#pragma unroll
+      for (int i = 0; i < OB; ++i) {
+        const int sp = sp0 + i;
+        if (sp >= nsplit) break;
+        float2 ml = make_float2(-1e30f, 0.f);
+        if (ml_cached) {
+#pragma unroll
+          for (int q2 = 0; q2 < MLB; ++q2)
+            if (q2 == sp) ml = mlr[q2];
+        } else {
+          ml = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                                              rm, (sp * total_q * Hq + row) * 8, 0, 16));
+        }
+        const float w = exp2f(ml.x - msx);
+        L += w * ml.y;
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[4 * k + e] += w * v[i][k][e];
+      }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    bf16_t* orow = out + tokr * (size_t)o_stride + (size_t)hr * D + c0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      *reinterpret_cast<uint2*>(orow + 4 * k) =
+          make_uint2(pack_bf16x2(o[4 * k] * inv, o[4 * k + 1] * inv),
+                     pack_bf16x2(o[4 * k + 2] * inv, o[4 * k + 3] * inv));
+  }
 }
 
 // q: [Tq, >=Hq*D] bf16; K/V paged caches [nb, Hkv, blk, D] (block_tables) or

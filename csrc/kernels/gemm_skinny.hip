@@ -35,6 +35,15 @@ __device__ __forceinline__ bf16x8 ldx(const bf16_t* p) {
   return *reinterpret_cast<bf16x8*>(&v);
 }
 
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
+// for its outstanding global loads (__syncthreads' release fence would drain
+// the weight prefetch)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int RT, int MT, int U>
 struct Frag {
   bf16x8 a[U][RT];
@@ -64,6 +73,41 @@ __device__ __forceinline__ void mma_frag(const Frag<RT, MT, U>& f, float4v_ (&ac
       for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(f.a[u][i], f.b[u][j], acc[i][j]);
 }
 
+// Ping-pong stream over ng groups of U k-steps; f0 already holds group 0.
+// The steady-state loop issues the next group UNCONDITIONALLY before consuming
+// the current one: a conditional refill inside the loop body makes the
+// consumer block a join point of the refill / no-refill paths, and hipcc's
+// waitcnt pass then takes the stricter count of the two (vmcnt(0)) - every
+// iteration drained the prefetch and only ONE group was ever in flight.
+template <int RT, int MT, int U>
+__device__ __forceinline__ void stream_k(Frag<RT, MT, U>& f0, Frag<RT, MT, U>& f1,
+                                         float4v_ (&acc)[RT][MT], const bf16_t* wp,
+                                         size_t tile_stride, const bf16_t* xp, long long ldx_,
+                                         int ks0, int ng) {
+  // sched_barrier(0) pins each phase: without it the machine scheduler sinks
+  // the refill loads between the MFMAs to save registers, collapsing the
+  // prefetch distance to 3-5 loads
+  int g = 0;
+  for (; g + 2 < ng; g += 2) {
+    load_frag(f1, wp, tile_stride, xp, ldx_, ks0 + (g + 1) * U);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_frag(f0, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    load_frag(f0, wp, tile_stride, xp, ldx_, ks0 + (g + 2) * U);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_frag(f1, acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (g + 1 < ng) {
+    load_frag(f1, wp, tile_stride, xp, ldx_, ks0 + (g + 1) * U);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_frag(f0, acc);
+    mma_frag(f1, acc);
+  } else {
+    mma_frag(f0, acc);
+  }
+}
+
 template <int RT, int MT, int U>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16_t* __restrict__ x, long long ldx_,
                                                           const bf16_t* __restrict__ Wp,
@@ -87,17 +131,9 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16_t* __restri
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
 
   // ping-pong register prefetch over groups of U k-steps
-  const int ng = kw / U;
   Frag<RT, MT, U> f0, f1;
   load_frag(f0, wp, tile_stride, xp, ldx_, ks0);
-  int g = 0;
-  for (; g + 2 <= ng; g += 2) {
-    load_frag(f1, wp, tile_stride, xp, ldx_, ks0 + (g + 1) * U);
-    mma_frag(f0, acc);
-    if (g + 2 < ng) load_frag(f0, wp, tile_stride, xp, ldx_, ks0 + (g + 2) * U);
-    mma_frag(f1, acc);
-  }
-  if (g < ng) mma_frag(f0, acc);
+  stream_k(f0, f1, acc, wp, tile_stride, xp, ldx_, ks0, kw / U);
 
   if (wave > 0) {
 #pragma unroll
@@ -227,6 +263,7 @@ struct FusedParams {
   const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
   int H, Hkv, D, blk;
   int rt;                 // output tile rows / 16 (1: residual / act modes only)
+  int wr;                 // waves along the rows (1, or 4 at Mpad 16 with S == 1)
 };
 
 struct FusedArgs {
@@ -240,20 +277,38 @@ struct FusedArgs {
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
 };
 
-template <int RT, int MT, int U, int MODE, int NORM>
+// WR: waves along the rows. WR = 1: the 4 waves split the tile's K range
+// (LDS reduce); WR = 4: every wave owns its own (16 * RT)-row tile over the
+// whole K range of the split - the 4 waves then read the SAME activation
+// fragments at about the same time, so x is fetched from L2 once per
+// workgroup (L1 hits for the other 3) instead of once per wave, and no
+// cross-wave reduction is needed (measured on cold weights, M = 16: the
+// gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
+template <int RT, int MT, int U, int WR, int MODE, int NORM>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   static_assert(RT == 2 || (MODE != EPI_SILU && MODE != EPI_ROPE), "paired epilogues need 32-row tiles");
-  __shared__ float4v_ red[3][RT * MT][64];
-  float* sred = reinterpret_cast<float*>(&red[0][0][0]);   // aliases: prologue / ticket
+  constexpr int WK = 4 / WR;                     // waves along K
+  constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
+  constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
+  __shared__ __attribute__((aligned(16))) float smem[NSM];
+  float4v_* red = reinterpret_cast<float4v_*>(smem);
+  float* sred = smem;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x;                   // (16 * RT)-row output tile
+  const int wr = wave % WR, wk = wave / WR;
+  const int tile = blockIdx.x * WR + wr;         // (16 * RT)-row output tile
   const int s = blockIdx.y;
   const int KS = a.K >> 5;
-  const int kw = KS / (a.S * 4);
-  const int ks0 = (s * 4 + wave) * kw;
+  const int kw = KS / (a.S * WK);
+  const int ks0 = (s * WK + wk) * kw;
   const size_t tile_stride = (size_t)KS * 512;
   const bf16_t* wp = a.Wp + (size_t)(tile * RT) * tile_stride + (size_t)lane * 8;
   const bf16_t* xp = a.x + (size_t)(lane & 15) * a.ldx + 8 * (lane >> 4);
+
+  // the first weight group is requested before the norm prologue: the row
+  // statistics only scale the accumulator, so the stream need not wait for
+  // them (the prologue's two L2 round trips then hide under the first fill)
+  Frag<RT, MT, U> f0, f1;
+  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0);
 
   float sc[MT], mu[MT];
 #pragma unroll
@@ -283,7 +338,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     }
     sred[g * Mp + m] = aq;
     if constexpr (NORM == NORM_LN) sred[512 + g * Mp + m] = as;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x < Mp) {
       float tq = 0.f, ts = 0.f;
       for (int q = 0; q < G; ++q) {
@@ -295,13 +350,13 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       sred[256 + threadIdx.x] = rsqrtf(var + a.eps);
       sred[256 + 64 + threadIdx.x] = mean;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       sc[j] = sred[256 + j * 16 + (lane & 15)];
       mu[j] = sred[256 + 64 + j * 16 + (lane & 15)];
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   float4v_ acc[RT][MT];
@@ -309,34 +364,28 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
-  const int ng = kw / U;
-  Frag<RT, MT, U> f0, f1;
-  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0);
-  int g = 0;
-  for (; g + 2 <= ng; g += 2) {
-    load_frag(f1, wp, tile_stride, xp, a.ldx, ks0 + (g + 1) * U);
-    mma_frag(f0, acc);
-    if (g + 2 < ng) load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + (g + 2) * U);
-    mma_frag(f1, acc);
-  }
-  if (g < ng) mma_frag(f0, acc);
+  stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, kw / U);
 
-  if (wave > 0) {
+  if constexpr (WK > 1) {
+    // red[wr][wk - 1][i * MT + j][lane]
+    auto ridx = [&](int q, int ij) { return ((wr * (WK - 1) + q) * RT * MT + ij) * 64 + lane; };
+    if (wk > 0) {
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+      for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) red[wave - 1][i * MT + j][lane] = acc[i][j];
+        for (int j = 0; j < MT; ++j) red[ridx(wk - 1, i * MT + j)] = acc[i][j];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j)
+#pragma unroll
+          for (int q = 0; q < WK - 1; ++q) acc[i][j] += red[ridx(q, i * MT + j)];
+    }
   }
-  __syncthreads();
-  if (wave == 0) {
-#pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
-      for (int j = 0; j < MT; ++j)
-        acc[i][j] = acc[i][j] + red[0][i * MT + j][lane] + red[1][i * MT + j][lane] +
-                    red[2][i * MT + j][lane];
-  }
-  if (a.S > 1) {
+  if (WR == 1 && a.S > 1) {
     // publish this split's partial (tile-contiguous slab, sc1 write-through),
     // take a ticket; the last arriver reduces with sc1 loads (no acquire fence:
     // every handed-off byte is stored and loaded sc1, guide §6 Guideline 16)
@@ -370,24 +419,37 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) tot[i][j] = float4v_{0.f, 0.f, 0.f, 0.f};
-    for (int q = 0; q < a.S; ++q) {
+    // QB slabs per batch, every load issued before the adds (a rolled loop
+    // pays one L2 round trip per split); out-of-range slots add exact zeros
+    constexpr int QB = (8 / (RT * MT)) > 2 ? 8 / (RT * MT) : 2;
+    for (int q0 = 0; q0 < a.S; q0 += QB) {
+      float4v_ v[QB][RT][MT];
 #pragma unroll
-      for (int i = 0; i < RT; ++i)
+      for (int qq = 0; qq < QB; ++qq)
 #pragma unroll
-        for (int j = 0; j < MT; ++j)
-          tot[i][j] += __builtin_bit_cast(
-              float4v_, __builtin_amdgcn_raw_buffer_load_b128(
-                            rsrc, (((slab0 + q * RT * MT) + i * MT + j) * 64 + lane) * 16, 0, 16));
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+          for (int j = 0; j < MT; ++j)
+            v[qq][i][j] = q0 + qq < a.S
+                              ? __builtin_bit_cast(float4v_, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rsrc, (((slab0 + (q0 + qq) * RT * MT) + i * MT + j) * 64 + lane) * 16, 0, 16))
+                              : float4v_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qq = 0; qq < QB; ++qq)
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+          for (int j = 0; j < MT; ++j) tot[i][j] += v[qq][i][j];
     }
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = tot[i][j];
-  } else if (wave != 0) {
+  } else if (wk != 0) {
     return;
   }
 
-  // ---- epilogue (wave 0): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
+  // ---- epilogue (the wk == 0 wave of each row tile): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
   const int nq = 4 * (lane >> 4);
   // Norms: the norm weight g is folded into W at load time, so the row scale
   // factors out of the k-sum: RMSNorm  y = s * (W g) x;  LayerNorm
@@ -538,45 +600,49 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   }
 }
 
-template <int RT, int MT, int MODE, int NORM>
+template <int RT, int MT, int WR, int MODE, int NORM>
 static int launch_fused(const FusedArgs& a, hipStream_t st) {
-  dim3 grid(a.N / (16 * RT), a.S);
-  const int kw = a.K / 32 / (a.S * 4);
+  constexpr int WK = 4 / WR;
+  dim3 grid(a.N / (16 * RT * WR), a.S);
+  const int kw = a.K / 32 / (a.S * WK);
   if (MT <= 2 && kw % 4 == 0)   // Mpad 64: at most 2 k-steps per prefetch group (VGPRs)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM>), grid, dim3(256), 0, st, a);
   else if (kw % 2 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, MODE, NORM>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
 template <int RT, int MODE, int NORM>
-static int dispatch_mt(const FusedArgs& a, hipStream_t st) {
+static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
   switch (a.Mpad) {
-    case 16: return launch_fused<RT, 1, MODE, NORM>(a, st);
-    case 32: return launch_fused<RT, 2, MODE, NORM>(a, st);
-    default: return launch_fused<RT, 4, MODE, NORM>(a, st);
+    case 16:
+      if (wr == 4) return launch_fused<RT, 1, 4, MODE, NORM>(a, st);
+      return launch_fused<RT, 1, 1, MODE, NORM>(a, st);
+    case 32: return launch_fused<RT, 2, 1, MODE, NORM>(a, st);
+    default: return launch_fused<RT, 4, 1, MODE, NORM>(a, st);
   }
 }
 
 // rt: rows per output tile / 16. The paired epilogues (SwiGLU gate|up, RoPE
 // halves) need 32-row tiles; residual / activation epilogues may use 16-row
 // tiles (twice the workgroups without a K split: no split-K reduction tail).
+// wr: waves along the rows (1 or 4; 4 only at Mpad 16 with S == 1).
 template <int MODE, int NORM>
-static int dispatch_fused(const FusedArgs& a, int rt, hipStream_t st) {
+static int dispatch_fused(const FusedArgs& a, int rt, int wr, hipStream_t st) {
   if constexpr (MODE == EPI_RESID || MODE == EPI_ACT) {
-    if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, st);
+    if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, wr, st);
   }
-  return dispatch_mt<2, MODE, NORM>(a, st);
+  return dispatch_mt<2, MODE, NORM>(a, wr, st);
 }
 
 template <int MODE>
-static int dispatch_norm(const FusedArgs& a, int norm, int rt, hipStream_t st) {
+static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, hipStream_t st) {
   switch (norm) {
-    case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, rt, st);
-    case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, rt, st);
-    case NORM_LN: return dispatch_fused<MODE, NORM_LN>(a, rt, st);
+    case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, rt, wr, st);
+    case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, rt, wr, st);
+    case NORM_LN: return dispatch_fused<MODE, NORM_LN>(a, rt, wr, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -602,16 +668,18 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   if ((p->rt != 1 && p->rt != 2) || ((p->mode == EPI_SILU || p->mode == EPI_ROPE) && p->rt != 2))
     return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
+  if (p->wr != 1 && (p->wr != 4 || Mpad != 16 || S != 1 || N % (64 * p->rt)))
+    return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
               p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,
               p->bias, (bf16_t*)p->out, p->ldo, p->act, (bf16_t*)p->residual, p->rowsq_out,
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   switch (p->mode) {
-    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, st);
-    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, st);
-    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, p->rt, st);
-    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, p->rt, st);
+    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, st);
+    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, st);
+    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, p->rt, p->wr, st);
+    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, p->rt, p->wr, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -14,6 +14,7 @@ elementwise/normalisation/attention/audio op around them is ours.
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import math
 
@@ -357,22 +358,31 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 _FSPLITS: dict = {}
 
 
-def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,)) -> tuple[int, int]:
-    """(split-K, tile rows / 16) for a fused-epilogue GEMM, measured:
-    ``run(s, rt)`` launches it. The in-launch reduce adds a store-drain +
-    ticket round trip to every workgroup's tail, so the best split is lower
-    than the plain GEMM's; 16-row tiles (rt=1, residual / act epilogues only)
-    double the workgroups without any reduction. ``key`` = (mode, N, K, Mpad)."""
+def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
+                      wr4: bool = False) -> tuple[int, int, int]:
+    """(split-K, tile rows / 16, waves along rows) for a fused-epilogue GEMM,
+    measured: ``run(s, rt, wr, i)`` launches it on weight copy ``i`` (the graph
+    cycles through ``ncopies`` copies so every call streams COLD weights, as a
+    decode step that reads the whole model does; a warm replay of one copy is
+    partly served by the 256 MB Infinity Cache and ranks the options wrongly).
+    The in-launch reduce adds a store-drain + ticket round trip to every
+    workgroup's tail, so the best split is lower than the plain GEMM's; 16-row
+    tiles (rt=1, residual / act epilogues only) double the workgroups without
+    any reduction; ``wr4`` adds the 4-waves-along-rows layout (S = 1 only).
+    ``key`` = (mode, N, K, Mpad)."""
     if key in _FSPLITS:
         return _FSPLITS[key]
-    best, best_t = (1, rts[-1]), float("inf")
-    for rt in rts:
-        for s in SPLIT_CANDIDATES:
-            if K % (s * 128):
-                continue
-            t = graph_time(lambda: run(s, rt), reps)
-            if t < best_t * 0.98:
-                best, best_t = (s, rt), t
+    N = key[1]
+    cands = [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
+    if wr4:
+        cands += [(1, rt, 4) for rt in rts if N % (64 * rt) == 0]
+    best, best_t = (1, rts[-1], 1), float("inf")
+    n = max(1, ncopies)
+    for c in cands:
+        it = iter(range(1 << 30))
+        t = graph_time(lambda: run(*c, next(it) % n), max(reps, 2 * n))
+        if t < best_t * 0.98:
+            best, best_t = c, t
     _FSPLITS[key] = best
     return best
 
@@ -815,6 +825,16 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
     scr = FusedScratch(dev)
     bf = dict(dtype=torch.bfloat16, device=dev)
     nrm = norm if norm is not None else (lin.norm if lin is not None else None)
+    # cold-weight timing: enough copies that the set outgrows the Infinity Cache
+    nbytes = w.numel() * w.element_size()
+    copies = [wp]
+    for _ in range(min(15, -(-(768 << 20) // nbytes) - 1)):
+        if lin is not None:
+            c = copy.copy(lin)
+            c.wp = lin.wp.clone()
+        else:
+            c = wp.clone()
+        copies.append(c)
     for Mpad in mpads:
         key = (mode, N, K, Mpad)
         if key in _FSPLITS:
@@ -837,8 +857,10 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
                       k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
                       head_dim=D)
         rts = (1, 2) if mode in ("resid", "act") else (2,)
-        tune_fused_splits(key, lambda sp, rt: skinny_fused(x, wp, mode, scr, splits=sp, rt=rt,
-                                                           norm=nrm, **kw), K, rts=rts)
+        tune_fused_splits(key, lambda sp, rt, wr, i: skinny_fused(
+            x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, **kw), K, rts=rts,
+            ncopies=len(copies), wr4=Mpad == 16)
+    del copies
 
 
 def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
@@ -853,7 +875,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
                  residual: torch.Tensor | None = None, positions=None, cos_sin=None, q_out=None,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
-                 row_sums: bool = False) -> torch.Tensor:
+                 row_sums: bool = False, wr: int | None = None) -> torch.Tensor:
     """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32 or 64.
 
     ``wp`` is a shuffled weight or a ``FusedLinear`` (which supplies the norm
@@ -880,6 +902,10 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     rt = rt or (tuned[1] if tuned else 2)
     if mode in ("silu", "rope"):
         rt = 2
+    if wr is None:
+        wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
+    if wr != 1 and (S != 1 or Mpad != 16 or N % (64 * rt)):
+        wr = 1
     if rowsq_tiles is None:
         rowsq_tiles = scratch.stat_tiles
     m = _FUSED_MODES[mode]
@@ -917,7 +943,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.positions, p.cs, p.q_out = ptr(positions), ptr(cos_sin), ptr(q_out)
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
-    p.rt = rt
+    p.rt, p.wr = rt, wr
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out

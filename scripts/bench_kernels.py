@@ -178,38 +178,72 @@ def tiny_bench():
 
 
 def fused_bench():
-    """Fused-epilogue decode GEMMs vs plain skinny GEMM at each split (graph-timed)."""
+    """Fused-epilogue decode GEMMs vs plain skinny GEMM at each split, graph-timed
+    on COLD weights: the graph cycles through enough weight copies (>= 1 GB) that
+    no call finds its weight in the 256 MB Infinity Cache, as in a real decode
+    step that streams the whole model."""
     scr = ops.FusedScratch(dev)
     M, d, H, Hkv, D, blk = 16, 4096, 32, 8, 128, 16
-    res_ = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
-    scr.rowsq[: 128 * M].fill_(float(d) / 128)
     pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
     cs = torch.randn(4096, D // 2, 2, device=dev)
     kc = torch.zeros(64, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
     vc = torch.zeros_like(kc)
     slots = torch.arange(M, dtype=torch.int32, device=dev)
     q = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
-    for name, (N, K), mode in (("qkv", (6144, 4096), "rope"), ("o", (4096, 4096), "resid"),
-                               ("gate_up", (28672, 4096), "silu"), ("down", (4096, 14336), "resid")):
-        wp = ops.shuffle_weight(torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02)
+    for name, (N, K), mode, rows in (("qkv", (6144, 4096), "rope", 128),
+                                     ("o", (4096, 4096), "resid", 0),
+                                     ("gate_up", (28672, 4096), "silu", 256),
+                                     ("down", (4096, 14336), "resid", 0)):
+        ncopy = max(2, -(-(1 << 30) // (N * K * 2)))
+        base = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+        wps = [ops.shuffle_weight(base) for _ in range(ncopy)]
+        del base
         xx = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-        res = {"kernel": "graph_fused", "shape": name, "mode": mode}
+        res_ = torch.randn(M, N if mode == "resid" else d, device=dev, dtype=torch.bfloat16)
+        if rows:
+            scr.rowsq[: rows * M].fill_(float(K) / rows)
+        gb = N * K * 2 / 1e9
+        res = {"kernel": "graph_fused_cold", "shape": name, "mode": mode, "copies": ncopy}
         for S in (1, 2, 4, 8):
             if K % (S * 128):
                 continue
             kw = dict(splits=S)
             if mode == "rope":
-                kw.update(norm=True, rowsq_tiles=128, positions=pos, cos_sin=cs, q_out=q,
+                kw.update(norm=True, rowsq_tiles=rows, positions=pos, cos_sin=cs, q_out=q,
                           k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv, head_dim=D)
             elif mode == "silu":
-                kw.update(norm=True, rowsq_tiles=128)
+                kw.update(norm=True, rowsq_tiles=rows)
             else:
                 kw.update(residual=res_)
-            t = gtime(lambda: ops.skinny_fused(xx, wp, mode, scr, **kw), inner=10)
+            it = iter(range(1 << 30))
+
+            def fused():
+                ops.skinny_fused(xx, wps[next(it) % ncopy], mode, scr, **kw)
+
+            def plain():
+                ops.skinny_gemm(xx, wps[next(it) % ncopy], S)
+            t = gtime(fused, inner=2 * ncopy)
             res[f"fusedS{S}_us"] = round(t, 2)
-            res[f"plainS{S}_us"] = round(gtime(lambda: ops.skinny_gemm(xx, wp, S), inner=10), 2)
+            if S == 1 and N % 128 == 0:
+                kw1 = dict(kw, wr=4)
+
+                def fused4():
+                    ops.skinny_fused(xx, wps[next(it) % ncopy], mode, scr, **kw1)
+                t4 = gtime(fused4, inner=2 * ncopy)
+                res["fusedS1wr4_us"] = round(t4, 2)
+                res["fusedS1wr4_TBps"] = round(gb / t4 * 1e3, 2)
+            res[f"fusedS{S}_TBps"] = round(gb / t * 1e3, 2)
+            res[f"plainS{S}_us"] = round(gtime(plain, inner=2 * ncopy), 2)
         emit(**res)
-        del wp
+        del wps
+
+
+def stream_bench():
+    """HBM read roofline of this box: torch sum over a 2 GB bf16 buffer."""
+    buf = torch.ones(1 << 30, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: buf.sum(dtype=torch.float32), reps=10)
+    emit(kernel="stream_sum_2GB", us=round(t, 2), TBps=round(2.0 * (1 << 30) / 1e6 / t, 2))
+    del buf
 
 
 def slab_bench():
@@ -233,6 +267,8 @@ if __name__ == "__main__":
         tiny_bench()
     if "fused" in which:
         fused_bench()
+    if "stream" in which:
+        stream_bench()
     if "gemm" in which:
         gemm_bench()
     if "attn" in which:

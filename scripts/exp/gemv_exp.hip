@@ -1,0 +1,191 @@
+// GEMV streaming experiments (M = 16 decode shape): which knob limits the
+// weight stream below the HBM roofline? Built separately (scripts/exp), not
+// part of libloqa_kernels.
+#include "../../csrc/kernels/common.h"
+
+typedef float float4v_ __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 ldw(const bf16_t* p) {
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return *reinterpret_cast<bf16x8*>(&v);
+}
+__device__ __forceinline__ bf16x8 ldw_plain(const bf16_t* p) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  return *reinterpret_cast<bf16x8*>(&v);
+}
+__device__ __forceinline__ bf16x8 ldx(const bf16_t* p) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  return *reinterpret_cast<bf16x8*>(&v);
+}
+
+// pure read roofline: grid-stride 16 B per lane
+__global__ __launch_bounds__(256) void stream_read(const u32x4* __restrict__ p, long long n, u32x4* out) {
+  u32x4 acc = {0, 0, 0, 0};
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(p + i + stride);
+    u32x4 c = __builtin_nontemporal_load(p + i + 2 * stride), d = __builtin_nontemporal_load(p + i + 3 * stride);
+    acc ^= a ^ b ^ c ^ d;
+  }
+  for (; i < n; i += stride) acc ^= p[i];
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = acc;
+}
+
+// V: 0 = full (W nt + x + MFMA), 1 = no x loads (constant B), 2 = read only
+// (xor W), 3 = full with plain (non-nt) W loads. STAG: rotate the k start of
+// every wave by its global wave index.
+template <int RT, int U, int V, int STAG>
+__global__ __launch_bounds__(256) void gemv_exp(const bf16_t* __restrict__ x, const bf16_t* __restrict__ Wp,
+                                                float* __restrict__ out, int N, int K, int S) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile0 = blockIdx.x * RT, s = blockIdx.y;
+  const int KS = K >> 5, kw = KS / (S * 4), ks0 = (s * 4 + wave) * kw;
+  const size_t ts = (size_t)KS * 512;
+  const bf16_t* wp = Wp + (size_t)tile0 * ts + (size_t)lane * 8;
+  const bf16_t* xp = x + (size_t)(lane & 15) * K + 8 * (lane >> 4);
+  const int ng = kw / U;
+  const int rot = STAG ? (int)((blockIdx.x * 4 + wave) % ng) : 0;
+  float4v_ acc[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) acc[i] = (float4v_){0, 0, 0, 0};
+  unsigned xr = 0;
+  bf16x8 bconst;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bconst[e] = (__bf16)1.0f;
+  bf16x8 a0[U][RT], a1[U][RT], b0[U], b1[U];
+  auto load = [&](bf16x8 (&a)[U][RT], bf16x8 (&b)[U], int gg) {
+    const int ks = ks0 + ((gg + rot) % ng) * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+        a[u][i] = V == 3 ? ldw_plain(wp + (size_t)i * ts + (size_t)(ks + u) * 512)
+                         : ldw(wp + (size_t)i * ts + (size_t)(ks + u) * 512);
+    if (V == 0 || V == 3) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) b[u] = ldx(xp + (size_t)(ks + u) * 32);
+    }
+  };
+  auto mma = [&](bf16x8 (&a)[U][RT], bf16x8 (&b)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        if (V == 2) {
+          u32x4 t = __builtin_bit_cast(u32x4, a[u][i]);
+          xr ^= t.x ^ t.y ^ t.z ^ t.w;
+        } else {
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], (V == 1) ? bconst : b[u], acc[i], 0, 0, 0);
+        }
+      }
+  };
+  load(a0, b0, 0);
+  int g = 0;
+  for (; g + 2 < ng; g += 2) {
+    load(a1, b1, g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(a0, b0, g + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (g + 1 < ng) { load(a1, b1, g + 1); mma(a0, b0); mma(a1, b1); } else { mma(a0, b0); }
+  float t = xr == 0x9e3779b9u ? 1.f : 0.f;
+#pragma unroll
+  for (int i = 0; i < RT; ++i) t += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (t == 12345.678f) out[blockIdx.x] = t;
+}
+
+extern "C" int exp_stream_read(const void* p, long long nbytes, void* out, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(stream_read, dim3(grid), dim3(256), 0, st, (const u32x4*)p, nbytes / 16, (u32x4*)out);
+  return (int)hipGetLastError();
+}
+
+#define CASE(RT_, U_, V_, ST_)                                                                    \
+  if (rt == RT_ && u == U_ && v == V_ && stag == ST_) {                                           \
+    hipLaunchKernelGGL((gemv_exp<RT_, U_, V_, ST_>), dim3(N / (16 * RT_), S), dim3(256), 0, st, \
+                       (const bf16_t*)x, (const bf16_t*)Wp, out, N, K, S);                        \
+    return (int)hipGetLastError();                                                                \
+  }
+
+extern "C" int exp_gemv(const void* x, const void* Wp, float* out, int N, int K, int S, int rt, int u,
+                        int v, int stag, hipStream_t st) {
+  if (K % (S * 4 * 32 * u)) return 1;
+#define VARS(RT_, U_) CASE(RT_, U_, 0, 0) CASE(RT_, U_, 1, 0) CASE(RT_, U_, 2, 0) CASE(RT_, U_, 3, 0) CASE(RT_, U_, 0, 1) CASE(RT_, U_, 2, 1)
+  VARS(1, 4) VARS(2, 4) VARS(4, 4) VARS(2, 2) VARS(2, 8) VARS(4, 2) VARS(1, 8)
+  return 2;
+}
+
+// Variant family 2: a workgroup = WR x WK waves; wave (wr, wk) streams 16*RT
+// rows (tile blockIdx.x*WR + wr) over the k-range wk of split s. XF: x is in
+// MFMA fragment order xf[K/32][64][8] (one contiguous KiB per k-step).
+template <int WR, int WK, int RT, int U, int XF>
+__global__ __launch_bounds__(64 * WR * WK) void gemv_exp2(const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ Wp,
+                                                         float* __restrict__ out, int N, int K, int S) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WR, wk = wave / WR;
+  const int tile0 = (blockIdx.x * WR + wr) * RT, s = blockIdx.y;
+  const int KS = K >> 5, kw = KS / (S * WK), ks0 = (s * WK + wk) * kw;
+  const size_t ts = (size_t)KS * 512;
+  const bf16_t* wp = Wp + (size_t)tile0 * ts + (size_t)lane * 8;
+  const bf16_t* xp = XF ? x + (size_t)lane * 8 : x + (size_t)(lane & 15) * K + 8 * (lane >> 4);
+  const int ng = kw / U;
+  float4v_ acc[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) acc[i] = (float4v_){0, 0, 0, 0};
+  bf16x8 a0[U][RT], a1[U][RT], b0[U], b1[U];
+  auto load = [&](bf16x8 (&a)[U][RT], bf16x8 (&b)[U], int gg) {
+    const int ks = ks0 + gg * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) a[u][i] = ldw(wp + (size_t)i * ts + (size_t)(ks + u) * 512);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ldx(xp + (size_t)(ks + u) * (XF ? 512 : 32));
+  };
+  auto mma = [&](bf16x8 (&a)[U][RT], bf16x8 (&b)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], b[u], acc[i], 0, 0, 0);
+  };
+  load(a0, b0, 0);
+  int g = 0;
+  for (; g + 2 < ng; g += 2) {
+    load(a1, b1, g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(a0, b0, g + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (g + 1 < ng) { load(a1, b1, g + 1); mma(a0, b0); mma(a1, b1); } else { mma(a0, b0); }
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < RT; ++i) t += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (t == 12345.678f) out[blockIdx.x] = t;
+}
+
+#define CASE2(WR_, WK_, RT_, U_, XF_)                                                              \
+  if (wr == WR_ && wk == WK_ && rt == RT_ && u == U_ && xf == XF_) {                              \
+    if (N % (16 * RT_ * WR_) || K % (S * WK_ * 32 * U_)) return 1;                                \
+    hipLaunchKernelGGL((gemv_exp2<WR_, WK_, RT_, U_, XF_>), dim3(N / (16 * RT_ * WR_), S),       \
+                       dim3(64 * WR_ * WK_), 0, st, (const bf16_t*)x, (const bf16_t*)Wp, out, N, K, S); \
+    return (int)hipGetLastError();                                                                \
+  }
+#define XFS(WR_, WK_, RT_, U_) CASE2(WR_, WK_, RT_, U_, 0) CASE2(WR_, WK_, RT_, U_, 1)
+
+extern "C" int exp_gemv2(const void* x, const void* Wp, float* out, int N, int K, int S, int wr, int wk,
+                         int rt, int u, int xf, hipStream_t st) {
+  XFS(1, 4, 1, 4) XFS(1, 4, 2, 4) XFS(1, 4, 2, 2) XFS(1, 4, 4, 2)
+  XFS(4, 1, 1, 4) XFS(4, 1, 1, 8) XFS(4, 1, 2, 4) XFS(4, 2, 1, 4) XFS(4, 2, 1, 8) XFS(2, 2, 1, 4)
+  XFS(2, 2, 2, 4) XFS(8, 1, 1, 4) XFS(4, 4, 1, 4) XFS(1, 8, 1, 4) XFS(1, 8, 2, 4)
+  return 2;
+}

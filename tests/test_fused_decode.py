@@ -109,6 +109,54 @@ def test_fused_resid_rowsq_and_silu_gpu():
         assert float((a.float() - expect.float()).norm() / expect.float().norm()) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
+def test_fused_rows_per_wave_layout_gpu(mode):
+    """wr=4 (every wave owns its own row tile over the full K range) is
+    bitwise identical to wr=1's 4-way K split except for the fp32 summation
+    order: compare both against each other and against the fp32 reference."""
+    from loqa_hub_amd.ops import reference as ref
+    dev = "cuda"
+    torch.manual_seed(3)
+    Mpad, K = 16, 1024
+    H, Hkv, D = 8, 2, 64
+    N = {"resid": 512, "silu": 1024, "act": 512, "rope": (H + 2 * Hkv) * D}[mode]
+    x = torch.randn(Mpad, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.03).bfloat16()
+    if mode == "silu":
+        w = w[ref.perm_gate_up(N // 2).to(dev)].contiguous()
+    wp = ops.shuffle_weight(w)
+    outs = []
+    res0 = torch.randn(Mpad, N, device=dev).bfloat16()
+    for wr in (1, 4):
+        scr = ops.FusedScratch(dev)
+        kw = dict(splits=1, wr=wr)
+        if mode == "resid":
+            res = res0.clone()
+            base = res.clone()
+            ops.skinny_fused(x, wp, "resid", scr, residual=res, **kw)
+            outs.append((res.float() - base.float(), scr.rowsq[: (N // 32) * Mpad].clone()))
+        elif mode == "rope":
+            kc = torch.zeros(4, Hkv, 16, D, device=dev).bfloat16()
+            vc = torch.zeros_like(kc)
+            pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
+            q = torch.empty(Mpad, H * D, device=dev).bfloat16()
+            ops.skinny_fused(x, wp, "rope", scr, positions=pos, cos_sin=None, q_out=q, k_cache=kc,
+                             v_cache=vc, slots=pos, n_heads=H, n_kv=Hkv, head_dim=D, **kw)
+            outs.append((q.float(), kc.float().sum() + vc.float().sum()))
+        else:
+            y = ops.skinny_fused(x, wp, mode, scr, **kw)
+            outs.append((y.float(), None))
+    a, b = outs
+    rel = float((a[0] - b[0]).norm() / a[0].norm())
+    assert rel < 1e-2, rel
+    if mode == "act":
+        expect = x.float() @ w.float().t()
+        assert float((b[0] - expect).norm() / expect.norm()) < 1e-2
+    if mode == "resid":
+        assert torch.allclose(a[1], b[1], rtol=1e-2, atol=1e-2)
+
+
 def _ln_case(dev, S=None, Mpad=16, rt=2):
     """LayerNorm-prologue GEMM (folded weight / shift / bias) with a GELU
     epilogue, against layernorm -> linear -> gelu in fp32."""
