@@ -78,6 +78,8 @@ def main(argv=None) -> int:
     ap.add_argument("--inflight", type=int, default=2,
                     help="--mode batch: batches in flight (2: next batch's STT overlaps the decode)")
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
+    ap.add_argument("--stt-priority", type=int, default=-1,
+                    help="HIP stream priority of the STT worker (-1 high, 0 normal)")
     args = ap.parse_args(argv)
 
     if args.cpu_smoke:
@@ -103,7 +105,9 @@ def main(argv=None) -> int:
     stt = STTEngine(whisper_config(args.stt), dev, seed=args.seed, max_batch=max(B, 8))
     llm = LLMEngine(llama_config(args.llm), dev, seed=args.seed, max_seqs=max(B, 8), max_seq_len=1024,
                     use_graphs=not args.no_graphs)
-    pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=B)
+    pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=B,
+                         stt_priority=args.stt_priority)
+    pipe.warmup()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t_init = time.perf_counter() - t_init
@@ -224,6 +228,7 @@ def main(argv=None) -> int:
             "command_count_match_rate": round(cmd_match, 4),
             "phase_ms_per_step": phase_ms,
             "llm_stats": llm.stats,
+            "stt_stats": stt.stats,
             "init_s": round(t_init, 2),
         }
         print(json.dumps(out), flush=True)

@@ -73,6 +73,8 @@ class LLMEngine:
                  weights: LlamaWeights | None = None, fused_decode: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.tp = tp or TPGroup()
         self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
         self.model = LlamaModel(self.weights)
@@ -104,7 +106,8 @@ class LLMEngine:
         self._on_done = None
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
-                      "prefill_s": 0.0, "decode_s": 0.0}
+                      "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
+                      "host_post_s": 0.0}
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
@@ -254,6 +257,26 @@ class LLMEngine:
         self._graphs[key] = g
         return g
 
+    def warmup_graphs(self) -> int:
+        """Capture every decode-step graph bucket up front (sequence x token x
+        context buckets). Serving then never captures: a capture on one worker
+        thread while another thread issues HIP calls can be invalidated, and a
+        first-time capture would stall that step by tens of ms."""
+        if not self.use_graphs:
+            return 0
+        n = 0
+        for b in self.SEQ_BUCKETS:
+            if b > max(1, self.max_seqs):
+                break
+            t_max = ops.mpad_for(min(ops.MPADS[-2], b * self.max_decode_q))
+            for t in ops.MPADS:
+                if t > t_max:
+                    break
+                for c in range(self.CTX_BUCKET, self.max_seq_len + self.CTX_BUCKET, self.CTX_BUCKET):
+                    self._decode_graph(b, t, min(c, self.max_seq_len))
+                    n += 1
+        return n
+
     # ------------------------------------------------------------ generate
     def submit(self, req: GenRequest) -> GenRequest:
         req.seq_id = self._next_id
@@ -330,6 +353,7 @@ class LLMEngine:
             else:
                 feeds.append(f)
                 carry.append(False)
+        t0 = time.perf_counter()
         B = len(live)
         T = sum(len(f) for f in feeds)
         rows = np.array([r.grammar.mask_row() for r in live], np.int32)
@@ -345,8 +369,12 @@ class LLMEngine:
             hb["mask_rows"][:B] = rows
             g["d32"].copy_(g["h32"], non_blocking=True)
             g["d64"].copy_(g["h64"], non_blocking=True)
+            t1 = time.perf_counter()
             g["graph"].replay()
             nxt = g["out"][:B].cpu().numpy()
+            t2 = time.perf_counter()
+            self.stats["host_pre_s"] += t1 - t0
+            self.stats["gpu_wait_s"] += t2 - t1
         else:
             max_q, max_ctx, host = self._meta(live, feeds, True, B, ops.mpad_for(T))
             host["mask_rows"] = rows
@@ -355,7 +383,9 @@ class LLMEngine:
             nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += T
-        self._sample_and_advance(live, nxt, time.perf_counter(), carry)
+        t3 = time.perf_counter()
+        self._sample_and_advance(live, nxt, t3, carry)
+        self.stats["host_post_s"] += time.perf_counter() - t3
 
     # --------------------------------------------- continuous batching
     def start(self, stream_priority: int = 0) -> None:
@@ -385,13 +415,26 @@ class LLMEngine:
         ``reqs`` when all of them are done."""
         self.start()
         fut: Future = Future()
+        if getattr(self, "_fatal", None) is not None:
+            fut.set_exception(self._fatal)
+            return fut
         self._inbox.put((reqs, on_done, fut))
         return fut
 
     def _schedule(self, stream_priority: int) -> None:
-        if self.is_gpu:
-            torch.cuda.set_device(self.device)
-            torch.cuda.set_stream(torch.cuda.Stream(self.device, priority=stream_priority))
+        try:
+            if self.is_gpu:
+                torch.cuda.set_device(self.device)
+                torch.cuda.set_stream(torch.cuda.Stream(self.device, priority=stream_priority))
+        except Exception as e:  # noqa: BLE001 - never leave submitters waiting
+            self._fatal = e
+            while True:
+                try:
+                    it = self._inbox.get_nowait()
+                except queue.Empty:
+                    return
+                if it is not None and not it[2].done():
+                    it[2].set_exception(e)
         live: list[GenRequest] = []
         cells: dict[int, list] = {}   # id(cell) -> [remaining, future, reqs]
         while self._running:

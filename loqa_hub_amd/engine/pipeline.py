@@ -59,7 +59,8 @@ class VoicePipeline:
                  queue_max_duration: float = 0.0, rollback: bool = True, tts=None,
                  response_audio: bool = False, overlap: bool = True,
                  continuous: bool | None = None, batch_window: float = 0.002,
-                 max_batch: int = 8):
+                 max_batch: int = 8, stt_priority: int = -1,
+                 stt_continuous: bool | None = None):
         self.stt, self.llm, self.nats = stt, llm, nats
         self.min_response_tokens = min_response_tokens
         self.queue_max_duration = queue_max_duration
@@ -74,12 +75,26 @@ class VoicePipeline:
         # (scheduler thread) instead of decoding batch by batch
         self.continuous = self.overlap if continuous is None else continuous
         self.batch_window, self.max_batch = batch_window, max_batch
+        self.stt_priority = stt_priority
+        # continuous STT: arrivals join the running Whisper decode batch
+        self.stt_continuous = self.continuous if stt_continuous is None else stt_continuous
         self._pool: ThreadPoolExecutor | None = None
         self._stt_pool: ThreadPoolExecutor | None = None
         self._pending: list[tuple[PipelineJob, asyncio.Future]] = []
         self._batcher: asyncio.Task | None = None
         self._stt_lock: asyncio.Lock | None = None
         self.stats = {"stt_batches": 0, "utterances": 0}
+
+    def warmup(self) -> dict:
+        """Capture every decode graph bucket of both engines before serving
+        (the two engines run on their own threads; no capture may happen
+        while the other thread is issuing HIP calls)."""
+        out = {"stt_graphs": 0, "llm_graphs": 0}
+        if self.overlap:
+            out["stt_graphs"] = self.stt.warmup_graphs()
+            out["llm_graphs"] = self.llm.warmup_graphs()
+            torch.cuda.synchronize(self.llm.device)
+        return out
 
     # --------------------------------------------------------------- stages
     def transcribe(self, jobs: list[PipelineJob], device_pcm=None) -> None:
@@ -89,15 +104,17 @@ class VoicePipeline:
             cur.wait_stream(torch.cuda.default_stream(device_pcm.device))
         reqs = [STTRequest(j.pcm, transcript=j.transcript_hint) for j in jobs]
         self.stt.transcribe(reqs, device_pcm)
-        now = time.perf_counter()
-        fi = faults()
         for j, r in zip(jobs, reqs):
-            j.raw_text, j.rms = r.text, r.rms
-            j.t["stt_done"] = now
-            if fi and fi.active("stt_error"):
-                j.stt_failed, j.error = True, "stt: injected fault"
-                continue
-            j.transcription = to_transcription_result(r.text)
+            self._stt_post(j, r)
+
+    def _stt_post(self, j: PipelineJob, r: STTRequest) -> None:
+        j.raw_text, j.rms = r.text, r.rms
+        j.t["stt_done"] = time.perf_counter()
+        fi = faults()
+        if fi and fi.active("stt_error"):
+            j.stt_failed, j.error = True, "stt: injected fault"
+            return
+        j.transcription = to_transcription_result(r.text)
 
     def build_request(self, j: PipelineJob) -> GenRequest | None:
         if j.stt_failed:
@@ -149,14 +166,14 @@ class VoicePipeline:
         j.t["queue_done"] = time.perf_counter()
 
     # ------------------------------------------------------------- batch run
-    def _worker(self, name: str, own_stream: bool) -> ThreadPoolExecutor:
+    def _worker(self, name: str, own_stream: bool, priority: int = 0) -> ThreadPoolExecutor:
         dev = self.llm.device
 
         def init():
             if dev.type == "cuda":
                 torch.cuda.set_device(dev)
                 if own_stream:
-                    torch.cuda.set_stream(torch.cuda.Stream(dev))
+                    torch.cuda.set_stream(torch.cuda.Stream(dev, priority=priority))
         return ThreadPoolExecutor(1, thread_name_prefix=name, initializer=init)
 
     def _gpu_executor(self) -> ThreadPoolExecutor:
@@ -168,7 +185,10 @@ class VoicePipeline:
         if not self.overlap:
             return self._gpu_executor()
         if self._stt_pool is None:
-            self._stt_pool = self._worker("stt-worker", True)
+            # the Whisper decoder is a latency-bound chain of small launches:
+            # on a high-priority queue its workgroups are dispatched ahead of
+            # the concurrent (bandwidth-bound) LLM decode GEMMs
+            self._stt_pool = self._worker("stt-worker", True, self.stt_priority)
         return self._stt_pool
 
     # ------------------------------------------------------------ serving
@@ -189,9 +209,12 @@ class VoicePipeline:
             self._stt_lock = asyncio.Lock()
         while self._pending:
             await asyncio.sleep(self.batch_window)
+            batch = self._pending[: self.max_batch]
+            self._pending = self._pending[self.max_batch:]
+            if self.stt_continuous:
+                self._submit_stt(batch)
+                continue
             async with self._stt_lock:
-                batch = self._pending[: self.max_batch]
-                self._pending = self._pending[self.max_batch:]
                 jobs = [j for j, _ in batch]
                 try:
                     await self._stt_stage(jobs)
@@ -201,6 +224,45 @@ class VoicePipeline:
                             f.set_exception(e)
                     continue
             asyncio.ensure_future(self._finish(batch))
+
+    def _submit_stt(self, batch) -> None:
+        """Continuous STT: the micro-batch joins the STT engine's running
+        decoder batch (no wait for an earlier batch to drain) and every
+        utterance moves on to the LLM the moment its OWN transcript is done."""
+        loop = asyncio.get_running_loop()
+        t0 = time.perf_counter()
+        reqs = []
+        owner = {}
+        for j, f in batch:
+            j.t["start"] = j.t.get("start", t0)
+            r = STTRequest(j.pcm, transcript=j.transcript_hint)
+            reqs.append(r)
+            owner[id(r)] = (j, f)
+        self.stats["stt_batches"] += 1
+        self.stats["utterances"] += len(reqs)
+
+        def start_llm(r: STTRequest) -> None:
+            j, f = owner[id(r)]
+            self._stt_post(j, r)
+            asyncio.ensure_future(self._finish([(j, f)]))
+
+        def on_stt_done(r: STTRequest) -> None:      # STT scheduler thread
+            loop.call_soon_threadsafe(start_llm, r)
+
+        self.stt.start(self.stt_priority)
+        fut = self.stt.submit_batch(reqs, on_stt_done)
+
+        def failed(ft) -> None:
+            e = ft.exception()
+            if e is None:
+                return
+
+            def fail():
+                for j, f in batch:
+                    if not f.done():
+                        f.set_exception(e)
+            loop.call_soon_threadsafe(fail)
+        fut.add_done_callback(failed)
 
     async def _finish(self, batch) -> None:
         futs = {id(j): f for j, f in batch}

@@ -11,7 +11,10 @@ of the same length; only the fed-back token is the reference one.
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
+from concurrent.futures import Future
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -27,7 +30,7 @@ from .tokenizer import get_tokenizer
 N_SAMPLES = 480000  # 30 s @ 16 kHz
 
 
-@dataclass
+@dataclass(eq=False)
 class STTRequest:
     pcm: np.ndarray                   # int16 samples @ 16 kHz
     transcript: str | None = None     # teacher-forcing target (synthetic mode)
@@ -39,6 +42,12 @@ class STTRequest:
     tokens: list[int] = field(default_factory=list)
     seq_id: int = -1
     t_done: float = 0.0
+    # decoder state (engine-owned)
+    slot: int = -1                    # cross-attention K|V slot (encoder rows)
+    target: list[int] | None = None
+    feed: list[int] = field(default_factory=list)
+    step: int = 0
+    on_done: object = None
 
 
 class STTEngine:
@@ -50,6 +59,8 @@ class STTEngine:
                  fused: bool = True, weights: WhisperWeights | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
         self.model = WhisperModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
@@ -65,7 +76,8 @@ class STTEngine:
                                     max((cfg.n_audio_ctx + 255) // 256, (cfg.n_text_ctx + 255) // 256)
                                     ) if self.is_gpu else None
         self._next = 1
-        self.stats = {"utterances": 0, "decode_steps": 0}
+        self.stats = {"utterances": 0, "decode_steps": 0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
+                      "encode_s": 0.0}
         self.max_batch = max_batch
         self.fast_decode = fast_decode
         # fused-epilogue decoder GEMMs (8 launches per layer) for Mpad <= 64
@@ -123,14 +135,28 @@ class STTEngine:
         return audio
 
     # -------------------------------------------------------------- decode
-    def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:
-        rows = enc.shape[0]
-        assert rows <= self.xkv[0].shape[0], "batch exceeds max_batch"
+    def cross_kv(self, enc: torch.Tensor, slots: list[int] | None = None) -> list[torch.Tensor]:
+        """Cross-attention K|V of every decoder layer for the encoder rows of
+        ``enc`` ([n * T_enc, d]), written to the requests' slots (default:
+        slots 0..n-1, one GEMM per layer; contiguous slot runs share a GEMM)."""
+        T = self.cfg.n_audio_ctx
+        n = enc.shape[0] // T
+        slots = list(range(n)) if slots is None else slots
+        assert max(slots) < self.max_batch, "slot exceeds max_batch"
+        runs, i = [], 0                     # (first request, first slot, length)
+        while i < n:
+            j = i
+            while j + 1 < n and slots[j + 1] == slots[j] + 1:
+                j += 1
+            runs.append((i, slots[i], j - i + 1))
+            i = j + 1
         for L, buf in zip(self.weights.dec, self.xkv):
-            torch.addmm(L["xkv_b"], enc, L["xkv"].t(), out=buf[:rows])
+            for i0, s0, m in runs:
+                torch.addmm(L["xkv_b"], enc[i0 * T:(i0 + m) * T], L["xkv"].t(),
+                            out=buf[s0 * T:(s0 + m) * T])
         return self.xkv
 
-    def _host_meta(self, reqs, live, feeds, B_pad: int, T_pad: int,
+    def _host_meta(self, live: list[STTRequest], B_pad: int, T_pad: int,
                    out: dict | None = None) -> tuple[int, dict]:
         T_enc = self.cfg.n_audio_ctx
         L = max(16, ops.mpad_for(B_pad))
@@ -152,8 +178,8 @@ class STTEngine:
             lidx = np.zeros(L, np.int64)
         off, max_q = 0, 1
         pool = self.kv.pool
-        for j, i in enumerate(live):
-            r, f = reqs[i], feeds[i]
+        for j, r in enumerate(live):
+            f = r.feed
             n = len(f)
             start = pool.seq_len(r.seq_id)
             sl = pool.append(r.seq_id, n)
@@ -167,7 +193,7 @@ class STTEngine:
             ctx[j] = start + n
             tab = pool.block_table(r.seq_id)
             bt[j, :len(tab)] = tab
-            enc_starts[j] = i * T_enc
+            enc_starts[j] = r.slot * T_enc
             enc_lens[j] = T_enc
             lidx[j] = off - 1
             max_q = max(max_q, n)
@@ -253,34 +279,58 @@ class STTEngine:
         self._graphs[key] = g
         return g
 
-    def _step(self, reqs, live, feeds) -> np.ndarray:
+    def warmup_graphs(self) -> int:
+        """Capture every decoder-step graph bucket up front (see
+        ``LLMEngine.warmup_graphs``): sequence x token x context buckets."""
+        if not self.use_graphs:
+            return 0
+        n = 0
+        n_sot = len(self.sot)
+        for b in self.SEQ_BUCKETS:
+            if b > self.max_batch:
+                break
+            t_max = ops.mpad_for(min(64, b * n_sot))
+            for t in ops.MPADS:
+                if t > t_max:
+                    break
+                for c in range(self.SPLIT_KEYS, self.cfg.n_text_ctx + self.SPLIT_KEYS, self.SPLIT_KEYS):
+                    self._graph(b, t, min(c, self.cfg.n_text_ctx))
+                    n += 1
+        return n
+
+    def _step(self, live: list[STTRequest]) -> np.ndarray:
+        """One decoder step for every live request (its ``feed`` tokens)."""
         B = len(live)
-        T = sum(len(feeds[i]) for i in live)
+        T = sum(len(r.feed) for r in live)
         if self.fast_decode:
             B_pad = next((b for b in self.SEQ_BUCKETS if b >= B), B)
             T_pad = ops.mpad_for(T)
             if self.use_graphs:
-                ctx = max(self.kv.pool.seq_len(reqs[i].seq_id) + len(feeds[i]) for i in live)
+                ctx = max(self.kv.pool.seq_len(r.seq_id) + len(r.feed) for r in live)
                 C = min(self.cfg.n_text_ctx, -(-ctx // self.SPLIT_KEYS) * self.SPLIT_KEYS)
+                t0 = time.perf_counter()
                 g = self._graph(B_pad, T_pad, C)
-                self._host_meta(reqs, live, feeds, B_pad, T_pad, out=g["host"])
+                self._host_meta(live, B_pad, T_pad, out=g["host"])
                 g["d32"].copy_(g["h32"], non_blocking=True)
                 g["d64"].copy_(g["h64"], non_blocking=True)
+                t1 = time.perf_counter()
                 g["graph"].replay()
-                return g["out"][:B].cpu().numpy()
-            max_q, host = self._host_meta(reqs, live, feeds, B_pad, T_pad)
+                out = g["out"][:B].cpu().numpy()
+                self.stats["host_pre_s"] += t1 - t0
+                self.stats["gpu_wait_s"] += time.perf_counter() - t1
+                return out
+            max_q, host = self._host_meta(live, B_pad, T_pad)
             return self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
-        return self._eager_step(reqs, live, feeds)
+        return self._eager_step(live)
 
-    def _eager_step(self, reqs, live, feeds) -> np.ndarray:
+    def _eager_step(self, live: list[STTRequest]) -> np.ndarray:
         """Reference decode path (hipBLASLt GEMMs, eager launches)."""
         T_enc = self.cfg.n_audio_ctx
         toks, pos, slots, cu, ctx, lidx = [], [], [], [0], [], []
         bt = np.zeros((len(live), self.max_blocks), np.int32)
         max_q, max_ctx = 1, 1
-        for j, i in enumerate(live):
-            r = reqs[i]
-            f = feeds[i]
+        for j, r in enumerate(live):
+            f = r.feed
             start = self.kv.pool.seq_len(r.seq_id)
             sl = self.kv.pool.append(r.seq_id, len(f))
             toks += f
@@ -294,7 +344,7 @@ class STTEngine:
             max_q = max(max_q, len(f))
             max_ctx = max(max_ctx, start + len(f))
         dev = lambda a, dt: torch.tensor(a, dtype=dt).to(self.device, non_blocking=True)
-        enc_starts = dev([i * T_enc for i in live], torch.int32)
+        enc_starts = dev([r.slot * T_enc for r in live], torch.int32)
         enc_lens = dev([T_enc] * len(live), torch.int32)
         logits = self.model.decode_step(
             dev(toks, torch.int32), dev(pos, torch.int32), dev(slots, torch.int32),
@@ -302,55 +352,167 @@ class STTEngine:
             self.kv.k, self.kv.v, self.xkv, enc_starts, enc_lens, dev(lidx, torch.int64), self.ws)
         return ops.masked_argmax(logits).cpu().numpy()
 
-    def transcribe(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
-                   ) -> list[STTRequest]:
-        if not reqs:
-            return reqs
-        assert len(reqs) <= self.max_batch, "batch exceeds max_batch"
+    # ----------------------------------------------------------- admission
+    def _admit(self, reqs: list[STTRequest], slots: list[int],
+               device_pcm: torch.Tensor | None = None) -> None:
+        """Front end + encoder for newly arrived requests, their cross-attention
+        K|V into ``slots``, and their decoder sequences (fed the SOT prompt)."""
         tr = tracer()
         dev = self.device if self.is_gpu else None
         with tr.span("h2d", dev, batch=len(reqs)):
             audio, sumsq = self.upload(reqs, device_pcm)
+        t0 = time.perf_counter()
         with tr.span("encode", dev, batch=len(reqs)):
             enc = self.model.encode(audio)
-            self.cross_kv(enc)
-        t_dec = time.monotonic()
-        B = len(reqs)
-        targets = []
-        for r in reqs:
-            r.seq_id = self._next
-            self._next += 1
-            self.kv.pool.add_seq(r.seq_id, [])
-            tgt = None
-            if r.transcript is not None:
-                tgt = self.tok.encode(" " + r.transcript.strip())[: self.cfg.n_text_ctx - 8] + [self.eot]
-            targets.append(tgt)
-        feeds = [list(self.sot) for _ in reqs]
-        live = list(range(B))
-        step = 0
-        while live:
-            nxt = self._step(reqs, live, feeds)
-            self.stats["decode_steps"] += 1
-            still = []
-            for j, i in enumerate(live):
-                r = reqs[i]
-                tgt = targets[i]
-                t = int(tgt[step]) if tgt is not None else int(nxt[j])
-                r.tokens.append(t)
-                if t == self.eot or len(r.tokens) >= r.max_new_tokens or (tgt is not None and step + 1 >= len(tgt)):
-                    r.t_done = time.perf_counter()
-                    continue
-                feeds[i] = [t]
-                still.append(i)
-            live = still
-            step += 1
-        tr.record("stt_decode", t_dec, time.monotonic(), steps=step, batch=B)
+            self.cross_kv(enc, slots)
         ss = sumsq.cpu().numpy()
-        for i, r in enumerate(reqs):
+        self.stats["encode_s"] += time.perf_counter() - t0
+        for i, (r, sl) in enumerate(zip(reqs, slots)):
             n = max(1, min(len(r.pcm), N_SAMPLES))
             r.sumsq = float(ss[i])
             r.rms = float(np.sqrt(ss[i] / n))
-            r.text = self.tok.decode([t for t in r.tokens if t != self.eot]).strip()
-            self.kv.pool.free_seq(r.seq_id)
-        self.stats["utterances"] += B
+            r.slot = sl
+            r.seq_id = self._next
+            self._next += 1
+            self.kv.pool.add_seq(r.seq_id, [])
+            r.tokens, r.step, r.feed, r.t_done = [], 0, list(self.sot), 0.0
+            r.target = None
+            if r.transcript is not None:
+                r.target = self.tok.encode(" " + r.transcript.strip())[: self.cfg.n_text_ctx - 8] + [self.eot]
+
+    def _decode_once(self, live: list[STTRequest]) -> list[STTRequest]:
+        """One decoder step over ``live``; returns the requests that finished."""
+        nxt = self._step(live)
+        self.stats["decode_steps"] += 1
+        done = []
+        for j, r in enumerate(live):
+            t = int(r.target[r.step]) if r.target is not None else int(nxt[j])
+            r.tokens.append(t)
+            r.step += 1
+            if t == self.eot or len(r.tokens) >= r.max_new_tokens or \
+                    (r.target is not None and r.step >= len(r.target)):
+                r.t_done = time.perf_counter()
+                r.text = self.tok.decode([x for x in r.tokens if x != self.eot]).strip()
+                self.kv.pool.free_seq(r.seq_id)
+                self.stats["utterances"] += 1
+                done.append(r)
+            else:
+                r.feed = [t]
+        return done
+
+    def transcribe(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
+                   ) -> list[STTRequest]:
+        """Synchronous batch: encode all, decode until every request is done."""
+        if not reqs:
+            return reqs
+        assert len(reqs) <= self.max_batch, "batch exceeds max_batch"
+        self._admit(reqs, list(range(len(reqs))), device_pcm)
+        t_dec = time.monotonic()
+        live, steps = list(reqs), 0
+        while live:
+            self._decode_once(live)
+            steps += 1
+            live = [r for r in live if r.t_done == 0.0]
+        tracer().record("stt_decode", t_dec, time.monotonic(), steps=steps, batch=len(reqs))
         return reqs
+
+    # --------------------------------------------- continuous batching
+    def start(self, stream_priority: int = 0) -> None:
+        """Start the STT scheduler thread: requests submitted with
+        ``submit_batch`` are encoded on arrival and join the RUNNING decoder
+        batch at the next step boundary (each in its own cross-attention slot),
+        so an utterance never waits for an earlier batch's decode to drain."""
+        if getattr(self, "_sched", None) is not None:
+            return
+        self._inbox: queue.Queue = queue.Queue()
+        self._running = True
+        self._free_slots = list(range(self.max_batch))
+        self._sched = threading.Thread(target=self._schedule, args=(stream_priority,),
+                                       name="stt-scheduler", daemon=True)
+        self._sched.start()
+
+    def stop(self) -> None:
+        if getattr(self, "_sched", None) is None:
+            return
+        self._running = False
+        self._inbox.put(None)
+        self._sched.join(timeout=60)
+        self._sched = None
+
+    def submit_batch(self, reqs: list[STTRequest], on_done=None) -> Future:
+        """Queue requests; ``on_done(req)`` fires on the scheduler thread as
+        each finishes; the future resolves with ``reqs`` when all are done."""
+        self.start()
+        fut: Future = Future()
+        if getattr(self, "_fatal", None) is not None:
+            fut.set_exception(self._fatal)
+            return fut
+        self._inbox.put((list(reqs), on_done, fut))
+        return fut
+
+    def _schedule(self, stream_priority: int) -> None:
+        try:
+            if self.is_gpu:
+                torch.cuda.set_device(self.device)
+                torch.cuda.set_stream(torch.cuda.Stream(self.device, priority=stream_priority))
+        except Exception as e:  # noqa: BLE001 - never leave submitters waiting
+            self._fatal = e
+            while True:
+                try:
+                    it = self._inbox.get_nowait()
+                except queue.Empty:
+                    return
+                if it is not None and not it[2].done():
+                    it[2].set_exception(e)
+        live: list[STTRequest] = []
+        waiting: list[tuple] = []          # (reqs, cb, fut) not yet admitted (no free slot)
+        cells: dict[int, list] = {}
+        while self._running:
+            items = [self._inbox.get()] if not live and not waiting else []
+            while True:
+                try:
+                    items.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            for it in items:
+                if it is not None:
+                    waiting.append(it)
+            try:
+                new: list[STTRequest] = []
+                while waiting and len(waiting[0][0]) <= len(self._free_slots) - len(new):
+                    reqs, cb, fut = waiting.pop(0)
+                    if not reqs:
+                        fut.set_result(reqs)
+                        continue
+                    cell = [len(reqs), fut, reqs, cb]
+                    cells[id(cell)] = cell
+                    for r in reqs:
+                        r.on_done = cell
+                    new += reqs
+                if new:
+                    slots = [self._free_slots.pop(0) for _ in new]
+                    self._admit(new, slots)
+                    live += new
+                if live:
+                    for r in self._decode_once(live):
+                        self._free_slots.append(r.slot)
+                        self._free_slots.sort()
+                        cell = r.on_done
+                        if cell[3] is not None:
+                            cell[3](r)
+                        cell[0] -= 1
+                        if cell[0] == 0:
+                            cells.pop(id(cell), None)
+                            cell[1].set_result(cell[2])
+                    live = [r for r in live if r.t_done == 0.0]
+            except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
+                for cell in list(cells.values()):
+                    if not cell[1].done():
+                        cell[1].set_exception(e)
+                for r in live:
+                    self.kv.pool.free_seq(r.seq_id)
+                for _, _, fut in waiting:
+                    if not fut.done():
+                        fut.set_exception(e)
+                live, waiting, cells = [], [], {}
+                self._free_slots = list(range(self.max_batch))

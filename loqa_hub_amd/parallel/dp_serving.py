@@ -58,6 +58,7 @@ def _build_worker_processor(spec: dict, device: str):
                     max_seqs=spec.get("max_batch", 8), max_seq_len=spec.get("max_seq_len", 1024),
                     use_graphs=spec.get("use_graphs", True))
     pipe = VoicePipeline(stt, llm, None, min_response_tokens=spec.get("min_response_tokens", 8))
+    pipe.warmup()
     return GPUVoiceProcessor(pipe, max_batch=spec.get("max_batch", 8),
                              batch_window=spec.get("batch_window", 0.005))
 

@@ -56,6 +56,7 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None):
     llm = LLMEngine(lcfg, device, seed=g.seed, max_seqs=g.max_batch, weights=lw,
                     max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs)
     pipe = VoicePipeline(stt, llm, nats)
+    pipe.warmup()
     return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64))
 
 

@@ -223,16 +223,16 @@ def test_whisper_fast_decode_matches_eager_cpu():
         reqs = [STTRequest(u.pcm) for u in utts]
         audio, _ = eng.upload(reqs)
         eng.cross_kv(eng.model.encode(audio))
-        for r in reqs:
+        for i, r in enumerate(reqs):
             r.seq_id = eng._next
+            r.slot = i
+            r.feed = list(eng.sot)
             eng._next += 1
             eng.kv.pool.add_seq(r.seq_id, [])
-        feeds = [list(eng.sot) for _ in reqs]
-        live = [0, 1]
         B_pad, T_pad = 2, 16
         res = []
         for step in range(2):
-            max_q, host = eng._host_meta(reqs, live, feeds, B_pad, T_pad)
+            max_q, host = eng._host_meta(reqs, B_pad, T_pad)
             dev = eng._dev(host)
             if mode == "fused":
                 from loqa_hub_amd.models.whisper import decode_step_fused
@@ -257,7 +257,7 @@ def test_whisper_fast_decode_matches_eager_cpu():
                     eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"][:2], dev["enc_lens"][:2],
                     dev["logit_idx"][:2], None).float()
             res.append(lg)
-            feeds = [[11], [12]]
+            reqs[0].feed, reqs[1].feed = [11], [12]
         outs.append(res)
     for other in outs[:2]:
         for a, b in zip(other, outs[2]):
@@ -344,3 +344,66 @@ def test_pipeline_submit_continuous_cpu():
     llm.stop()
     assert [j.n_commands for j in jobs] == [j.n_expected for j in jobs] == [1, 2, 3, 4]
     assert pipe.stats["utterances"] == 4
+
+
+def test_stt_continuous_batching_matches_batch_cpu():
+    """Requests that join a RUNNING Whisper decode batch (scheduler thread,
+    per-request cross-attention slots) decode exactly as in a one-shot batch."""
+    import time as _t
+
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    cfg = whisper_config("test-whisper")
+    utts = make_batch(5, 4, [1, 2, 3, 1])
+    ref = STTEngine(cfg, torch.device("cpu"), seed=2, max_batch=4)
+    solo = [STTRequest(u.pcm, max_new_tokens=6) for u in utts]
+    ref.transcribe(solo)
+    eng = STTEngine(cfg, torch.device("cpu"), seed=2, max_batch=4)
+    a = [STTRequest(u.pcm, max_new_tokens=6) for u in utts[:2]]
+    b = [STTRequest(u.pcm, max_new_tokens=6) for u in utts[2:3]]
+    c = [STTRequest(u.pcm, transcript=u.text) for u in utts[3:]]
+    seen = []
+    fa = eng.submit_batch(a, lambda r: seen.append(r))
+    _t.sleep(0.05)                      # b and c arrive mid-decode
+    fb = eng.submit_batch(b)
+    fc = eng.submit_batch(c)
+    for f in (fa, fb, fc):
+        f.result(timeout=120)
+    eng.stop()
+    assert len(seen) == 2
+    for got, want in zip(a + b, solo[:3]):
+        assert got.tokens == want.tokens
+        assert abs(got.rms - want.rms) < 1e-6
+    assert c[0].text.lower().startswith(utts[3].text.lower().split()[0])
+    assert sorted(eng._free_slots) == list(range(4))
+
+
+def test_pipeline_continuous_stt_cpu():
+    """Pipeline with continuous STT + continuous LLM on the CPU: every utterance
+    gets its own reply with the expected command count."""
+    import asyncio
+
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline
+    from loqa_hub_amd.engine.stt_engine import STTEngine
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import llama_config, whisper_config
+    stt = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4)
+    llm = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=8,
+                    max_seq_len=1024, use_graphs=False)
+    pipe = VoicePipeline(stt, llm, None, min_response_tokens=2, continuous=True,
+                         stt_continuous=True, max_batch=4)
+    utts = make_batch(1, 6, [1, 2, 3])
+
+    async def main():
+        jobs = [PipelineJob(u.relay_id, f"r{i}", u.pcm, transcript_hint=u.text)
+                for i, u in enumerate(utts)]
+        return await asyncio.gather(*[pipe.submit(j) for j in jobs])
+    try:
+        res = asyncio.run(main())
+    finally:
+        stt.stop()
+        llm.stop()
+    assert [j.n_commands for j in res] == [u.n_commands for u in utts]
+    assert all(j.queue is not None and j.transcription is not None for j in res)

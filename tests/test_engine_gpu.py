@@ -67,13 +67,13 @@ def _whisper_first_logits(eng, pcms):
     reqs = [STTRequest(p) for p in pcms]
     audio, _ = eng.upload(reqs)
     eng.cross_kv(eng.model.encode(audio))
-    for r in reqs:
+    for i, r in enumerate(reqs):
         r.seq_id = eng._next
+        r.slot = i
+        r.feed = list(eng.sot)
         eng._next += 1
         eng.kv.pool.add_seq(r.seq_id, [])
-    feeds = [list(eng.sot) for _ in reqs]
-    live = list(range(len(reqs)))
-    max_q, host = eng._host_meta(reqs, live, feeds, 2, 16)
+    max_q, host = eng._host_meta(reqs, 2, 16)
     dev = eng._dev(host)
     if eng.fast_decode:
         lg = decode_step_fast(eng.model, dev["tokens"], dev["positions"], dev["slots"],
@@ -123,3 +123,26 @@ def test_vits_tts_gpu():
     assert len(outs) == 2 and outs[0].dtype == np.int16
     assert outs[0].size % 256 == 0 and outs[0].size > outs[1].size > 0
     assert np.abs(outs[0].astype(np.float32)).mean() > 100
+
+
+def test_stt_continuous_batching_gpu():
+    """Graph-replayed Whisper decode with requests joining a running batch
+    (per-request cross-attention slots) equals the one-shot batch."""
+    import time as _t
+    cfg = whisper_config("whisper-tiny")
+    rng = np.random.default_rng(1)
+    pcms = [(rng.standard_normal(16000 * (i + 1)) * 3000).astype(np.int16) for i in range(3)]
+    ref = STTEngine(cfg, "cuda", seed=1, max_batch=4)
+    solo = [STTRequest(p, max_new_tokens=8) for p in pcms]
+    ref.transcribe(solo)
+    eng = STTEngine(cfg, "cuda", seed=1, max_batch=4)
+    a = [STTRequest(p, max_new_tokens=8) for p in pcms[:2]]
+    b = [STTRequest(pcms[2], max_new_tokens=8)]
+    fa = eng.submit_batch(a)
+    _t.sleep(0.02)
+    fb = eng.submit_batch(b)
+    fa.result(timeout=120)
+    fb.result(timeout=120)
+    eng.stop()
+    for got, want in zip(a + b, solo):
+        assert got.tokens == want.tokens

@@ -215,14 +215,15 @@ def test_whisper_fused_decode_matches_fast_gpu():
         reqs = [STTRequest(u.pcm) for u in utts]
         audio, _ = eng.upload(reqs)
         eng.cross_kv(eng.model.encode(audio))
-        for r in reqs:
+        for i, r in enumerate(reqs):
             r.seq_id = eng._next
+            r.slot = i
+            r.feed = list(eng.sot)
             eng._next += 1
             eng.kv.pool.add_seq(r.seq_id, [])
-        feeds = [list(eng.sot) for _ in reqs]
         res = []
         for step in range(3):
-            max_q, host = eng._host_meta(reqs, [0, 1, 2], feeds, 4, 16)
+            max_q, host = eng._host_meta(reqs, 4, 16)
             dev = eng._dev(host)
             args = (eng.model, dev["tokens"], dev["positions"], dev["slots"], dev["cu_q"],
                     dev["ctx_lens"], dev["block_tables"], max_q, eng.kv.k, eng.kv.v, eng.xkv,
@@ -232,7 +233,8 @@ def test_whisper_fused_decode_matches_fast_gpu():
             else:
                 lg = decode_step_fast(*args, eng.self_splits)
             res.append(lg[:3, : cfg.vocab_size].float().cpu())
-            feeds = [[11 + step], [12 + step], [13 + step]]
+            for i, r in enumerate(reqs):
+                r.feed = [11 + step + i]
         outs[mode] = res
     for a, b in zip(outs["fused"], outs["fast"]):
         rel = float((a - b).norm() / b.norm())
