@@ -73,7 +73,8 @@ __device__ __forceinline__ void mma_frag(const Frag<RT, MT, U>& f, float4v_ (&ac
       for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(f.a[u][i], f.b[u][j], acc[i][j]);
 }
 
-// Ping-pong stream over ng groups of U k-steps; f0 already holds group 0.
+// Ping-pong stream over ng groups of U k-steps; f0 already holds group
+// ``rot`` (groups are visited in the rotated order rot, rot+1, ... mod ng).
 // The steady-state loop issues the next group UNCONDITIONALLY before consuming
 // the current one: a conditional refill inside the loop body makes the
 // consumer block a join point of the refill / no-refill paths, and hipcc's
@@ -83,23 +84,24 @@ template <int RT, int MT, int U>
 __device__ __forceinline__ void stream_k(Frag<RT, MT, U>& f0, Frag<RT, MT, U>& f1,
                                          float4v_ (&acc)[RT][MT], const bf16_t* wp,
                                          size_t tile_stride, const bf16_t* xp, long long ldx_,
-                                         int ks0, int ng) {
+                                         int ks0, int ng, int rot) {
+  auto ks = [&](int g) { int q = g + rot; q -= q >= ng ? ng : 0; return ks0 + q * U; };
   // sched_barrier(0) pins each phase: without it the machine scheduler sinks
   // the refill loads between the MFMAs to save registers, collapsing the
   // prefetch distance to 3-5 loads
   int g = 0;
   for (; g + 2 < ng; g += 2) {
-    load_frag(f1, wp, tile_stride, xp, ldx_, ks0 + (g + 1) * U);
+    load_frag(f1, wp, tile_stride, xp, ldx_, ks(g + 1));
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f0, acc);
     __builtin_amdgcn_sched_barrier(0);
-    load_frag(f0, wp, tile_stride, xp, ldx_, ks0 + (g + 2) * U);
+    load_frag(f0, wp, tile_stride, xp, ldx_, ks(g + 2));
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f1, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (g + 1 < ng) {
-    load_frag(f1, wp, tile_stride, xp, ldx_, ks0 + (g + 1) * U);
+    load_frag(f1, wp, tile_stride, xp, ldx_, ks(g + 1));
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f0, acc);
     mma_frag(f1, acc);
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16_t* __restri
   // ping-pong register prefetch over groups of U k-steps
   Frag<RT, MT, U> f0, f1;
   load_frag(f0, wp, tile_stride, xp, ldx_, ks0);
-  stream_k(f0, f1, acc, wp, tile_stride, xp, ldx_, ks0, kw / U);
+  stream_k(f0, f1, acc, wp, tile_stride, xp, ldx_, ks0, kw / U, 0);
 
   if (wave > 0) {
 #pragma unroll
@@ -263,7 +265,7 @@ struct FusedParams {
   const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
   int H, Hkv, D, blk;
   int rt;                 // output tile rows / 16 (1: residual / act modes only)
-  int wr;                 // waves along the rows (1, or 4 at Mpad 16 with S == 1)
+  int wr;                 // waves along the rows (1, or 4 at Mpad <= 32 with S == 1)
 };
 
 struct FusedArgs {
@@ -308,7 +310,68 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   // statistics only scale the accumulator, so the stream need not wait for
   // them (the prologue's two L2 round trips then hide under the first fill)
   Frag<RT, MT, U> f0, f1;
-  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0);
+  const int ng = kw / U;
+  // (a k-start rotation per workgroup measured 5-10 % SLOWER on every shape:
+  // the in-step x reuse across neighbouring workgroups in L2 matters more)
+  const int rot = 0;
+  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + rot * U);
+
+  // Epilogue operands (residual tile, bias, LayerNorm column sums, RoPE
+  // positions / cos-sin / cache slots) are requested now, by the epilogue
+  // wave only: their latency hides under the weight stream instead of adding
+  // one or two dependent round trips after the last MFMA.
+  const int nq = 4 * (lane >> 4);
+  uint2 rres[RT][MT];
+  float4 bvec[RT], cvec[RT];
+  int eslot[MT];
+  float2 ecs[MT][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) {
+    bvec[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    cvec[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < MT; ++j) rres[i][j] = make_uint2(0u, 0u);
+  }
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    eslot[j] = -1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ecs[j][r] = make_float2(1.f, 0.f);
+  }
+  if (wk == 0) {
+    if (a.bias) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+        bvec[i] = *reinterpret_cast<const float4*>(a.bias + tile * (16 * RT) + i * 16 + nq);
+    }
+    if constexpr (NORM == NORM_LN) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+        cvec[i] = *reinterpret_cast<const float4*>(a.colsum + tile * (16 * RT) + i * 16 + nq);
+    }
+    if constexpr (MODE == EPI_RESID) {
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+          rres[i][j] = *reinterpret_cast<const uint2*>(
+              a.residual + (size_t)(j * 16 + (lane & 15)) * a.N + tile * (16 * RT) + i * 16 + nq);
+    } else if constexpr (MODE == EPI_ROPE) {
+      const int tph = a.D / 32, nq_t = a.H * tph, nk_t = a.Hkv * tph;
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int m = j * 16 + (lane & 15);
+        eslot[j] = a.slots[m];
+        if (a.cs && tile < nq_t + nk_t) {
+          const int tt = tile >= nq_t ? tile - nq_t : tile;
+          const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
+          const float2* e = a.cs + (size_t)a.positions[m] * (a.D >> 1) + c;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ecs[j][r] = e[r];
+        }
+      }
+    }
+  }
 
   float sc[MT], mu[MT];
 #pragma unroll
@@ -364,7 +427,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
-  stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, kw / U);
+  stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, ng, rot);
 
   if constexpr (WK > 1) {
     // red[wr][wk - 1][i * MT + j][lane]
@@ -450,7 +513,6 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   }
 
   // ---- epilogue (the wk == 0 wave of each row tile): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
-  const int nq = 4 * (lane >> 4);
   // Norms: the norm weight g is folded into W at load time, so the row scale
   // factors out of the k-sum: RMSNorm  y = s * (W g) x;  LayerNorm
   // y = s * ((W g) x - mean * colsum) with colsum[n] = sum_k (W g)[n][k]; the
@@ -463,7 +525,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   } else if constexpr (NORM == NORM_LN) {
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-      const float4 cv = *reinterpret_cast<const float4*>(a.colsum + tile * (16 * RT) + i * 16 + nq);
+      const float4 cv = cvec[i];
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         acc[i][j][0] = sc[j] * (acc[i][j][0] - mu[j] * cv.x);
@@ -476,7 +538,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   if (a.bias) {
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.bias + tile * (16 * RT) + i * 16 + nq);
+      const float4 bv = bvec[i];
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         acc[i][j][0] += bv.x; acc[i][j][1] += bv.y; acc[i][j][2] += bv.z; acc[i][j][3] += bv.w;
@@ -506,7 +568,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
         bf16_t* rp = a.residual + (size_t)m * a.N + tile * (16 * RT) + i * 16 + nq;
-        uint2 rv = *reinterpret_cast<const uint2*>(rp);
+        const uint2 rv = rres[i][j];
         const float r0 = bf2f(rv.x & 0xffff), r1 = bf2f(rv.x >> 16);
         const float r2 = bf2f(rv.y & 0xffff), r3 = bf2f(rv.y >> 16);
         const float h0 = bf2f(f2bf(acc[i][j][0] + r0)), h1 = bf2f(f2bf(acc[i][j][1] + r1));
@@ -533,18 +595,17 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       const int m = j * 16 + (lane & 15);
-      const int slot = a.slots[m];
+      const int slot = eslot[j];
       if (tile < nq_t + nk_t) {
         const bool isk = tile >= nq_t;
         const int tt = isk ? tile - nq_t : tile;
         const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
         float ra[4], rb[4];
         if (a.cs) {
-          const float2* e = a.cs + (size_t)a.positions[m] * half + c;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x0 = bf2f(f2bf(acc[0][j][r])), x1 = bf2f(f2bf(acc[1][j][r]));
-            const float2 cs = e[r];
+            const float2 cs = ecs[j][r];
             ra[r] = x0 * cs.x - x1 * cs.y;
             rb[r] = x1 * cs.x + x0 * cs.y;
           }
@@ -620,7 +681,9 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
     case 16:
       if (wr == 4) return launch_fused<RT, 1, 4, MODE, NORM>(a, st);
       return launch_fused<RT, 1, 1, MODE, NORM>(a, st);
-    case 32: return launch_fused<RT, 2, 1, MODE, NORM>(a, st);
+    case 32:
+      if (wr == 4) return launch_fused<RT, 2, 4, MODE, NORM>(a, st);
+      return launch_fused<RT, 2, 1, MODE, NORM>(a, st);
     default: return launch_fused<RT, 4, 1, MODE, NORM>(a, st);
   }
 }
@@ -628,7 +691,7 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
 // rt: rows per output tile / 16. The paired epilogues (SwiGLU gate|up, RoPE
 // halves) need 32-row tiles; residual / activation epilogues may use 16-row
 // tiles (twice the workgroups without a K split: no split-K reduction tail).
-// wr: waves along the rows (1 or 4; 4 only at Mpad 16 with S == 1).
+// wr: waves along the rows (1 or 4; 4 only at Mpad <= 32 with S == 1).
 template <int MODE, int NORM>
 static int dispatch_fused(const FusedArgs& a, int rt, int wr, hipStream_t st) {
   if constexpr (MODE == EPI_RESID || MODE == EPI_ACT) {
@@ -668,7 +731,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   if ((p->rt != 1 && p->rt != 2) || ((p->mode == EPI_SILU || p->mode == EPI_ROPE) && p->rt != 2))
     return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
-  if (p->wr != 1 && (p->wr != 4 || Mpad != 16 || S != 1 || N % (64 * p->rt)))
+  if (p->wr != 1 && (p->wr != 4 || Mpad > 32 || S != 1 || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
               p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,

@@ -859,7 +859,7 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
         rts = (1, 2) if mode in ("resid", "act") else (2,)
         tune_fused_splits(key, lambda sp, rt, wr, i: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, **kw), K, rts=rts,
-            ncopies=len(copies), wr4=Mpad == 16)
+            ncopies=len(copies), wr4=Mpad <= 32)
     del copies
 
 
@@ -904,7 +904,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
         rt = 2
     if wr is None:
         wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
-    if wr != 1 and (S != 1 or Mpad != 16 or N % (64 * rt)):
+    if wr != 1 and (S != 1 or Mpad > 32 or N % (64 * rt)):
         wr = 1
     if rowsq_tiles is None:
         rowsq_tiles = scratch.stat_tiles

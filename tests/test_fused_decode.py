@@ -111,14 +111,15 @@ def test_fused_resid_rowsq_and_silu_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
-def test_fused_rows_per_wave_layout_gpu(mode):
+@pytest.mark.parametrize("Mpad", [16, 32])
+def test_fused_rows_per_wave_layout_gpu(mode, Mpad):
     """wr=4 (every wave owns its own row tile over the full K range) is
     bitwise identical to wr=1's 4-way K split except for the fp32 summation
     order: compare both against each other and against the fp32 reference."""
     from loqa_hub_amd.ops import reference as ref
     dev = "cuda"
     torch.manual_seed(3)
-    Mpad, K = 16, 1024
+    K = 1024
     H, Hkv, D = 8, 2, 64
     N = {"resid": 512, "silu": 1024, "act": 512, "rope": (H + 2 * Hkv) * D}[mode]
     x = torch.randn(Mpad, K, device=dev).bfloat16()
