@@ -37,6 +37,7 @@ class PipelineJob:
     request_id: str
     pcm: np.ndarray
     transcript_hint: str | None = None     # synthetic ground truth (teacher forcing)
+    on_tokens: object = None               # streaming hook: called with each step's token ids
     # results
     transcription: TranscriptionResult | None = None
     raw_text: str = ""
@@ -133,12 +134,12 @@ class VoicePipeline:
             j.n_expected = n
             prompt = build_multi_command_prompt(text)
             schema = multi_command_schema(n, min_response_tokens=self.min_response_tokens)
-            r = GenRequest(tok.encode(prompt, bos=True), schema)
+            r = GenRequest(tok.encode(prompt, bos=True), schema, on_tokens=j.on_tokens)
             r.kind = "multi"  # type: ignore[attr-defined]
         else:
             j.n_expected = 1
             schema = single_command_schema(max_response_tokens=12)
-            r = GenRequest(tok.encode(build_prompt(text), bos=True), schema)
+            r = GenRequest(tok.encode(build_prompt(text), bos=True), schema, on_tokens=j.on_tokens)
             r.kind = "single"  # type: ignore[attr-defined]
         return r
 

@@ -114,3 +114,8 @@ def llama_config(name: str, **over) -> LlamaConfig:
 def whisper_config(name: str, **over) -> WhisperConfig:
     c = WHISPER_CONFIGS[name]
     return replace(c, **over) if over else c
+
+
+def vits_config(name: str, **over) -> VitsConfig:
+    c = VITS_CONFIGS[name]
+    return replace(c, **over) if over else c
