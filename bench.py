@@ -229,6 +229,8 @@ def main(argv=None) -> int:
             "phase_ms_per_step": phase_ms,
             "llm_stats": llm.stats,
             "stt_stats": stt.stats,
+            "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v)
+                                  for k, v in __import__("loqa_hub_amd.ops", fromlist=["_FSPLITS"])._FSPLITS.items()},
             "init_s": round(t_init, 2),
         }
         print(json.dumps(out), flush=True)

@@ -117,52 +117,59 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16_t* __restri
                                                           int S, int Mpad) {
   __shared__ float4v_ red[3][RT * MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tile0 = blockIdx.x * RT;          // first 16-row tile
   const int s = blockIdx.y;
   const int KS = K >> 5;                      // k-steps of 32
   const int kw = KS / (S * 4);                // k-steps per wave
   const int ks0 = (s * 4 + wave) * kw;
   const size_t tile_stride = (size_t)KS * 512;  // elements per 16-row tile
-  const bf16_t* wp = Wp + (size_t)tile0 * tile_stride + (size_t)lane * 8;
   const bf16_t* xp = x + (size_t)(lane & 15) * ldx_ + 8 * (lane >> 4);
-
-  float4v_ acc[RT][MT];
-#pragma unroll
-  for (int i = 0; i < RT; ++i)
-#pragma unroll
-    for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
-
-  // ping-pong register prefetch over groups of U k-steps
-  Frag<RT, MT, U> f0, f1;
-  load_frag(f0, wp, tile_stride, xp, ldx_, ks0);
-  stream_k(f0, f1, acc, wp, tile_stride, xp, ldx_, ks0, kw / U, 0);
-
-  if (wave > 0) {
+  const int ngroups = N / (16 * RT);
+  // grid-stride over tile groups: a capped grid (one workgroup per CU) leaves
+  // CU slots free for the concurrent decoder stream (see tune_fused_splits)
+  for (int tg = blockIdx.x; tg < ngroups; tg += gridDim.x) {
+    const int tile0 = tg * RT;                  // first 16-row tile
+    const bf16_t* wp = Wp + (size_t)tile0 * tile_stride + (size_t)lane * 8;
+    float4v_ acc[RT][MT];
 #pragma unroll
     for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) red[wave - 1][i * MT + j][lane] = acc[i][j];
-  }
-  __syncthreads();
-  if (wave == 0) {
+      for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
+
+    // ping-pong register prefetch over groups of U k-steps
+    Frag<RT, MT, U> f0, f1;
+    load_frag(f0, wp, tile_stride, xp, ldx_, ks0);
+    stream_k(f0, f1, acc, wp, tile_stride, xp, ldx_, ks0, kw / U, 0);
+
+    if (wave > 0) {
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+      for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        float4v_ v = acc[i][j] + red[0][i * MT + j][lane] + red[1][i * MT + j][lane] +
-                     red[2][i * MT + j][lane];
-        // C layout (16x16): col = lane&15 (token m), rows n = 4*(lane>>4) + reg
-        const int m = j * 16 + (lane & 15);
-        const int n = (tile0 + i) * 16 + 4 * (lane >> 4);
-        *reinterpret_cast<float4v_*>(part + ((size_t)s * Mpad + m) * N + n) = v;
-      }
+        for (int j = 0; j < MT; ++j) red[wave - 1][i * MT + j][lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+          float4v_ v = acc[i][j] + red[0][i * MT + j][lane] + red[1][i * MT + j][lane] +
+                       red[2][i * MT + j][lane];
+          // C layout (16x16): col = lane&15 (token m), rows n = 4*(lane>>4) + reg
+          const int m = j * 16 + (lane & 15);
+          const int n = (tile0 + i) * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<float4v_*>(part + ((size_t)s * Mpad + m) * N + n) = v;
+        }
+    }
+    __syncthreads();                            // red is reused by the next group
   }
 }
 
 template <int RT, int MT>
 static int launch_skinny(const void* x, long long ldx_, const void* Wp, float* part, int N, int K,
-                         int S, int Mpad, hipStream_t st) {
-  dim3 grid(N / (16 * RT), S);
+                         int S, int Mpad, int max_wgs, hipStream_t st) {
+  int gx = N / (16 * RT);
+  if (max_wgs > 0 && gx * S > max_wgs) gx = max_wgs / S > 0 ? max_wgs / S : 1;
+  dim3 grid(gx, S);
   const int kw = K / 32 / (S * 4);
   if constexpr (MT <= 2) {
     if (kw % 4 == 0) {
@@ -182,22 +189,23 @@ static int launch_skinny(const void* x, long long ldx_, const void* Wp, float* p
 
 // x: [Mpad, >=K] bf16 (row stride ldx), rows >= M must be finite (zeros);
 // Wp: pre-shuffled weight (loqa_shuffle_weight); part: [S, Mpad, N] f32.
+// max_wgs > 0 caps the grid (workgroups loop over tile groups).
 extern "C" int loqa_skinny_gemm(const void* x, long long ldx_, const void* Wp, float* part, int Mpad,
-                                int N, int K, int S, hipStream_t st) {
+                                int N, int K, int S, int max_wgs, hipStream_t st) {
   if (S < 1 || K % (S * 4 * 32) != 0 || ldx_ % 8 != 0 || N % 16 != 0) return (int)hipErrorInvalidValue;
   switch (Mpad) {
     case 16:
       if (N % 32) return (int)hipErrorInvalidValue;
-      return launch_skinny<2, 1>(x, ldx_, Wp, part, N, K, S, Mpad, st);
+      return launch_skinny<2, 1>(x, ldx_, Wp, part, N, K, S, Mpad, max_wgs, st);
     case 32:
       if (N % 32) return (int)hipErrorInvalidValue;
-      return launch_skinny<2, 2>(x, ldx_, Wp, part, N, K, S, Mpad, st);
+      return launch_skinny<2, 2>(x, ldx_, Wp, part, N, K, S, Mpad, max_wgs, st);
     case 64:
       if (N % 64) return (int)hipErrorInvalidValue;
-      return launch_skinny<4, 4>(x, ldx_, Wp, part, N, K, S, Mpad, st);
+      return launch_skinny<4, 4>(x, ldx_, Wp, part, N, K, S, Mpad, max_wgs, st);
     case 128:
       if (N % 64) return (int)hipErrorInvalidValue;
-      return launch_skinny<4, 8>(x, ldx_, Wp, part, N, K, S, Mpad, st);
+      return launch_skinny<4, 8>(x, ldx_, Wp, part, N, K, S, Mpad, max_wgs, st);
     default:
       return (int)hipErrorInvalidValue;
   }
@@ -288,7 +296,6 @@ struct FusedArgs {
 // gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
 template <int RT, int MT, int U, int WR, int MODE, int NORM>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
-  static_assert(RT == 2 || (MODE != EPI_SILU && MODE != EPI_ROPE), "paired epilogues need 32-row tiles");
   constexpr int WK = 4 / WR;                     // waves along K
   constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
   constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   uint2 rres[RT][MT];
   float4 bvec[RT], cvec[RT];
   int eslot[MT];
-  float2 ecs[MT][4];
+  float2 ecs[RT][MT][4];
 #pragma unroll
   for (int i = 0; i < RT; ++i) {
     bvec[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -336,7 +343,9 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   for (int j = 0; j < MT; ++j) {
     eslot[j] = -1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ecs[j][r] = make_float2(1.f, 0.f);
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ecs[i][j][r] = make_float2(1.f, 0.f);
   }
   if (wk == 0) {
     if (a.bias) {
@@ -357,17 +366,26 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
           rres[i][j] = *reinterpret_cast<const uint2*>(
               a.residual + (size_t)(j * 16 + (lane & 15)) * a.N + tile * (16 * RT) + i * 16 + nq);
     } else if constexpr (MODE == EPI_ROPE) {
-      const int tph = a.D / 32, nq_t = a.H * tph, nk_t = a.Hkv * tph;
+      // 16-row pair tiles: rows 0-7 = features c..c+7 of the first half, rows
+      // 8-15 = their RoPE partners c+D/2..; lanes (l>>4) & 1 pick c's 4-row half
+      const int tph = a.D / 16, nq_t = a.H * tph, nk_t = a.Hkv * tph;
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         const int m = j * 16 + (lane & 15);
         eslot[j] = a.slots[m];
-        if (a.cs && tile < nq_t + nk_t) {
-          const int tt = tile >= nq_t ? tile - nq_t : tile;
-          const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
-          const float2* e = a.cs + (size_t)a.positions[m] * (a.D >> 1) + c;
+        if (a.cs) {
+          const int pos = a.positions[m];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ecs[j][r] = e[r];
+          for (int i = 0; i < RT; ++i) {
+            const int pt = tile * RT + i;
+            if (pt < nq_t + nk_t) {
+              const int tt = pt >= nq_t ? pt - nq_t : pt;
+              const int c = (tt % tph) * 8 + 4 * ((lane >> 4) & 1);
+              const float2* e = a.cs + (size_t)pos * (a.D >> 1) + c;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) ecs[i][j][r] = e[r];
+            }
+          }
         }
       }
     }
@@ -546,20 +564,27 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
     }
   }
   if constexpr (MODE == EPI_SILU) {
+    // 16-row pair tiles (perm_gate_up): rows 0-7 gate, rows 8-15 the matching
+    // up rows -> lane l (l < 32) holds gate, lane l ^ 32 its up partner
 #pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int m = j * 16 + (lane & 15);
-      float o[4];
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gg = bf2f(f2bf(acc[0][j][r])), uu = bf2f(f2bf(acc[1][j][r]));
-        o[r] = gg / (1.f + __expf(-gg)) * uu;
+      for (int j = 0; j < MT; ++j) {
+        const int m = j * 16 + (lane & 15);
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float own = bf2f(f2bf(acc[i][j][r]));
+          const float oth = __shfl_xor(own, 32, 64);
+          o[r] = own / (1.f + __expf(-own)) * oth;
+        }
+        if (lane < 32) {
+          uint2 w2;
+          w2.x = pack_bf16x2(o[0], o[1]);
+          w2.y = pack_bf16x2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + (tile * RT + i) * 8 + nq) = w2;
+        }
       }
-      uint2 w2;
-      w2.x = pack_bf16x2(o[0], o[1]);
-      w2.y = pack_bf16x2(o[2], o[3]);
-      *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * 16 + nq) = w2;
-    }
   } else if constexpr (MODE == EPI_RESID) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
@@ -590,48 +615,54 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       }
     }
   } else if constexpr (MODE == EPI_ROPE) {
-    const int D = a.D, half = D >> 1, tph = D / 32;
+    // perm_rope_qkv: q / k as 16-row pair tiles (rows 0-7 = first-half features
+    // c.., rows 8-15 = partners c+D/2..: lane l and l ^ 32 hold a RoPE pair);
+    // v rows in natural order
+    const int D = a.D, half = D >> 1, tph = D / 16;
     const int nq_t = a.H * tph, nk_t = a.Hkv * tph;
+    const bool lower = lane < 32;
 #pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int m = j * 16 + (lane & 15);
-      const int slot = eslot[j];
-      if (tile < nq_t + nk_t) {
-        const bool isk = tile >= nq_t;
-        const int tt = isk ? tile - nq_t : tile;
-        const int head = tt / tph, c = (tt - head * tph) * 16 + nq;
-        float ra[4], rb[4];
-        if (a.cs) {
+    for (int i = 0; i < RT; ++i) {
+      const int pt = tile * RT + i;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float x0 = bf2f(f2bf(acc[0][j][r])), x1 = bf2f(f2bf(acc[1][j][r]));
-            const float2 cs = ecs[j][r];
-            ra[r] = x0 * cs.x - x1 * cs.y;
-            rb[r] = x1 * cs.x + x0 * cs.y;
+      for (int j = 0; j < MT; ++j) {
+        const int m = j * 16 + (lane & 15);
+        const int slot = eslot[j];
+        if (pt < nq_t + nk_t) {
+          const bool isk = pt >= nq_t;
+          const int tt = isk ? pt - nq_t : pt;
+          const int head = tt / tph;
+          const int c = (tt - head * tph) * 8 + 4 * ((lane >> 4) & 1) + (lower ? 0 : half);
+          float ov[4];
+          if (a.cs) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float own = bf2f(f2bf(acc[i][j][r]));
+              const float oth = __shfl_xor(own, 32, 64);
+              const float2 cs = ecs[i][j][r];
+              // lower: x0 cos - x1 sin; upper (own = x1, oth = x0): x1 cos + x0 sin
+              ov[r] = own * cs.x + (lower ? -oth : oth) * cs.y;
+            }
+          } else {  // no rotary embedding (Whisper): plain q / k rows
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ov[r] = acc[i][j][r];
           }
-        } else {  // no rotary embedding (Whisper): plain q / k halves
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ra[r] = acc[0][j][r], rb[r] = acc[1][j][r];
-        }
-        uint2 lo, hi;
-        lo.x = pack_bf16x2(ra[0], ra[1]); lo.y = pack_bf16x2(ra[2], ra[3]);
-        hi.x = pack_bf16x2(rb[0], rb[1]); hi.y = pack_bf16x2(rb[2], rb[3]);
-        bf16_t* dst;
-        if (!isk) {
-          dst = a.q_out + (size_t)m * a.H * D + head * D;
+          uint2 w2;
+          w2.x = pack_bf16x2(ov[0], ov[1]);
+          w2.y = pack_bf16x2(ov[2], ov[3]);
+          bf16_t* dst;
+          if (!isk) {
+            dst = a.q_out + (size_t)m * a.H * D + head * D;
+          } else {
+            if (slot < 0) continue;
+            const int bb = slot / a.blk, o = slot - bb * a.blk;
+            dst = a.kc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D;
+          }
+          *reinterpret_cast<uint2*>(dst + c) = w2;
         } else {
           if (slot < 0) continue;
           const int bb = slot / a.blk, o = slot - bb * a.blk;
-          dst = a.kc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D;
-        }
-        *reinterpret_cast<uint2*>(dst + c) = lo;
-        *reinterpret_cast<uint2*>(dst + c + half) = hi;
-      } else {
-        if (slot < 0) continue;
-        const int bb = slot / a.blk, o = slot - bb * a.blk;
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          const int row = (tile - nq_t - nk_t) * 32 + i * 16 + nq;
+          const int row = (pt - nq_t - nk_t) * 16 + nq;
           const int head = row / D, c = row - head * D;
           uint2 w2;
           w2.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
@@ -688,15 +719,13 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
   }
 }
 
-// rt: rows per output tile / 16. The paired epilogues (SwiGLU gate|up, RoPE
-// halves) need 32-row tiles; residual / activation epilogues may use 16-row
-// tiles (twice the workgroups without a K split: no split-K reduction tail).
+// rt: rows per output tile / 16 (1 or 2, every mode: the paired epilogues pair
+// rows inside each 16-row tile through a lane shuffle, so 16-row tiles give
+// twice the workgroups without a K split, i.e. without a reduction tail).
 // wr: waves along the rows (1 or 4; 4 only at Mpad <= 32 with S == 1).
 template <int MODE, int NORM>
 static int dispatch_fused(const FusedArgs& a, int rt, int wr, hipStream_t st) {
-  if constexpr (MODE == EPI_RESID || MODE == EPI_ACT) {
-    if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, wr, st);
-  }
+  if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, wr, st);
   return dispatch_mt<2, MODE, NORM>(a, wr, st);
 }
 
@@ -724,12 +753,11 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   if (S > 1 && (!p->part || !p->counters)) return (int)hipErrorInvalidValue;
   if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1)) return (int)hipErrorInvalidValue;
   if (p->norm == NORM_LN && (!p->rowsum_in || !p->colsum)) return (int)hipErrorInvalidValue;
-  if (p->mode == EPI_ROPE && (p->D % 32 || N != (p->H + 2 * p->Hkv) * p->D))
+  if (p->mode == EPI_ROPE && (p->D % 16 || N != (p->H + 2 * p->Hkv) * p->D))
     return (int)hipErrorInvalidValue;
   if ((p->mode == EPI_SILU || p->mode == EPI_ACT) && (!p->out || p->ldo % 4))
     return (int)hipErrorInvalidValue;
-  if ((p->rt != 1 && p->rt != 2) || ((p->mode == EPI_SILU || p->mode == EPI_ROPE) && p->rt != 2))
-    return (int)hipErrorInvalidValue;
+  if (p->rt != 1 && p->rt != 2) return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
   if (p->wr != 1 && (p->wr != 4 || Mpad > 32 || S != 1 || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;

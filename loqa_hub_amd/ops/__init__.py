@@ -17,6 +17,7 @@ from __future__ import annotations
 import copy
 import ctypes
 import math
+import os
 
 import torch
 
@@ -356,6 +357,7 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 
 
 _FSPLITS: dict = {}
+MAX_DECODE_WGS = int(os.environ.get("LOQA_MAX_DECODE_WGS", "256"))
 
 
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
@@ -376,6 +378,13 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     cands = [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
     if wr4:
         cands += [(1, rt, 4) for rt in rts if N % (64 * rt) == 0]
+    # co-scheduling cap: the STT and LLM decoders run concurrently on their own
+    # streams; a grid that fills every CU slot makes the other stream's small
+    # latency-bound kernels wait for it to drain (measured: a 768-workgroup
+    # qkv GEMM, fastest in isolation, slowed the concurrent Whisper decoder 5x
+    # and the whole pipeline 1.8x). Keep at most one workgroup per CU.
+    capped = [c for c in cands if (N // (16 * c[1] * c[2])) * c[0] <= MAX_DECODE_WGS]
+    cands = capped or cands[:1]
     best, best_t = (1, rts[-1], 1), float("inf")
     n = max(1, ncopies)
     for c in cands:
@@ -433,6 +442,21 @@ def choose_splits(N: int, K: int, Mpad: int, target_wgs: int = 512) -> int:
     return best
 
 
+def decode_attn_splits(max_ctx: int, units: int, split_keys: int = 128,
+                       max_wgs: int | None = None) -> tuple[int, int]:
+    """(num_splits, split_keys) of the split-key decode attention for a
+    context bound and ``units`` = sequences x kv heads workgroup rows: splits of
+    ``split_keys`` keys, but at most ``max_wgs`` workgroups in all (the
+    co-scheduling cap of ``tune_fused_splits``) - longer splits then loop."""
+    max_wgs = MAX_DECODE_WGS if max_wgs is None else max_wgs
+    ns = max(1, -(-max_ctx // split_keys))
+    cap = max(1, max_wgs // max(1, units))
+    if ns > cap:
+        ns = cap
+        split_keys = -(-(-(-max_ctx // ns)) // 32) * 32
+    return ns, split_keys
+
+
 def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
     """[N, K] bf16 -> MFMA-fragment-ordered [N/16, K/32, 64, 8] (skinny GEMM layout)."""
     N, K = w.shape
@@ -445,7 +469,8 @@ def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def skinny_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+def skinny_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int | None = None,
+                max_wgs: int = 0) -> torch.Tensor:
     """x [Mpad, K] bf16 (Mpad in 16/32/64/128, padded rows finite) @ W^T with W
     given pre-shuffled (``shuffle_weight``) -> split-K partial slabs
     [S, Mpad, N] f32 (sum over S = x @ W^T)."""
@@ -459,7 +484,7 @@ def skinny_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int | None = None) ->
     _bf16_contig(wp, "wp")
     part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device)
     check(kernels().loqa_skinny_gemm(ptr(x), x.stride(0), ptr(wp), ptr(part), Mpad, N, K, S,
-                                     stream_ptr(x)), "skinny_gemm")
+                                     max_wgs, stream_ptr(x)), "skinny_gemm")
     return part
 
 
@@ -856,7 +881,7 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
             kw.update(positions=pos, cos_sin=cos_sin, q_out=torch.empty(Mpad, H * D, **bf),
                       k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
                       head_dim=D)
-        rts = (1, 2) if mode in ("resid", "act") else (2,)
+        rts = (1, 2)
         tune_fused_splits(key, lambda sp, rt, wr, i: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, **kw), K, rts=rts,
             ncopies=len(copies), wr4=Mpad <= 32)
@@ -900,8 +925,6 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     tuned = _FSPLITS.get((mode, N, K, Mpad))
     S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
     rt = rt or (tuned[1] if tuned else 2)
-    if mode in ("silu", "rope"):
-        rt = 2
     if wr is None:
         wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
     if wr != 1 and (S != 1 or Mpad > 32 or N % (64 * rt)):

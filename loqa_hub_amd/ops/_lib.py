@@ -62,7 +62,8 @@ _KERNEL_SIGS = {
                      c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "loqa_im2col_k3": [c_void_p, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_void_p,
                        c_void_p],
-    "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "loqa_skinny_gemm": [c_void_p, c_ll, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                         c_void_p],
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "loqa_skinny_fused": [c_void_p, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,

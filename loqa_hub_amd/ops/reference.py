@@ -434,25 +434,26 @@ def expand_sample(stats, cum, flen, F, noise_scale, noise=None):
 
 # ------------------------------------------------------------ fused decode GEMMs
 def perm_rope_qkv(H, Hkv, D):
-    """Row order of the fused qkv weight: per q / k head, 32-row tiles holding
-    16 first-half rows c0.. and their RoPE partners c0 + D/2; v rows unchanged."""
+    """Row order of the fused qkv weight: per q / k head, 16-row pair tiles
+    holding 8 first-half rows c0.. and their RoPE partners c0 + D/2 (the
+    epilogue pairs lane l with lane l ^ 32); v rows unchanged."""
     half = D // 2
     rows = []
     for base, n in ((0, H), (H * D, Hkv)):
         for h in range(n):
-            for s in range(D // 32):
-                c0 = 16 * s
-                rows += list(range(base + h * D + c0, base + h * D + c0 + 16))
-                rows += list(range(base + h * D + half + c0, base + h * D + half + c0 + 16))
+            for s in range(D // 16):
+                c0 = 8 * s
+                rows += list(range(base + h * D + c0, base + h * D + c0 + 8))
+                rows += list(range(base + h * D + half + c0, base + h * D + half + c0 + 8))
     rows += list(range((H + Hkv) * D, (H + 2 * Hkv) * D))
     return torch.tensor(rows, dtype=torch.long)
 
 
 def perm_gate_up(F):
-    """Row order of the fused gate|up weight: 32-row tiles of (16 gate, 16 up)."""
+    """Row order of the fused gate|up weight: 16-row pair tiles of (8 gate, 8 up)."""
     rows = []
-    for t in range(F // 16):
-        rows += list(range(16 * t, 16 * t + 16)) + list(range(F + 16 * t, F + 16 * t + 16))
+    for t in range(F // 8):
+        rows += list(range(8 * t, 8 * t + 8)) + list(range(F + 8 * t, F + 8 * t + 8))
     return torch.tensor(rows, dtype=torch.long)
 
 

@@ -17,7 +17,7 @@ from loqa_hub_amd import ops  # noqa: E402
 dev = torch.device("cuda")
 out_path = "gpurun_out/kbench.jsonl"
 os.makedirs("gpurun_out", exist_ok=True)
-fout = open(out_path, "w")
+fout = open(out_path, "a")
 
 
 def timeit(fn, reps=50, warm=5):
@@ -207,7 +207,7 @@ def fused_bench():
         for S in (1, 2, 4, 8):
             if K % (S * 128):
                 continue
-            kw = dict(splits=S)
+            kw = dict(splits=S, rt=1)
             if mode == "rope":
                 kw.update(norm=True, rowsq_tiles=rows, positions=pos, cos_sin=cs, q_out=q,
                           k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv, head_dim=D)

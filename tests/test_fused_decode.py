@@ -112,50 +112,52 @@ def test_fused_resid_rowsq_and_silu_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
 @pytest.mark.parametrize("Mpad", [16, 32])
-def test_fused_rows_per_wave_layout_gpu(mode, Mpad):
-    """wr=4 (every wave owns its own row tile over the full K range) is
-    bitwise identical to wr=1's 4-way K split except for the fp32 summation
-    order: compare both against each other and against the fp32 reference."""
+@pytest.mark.parametrize("rt", [1, 2])
+def test_fused_rows_per_wave_layout_gpu(mode, Mpad, rt):
+    """Every (rt, wr) layout of the fused GEMM against the fp32 CPU reference of
+    the same call: 16-row pair tiles (SwiGLU / RoPE partners exchanged across
+    lanes l, l ^ 32) and 4-waves-along-rows tiles."""
     from loqa_hub_amd.ops import reference as ref
-    dev = "cuda"
     torch.manual_seed(3)
     K = 1024
     H, Hkv, D = 8, 2, 64
     N = {"resid": 512, "silu": 1024, "act": 512, "rope": (H + 2 * Hkv) * D}[mode]
-    x = torch.randn(Mpad, K, device=dev).bfloat16()
-    w = (torch.randn(N, K, device=dev) * 0.03).bfloat16()
+    x = torch.randn(Mpad, K).bfloat16()
+    w = (torch.randn(N, K) * 0.03).bfloat16()
     if mode == "silu":
-        w = w[ref.perm_gate_up(N // 2).to(dev)].contiguous()
-    wp = ops.shuffle_weight(w)
-    outs = []
-    res0 = torch.randn(Mpad, N, device=dev).bfloat16()
-    for wr in (1, 4):
+        w = w[ref.perm_gate_up(N // 2)].contiguous()
+    elif mode == "rope":
+        w = w[ref.perm_rope_qkv(H, Hkv, D)].contiguous()
+    res0 = torch.randn(Mpad, N).bfloat16()
+    cs = ref.rope_cos_sin(D, 256, 10000.0)
+
+    def run(dev, wr):
+        wp = ops.shuffle_weight(w.to(dev))
         scr = ops.FusedScratch(dev)
-        kw = dict(splits=1, wr=wr)
+        kw = dict(splits=1, wr=wr, rt=rt)
+        xd = x.to(dev)
         if mode == "resid":
-            res = res0.clone()
-            base = res.clone()
-            ops.skinny_fused(x, wp, "resid", scr, residual=res, **kw)
-            outs.append((res.float() - base.float(), scr.rowsq[: (N // 32) * Mpad].clone()))
-        elif mode == "rope":
+            res = res0.clone().to(dev)
+            ops.skinny_fused(xd, wp, "resid", scr, residual=res, **kw)
+            return [res.float().cpu(), scr.rowsq[: (N // (16 * rt)) * Mpad].float().cpu()]
+        if mode == "rope":
             kc = torch.zeros(4, Hkv, 16, D, device=dev).bfloat16()
             vc = torch.zeros_like(kc)
-            pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
+            pos = (torch.arange(Mpad, dtype=torch.int32) * 3 + 5).to(dev)
+            slots = torch.arange(Mpad, dtype=torch.int32, device=dev)
             q = torch.empty(Mpad, H * D, device=dev).bfloat16()
-            ops.skinny_fused(x, wp, "rope", scr, positions=pos, cos_sin=None, q_out=q, k_cache=kc,
-                             v_cache=vc, slots=pos, n_heads=H, n_kv=Hkv, head_dim=D, **kw)
-            outs.append((q.float(), kc.float().sum() + vc.float().sum()))
-        else:
-            y = ops.skinny_fused(x, wp, mode, scr, **kw)
-            outs.append((y.float(), None))
-    a, b = outs
-    rel = float((a[0] - b[0]).norm() / a[0].norm())
-    assert rel < 1e-2, rel
-    if mode == "act":
-        expect = x.float() @ w.float().t()
-        assert float((b[0] - expect).norm() / expect.norm()) < 1e-2
-    if mode == "resid":
-        assert torch.allclose(a[1], b[1], rtol=1e-2, atol=1e-2)
+            ops.skinny_fused(xd, wp, "rope", scr, positions=pos, cos_sin=cs.to(dev), q_out=q,
+                             k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv,
+                             head_dim=D, **kw)
+            return [q.float().cpu(), kc.float().cpu(), vc.float().cpu()]
+        return [ops.skinny_fused(xd, wp, mode, scr, **kw).float().cpu()]
+
+    expect = run("cpu", 1)
+    for wr in (1, 4):
+        got = run("cuda", wr)
+        for a, b in zip(got, expect):
+            rel = float((a - b).norm() / b.norm().clamp_min(1e-6))
+            assert rel < 1e-2, (wr, rel)
 
 
 def _ln_case(dev, S=None, Mpad=16, rt=2):
