@@ -21,7 +21,7 @@ from __future__ import annotations
 import queue
 import threading
 import time
-from concurrent.futures import Future
+from concurrent.futures import FIRST_COMPLETED, Future, ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -104,6 +104,9 @@ class LLMEngine:
         self._graphs: dict[tuple[int, int], dict] = {}
         self._next_id = 1
         self._on_done = None
+        self._cells_lock = threading.Lock()
+        # overlapped prefill (continuous-batching scheduler): GPU only
+        self.overlap_prefill = self.is_gpu
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
@@ -437,8 +440,16 @@ class LLMEngine:
                     it[2].set_exception(e)
         live: list[GenRequest] = []
         cells: dict[int, list] = {}   # id(cell) -> [remaining, future, reqs]
+        # prefills run on their own worker thread + stream, OVERLAPPED with the
+        # running decode batch (a new arrival no longer stalls every live
+        # sequence for a whole prefill pass); a request joins the decode batch
+        # at the first step boundary after its prefill completed (the worker
+        # synchronises on its first sampled token, so its KV writes are done)
+        pending: list[tuple[list[GenRequest], Future]] = []
+        pf_pool = self._prefill_executor() if self.overlap_prefill else None
         while self._running:
-            items = [self._inbox.get()] if not live else []   # idle: block for work
+            idle = not live and not pending
+            items = [self._inbox.get()] if idle else []   # idle: block for work
             while True:
                 try:
                     items.append(self._inbox.get_nowait())
@@ -453,41 +464,74 @@ class LLMEngine:
                     fut.set_result(reqs)
                     continue
                 cell = [len(reqs), fut, reqs]
-                cells[id(cell)] = cell
+                with self._cells_lock:
+                    cells[id(cell)] = cell
                 for r in reqs:
                     r.on_done = self._completion(cb, cell, cells)
                     self.submit(r)
                 new += reqs
             try:
                 if new:
-                    t0 = time.perf_counter()
-                    self.prefill(new)
-                    self.stats["prefill_s"] += time.perf_counter() - t0
-                    live += [r for r in new if not r.done]
+                    if pf_pool is not None:
+                        pending.append((new, pf_pool.submit(self._prefill_timed, new)))
+                    else:
+                        self._prefill_timed(new)
+                        live += [r for r in new if not r.done]
+                if pending:
+                    if not live:   # nothing to decode: wait for a prefill (or new work)
+                        wait([f for _, f in pending], timeout=0.002, return_when=FIRST_COMPLETED)
+                    still = []
+                    for reqs, f in pending:
+                        if f.done():
+                            f.result()                     # re-raise a prefill failure
+                            live += [r for r in reqs if not r.done]
+                        else:
+                            still.append((reqs, f))
+                    pending = still
                 if live:
                     t0 = time.perf_counter()
                     self.decode_step(live)
                     self.stats["decode_s"] += time.perf_counter() - t0
                     live = [r for r in live if not r.done]
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
-                for cell in list(cells.values()):
-                    if not cell[1].done():
-                        cell[1].set_exception(e)
-                    for r in cell[2]:
-                        if not r.done:
-                            self.kv.pool.free_seq(r.seq_id)
-                live, cells = [], {}
+                with self._cells_lock:
+                    for cell in list(cells.values()):
+                        if not cell[1].done():
+                            cell[1].set_exception(e)
+                        for r in cell[2]:
+                            if not r.done:
+                                self.kv.pool.free_seq(r.seq_id)
+                    cells.clear()
+                live, pending = [], []
+
+    def _prefill_timed(self, reqs: list[GenRequest]) -> None:
+        t0 = time.perf_counter()
+        self.prefill(reqs)
+        self.stats["prefill_s"] += time.perf_counter() - t0
+
+    def _prefill_executor(self) -> ThreadPoolExecutor:
+        if getattr(self, "_pf_pool", None) is None:
+            dev = self.device
+
+            def init():
+                if dev.type == "cuda":
+                    torch.cuda.set_device(dev)
+                    torch.cuda.set_stream(torch.cuda.Stream(dev))
+            self._pf_pool = ThreadPoolExecutor(1, thread_name_prefix="llm-prefill", initializer=init)
+        return self._pf_pool
 
     def _completion(self, cb, cell, cells):
-        def done(r: GenRequest) -> None:
+        def done(r: GenRequest) -> None:   # scheduler or prefill thread
             self.kv.pool.free_seq(r.seq_id)
             if cb is not None:
                 cb(r)
-            cell[0] -= 1
-            if cell[0] == 0:
-                cells.pop(id(cell), None)
-                if not cell[1].done():
-                    cell[1].set_result(cell[2])
+            with self._cells_lock:
+                cell[0] -= 1
+                last = cell[0] == 0
+                if last:
+                    cells.pop(id(cell), None)
+            if last and not cell[1].done():
+                cell[1].set_result(cell[2])
         return done
 
     def generate(self, reqs: list[GenRequest], on_done=None) -> list[GenRequest]:

@@ -14,7 +14,7 @@ from __future__ import annotations
 import queue
 import threading
 import time
-from concurrent.futures import Future
+from concurrent.futures import FIRST_COMPLETED, Future, ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -357,6 +357,14 @@ class STTEngine:
                device_pcm: torch.Tensor | None = None) -> None:
         """Front end + encoder for newly arrived requests, their cross-attention
         K|V into ``slots``, and their decoder sequences (fed the SOT prompt)."""
+        self._encode(reqs, slots, device_pcm)
+        self._start_decode(reqs)
+
+    def _encode(self, reqs: list[STTRequest], slots: list[int],
+                device_pcm: torch.Tensor | None = None) -> None:
+        """GPU half of admission (any thread with its own stream): PCM upload,
+        log-mel + encoder, cross-attention K|V into the requests' slots; returns
+        once that work is complete (the RMS read-back synchronises)."""
         tr = tracer()
         dev = self.device if self.is_gpu else None
         with tr.span("h2d", dev, batch=len(reqs)):
@@ -366,12 +374,18 @@ class STTEngine:
             enc = self.model.encode(audio)
             self.cross_kv(enc, slots)
         ss = sumsq.cpu().numpy()
+        if self.is_gpu:
+            torch.cuda.current_stream(self.device).synchronize()
         self.stats["encode_s"] += time.perf_counter() - t0
         for i, (r, sl) in enumerate(zip(reqs, slots)):
             n = max(1, min(len(r.pcm), N_SAMPLES))
             r.sumsq = float(ss[i])
             r.rms = float(np.sqrt(ss[i] / n))
             r.slot = sl
+
+    def _start_decode(self, reqs: list[STTRequest]) -> None:
+        """Decoder sequences for encoded requests (scheduler thread)."""
+        for r in reqs:
             r.seq_id = self._next
             self._next += 1
             self.kv.pool.add_seq(r.seq_id, [])
@@ -466,9 +480,16 @@ class STTEngine:
                     it[2].set_exception(e)
         live: list[STTRequest] = []
         waiting: list[tuple] = []          # (reqs, cb, fut) not yet admitted (no free slot)
+        encoding: list[tuple] = []         # (reqs, future) on the encoder worker
         cells: dict[int, list] = {}
+        # the encoder runs on its own worker thread + stream, overlapped with
+        # the running decoder batch (an arrival's encode no longer stalls every
+        # live transcription); requests join at the next step boundary after
+        # their encoder output and cross-attention K|V are complete
+        enc_pool = self._encoder_executor() if self.is_gpu else None
         while self._running:
-            items = [self._inbox.get()] if not live and not waiting else []
+            idle = not live and not waiting and not encoding
+            items = [self._inbox.get()] if idle else []
             while True:
                 try:
                     items.append(self._inbox.get_nowait())
@@ -491,8 +512,23 @@ class STTEngine:
                     new += reqs
                 if new:
                     slots = [self._free_slots.pop(0) for _ in new]
-                    self._admit(new, slots)
-                    live += new
+                    if enc_pool is not None:
+                        encoding.append((new, enc_pool.submit(self._encode, new, slots)))
+                    else:
+                        self._admit(new, slots)
+                        live += new
+                if encoding:
+                    if not live:
+                        wait([f for _, f in encoding], timeout=0.002, return_when=FIRST_COMPLETED)
+                    still = []
+                    for reqs, f in encoding:
+                        if f.done():
+                            f.result()
+                            self._start_decode(reqs)
+                            live += reqs
+                        else:
+                            still.append((reqs, f))
+                    encoding = still
                 if live:
                     for r in self._decode_once(live):
                         self._free_slots.append(r.slot)
@@ -514,5 +550,15 @@ class STTEngine:
                 for _, _, fut in waiting:
                     if not fut.done():
                         fut.set_exception(e)
-                live, waiting, cells = [], [], {}
+                live, waiting, cells, encoding = [], [], {}, []
                 self._free_slots = list(range(self.max_batch))
+
+    def _encoder_executor(self) -> ThreadPoolExecutor:
+        if getattr(self, "_enc_pool", None) is None:
+            dev = self.device
+
+            def init():
+                torch.cuda.set_device(dev)
+                torch.cuda.set_stream(torch.cuda.Stream(dev))
+            self._enc_pool = ThreadPoolExecutor(1, thread_name_prefix="stt-encoder", initializer=init)
+        return self._enc_pool
