@@ -225,13 +225,13 @@ def fused_bench():
             t = gtime(fused, inner=2 * ncopy)
             res[f"fusedS{S}_us"] = round(t, 2)
             if S == 1 and N % 128 == 0:
-                kw1 = dict(kw, wr=4)
+                for rt4 in (1, 2):
+                    kw1 = dict(kw, wr=4, rt=rt4)
 
-                def fused4():
-                    ops.skinny_fused(xx, wps[next(it) % ncopy], mode, scr, **kw1)
-                t4 = gtime(fused4, inner=2 * ncopy)
-                res["fusedS1wr4_us"] = round(t4, 2)
-                res["fusedS1wr4_TBps"] = round(gb / t4 * 1e3, 2)
+                    def fused4():
+                        ops.skinny_fused(xx, wps[next(it) % ncopy], mode, scr, **kw1)
+                    t4 = gtime(fused4, inner=2 * ncopy)
+                    res[f"fusedS1wr4rt{rt4}_us"] = round(t4, 2)
             res[f"fusedS{S}_TBps"] = round(gb / t * 1e3, 2)
             res[f"plainS{S}_us"] = round(gtime(plain, inner=2 * ncopy), 2)
         emit(**res)
