@@ -427,8 +427,9 @@ class LLMEngine:
     def _schedule(self, stream_priority: int) -> None:
         try:
             if self.is_gpu:
+                from ..utils.streams import stream_for
                 torch.cuda.set_device(self.device)
-                torch.cuda.set_stream(torch.cuda.Stream(self.device, priority=stream_priority))
+                torch.cuda.set_stream(stream_for(self.device, "LOQA_LLM_CUS", stream_priority))
         except Exception as e:  # noqa: BLE001 - never leave submitters waiting
             self._fatal = e
             while True:
