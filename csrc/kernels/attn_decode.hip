@@ -51,7 +51,7 @@ struct DecSmem {
 // K/V source: paged caches [nb, Hkv, blk, D] via block_tables, or (block_tables
 // == nullptr) contiguous rows kc/vc[(kv_start[b] + key) * kv_stride + kvh * D]
 // (Whisper cross-attention over the encoder output, read in place).
-template <int D>
+template <int D, int PF>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, long long q_stride, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, long long kv_stride, const int* __restrict__ kv_start,
@@ -101,40 +101,39 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   float m_run = -1e30f, l_run = 0.f;
 
-  for (int kt = kbeg + wave * DEC_TILE; kt < kend; kt += DEC_WAVES * DEC_TILE) {
-    // issue K (-> registers) and V (-> registers -> LDS) loads of this wave's tile
-    uint4 kraw[NS], vraw[VPL];
-    {
-      // the tile's (at most two) cache blocks: wave-uniform scalar lookups
-      int base0 = 0, base1 = 0, bi0 = 0;
-      if (paged) {
-        bi0 = kt / blk;
-        base0 = bt[bi0];
-        base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? bt[bi0 + 1] : base0;
-      }
-      auto row_off = [&](int key) -> size_t {
-        if (paged) {
-          const int local = key - bi0 * blk;
-          const int bid = local >= blk ? base1 : base0;
-          return (((size_t)bid * Hkv + kvh) * blk + (local & (blk - 1))) * D;
-        }
-        return (kv0 + key) * (size_t)kv_stride + (size_t)kvh * D;
-      };
-      const int key = kt + r;
-      const bool ok = key < kend;
-      const size_t off = row_off(ok ? key : kt);
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        kraw[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        const int c = lane + 64 * i;
-        const int kr = c / CH, cc = (c - kr * CH) * 8;
-        const int k2 = kt + kr;
-        vraw[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + row_off(k2) + cc)
-                            : make_uint4(0, 0, 0, 0);
-      }
+  // the tile's (at most two) cache blocks: wave-uniform scalar lookups
+  auto load_tile = [&](int kt, uint4 (&kraw)[NS], uint4 (&vraw)[VPL]) {
+    int base0 = 0, base1 = 0, bi0 = 0;
+    if (paged) {
+      bi0 = kt / blk;
+      base0 = bt[bi0];
+      base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? bt[bi0 + 1] : base0;
     }
+    auto row_off = [&](int key) -> size_t {
+      if (paged) {
+        const int local = key - bi0 * blk;
+        const int bid = local >= blk ? base1 : base0;
+        return (((size_t)bid * Hkv + kvh) * blk + (local & (blk - 1))) * D;
+      }
+      return (kv0 + key) * (size_t)kv_stride + (size_t)kvh * D;
+    };
+    const int key = kt + r;
+    const bool ok = key < kend;
+    const size_t off = row_off(ok ? key : kt);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      kraw[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      const int kr = c / CH, cc = (c - kr * CH) * 8;
+      const int k2 = kt + kr;
+      vraw[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + row_off(k2) + cc)
+                          : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  auto process_tile = [&](int kt, uint4 (&kraw)[NS], uint4 (&vraw)[VPL]) {
     // S^T = K Q^T
     float16v st;
 #pragma unroll
@@ -198,6 +197,35 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  };
+
+  constexpr int STEP = DEC_WAVES * DEC_TILE;
+  int kt = kbeg + wave * DEC_TILE;
+  if constexpr (PF) {
+    // ping-pong: the next tile's K / V are requested before this tile is
+    // consumed (a key split longer than 4 tiles otherwise pays one memory
+    // round trip per tile). The prefetch is unconditional (clamped to the
+    // current tile past the end) so no join point drains it (see stream_k).
+    // Measured on the Whisper cross-attention (1500 keys, 3-12 splits): no
+    // gain at 512-key splits and a loss at shorter ones (183 vs 120 VGPRs
+    // halves occupancy), so both head dims launch PF = 0.
+    uint4 ka[NS], va[VPL], kb[NS], vb[VPL];
+    if (kt < kend) load_tile(kt, ka, va);
+    while (kt < kend) {
+      load_tile(kt + STEP < kend ? kt + STEP : kt, kb, vb);
+      process_tile(kt, ka, va);
+      kt += STEP;
+      if (kt >= kend) break;
+      load_tile(kt + STEP < kend ? kt + STEP : kt, ka, va);
+      process_tile(kt, kb, vb);
+      kt += STEP;
+    }
+  } else {
+    for (; kt < kend; kt += STEP) {
+      uint4 kraw[NS], vraw[VPL];
+      load_tile(kt, kraw, vraw);
+      process_tile(kt, kraw, vraw);
+    }
   }
 
   // ---- merge the 4 waves' online-softmax states through LDS (o aliases v: every
@@ -376,12 +404,12 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   dim3 grid(num_splits, Hkv, B);
   const float sl2 = scale * 1.4426950408889634f;
   if (D == 128)
-    hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
+    hipLaunchKernelGGL((attn_decode_kernel<128, 0>), grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
                        block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
                        part_o, part_ml, total_q, counters, (bf16_t*)o, o_stride);
   else
-    hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
+    hipLaunchKernelGGL((attn_decode_kernel<64, 0>), grid, dim3(256), 0, s, (const bf16_t*)q, q_stride,
                        (const bf16_t*)kc, (const bf16_t*)vc, kv_stride, kv_start, cu_q, ctx_lens,
                        block_tables, max_blocks, blk, Hq, Hkv, sl2, causal, split_keys, num_splits,
                        part_o, part_ml, total_q, counters, (bf16_t*)o, o_stride);

@@ -3,7 +3,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 > gpurun_out/prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 2 > gpurun_out/prof.log 2>&1
 rc=$?
 echo "profile rc=$rc"
 grep -v amdgpu.ids gpurun_out/prof.log | tail -1 | cut -c1-300
