@@ -76,7 +76,11 @@ class LLMEngine:
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.tp = tp or TPGroup()
-        self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
+        from ..utils.streams import decode_cus
+        self.max_wgs = decode_cus(self.device, "LOQA_LLM_CUS", "LOQA_LLM_MAX_WGS")
+        with ops.decode_cap(self.max_wgs):
+            self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
+        self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = LlamaModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
         self.grammar = GrammarTables(self.tok, self.device)

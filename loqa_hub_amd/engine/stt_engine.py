@@ -61,7 +61,11 @@ class STTEngine:
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
+        from ..utils.streams import decode_cus
+        self.max_wgs = decode_cus(self.device, "LOQA_STT_CUS", "LOQA_STT_MAX_WGS")
+        with ops.decode_cap(self.max_wgs):
+            self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
+        self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = WhisperModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
         self.sot = [self.tok.token_id(s) for s in

@@ -294,7 +294,7 @@ class LlamaModel:
             tp.all_reduce_(down)
         hf = ops.slab_rmsnorm(down, residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx,
                               write_residual=False)
-        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=ops.MAX_DECODE_WGS)[0]
+        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
     def forward_decode_fused(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
                              attn_ws: ops.AttnWorkspace | None, scratch: ops.FusedScratch,
@@ -311,7 +311,7 @@ class LlamaModel:
         # layer 0's RMSNorm row scale: one partial sum of squares per row
         scratch.seed_stats(residual, sums=False)
         num_splits, split_keys = ops.decode_attn_splits(meta.max_ctx, meta.ctx_lens.numel() * Hkv,
-                                                        split_keys)
+                                                        split_keys, getattr(w, "max_wgs", None))
         q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
@@ -331,7 +331,7 @@ class LlamaModel:
             ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
         sel = residual.index_select(0, meta.logit_idx).contiguous()
         hf = ops.rmsnorm(sel, w.final_norm, cfg.norm_eps)
-        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=ops.MAX_DECODE_WGS)[0]
+        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """Local vocab shard logits [B, V/tp] (bf16)."""

@@ -279,7 +279,7 @@ def decode_step_fast(model: "WhisperModel", tokens: torch.Tensor, positions: tor
         part = ops.skinny_gemm(m, P["fc2"])
     hf = ops.slab_layernorm(part, residual, w.dec_ln_w, w.dec_ln_b, 1e-5,
                             bias=w.dec[-1]["fc2_b"], row_idx=logit_idx, write_residual=False)
-    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=ops.MAX_DECODE_WGS)[0]
+    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
 
 def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: torch.Tensor,
@@ -325,7 +325,7 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
         ops.skinny_fused(m, F["fc2"], "resid", scratch, residual=residual, row_sums=True)
     sel = residual.index_select(0, logit_idx).contiguous()
     hf = ops.layernorm(sel, w.dec_ln_w, w.dec_ln_b, 1e-5)
-    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=ops.MAX_DECODE_WGS)[0]
+    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
 
 def pad_or_trim(audio: np.ndarray, n: int = 480000) -> np.ndarray:

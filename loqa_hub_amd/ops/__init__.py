@@ -358,6 +358,23 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 
 _FSPLITS: dict = {}
 MAX_DECODE_WGS = int(os.environ.get("LOQA_MAX_DECODE_WGS", "256"))
+_CAP = [MAX_DECODE_WGS]   # active co-scheduling cap while tuning (see decode_cap)
+
+
+class decode_cap:
+    """Context: tune decode GEMMs for a grid of at most ``n`` workgroups (an
+    engine confined to n CUs by a CU mask gets n; default MAX_DECODE_WGS)."""
+
+    def __init__(self, n: int | None):
+        self.n = n or MAX_DECODE_WGS
+
+    def __enter__(self):
+        self.prev = _CAP[0]
+        _CAP[0] = self.n
+        return self
+
+    def __exit__(self, *exc):
+        _CAP[0] = self.prev
 
 
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
@@ -383,7 +400,7 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     # latency-bound kernels wait for it to drain (measured: a 768-workgroup
     # qkv GEMM, fastest in isolation, slowed the concurrent Whisper decoder 5x
     # and the whole pipeline 1.8x). Keep at most one workgroup per CU.
-    capped = [c for c in cands if (N // (16 * c[1] * c[2])) * c[0] <= MAX_DECODE_WGS]
+    capped = [c for c in cands if (N // (16 * c[1] * c[2])) * c[0] <= _CAP[0]]
     cands = capped or cands[:1]
     best, best_t = (1, rts[-1], 1), float("inf")
     n = max(1, ncopies)

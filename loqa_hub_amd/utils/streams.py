@@ -76,3 +76,16 @@ def stream_for(device: torch.device, env_key: str, priority: int = 0):
         n = torch.cuda.get_device_properties(device).multi_processor_count
         return cu_masked_stream(device, parse_cu_spec(spec, n))
     return torch.cuda.Stream(device, priority=priority)
+
+
+def decode_cus(device: torch.device, cus_env: str, cap_env: str) -> int | None:
+    """Workgroup cap for an engine's decode grids: ``cap_env`` if set, else the
+    number of CUs its stream is confined to by ``cus_env``, else None (the
+    global default). A grid wider than its CU share would run in two rounds."""
+    if os.environ.get(cap_env):
+        return int(os.environ[cap_env])
+    spec = os.environ.get(cus_env, "")
+    if spec and torch.device(device).type == "cuda":
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        return len(parse_cu_spec(spec, n))
+    return None

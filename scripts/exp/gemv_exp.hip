@@ -189,3 +189,29 @@ extern "C" int exp_gemv2(const void* x, const void* Wp, float* out, int N, int K
   XFS(2, 2, 2, 4) XFS(8, 1, 1, 4) XFS(4, 4, 1, 4) XFS(1, 8, 1, 4) XFS(1, 8, 2, 4)
   return 2;
 }
+
+// background load generators for the contention study
+__global__ __launch_bounds__(256) void hog_stream(const u32x4* __restrict__ p, long long n, int iters, u32x4* out) {
+  u32x4 acc = {0, 0, 0, 0};
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (int it = 0; it < iters; ++it)
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+      acc ^= __builtin_nontemporal_load(p + i);
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void hog_alu(int iters, float* out) {
+  float a = threadIdx.x * 1e-3f, b = 1.0001f;
+  for (int i = 0; i < iters; ++i) { a = a * b + 1e-7f; b = b * 0.99999f + 1e-6f; }
+  if (a == 12345.f) out[0] = a + b;
+}
+
+extern "C" int exp_hog_stream(const void* p, long long nbytes, int iters, void* out, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(hog_stream, dim3(grid), dim3(256), 0, st, (const u32x4*)p, nbytes / 16, iters, (u32x4*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int exp_hog_alu(int iters, void* out, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(hog_alu, dim3(grid), dim3(256), 0, st, iters, (float*)out);
+  return (int)hipGetLastError();
+}
