@@ -70,7 +70,8 @@ class LLMEngine:
     def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
                  tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192,
-                 weights: LlamaWeights | None = None, fused_decode: bool = True):
+                 weights: LlamaWeights | None = None, fused_decode: bool = True,
+                 compact: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -79,7 +80,8 @@ class LLMEngine:
         from ..utils.streams import decode_cus
         self.max_wgs = decode_cus(self.device, "LOQA_LLM_CUS", "LOQA_LLM_MAX_WGS")
         with ops.decode_cap(self.max_wgs):
-            self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp)
+            self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp,
+                                                   compact=compact)
         self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = LlamaModel(self.weights)
         self.tok = get_tokenizer(cfg.vocab_size)
@@ -330,6 +332,8 @@ class LLMEngine:
 
     def prefill(self, reqs: list[GenRequest]) -> None:
         """Run the prompts (chunked) and sample each sequence's first token."""
+        if getattr(self.weights, "compact", False):
+            return self._prefill_fused(reqs)
         i = 0
         while i < len(reqs):
             batch, T = [], 0
@@ -348,6 +352,30 @@ class LLMEngine:
             for r in batch:
                 self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
             self._sample_and_advance(batch, nxt, time.perf_counter())
+
+    PREFILL_CHUNK_FUSED = 64
+
+    def _prefill_fused(self, reqs: list[GenRequest]) -> None:
+        """Prefill through the fused decode GEMMs (compact single-copy weights):
+        each prompt in <= 64-token chunks (one weight pass per chunk; attention
+        falls back to the varlen flash kernel past the decode kernel's row
+        limit). Prompts mostly hit the prefix cache, so a request typically
+        costs one chunk."""
+        C = self.PREFILL_CHUNK_FUSED
+        for r in reqs:
+            feed = r.feed
+            nxt = None
+            for c0 in range(0, len(feed), C):
+                chunk = feed[c0:c0 + C]
+                T_pad = ops.mpad_for(len(chunk))
+                max_q, max_ctx, host = self._meta([r], [chunk], True, 1, T_pad)
+                host["mask_rows"] = np.array([r.grammar.mask_row()], np.int32)
+                dev = self._to_device(host)
+                meta = self._build_meta(dev, max_q, max_ctx, True)
+                nxt = self._forward_sample(meta, dev["mask_rows"])
+            self.stats["prefill_tokens"] += len(feed)
+            self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
+            self._sample_and_advance([r], nxt.cpu().numpy(), time.perf_counter())
 
     def decode_step(self, live: list[GenRequest]) -> None:
         feeds, carry = [], []

@@ -71,9 +71,15 @@ class TPGroup:
 
 class LlamaWeights:
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0,
-                 tp: TPGroup | None = None):
+                 tp: TPGroup | None = None, compact: bool = False):
         tp = tp or TPGroup()
         self.cfg, self.tp = cfg, tp
+        # compact: ONE copy of every projection, in the fused decode layout
+        # (prefill then runs through the fused GEMMs in <= 64-token chunks).
+        # Llama-3-70B bf16 (141 GB) fits one 288 GB MI355X this way; the
+        # default keeps row-major copies for hipBLASLt prefill as well.
+        self.compact = compact
+        assert not compact or tp.world == 1, "compact weights are single-GPU"
         assert cfg.n_heads % tp.world == 0 and cfg.n_kv_heads % tp.world == 0
         assert cfg.ffn_dim % tp.world == 0 and cfg.vocab_size % tp.world == 0
         self.h = cfg.n_heads // tp.world
@@ -95,22 +101,47 @@ class LlamaWeights:
         # std 0.02 everywhere keeps activations O(1) through random layers
         self.embed = rnd(self.v, d)
         self.layers = []
+        if compact:
+            self.decode_layers = []
         for _ in range(cfg.n_layers):
-            self.layers.append({
+            L = {
                 "attn_norm": ones(d),
                 "wqkv": rnd((self.h + 2 * self.hkv) * D, d),
                 "wo": rnd(d, self.h * D),
                 "mlp_norm": ones(d),
                 "w_gate_up": rnd(2 * self.f, d),
                 "w_down": rnd(d, self.f),
-            })
+            }
+            if compact:   # convert layer by layer: peak = one layer's row-major copy
+                self.decode_layers.append(self._compact_layer(L))
+                L = {"attn_norm": L["attn_norm"], "mlp_norm": L["mlp_norm"]}
+            self.layers.append(L)
         self.final_norm = ones(d)
         self.lm_head = self.embed if cfg.tie_embeddings else rnd(self.v, d)
         self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
         self._finalize()
 
+    def _compact_layer(self, L: dict) -> dict:
+        from ..ops import reference as _ref
+        dev = L["wqkv"].device
+        pq = _ref.perm_rope_qkv(self.h, self.hkv, self.cfg.head_dim).to(dev)
+        pg = _ref.perm_gate_up(self.f).to(dev)
+        return {"wqkv_f": ops.shuffle_weight(ops.fold_norm(L["wqkv"], L["attn_norm"])[pq].contiguous()),
+                "w_gate_up_f": ops.shuffle_weight(
+                    ops.fold_norm(L["w_gate_up"], L["mlp_norm"])[pg].contiguous()),
+                "wo": ops.shuffle_weight(L["wo"]), "w_down": ops.shuffle_weight(L["w_down"])}
+
     def _finalize(self) -> None:
         """Derived decode copies + split-K tuning (after the base tensors exist)."""
+        if getattr(self, "compact", False):
+            self.lm_head_p = ops.shuffle_weight(self.lm_head)
+            if not self.cfg.tie_embeddings:
+                del self.lm_head          # only the shuffled copy is read
+            self.fused = True
+            if self.embed.device.type == "cuda":
+                ops.tune_skinny_splits(self.lm_head_p)
+                self._tune_fused()
+            return
         # decode copies in MFMA-fragment order for the weight-streaming skinny GEMM
         # (prefill keeps the row-major copies for hipBLASLt; 288 GB of HBM makes
         # the duplicate affordable and each path gets its ideal layout)
@@ -313,6 +344,9 @@ class LlamaModel:
         num_splits, split_keys = ops.decode_attn_splits(meta.max_ctx, meta.ctx_lens.numel() * Hkv,
                                                         split_keys, getattr(w, "max_wgs", None))
         q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
+        # chunked prefill through this path (compact weights) can exceed the
+        # grouped kernels' row limit: plain varlen flash attention then
+        grouped = (H // Hkv) * meta.max_q <= 128
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
             ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True,
@@ -322,9 +356,9 @@ class LlamaModel:
                              n_heads=H, n_kv=Hkv, head_dim=D)
             attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
                                  head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
-                                 block_tables=meta.block_tables, grouped=True,
-                                 split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
-                                 max_k=meta.max_ctx)
+                                 block_tables=meta.block_tables, grouped=grouped,
+                                 split_keys=split_keys, num_splits=num_splits if grouped else 1,
+                                 workspace=attn_ws, max_k=meta.max_ctx)
             ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
             a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
                                  eps=cfg.norm_eps)

@@ -10,10 +10,11 @@
               command; every 4th utterance runs with NATS publishes failing
               at random (p = 0.5) so the queue's rollback path executes.
   --config 5  Whisper-large-v3 + Llama-3-70B + VITS TTS of every reply, on ONE
-              GPU at TP=1 (70B bf16 = 141 GB fits in 288 GB HBM3E; the TP=8
-              path is exercised by tests/test_tp.py and the driver's 8-GPU
-              node): 8 closed-loop streams, utterances/s, ms per added command,
-              TTS time per reply.
+              GPU at TP=1: compact single-copy weights (fused decode layout,
+              chunked fused prefill), so 70B bf16 = 141 GB fits in 288 GB
+              HBM3E (the TP=8 path is exercised by tests/test_tp.py): 8
+              closed-loop streams, utterances/s, ms per added command, TTS
+              time per reply.
 
 Synthetic speech-like audio, random-init weights (teacher-forced STT,
 grammar-constrained LLM) as in bench.py. Prints one JSON line per config.
@@ -50,9 +51,9 @@ def _closed_loop(pipe, utts, streams: int, per_stream: int, tts=None):
             u = utts[(ci * per_stream + k) % len(utts)]
             j = PipelineJob(u.relay_id, f"c{ci}-{k}", u.pcm, transcript_hint=u.text)
             await pipe.submit(j)
-            if tts is not None and j.multi is not None and j.multi.response:
+            if tts is not None and j.multi is not None and j.multi.combined_response:
                 t0 = time.perf_counter()
-                await tts.synthesize(j.multi.response)
+                await tts.synthesize(j.multi.combined_response)
                 tts_s.append(time.perf_counter() - t0)
                 j.t["tts_done"] = time.perf_counter()
             jobs.append(j)
@@ -76,7 +77,9 @@ def config_2_or_5(cfg_id: int, args, dev, nats) -> dict:
         stt_name, llm_name, streams = "whisper-large-v3", "llama3-70b", 8
     t0 = time.perf_counter()
     stt = STTEngine(whisper_config(stt_name), dev, seed=0, max_batch=8)
-    llm = LLMEngine(llama_config(llm_name), dev, seed=0, max_seqs=8, max_seq_len=1024)
+    # 70B at TP=1: one weight copy in the fused decode layout (141 GB)
+    llm = LLMEngine(llama_config(llm_name), dev, seed=0, max_seqs=8, max_seq_len=1024,
+                    compact=llm_name == "llama3-70b")
     pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=8)
     pipe.warmup()
     tts = None

@@ -407,3 +407,23 @@ def test_pipeline_continuous_stt_cpu():
         llm.stop()
     assert [j.n_commands for j in res] == [u.n_commands for u in utts]
     assert all(j.queue is not None and j.transcription is not None for j in res)
+
+
+def test_llm_compact_weights_match_default_cpu():
+    """Compact single-copy weights (fused layout only, chunked fused prefill)
+    produce the same constrained output as the default two-copy layout."""
+    from loqa_hub_amd.engine.grammar import multi_command_schema
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    cfg = llama_config("test-tiny")
+    outs = []
+    for compact in (False, True):
+        eng = LLMEngine(cfg, torch.device("cpu"), seed=4, max_seqs=4, max_seq_len=512,
+                        use_graphs=False, compact=compact)
+        if compact:
+            assert "wqkv" not in eng.weights.layers[0] and "wqkv_f" in eng.weights.decode_layers[0]
+        reqs = [GenRequest(list(range(10, 10 + 70 + 9 * i)), multi_command_schema(2, min_response_tokens=2))
+                for i in range(2)]
+        eng.generate(reqs)
+        outs.append([r.output for r in reqs])
+    assert outs[0] == outs[1]
