@@ -56,14 +56,17 @@ class STTEngine:
 
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
                  block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
-                 fused: bool = True, weights: WhisperWeights | None = None):
+                 fused: bool = True, weights: WhisperWeights | None = None,
+                 contended_tuning: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         from ..utils.streams import decode_cus
         self.max_wgs = decode_cus(self.device, "LOQA_STT_CUS", "LOQA_STT_MAX_WGS")
-        with ops.decode_cap(self.max_wgs):
+        # optional: tune the decode GEMMs under a background weight stream
+        # (ops.contended_tuning; measured noisier and 5 % slower end to end)
+        with ops.decode_cap(self.max_wgs), ops.contended_tuning(self.device, contended_tuning):
             self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
         self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = WhisperModel(self.weights)

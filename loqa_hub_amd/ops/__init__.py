@@ -377,6 +377,69 @@ class decode_cap:
         _CAP[0] = self.prev
 
 
+class contended_tuning:
+    """Context: while tuning, keep a Llama-3-8B-like gate|up weight stream
+    (rows-per-wave fused GEMM over ~700 MB of cold weights) running on a
+    background stream. The Whisper decoder always runs beside the LLM decode;
+    its kernels' best split-K / tile shape under that load differs from the
+    isolated optimum (split-K hand-offs cost extra memory round trips that
+    queue behind the co-resident weight stream)."""
+
+    def __init__(self, device, enabled: bool = True):
+        self.device, self.enabled = torch.device(device), enabled
+
+    def __enter__(self):
+        if not (self.enabled and self.device.type == "cuda"):
+            return self
+        import threading
+        dev = self.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self._ws = [shuffle_weight(torch.randn(28672, 4096, **bf) * 0.02) for _ in range(3)]
+        self._x = torch.randn(16, 4096, **bf)
+        self._scr = FusedScratch(dev)
+        self._scr.rowsq[: 128 * 16].fill_(32.0)
+        self._stop = threading.Event()
+        self._stream = torch.cuda.Stream(dev)
+        ready = threading.Event()
+
+        # the background work is one captured graph, replayed and paced by
+        # event polling: no synchronising HIP call while the tuner captures
+        with torch.cuda.stream(self._stream):
+            for i in range(3):
+                skinny_fused(self._x, self._ws[i], "silu", self._scr, splits=1, rt=2, wr=4, norm=True,
+                             rowsq_tiles=128)
+        self._stream.synchronize()
+        self._g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g, stream=self._stream):
+            for i in range(12):
+                skinny_fused(self._x, self._ws[i % 3], "silu", self._scr, splits=1, rt=2, wr=4,
+                             norm=True, rowsq_tiles=128)
+
+        def loop():
+            import time as _time
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(self._stream):
+                while not self._stop.is_set():
+                    self._g.replay()
+                    ev = torch.cuda.Event()
+                    ev.record(self._stream)
+                    while not ev.query():
+                        _time.sleep(0.0002)
+                    ready.set()
+        self._th = threading.Thread(target=loop, daemon=True)
+        self._th.start()
+        ready.wait(30)
+        return self
+
+    def __exit__(self, *exc):
+        if getattr(self, "_th", None) is not None:
+            self._stop.set()
+            self._th.join()
+            torch.cuda.synchronize(self.device)
+            del self._g, self._ws, self._x, self._scr
+            self._th = None
+
+
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
                       wr4: bool = False) -> tuple[int, int, int]:
     """(split-K, tile rows / 16, waves along rows) for a fused-epilogue GEMM,
