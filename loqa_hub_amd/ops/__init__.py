@@ -377,6 +377,19 @@ class decode_cap:
         _CAP[0] = self.prev
 
 
+def _fsplit_override(key: tuple) -> tuple[int, int, int] | None:
+    """``LOQA_FSPLIT_OVERRIDE="silu:28672x4096:M16=2,2,1;..."`` pins the
+    (split-K, rt, wr) of a fused GEMM shape (experiments / deployment pins)."""
+    spec = os.environ.get("LOQA_FSPLIT_OVERRIDE", "")
+    name = f"{key[0]}:{key[1]}x{key[2]}:M{key[3]}"
+    for item in spec.split(";"):
+        if "=" in item:
+            k, v = item.split("=", 1)
+            if k.strip() == name:
+                return tuple(int(t) for t in v.split(","))
+    return None
+
+
 class contended_tuning:
     """Context: while tuning, keep a Llama-3-8B-like gate|up weight stream
     (rows-per-wave fused GEMM over ~700 MB of cold weights) running on a
@@ -454,6 +467,10 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     ``key`` = (mode, N, K, Mpad)."""
     if key in _FSPLITS:
         return _FSPLITS[key]
+    ov = _fsplit_override(key)
+    if ov is not None:
+        _FSPLITS[key] = ov
+        return ov
     N = key[1]
     cands = [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
     if wr4:

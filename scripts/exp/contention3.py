@@ -50,16 +50,20 @@ cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
 cl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
 aws = ops.AttnWorkspace(dev, 256, H, D, 32)
 it = iter(range(1 << 40))
+def gu(S, rt, wr):
+    return lambda: ops.skinny_fused(x, ws["gate_up"][next(it) % 3], "silu", scr, splits=S, rt=rt, wr=wr,
+                                    norm=True, rowsq_tiles=128)
+
+
+def dn(S, rt, wr):
+    return lambda: ops.skinny_fused(xd, ws["down"][next(it) % 6], "resid", scr, splits=S, rt=rt, wr=wr,
+                                    residual=res)
+
+
 kernels = {
-    "gate_up_wr4": lambda: ops.skinny_fused(x, ws["gate_up"][next(it) % 3], "silu", scr, splits=1, rt=2, wr=4,
-                                           norm=True, rowsq_tiles=128),
-    "down_S2": lambda: ops.skinny_fused(xd, ws["down"][next(it) % 6], "resid", scr, splits=2, rt=2, wr=1,
-                                       residual=res),
-    "o_S1": lambda: ops.skinny_fused(x, ws["o"][next(it) % 16], "resid", scr, splits=1, rt=1, wr=1, residual=res),
-    "attn": lambda: ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True, max_q=1,
-                                  ctx_lens=cl, block_tables=bt, grouped=True, split_keys=128, num_splits=4,
-                                  workspace=aws),
-    "lm_head": lambda: ops.skinny_gemm(x, ws["lm"][0], 1, max_wgs=256),
+    "gu_S1rt2wr4": gu(1, 2, 4), "gu_S1rt1wr4": gu(1, 1, 4), "gu_S1rt2wr1": gu(1, 2, 1),
+    "gu_S2rt2wr1": gu(2, 2, 1), "gu_S1rt1wr1": gu(1, 1, 1),
+    "dn_S2rt2wr1": dn(2, 2, 1), "dn_S1rt1wr1": dn(1, 1, 1), "dn_S1rt2wr1": dn(1, 2, 1),
 }
 stop = threading.Event()
 
@@ -79,6 +83,10 @@ def bg(fn, stream):
         stream.synchronize()
 
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench_kernels import gtime  # noqa: E402
+alone = {n: round(gtime(f, inner=24), 2) for n, f in kernels.items()}
+print(json.dumps({"kernel_alone_us": alone}), flush=True)
 torch.cuda.set_stream(torch.cuda.Stream(dev))
 out = {"stt_alone": timed(stt_step)}
 for name, fn in kernels.items():
