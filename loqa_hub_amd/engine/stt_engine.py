@@ -11,6 +11,7 @@ of the same length; only the fed-back token is the reference one.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -92,6 +93,8 @@ class STTEngine:
         self.scratch = ops.FusedScratch(self.device) if self.fused else None
         self.use_graphs = use_graphs and self.is_gpu and fast_decode
         self.self_splits = (cfg.n_text_ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS
+        # cross-attention keys per split (the workspace holds n_audio_ctx / 128 splits)
+        self.cross_split_keys = max(self.SPLIT_KEYS, int(os.environ.get("LOQA_XATTN_SPLIT_KEYS", "256")) // 32 * 32)
         if fast_decode and self.is_gpu:
             self.ws = ops.AttnWorkspace(self.device, 128, cfg.n_heads, cfg.head_dim,
                                         max(self.self_splits, (cfg.n_audio_ctx + self.SPLIT_KEYS - 1)
@@ -235,7 +238,7 @@ class STTEngine:
                                        dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
                                        self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
                                        dev["enc_lens"], dev["logit_idx"], self.ws, self.scratch,
-                                       ns, self.SPLIT_KEYS)
+                                       ns, self.SPLIT_KEYS, self.cross_split_keys)
             return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
         logits = decode_step_fast(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                   dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,

@@ -215,3 +215,36 @@ extern "C" int exp_hog_alu(int iters, void* out, int grid, hipStream_t st) {
   hipLaunchKernelGGL(hog_alu, dim3(grid), dim3(256), 0, st, iters, (float*)out);
   return (int)hipGetLastError();
 }
+
+// grid-barrier cost study: G workgroups, `phases` barriers (monotonic counter,
+// agent-scope release/acquire fences, bounded spin). Each phase optionally
+// touches a 4 KB hand-off buffer (store by one WG, load by all).
+__global__ __launch_bounds__(256) void barrier_probe(unsigned* ctr, unsigned base, int phases, float* buf,
+                                                     int* err) {
+  const unsigned G = gridDim.x;
+  float acc = 0.f;
+  for (int p = 0; p < phases; ++p) {
+    if (blockIdx.x == (unsigned)(p % G) && threadIdx.x < 256) buf[threadIdx.x] = (float)p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = base + (unsigned)(p + 1) * G;
+      int spins = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target > 0x7fffffffu) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 24)) { *err = 1; break; }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    acc += buf[threadIdx.x & 255];
+  }
+  if (acc == -1.f) buf[0] = acc;
+}
+
+extern "C" int exp_barrier(void* ctr, unsigned base, int phases, void* buf, void* err, int G, hipStream_t st) {
+  hipLaunchKernelGGL(barrier_probe, dim3(G), dim3(256), 0, st, (unsigned*)ctr, base, phases, (float*)buf,
+                     (int*)err);
+  return (int)hipGetLastError();
+}
