@@ -18,6 +18,7 @@ sequence) plus one small pinned H2D copy of the step metadata.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -102,6 +103,8 @@ class LLMEngine:
         self.max_decode_q = max(1, 32 // (self.weights.h // self.weights.hkv))
         self.attn_ws = ops.AttnWorkspace(self.device, 128, self.weights.h, cfg.head_dim,
                                          (max_seq_len + 127) // 128) if self.is_gpu else None
+        # decode-attention keys per split (>= 128: the workspace holds max_seq_len / 128 splits)
+        self.attn_split_keys = max(128, int(os.environ.get("LOQA_LLM_ATTN_SPLIT_KEYS", "128")) // 32 * 32)
         self.use_graphs = use_graphs and self.is_gpu
         # fused-epilogue decode GEMMs (single GPU, <= 32 tokens per step)
         self.fused_decode = fused_decode and self.weights.fused
@@ -186,7 +189,7 @@ class LLMEngine:
         if meta.decode:
             if self.fused_decode and meta.tokens.numel() <= 64:
                 logits = self.model.forward_decode_fused(meta, self.kv.k, self.kv.v, self.attn_ws,
-                                                         self.scratch)
+                                                         self.scratch, self.attn_split_keys)
             else:
                 logits = self.model.forward_decode(meta, self.kv.k, self.kv.v, self.attn_ws)
             logits = logits[: mask_rows.numel()]

@@ -471,7 +471,28 @@ class STTEngine:
         if getattr(self, "_fatal", None) is not None:
             fut.set_exception(self._fatal)
             return fut
-        self._inbox.put((list(reqs), on_done, fut))
+        reqs = list(reqs)
+        if len(reqs) > self.max_batch:
+            # admission needs a free slot for every request of an inbox item:
+            # an oversize batch would wait forever, so it goes in max_batch chunks
+            parts = [self.submit_batch(reqs[i:i + self.max_batch], on_done)
+                     for i in range(0, len(reqs), self.max_batch)]
+            left = [len(parts)]
+            lock = threading.Lock()
+
+            def _part_done(f: Future) -> None:
+                with lock:
+                    left[0] -= 1
+                    if fut.done():
+                        return
+                    if f.exception() is not None:
+                        fut.set_exception(f.exception())
+                    elif left[0] == 0:
+                        fut.set_result(reqs)
+            for p in parts:
+                p.add_done_callback(_part_done)
+            return fut
+        self._inbox.put((reqs, on_done, fut))
         return fut
 
     def _schedule(self, stream_priority: int) -> None:

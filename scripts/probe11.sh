@@ -6,7 +6,11 @@ run() {
   env "$@" timeout -k 10 300 python bench.py --steps 4 --warmup 2 > gpurun_out/bench_$name.log 2>&1 || { tail -20 gpurun_out/bench_$name.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/bench_$name.log | tail -1 | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print("'$name'", d["value"], d["ms_per_added_command_e2e_marginal"], d["phase_ms_per_step"]["stt"], d["llm_stats"]["gpu_wait_s"]/d["llm_stats"]["decode_steps"], d["stt_stats"]["gpu_wait_s"]/d["stt_stats"]["decode_steps"])'
 }
-run XK128 LOQA_XATTN_SPLIT_KEYS=128
-run XK256 LOQA_XATTN_SPLIT_KEYS=256
-run XK512 LOQA_XATTN_SPLIT_KEYS=512
-run XK768 LOQA_XATTN_SPLIT_KEYS=768
+
+
+
+
+run LK128 LOQA_LLM_ATTN_SPLIT_KEYS=128
+run LK256 LOQA_LLM_ATTN_SPLIT_KEYS=256
+run LK512 LOQA_LLM_ATTN_SPLIT_KEYS=512
+run LK128b LOQA_LLM_ATTN_SPLIT_KEYS=128

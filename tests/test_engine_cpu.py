@@ -379,6 +379,28 @@ def test_stt_continuous_batching_matches_batch_cpu():
     assert sorted(eng._free_slots) == list(range(4))
 
 
+def test_stt_oversize_batch_is_chunked_cpu():
+    """A batch larger than the engine's slot count is admitted in max_batch
+    chunks (it would otherwise never find enough free slots)."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    cfg = whisper_config("test-whisper")
+    utts = make_batch(7, 5, [1, 2, 1, 1, 2])
+    ref = STTEngine(cfg, torch.device("cpu"), seed=2, max_batch=8)
+    solo = [STTRequest(u.pcm, max_new_tokens=4) for u in utts]
+    ref.transcribe(solo)
+    eng = STTEngine(cfg, torch.device("cpu"), seed=2, max_batch=2)
+    reqs = [STTRequest(u.pcm, max_new_tokens=4) for u in utts]
+    done = []
+    out = eng.submit_batch(reqs, lambda r: done.append(r)).result(timeout=120)
+    eng.stop()
+    assert out == reqs and len(done) == 5
+    for got, want in zip(reqs, solo):
+        assert got.tokens == want.tokens
+    assert sorted(eng._free_slots) == [0, 1]
+
+
 def test_pipeline_continuous_stt_cpu():
     """Pipeline with continuous STT + continuous LLM on the CPU: every utterance
     gets its own reply with the expected command count."""
