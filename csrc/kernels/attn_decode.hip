@@ -68,6 +68,19 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
   const int h = lane >> 5, r = lane & 31;
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int G = Hq / Hkv;
+  const bool paged = block_tables != nullptr;
+  const int* bt = paged ? block_tables + (size_t)b * max_blocks : nullptr;
+  // the first tile's block-table entries do not depend on the context length:
+  // request them (clamped in-row) together with the sequence metadata below,
+  // so the first K/V loads wait for one scalar round trip instead of two
+  int nbt0 = 0, nbt1 = 0;
+  {
+    const int bi = min((split * split_keys + wave * DEC_TILE) / blk, max_blocks - 1);
+    if (paged) {
+      nbt0 = bt[bi];
+      nbt1 = bt[min(bi + 1, max_blocks - 1)];
+    }
+  }
   const int q0 = cu_q[b], qlen = cu_q[b + 1] - q0;
   const int klen = ctx_lens[b];
   const int qi = r / G;
@@ -81,8 +94,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
   // sized for the longest context a captured graph can see, so most of these
   // workgroups would otherwise occupy a CU for a full pass.
   if (split > 0 && kbeg >= klen) return;
-  const bool paged = block_tables != nullptr;
-  const int* bt = paged ? block_tables + (size_t)b * max_blocks : nullptr;
   const size_t kv0 = paged ? 0 : (size_t)kv_start[b];
 
   bf16x8 qf[NS];
@@ -102,12 +113,18 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
   float m_run = -1e30f, l_run = 0.f;
 
   // the tile's (at most two) cache blocks: wave-uniform scalar lookups
+  // nbt0 / nbt1 hold the block-table entries of tile kt on entry; the next
+  // tile's (kt + 4 * 32) are requested before this tile's K / V so the lookup
+  // is off the loop's dependent chain
   auto load_tile = [&](int kt, uint4 (&kraw)[NS], uint4 (&vraw)[VPL]) {
     int base0 = 0, base1 = 0, bi0 = 0;
     if (paged) {
       bi0 = kt / blk;
-      base0 = bt[bi0];
-      base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? bt[bi0 + 1] : base0;
+      base0 = nbt0;
+      base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? nbt1 : base0;
+      const int bn = min((kt + DEC_WAVES * DEC_TILE) / blk, max_blocks - 1);
+      nbt0 = bt[bn];
+      nbt1 = bt[min(bn + 1, max_blocks - 1)];
     }
     auto row_off = [&](int key) -> size_t {
       if (paged) {
@@ -326,6 +343,20 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
         part_o, 0, (int)((size_t)num_splits * total_q * Hq * D * 4), 0x00020000);
     const auto rm = __builtin_amdgcn_make_buffer_rsrc(
         part_ml, 0, (int)((size_t)num_splits * total_q * Hq * 2 * 4), 0x00020000);
+    // the first batch of partials is requested together with the (m, l)
+    // pairs: one L2 round trip before the first accumulate, not two
+    auto load_o = [&](int sp0, float4v (&v)[OB][NV]) {
+#pragma unroll
+      for (int i = 0; i < OB; ++i) {
+        const int sp = sp0 + i < nsplit ? sp0 + i : 0;
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          v[i][k] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    ro, ((sp * total_q * Hq + row) * D + c0 + 4 * k) * 4, 0, 16));
+      }
+    };
+    float4v v[OB][NV];
+    load_o(0, v);
     float msx = -1e30f;
     float2 mlr[MLB];
     for (int sp0 = 0; sp0 < nsplit; sp0 += MLB) {
@@ -344,15 +375,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     for (int c = 0; c < CW; ++c) o[c] = 0.f;
     float L = 0.f;
     for (int sp0 = 0; sp0 < nsplit; sp0 += OB) {
-      float4v v[OB][NV];
-#pragma unroll
-      for (int i = 0; i < OB; ++i) {
-        const int sp = sp0 + i < nsplit ? sp0 + i : 0;
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
-          v[i][k] = __builtin_bit_cast(float4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    ro, ((sp * total_q * Hq + row) * D + c0 + 4 * k) * 4, 0, 16));
-      }
+      if (sp0 > 0) load_o(sp0, v);
 #pragma unroll
       for (int i = 0; i < OB; ++i) {
         const int sp = sp0 + i;
