@@ -480,8 +480,15 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     # latency-bound kernels wait for it to drain (measured: a 768-workgroup
     # qkv GEMM, fastest in isolation, slowed the concurrent Whisper decoder 5x
     # and the whole pipeline 1.8x). Keep at most one workgroup per CU.
-    capped = [c for c in cands if (N // (16 * c[1] * c[2])) * c[0] <= _CAP[0]]
-    cands = capped or cands[:1]
+    units = {c: (N // (16 * c[1] * c[2])) * c[0] for c in cands}
+    capped = [c for c in cands if units[c] <= _CAP[0]]
+    if not capped:
+        # a GEMM too large for any layout under the cap (Llama-3-70B gate|up:
+        # >= 448 workgroups) takes the fewest-workgroup layouts (measured cold,
+        # 70B gate|up: 448 WGs 154 us vs 3584 WGs 169 us)
+        least = min(units.values())
+        capped = [c for c in cands if units[c] <= max(_CAP[0], 2 * least)]
+    cands = capped
     best, best_t = (1, rts[-1], 1), float("inf")
     n = max(1, ncopies)
     for c in cands:

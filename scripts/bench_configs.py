@@ -33,6 +33,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from loqa_hub_amd import ops  # noqa: E402
 from loqa_hub_amd.engine.llm_engine import LLMEngine  # noqa: E402
 from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline, added_command_stats  # noqa: E402
 from loqa_hub_amd.engine.stt_engine import STTEngine  # noqa: E402
@@ -110,6 +111,7 @@ def config_2_or_5(cfg_id: int, args, dev, nats) -> dict:
         "tts_ms_mean": round(float(np.mean(tts_s)) * 1e3, 1) if tts_s else None,
         "command_count_match": float(np.mean([j.n_commands == j.n_expected for j in jobs])),
         "init_s": round(init_s, 1),
+        "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v) for k, v in ops._FSPLITS.items()},
         "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT)",
     }
 

@@ -238,6 +238,55 @@ def fused_bench():
         del wps
 
 
+def fused70_bench():
+    """Llama-3-70B decode GEMM shapes (d 8192, ffn 28672, 64/8 heads) on the
+    fused kernel, every (split, tile rows, waves-along-rows) layout, cold
+    weights (copies cycled); ``units`` = workgroups before the co-scheduling cap."""
+    scr = ops.FusedScratch(dev)
+    M, d, H, Hkv, D, blk = 16, 8192, 64, 8, 128, 16
+    pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
+    cs = torch.randn(4096, D // 2, 2, device=dev)
+    kc = torch.zeros(64, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slots = torch.arange(M, dtype=torch.int32, device=dev)
+    q = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
+    rows = d // 32
+    for name, (N, K), mode in (("qkv", (10240, 8192), "rope"), ("o", (8192, 8192), "resid"),
+                               ("gate_up", (57344, 8192), "silu"), ("down", (8192, 28672), "resid")):
+        ncopy = max(2, -(-(3 << 30) // (N * K * 2)))
+        base = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+        wps = [ops.shuffle_weight(base) for _ in range(ncopy)]
+        del base
+        xx = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        res_ = torch.randn(M, N if mode == "resid" else d, device=dev, dtype=torch.bfloat16)
+        scr.rowsq[: rows * M].fill_(float(K) / rows)
+        gb = N * K * 2 / 1e9
+        res = {"kernel": "graph_fused_cold_70b", "shape": name, "mode": mode, "GB": round(gb, 3)}
+        for S in (1, 2, 4):
+            for rt in (1, 2):
+                for wr in (1, 4):
+                    if K % (S * 128) or (wr == 4 and S != 1) or N % (16 * rt * wr):
+                        continue
+                    kw = dict(splits=S, rt=rt, wr=wr)
+                    if mode == "rope":
+                        kw.update(norm=True, rowsq_tiles=rows, positions=pos, cos_sin=cs, q_out=q,
+                                  k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv,
+                                  head_dim=D)
+                    elif mode == "silu":
+                        kw.update(norm=True, rowsq_tiles=rows)
+                    else:
+                        kw.update(residual=res_)
+                    it = iter(range(1 << 30))
+
+                    def fused():
+                        ops.skinny_fused(xx, wps[next(it) % ncopy], mode, scr, **kw)
+                    t = gtime(fused, inner=2 * ncopy)
+                    units = (N // (16 * rt * wr)) * S
+                    res[f"S{S}rt{rt}wr{wr}_u{units}"] = [round(t, 2), round(gb / t * 1e3, 2)]
+        emit(**res)
+        del wps
+
+
 def stream_bench():
     """HBM read roofline of this box: torch sum over a 2 GB bf16 buffer."""
     buf = torch.ones(1 << 30, device=dev, dtype=torch.bfloat16)
@@ -267,6 +316,8 @@ if __name__ == "__main__":
         tiny_bench()
     if "fused" in which:
         fused_bench()
+    if "fused70" in which:
+        fused70_bench()
     if "stream" in which:
         stream_bench()
     if "gemm" in which:

@@ -1,6 +1,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "attention" > gpurun_out/attn_tests.log 2>&1 || { tail -30 gpurun_out/attn_tests.log; exit 1; }
-tail -2 gpurun_out/attn_tests.log
-timeout -k 10 300 python scripts/exp/attn_bench.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/attn_bench.log
+timeout -k 10 900 python scripts/bench_configs.py --config 5 --per-stream 2 > gpurun_out/cfg5b.log 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/cfg5b.log | tail -3 | cut -c1-2500
+exit $rc
