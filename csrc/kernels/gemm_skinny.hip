@@ -272,8 +272,8 @@ struct FusedParams {
   void* residual; float* rowsq_out; float* rowsum_out;
   const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
   int H, Hkv, D, blk;
-  int rt;                 // output tile rows / 16 (1: residual / act modes only)
-  int wr;                 // waves along the rows (1, or 4 at Mpad <= 32 with S == 1)
+  int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
+  int wr;                 // waves along the rows (1, or 4 with S == 1)
 };
 
 struct FusedArgs {
@@ -715,16 +715,24 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
     case 32:
       if (wr == 4) return launch_fused<RT, 2, 4, MODE, NORM>(a, st);
       return launch_fused<RT, 2, 1, MODE, NORM>(a, st);
-    default: return launch_fused<RT, 4, 1, MODE, NORM>(a, st);
+    default:
+      if (wr == 4) return launch_fused<RT, 4, 4, MODE, NORM>(a, st);
+      return launch_fused<RT, 4, 1, MODE, NORM>(a, st);
   }
 }
 
 // rt: rows per output tile / 16 (1 or 2, every mode: the paired epilogues pair
 // rows inside each 16-row tile through a lane shuffle, so 16-row tiles give
 // twice the workgroups without a K split, i.e. without a reduction tail).
-// wr: waves along the rows (1 or 4; 4 only at Mpad <= 32 with S == 1).
+// wr: waves along the rows (1 or 4; 4 only with S == 1).
 template <int MODE, int NORM>
 static int dispatch_fused(const FusedArgs& a, int rt, int wr, hipStream_t st) {
+  // 64-row tiles at Mpad 64 (chunked prefill through the compact weights):
+  // the activation tile is then re-read from L2 by half as many workgroups
+  if (rt == 4) {
+    if (wr == 4) return launch_fused<4, 4, 4, MODE, NORM>(a, st);
+    return launch_fused<4, 4, 1, MODE, NORM>(a, st);
+  }
   if (rt == 1) return dispatch_mt<1, MODE, NORM>(a, wr, st);
   return dispatch_mt<2, MODE, NORM>(a, wr, st);
 }
@@ -757,9 +765,9 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if ((p->mode == EPI_SILU || p->mode == EPI_ACT) && (!p->out || p->ldo % 4))
     return (int)hipErrorInvalidValue;
-  if (p->rt != 1 && p->rt != 2) return (int)hipErrorInvalidValue;
+  if (p->rt != 1 && p->rt != 2 && !(p->rt == 4 && Mpad == 64)) return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
-  if (p->wr != 1 && (p->wr != 4 || Mpad > 32 || S != 1 || N % (64 * p->rt)))
+  if (p->wr != 1 && (p->wr != 4 || S != 1 || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
               p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,

@@ -194,11 +194,12 @@ class LlamaWeights:
     def _tune_fused(self) -> None:
         """Measure the split-K of each fused decode GEMM shape (layer-0 weights)."""
         P, D = self.decode_layers[0], self.cfg.head_dim
+        pf = bool(getattr(self, "compact", False))
         ops.tune_fused(P["wqkv_f"], "rope", norm="rms", heads=(self.h, self.hkv, D),
-                       cos_sin=self.cos_sin)
-        ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms")
-        ops.tune_fused(P["wo"], "resid")
-        ops.tune_fused(P["w_down"], "resid")
+                       cos_sin=self.cos_sin, prefill=pf)
+        ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms", prefill=pf)
+        ops.tune_fused(P["wo"], "resid", prefill=pf)
+        ops.tune_fused(P["w_down"], "resid", prefill=pf)
 
     @classmethod
     def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":

@@ -454,7 +454,7 @@ class contended_tuning:
 
 
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
-                      wr4: bool = False) -> tuple[int, int, int]:
+                      wr4: bool = False, fewest: bool = True) -> tuple[int, int, int]:
     """(split-K, tile rows / 16, waves along rows) for a fused-epilogue GEMM,
     measured: ``run(s, rt, wr, i)`` launches it on weight copy ``i`` (the graph
     cycles through ``ncopies`` copies so every call streams COLD weights, as a
@@ -482,12 +482,18 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     # and the whole pipeline 1.8x). Keep at most one workgroup per CU.
     units = {c: (N // (16 * c[1] * c[2])) * c[0] for c in cands}
     capped = [c for c in cands if units[c] <= _CAP[0]]
-    if not capped:
+    if not capped and fewest:
         # a GEMM too large for any layout under the cap (Llama-3-70B gate|up:
         # >= 448 workgroups) takes the fewest-workgroup layouts (measured cold,
         # 70B gate|up: 448 WGs 154 us vs 3584 WGs 169 us)
         least = min(units.values())
         capped = [c for c in cands if units[c] <= max(_CAP[0], 2 * least)]
+    elif not capped:
+        # Llama-3-8B gate|up at Mpad 64 (jump-forward decode steps beside the
+        # Whisper decoder): the short-lived 16-row tiles. Measured in the
+        # pipeline: 18.9 utt/s, vs 17.2 for 896 longer 32-row workgroups
+        # (fastest alone) and 11.0 for 224 4-wave 32-row workgroups.
+        capped = cands[:1]
     cands = capped
     best, best_t = (1, rts[-1], 1), float("inf")
     n = max(1, ncopies)
@@ -942,9 +948,14 @@ class FusedLinear:
 
 
 def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none",
-               heads: tuple | None = None, cos_sin=None) -> None:
+               heads: tuple | None = None, cos_sin=None, prefill: bool = False) -> None:
     """Measure the split-K of one fused decode GEMM shape on dummy operands
-    (``heads`` = (H, Hkv, D) for "rope"); before any graph capture."""
+    (``heads`` = (H, Hkv, D) for "rope"); before any graph capture.
+    ``prefill``: Mpad 64 is the chunked prefill of compact weights (a whole
+    weight pass per 64 tokens, on its own stream): 64-row tiles and 4 waves
+    along rows are then candidates too (70B gate|up 64 tokens: 204 us vs 483 us
+    for 16-row tiles). Otherwise Mpad 64 is a decode step beside the Whisper
+    decoder, where those long-lived workgroups slow the pipeline."""
     lin = wp if isinstance(wp, FusedLinear) else None
     w = lin.wp if lin is not None else wp
     if not _gpu(w):
@@ -985,10 +996,11 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
             kw.update(positions=pos, cos_sin=cos_sin, q_out=torch.empty(Mpad, H * D, **bf),
                       k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
                       head_dim=D)
-        rts = (1, 2)
+        wide = Mpad <= 32 or prefill
+        rts = (1, 2, 4) if (prefill and Mpad == 64) else (1, 2)
         tune_fused_splits(key, lambda sp, rt, wr, i: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, **kw), K, rts=rts,
-            ncopies=len(copies), wr4=Mpad <= 32)
+            ncopies=len(copies), wr4=wide, fewest=wide)
     del copies
 
 
@@ -1031,7 +1043,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     rt = rt or (tuned[1] if tuned else 2)
     if wr is None:
         wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
-    if wr != 1 and (S != 1 or Mpad > 32 or N % (64 * rt)):
+    if wr != 1 and (S != 1 or N % (64 * rt)):
         wr = 1
     if rowsq_tiles is None:
         rowsq_tiles = scratch.stat_tiles

@@ -242,8 +242,9 @@ def fused70_bench():
     """Llama-3-70B decode GEMM shapes (d 8192, ffn 28672, 64/8 heads) on the
     fused kernel, every (split, tile rows, waves-along-rows) layout, cold
     weights (copies cycled); ``units`` = workgroups before the co-scheduling cap."""
+    M = int(os.environ.get("KB_M", "16"))
     scr = ops.FusedScratch(dev)
-    M, d, H, Hkv, D, blk = 16, 8192, 64, 8, 128, 16
+    d, H, Hkv, D, blk = 8192, 64, 8, 128, 16
     pos = torch.arange(M, dtype=torch.int32, device=dev) + 100
     cs = torch.randn(4096, D // 2, 2, device=dev)
     kc = torch.zeros(64, Hkv, blk, D, device=dev, dtype=torch.bfloat16)
@@ -261,9 +262,9 @@ def fused70_bench():
         res_ = torch.randn(M, N if mode == "resid" else d, device=dev, dtype=torch.bfloat16)
         scr.rowsq[: rows * M].fill_(float(K) / rows)
         gb = N * K * 2 / 1e9
-        res = {"kernel": "graph_fused_cold_70b", "shape": name, "mode": mode, "GB": round(gb, 3)}
+        res = {"kernel": "graph_fused_cold_70b", "M": M, "shape": name, "mode": mode, "GB": round(gb, 3)}
         for S in (1, 2, 4):
-            for rt in (1, 2):
+            for rt in ((1, 2, 4) if M == 64 else (1, 2)):
                 for wr in (1, 4):
                     if K % (S * 128) or (wr == 4 and S != 1) or N % (16 * rt * wr):
                         continue

@@ -111,8 +111,7 @@ def test_fused_resid_rowsq_and_silu_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
-@pytest.mark.parametrize("Mpad", [16, 32])
-@pytest.mark.parametrize("rt", [1, 2])
+@pytest.mark.parametrize("Mpad,rt", [(16, 1), (16, 2), (32, 1), (32, 2), (64, 1), (64, 2), (64, 4)])
 def test_fused_rows_per_wave_layout_gpu(mode, Mpad, rt):
     """Every (rt, wr) layout of the fused GEMM against the fp32 CPU reference of
     the same call: 16-row pair tiles (SwiGLU / RoPE partners exchanged across
