@@ -64,7 +64,10 @@ def start_broker() -> tuple[int, threading.Thread]:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    # 8 utterances per stream: a whole number of passes over the 4-way command
+    # mix for every stream (5 ends on an unbalanced tail: measured 17.4-17.5
+    # vs 18.7-18.9 utt/s at 4, 8 and 12)
+    ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch-per-gpu", type=int, default=8)
     ap.add_argument("--stt", default="whisper-large-v3")

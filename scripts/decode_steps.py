@@ -7,7 +7,7 @@ import statistics as st
 import sys
 
 
-def main(path, key="skinny_fused_kernel<2, 1, 4, 1, 1>"):
+def main(path, key="skinny_fused_kernel<2, 1, 4, 4, 1, 1>"):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
