@@ -6,7 +6,7 @@ run() {
   env "$@" timeout -k 10 300 python bench.py --steps 8 --warmup 2 > gpurun_out/bench_$name.log 2>&1 || { tail -20 gpurun_out/bench_$name.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/bench_$name.log | tail -1 | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print("'$name'", d["value"], d["ms_per_added_command_e2e_marginal"], d["phase_ms_per_step"]["stt"], d["llm_stats"]["gpu_wait_s"]/d["llm_stats"]["decode_steps"], d["stt_stats"]["gpu_wait_s"]/d["stt_stats"]["decode_steps"])'
 }
-run Q1 "LOQA_FSPLIT_OVERRIDE=rope:6144x4096:M16=1,1,1;rope:6144x4096:M32=1,1,1"
-run Q2 "LOQA_FSPLIT_OVERRIDE=rope:6144x4096:M16=2,2,1;rope:6144x4096:M32=2,2,1"
-run O2 "LOQA_FSPLIT_OVERRIDE=resid:4096x4096:M16=2,1,1"
+run HWQ1 GPU_MAX_HW_QUEUES=1
+run HWQ2 GPU_MAX_HW_QUEUES=2
 run BASE X=1
+run HWQ3 GPU_MAX_HW_QUEUES=3
