@@ -72,7 +72,24 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int h = lane >> 5;
-  const int b = blockIdx.z;
+  // XCD-aware order (prefill / encoder grids of hundreds to thousands of
+  // workgroups): the dispatcher deals consecutive ids round-robin over the 8
+  // XCDs, each with its own L2. Remap so each XCD gets a CONTIGUOUS run of
+  // logical (q-tile, head, sequence) ids: the q-tiles of one head, which all
+  // read that head's K/V, then share one L2 instead of filling eight.
+  // Bijective for any grid size (guide T1).
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (!GROUPED) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * gridDim.z;
+    const int lin = bx + gx * (by + gy * bz);
+    const int xcd = lin & 7, qn = n >> 3, rn = n & 7;
+    const int logical = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (lin >> 3);
+    bx = logical % gx;
+    by = (logical / gx) % gy;
+    bz = logical / (gx * gy);
+  }
+  const int b = bz;
   const int q0 = p.cu_q[b];
   const int qlen = p.cu_q[b + 1] - q0;
   int k0 = 0, klen;
@@ -90,16 +107,16 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
   int qi, head, kvh;
   int row_lo, row_hi;  // token range covered by the workgroup (for causal bound)
   if (GROUPED) {
-    kvh = blockIdx.y;
+    kvh = by;
     qi = r / G;
     head = kvh * G + (r - qi * G);
     row_lo = 0;
     row_hi = min(qlen, (ATT_WAVES * 32) / G) - 1;
   } else {
-    head = blockIdx.y;
+    head = by;
     kvh = head / G;
-    qi = blockIdx.x * (ATT_WAVES * 32) + r;
-    row_lo = blockIdx.x * (ATT_WAVES * 32);
+    qi = bx * (ATT_WAVES * 32) + r;
+    row_lo = bx * (ATT_WAVES * 32);
     row_hi = min(qlen - 1, row_lo + ATT_WAVES * 32 - 1);
   }
   if (!GROUPED && row_lo >= qlen) return;
@@ -111,7 +128,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
   int kbeg = 0, kend = klen;
   int split = 0;
   if (GROUPED) {
-    split = blockIdx.x;
+    split = bx;
     kbeg = split * p.split_keys;
     kend = min(klen, kbeg + p.split_keys);
   }

@@ -1,12 +1,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-run() {
-  name=$1; shift
-  env "$@" timeout -k 10 300 python bench.py --steps 8 --warmup 2 > gpurun_out/bench_$name.log 2>&1 || { tail -20 gpurun_out/bench_$name.log; exit 1; }
-  grep -v amdgpu.ids gpurun_out/bench_$name.log | tail -1 | python -c 'import sys,json; d=json.loads(sys.stdin.read()); print("'$name'", d["value"], d["ms_per_added_command_e2e_marginal"], d["phase_ms_per_step"]["stt"], d["llm_stats"]["gpu_wait_s"]/d["llm_stats"]["decode_steps"], d["stt_stats"]["gpu_wait_s"]/d["stt_stats"]["decode_steps"])'
-}
-run HWQ1 GPU_MAX_HW_QUEUES=1
-run HWQ2 GPU_MAX_HW_QUEUES=2
-run BASE X=1
-run HWQ3 GPU_MAX_HW_QUEUES=3
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "attention or attn" > gpurun_out/attn_tests.log 2>&1 || { tail -30 gpurun_out/attn_tests.log; exit 1; }
+tail -1 gpurun_out/attn_tests.log
+(cd ab_head && timeout -k 10 200 python ../scripts/exp/attn_fwd_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/OLD /')
+timeout -k 10 200 python scripts/exp/attn_fwd_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/NEW /'
