@@ -3,5 +3,5 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "attention or attn" > gpurun_out/attn_tests.log 2>&1 || { tail -30 gpurun_out/attn_tests.log; exit 1; }
 tail -1 gpurun_out/attn_tests.log
-(cd ab_head && timeout -k 10 200 python ../scripts/exp/attn_fwd_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/OLD /')
+(cd ab2 && timeout -k 10 200 python ../scripts/exp/attn_fwd_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/OLD /')
 timeout -k 10 200 python scripts/exp/attn_fwd_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/NEW /'
