@@ -64,8 +64,8 @@ __device__ __forceinline__ float16v mfma32(const bf16x8& a, const bf16x8& b, con
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int D, bool PAGED, bool GROUPED>
-__global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
+template <int D, bool PAGED, bool GROUPED, int QR>
+__global__ __launch_bounds__(ATT_THREADS, QR == 2 ? 2 : 1) void attn_fwd_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) AttnSmem<D> sm;
   constexpr int NS = D / 16;  // k-slices of the QK^T product
   constexpr int NDT = D / 32; // 32-wide d tiles of O^T
@@ -102,27 +102,34 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
   }
   const int G = p.Hq / p.Hkv;
 
-  // ---- row mapping: this lane's query row (token index within seq, head)
-  const int r = wave * 32 + (lane & 31);
-  int qi, head, kvh;
+  // ---- row mapping: this lane's query rows (token index within seq, head).
+  // Prefill at D = 64 gives each wave QR = 2 groups of 32 query rows: every K /
+  // V fragment read from LDS then feeds two MFMAs (the D = 64 kernel is bound
+  // by LDS read volume per wave, not by MFMA issue).
+  constexpr int RPW = 32 * QR;                // query rows per wave
+  int qi[QR], head, kvh;
   int row_lo, row_hi;  // token range covered by the workgroup (for causal bound)
+  bool row_valid[QR];
   if (GROUPED) {
+    const int r = wave * 32 + (lane & 31);
     kvh = by;
-    qi = r / G;
-    head = kvh * G + (r - qi * G);
+    qi[0] = r / G;
+    head = kvh * G + (r - qi[0] * G);
     row_lo = 0;
     row_hi = min(qlen, (ATT_WAVES * 32) / G) - 1;
+    row_valid[0] = qi[0] < qlen && (ATT_WAVES * 32) / G > 0 && r < (ATT_WAVES * 32 / G) * G;
   } else {
     head = by;
     kvh = head / G;
-    qi = bx * (ATT_WAVES * 32) + r;
-    row_lo = bx * (ATT_WAVES * 32);
-    row_hi = min(qlen - 1, row_lo + ATT_WAVES * 32 - 1);
+    row_lo = bx * (ATT_WAVES * RPW);
+    row_hi = min(qlen - 1, row_lo + ATT_WAVES * RPW - 1);
+#pragma unroll
+    for (int qh = 0; qh < QR; ++qh) {
+      qi[qh] = row_lo + wave * RPW + qh * 32 + (lane & 31);
+      row_valid[qh] = qi[qh] < qlen;
+    }
   }
   if (!GROUPED && row_lo >= qlen) return;
-  const bool row_valid = GROUPED ? (qi < qlen && (ATT_WAVES * 32) / G > 0 && r < (ATT_WAVES * 32 / G) * G)
-                                 : (qi < qlen);
-  const int qpos = klen - qlen + qi;  // absolute position for causal masking
 
   // ---- key range of this workgroup
   int kbeg = 0, kend = klen;
@@ -135,22 +142,28 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
   if (p.causal) kend = min(kend, klen - qlen + row_hi + 1);
 
   // ---- Q^T fragments (B operand): lane (query, h) holds Q[q][16s + 8h .. +7]
-  bf16x8 qf[NS];
-  {
-    const bf16_t* qrow = p.q + (size_t)(q0 + (row_valid ? qi : 0)) * p.q_stride + (size_t)head * D;
+  bf16x8 qf[QR][NS];
+#pragma unroll
+  for (int qh = 0; qh < QR; ++qh) {
+    const bf16_t* qrow = p.q + (size_t)(q0 + (row_valid[qh] ? qi[qh] : 0)) * p.q_stride + (size_t)head * D;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      uint4 v = row_valid ? *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
-      qf[s] = *reinterpret_cast<bf16x8*>(&v);
+      uint4 v = row_valid[qh] ? *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      qf[qh][s] = *reinterpret_cast<bf16x8*>(&v);
     }
   }
 
-  float16v acc[NDT];
+  float16v acc[QR][NDT];
+  float m_run[QR], l_run[QR];
 #pragma unroll
-  for (int i = 0; i < NDT; ++i)
+  for (int qh = 0; qh < QR; ++qh) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
-  float m_run = -1e30f, l_run = 0.f;
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[qh][i][j] = 0.f;
+    m_run[qh] = -1e30f;
+    l_run[qh] = 0.f;
+  }
 
   const int* btab = PAGED ? p.block_tables + (size_t)b * p.max_blocks : nullptr;
   constexpr int CH = D / 8;  // 16-byte chunks per row
@@ -179,54 +192,61 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
     }
     __syncthreads();
 
-    // ---- S^T = K Q^T for the two 32-key halves
-    float16v st[2];
+    // ---- S^T = K Q^T for the two 32-key halves (each K fragment feeds QR MFMAs)
+    float16v st[QR][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) st[t][j] = 0.f;
+      for (int qh = 0; qh < QR; ++qh)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) st[qh][t][j] = 0.f;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sm.k[32 * t + (lane & 31)][16 * s + 8 * h]);
-        st[t] = mfma32(a, qf[s], st[t]);
+#pragma unroll
+        for (int qh = 0; qh < QR; ++qh) st[qh][t] = mfma32(a, qf[qh][s], st[qh][t]);
       }
     }
     // ---- mask + online softmax (row = this lane's query)
-    float mx = -INFINITY;
+    bf16x8 pf[QR][2][2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int qh = 0; qh < QR; ++qh) {
+      const int qpos = klen - qlen + qi[qh];  // absolute position for causal masking
+      float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int key = kt + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * h;
-        float sv = st[t][j] * p.scale_log2;
-        if (key >= kend || (p.causal && key > qpos)) sv = -INFINITY;
-        st[t][j] = sv;
-        mx = fmaxf(mx, sv);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
-    float ls = 0.f;
-    bf16x8 pf[2][2];
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float e = exp2f(st[t][8 * s2 + j] - m_new);
-          ls += e;
-          pf[t][s2][j] = (__bf16)e;
+        for (int j = 0; j < 16; ++j) {
+          const int key = kt + 32 * t + (j & 3) + 8 * (j >> 2) + 4 * h;
+          float sv = st[qh][t][j] * p.scale_log2;
+          if (key >= kend || (p.causal && key > qpos)) sv = -INFINITY;
+          st[qh][t][j] = sv;
+          mx = fmaxf(mx, sv);
         }
-    ls += __shfl_xor(ls, 32, 64);
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[qh], mx);
+      const float alpha = exp2f(m_run[qh] - m_new);
+      float ls = 0.f;
 #pragma unroll
-    for (int i = 0; i < NDT; ++i)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = exp2f(st[qh][t][8 * s2 + j] - m_new);
+            ls += e;
+            pf[qh][t][s2][j] = (__bf16)e;
+          }
+      ls += __shfl_xor(ls, 32, 64);
+      l_run[qh] = l_run[qh] * alpha + ls;
+      m_run[qh] = m_new;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[qh][i][j] *= alpha;
+    }
 
-    // ---- O^T += V^T P^T
+    // ---- O^T += V^T P^T (each V^T fragment feeds QR MFMAs)
     const int g = lane >> 4, li = lane & 15;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
@@ -243,43 +263,48 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnParams p) {
           short8 a8;
           a8[0] = lo[0]; a8[1] = lo[1]; a8[2] = lo[2]; a8[3] = lo[3];
           a8[4] = hi[0]; a8[5] = hi[1]; a8[6] = hi[2]; a8[7] = hi[3];
-          acc[dt] = mfma32(*reinterpret_cast<bf16x8*>(&a8), pf[t][s2], acc[dt]);
+#pragma unroll
+          for (int qh = 0; qh < QR; ++qh)
+            acc[qh][dt] = mfma32(*reinterpret_cast<bf16x8*>(&a8), pf[qh][t][s2], acc[qh][dt]);
         }
     }
   }
 
-  if (!row_valid) return;
-  const size_t tok = (size_t)(q0 + qi);
-  if (GROUPED && p.num_splits > 1) {
-    // unnormalised partial result + (m, l) for the combine kernel
-    float* po = p.part_o + (((size_t)split * p.total_q + tok) * p.Hq + head) * D;
+#pragma unroll
+  for (int qh = 0; qh < QR; ++qh) {
+    if (!row_valid[qh]) continue;
+    const size_t tok = (size_t)(q0 + qi[qh]);
+    if (GROUPED && p.num_splits > 1) {
+      // unnormalised partial result + (m, l) for the combine kernel
+      float* po = p.part_o + (((size_t)split * p.total_q + tok) * p.Hq + head) * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(po + d0) = make_float4(acc[qh][dt][4 * g4], acc[qh][dt][4 * g4 + 1],
+                                                            acc[qh][dt][4 * g4 + 2], acc[qh][dt][4 * g4 + 3]);
+        }
+      if (h == 0) {
+        float* pm = p.part_ml + (((size_t)split * p.total_q + tok) * p.Hq + head) * 2;
+        pm[0] = m_run[qh];
+        pm[1] = l_run[qh];
+      }
+      continue;
+    }
+    const float inv = l_run[qh] > 0.f ? 1.f / l_run[qh] : 0.f;
+    bf16_t* orow = p.o + tok * p.o_stride + (size_t)head * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int d0 = 32 * dt + 8 * g4 + 4 * h;
-        *reinterpret_cast<float4*>(po + d0) =
-            make_float4(acc[dt][4 * g4], acc[dt][4 * g4 + 1], acc[dt][4 * g4 + 2], acc[dt][4 * g4 + 3]);
+        uint2 w;
+        w.x = pack_bf16x2(acc[qh][dt][4 * g4] * inv, acc[qh][dt][4 * g4 + 1] * inv);
+        w.y = pack_bf16x2(acc[qh][dt][4 * g4 + 2] * inv, acc[qh][dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d0) = w;
       }
-    if (h == 0) {
-      float* pm = p.part_ml + (((size_t)split * p.total_q + tok) * p.Hq + head) * 2;
-      pm[0] = m_run;
-      pm[1] = l_run;
-    }
-    return;
   }
-  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  bf16_t* orow = p.o + tok * p.o_stride + (size_t)head * D;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d0 = 32 * dt + 8 * g4 + 4 * h;
-      uint2 w;
-      w.x = pack_bf16x2(acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv);
-      w.y = pack_bf16x2(acc[dt][4 * g4 + 2] * inv, acc[dt][4 * g4 + 3] * inv);
-      *reinterpret_cast<uint2*>(orow + d0) = w;
-    }
 }
 
 // Combine split-K partials: one workgroup of D threads per (token, head).
@@ -304,11 +329,13 @@ __global__ void attn_combine_kernel(const float* __restrict__ part_o,
 template <int D, bool PAGED, bool GROUPED>
 static int launch_attn(const AttnParams& p, int B, int max_q, hipStream_t s) {
   dim3 grid;
+  // QR = 2 (64 query rows per wave) where it pays: D = 64 prefill / encoder
+  constexpr int QR = (!GROUPED && D == 64) ? 2 : 1;
   if (GROUPED)
     grid = dim3(p.num_splits, p.Hkv, B);
   else
-    grid = dim3((max_q + ATT_WAVES * 32 - 1) / (ATT_WAVES * 32), p.Hq, B);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, PAGED, GROUPED>), grid, dim3(ATT_THREADS), 0, s, p);
+    grid = dim3((max_q + ATT_WAVES * 32 * QR - 1) / (ATT_WAVES * 32 * QR), p.Hq, B);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, PAGED, GROUPED, QR>), grid, dim3(ATT_THREADS), 0, s, p);
   return (int)hipGetLastError();
 }
 
