@@ -225,7 +225,14 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(
     // current tile past the end) so no join point drains it (see stream_k).
     // Measured on the Whisper cross-attention (1500 keys, 3-12 splits): no
     // gain at 512-key splits and a loss at shorter ones (183 vs 120 VGPRs
-    // halves occupancy), so both head dims launch PF = 0.
+    // halves occupancy), so both head dims launch PF = 0. (The ISA shows why
+    // it cannot gain as written: the per-lane predicated loads and the
+    // run-time paged / contiguous branch put every consumer behind a join,
+    // so the waitcnt pass drains the prefetch - only vmcnt(0) waits. A
+    // version with clamped unconditional loads, a compile-time PAGED flag and
+    // a peeled ping-pong got partial waits but measured 10-60% slower: the
+    // allocator then recycles the in-flight buffers' registers as MFMA
+    // destinations, which forces early waits.)
     uint4 ka[NS], va[VPL], kb[NS], vb[VPL];
     if (kt < kend) load_tile(kt, ka, va);
     while (kt < kend) {

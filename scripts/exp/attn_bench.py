@@ -5,7 +5,7 @@ LLM: Llama-3-8B shapes (Hkv 8, G 4, D 128, paged blk 16), B sequences at ctx.
 STT: Whisper-large-v3 cross-attention (H 20, D 64, 1500 contiguous rows)."""
 import json, os, sys
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.getcwd())
 from loqa_hub_amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
