@@ -114,8 +114,11 @@ def test_attention_prefill_contiguous(D, H, Hkv, causal):
 
 
 @pytest.mark.parametrize("G", [1, 4])
-def test_attention_prefill_paged_with_prefix(G):
-    D, Hkv = 128, 2
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_prefill_paged_with_prefix(G, D):
+    """Paged causal prefill behind a cached prefix; D = 64 runs the 64-rows-
+    per-wave variant (partial 256-row tile, causal bound per row group)."""
+    Hkv = 2
     H = Hkv * G
     blk = 16
     ctx = [400, 90, 33]
