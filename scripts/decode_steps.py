@@ -1,46 +1,58 @@
-"""Per-decode-step anatomy from a rocprofv3 kernel trace: for the stream that
-runs the Llama gate|up GEMM, split the kernel sequence into steps at each
-masked argmax and report, per step, the GPU span, the summed kernel time,
-the in-step gaps and the host gap before the next step (median over steps)."""
+"""Per-decode-step anatomy from a rocprofv3 kernel trace.
+
+Graph replays are not reliably attributed to one (queue, stream) pair, so the
+steps of an engine are picked out by kernel NAME instead: ``llm`` takes the
+Llama-3-8B decode kernels (fused GEMMs with 4-step prefetch groups, D = 128
+decode attention, the 4-wide lm_head GEMM), ``stt`` the Whisper decoder's
+(2-step groups, D = 64 attention, its lm_head). A step ends at the engine's
+lm_head GEMM. Per step: GPU span (first start to last end, so time the other
+engine's kernels interleave is included), summed kernel time, and the per-kernel
+breakdown (medians over steps)."""
 import csv
+import re
 import statistics as st
 import sys
 
+ENGINES = {
+    "llm": (re.compile(r"skinny_fused_kernel<\d, \d, 4, |attn_decode_kernel<128|skinny_gemm_kernel<2, 1, 4>"),
+            "skinny_gemm_kernel<2, 1, 4>"),
+    "stt": (re.compile(r"skinny_fused_kernel<\d, \d, 2, |attn_decode_kernel<64|skinny_gemm_kernel<2, 1, 2>"),
+            "skinny_gemm_kernel<2, 1, 2>"),
+}
 
-def main(path, key="skinny_fused_kernel<2, 1, 4, 4, 1, 1>"):
+
+def main(path, engine="llm"):
+    pat, delim = ENGINES[engine]
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
-                         (r["Queue_Id"], r["Stream_Id"])))
+            if pat.search(r["Kernel_Name"]):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    qs = {r[3] for r in rows if key in r[2]}
-    for q in sorted(qs):
-        ks = [r for r in rows if r[3] == q]
-        steps, cur = [], []
-        for r in ks:
-            cur.append(r)
-            if "masked_argmax" in r[2] or "argmax" in r[2]:
-                steps.append(cur)
-                cur = []
-        steps = [s for s in steps if sum(key in r[2] for r in s) >= 8]
-        if not steps:
-            continue
-        span = [(s[-1][1] - s[0][0]) / 1e3 for s in steps]
-        busy = [sum(r[1] - r[0] for r in s) / 1e3 for s in steps]
-        host = [(b[0][0] - a[-1][1]) / 1e3 for a, b in zip(steps, steps[1:])]
-        by = {}
-        for s in steps:
-            for r in s:
-                n = r[2].split("(")[0][:60]
-                by.setdefault(n, []).append((r[1] - r[0]) / 1e3)
-        print(f"queue {q}: {len(steps)} steps; median span {st.median(span):.1f} us, "
-              f"busy {st.median(busy):.1f} us, host gap {st.median(host) if host else 0:.1f} us "
-              f"(p90 {sorted(host)[int(0.9 * len(host))] if host else 0:.1f})")
-        per = sorted(((sum(v) / len(steps), n, len(v) / len(steps), st.median(v)) for n, v in by.items()),
-                     reverse=True)
-        for tot, n, c, med in per[:14]:
-            print(f"   {tot:8.1f} us/step  {c:5.1f} calls  median {med:6.1f} us  {n}")
+    steps, cur = [], []
+    for r in rows:
+        cur.append(r)
+        if delim in r[2]:
+            steps.append(cur)
+            cur = []
+    # decode steps only (tuning sweeps and prefill chunks have other shapes)
+    steps = [s for s in steps if 100 <= len(s) <= 400]
+    if not steps:
+        print(f"{engine}: no steps found")
+        return
+    span = [(s[-1][1] - s[0][0]) / 1e3 for s in steps]
+    busy = [sum(r[1] - r[0] for r in s) / 1e3 for s in steps]
+    by = {}
+    for s in steps:
+        for r in s:
+            n = r[2].split("(")[0][:60]
+            by.setdefault(n, []).append((r[1] - r[0]) / 1e3)
+    print(f"{engine}: {len(steps)} steps; median span {st.median(span):.1f} us, "
+          f"summed kernel time {st.median(busy):.1f} us, {st.median([len(s) for s in steps]):.0f} launches")
+    per = sorted(((sum(v) / len(steps), n, len(v) / len(steps), st.median(v)) for n, v in by.items()),
+                 reverse=True)
+    for tot, n, c, med in per[:12]:
+        print(f"   {tot:8.1f} us/step  {c:5.1f} calls  median {med:6.1f} us  {n}")
 
 
 if __name__ == "__main__":

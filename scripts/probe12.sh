@@ -1,7 +1,11 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_fused_decode.py > gpurun_out/attn_tests.log 2>&1 || { tail -30 gpurun_out/attn_tests.log; exit 1; }
-tail -1 gpurun_out/attn_tests.log
-(cd ab2 && timeout -k 10 200 python ../scripts/exp/attn_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/OLD /')
-timeout -k 10 200 python scripts/exp/attn_bench.py 2>&1 | grep -v amdgpu.ids | sed 's/^/NEW /'
+export TMPDIR=/tmp
+rm -rf gpurun_out/finalprof
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/finalprof -o run -- python bench.py --steps 3 --warmup 2 > gpurun_out/final_prof.log 2>&1 || { tail -20 gpurun_out/final_prof.log; exit 1; }
+f=$(ls gpurun_out/finalprof/run_kernel_trace.csv gpurun_out/finalprof/*/run_kernel_trace.csv 2>/dev/null | head -1)
+python scripts/decode_steps.py "$f" llm > gpurun_out/final_anatomy.txt 2>&1
+python scripts/decode_steps.py "$f" stt > gpurun_out/final_anatomy_stt.txt 2>&1
+head -16 gpurun_out/final_anatomy.txt; head -12 gpurun_out/final_anatomy_stt.txt
+rm -f "$f"
