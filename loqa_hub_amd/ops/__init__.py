@@ -506,10 +506,31 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     return best
 
 
+_TUNE_STREAM: dict = {}
+
+
+def _tune_stream() -> "torch.cuda.Stream":
+    """One side stream per device for every tuning capture. ``torch.cuda.Stream()``
+    and ``torch.cuda.graph()`` without a stream take the NEXT stream of
+    PyTorch's round-robin pool, and pool streams land on the process's few HIP
+    hardware queues in creation order: a tuner that drew one pool stream per
+    candidate left the decoder streams created after it on queues that
+    depended on how many layouts were timed (see docs/PERF.md, the cliff)."""
+    d = torch.cuda.current_device()
+    if d not in _TUNE_STREAM:
+        _TUNE_STREAM[d] = torch.cuda.Stream()
+    return _TUNE_STREAM[d]
+
+
 def graph_time(fn, reps: int = 8, trials: int = 3) -> float:
     """Device time (ms) of ``reps`` back-to-back calls of ``fn`` replayed from
     a captured HIP graph (no host launch overhead in the measurement: a few-µs
     kernel is otherwise hidden behind its own launch cost); min over trials."""
+    # A new pool stream per call, on purpose: the stream-pool cursor this
+    # leaves behind decides which hardware queues the decoder streams created
+    # later land on, and the measured-best placement (18.7-19.2 utt/s) is the
+    # one this produces. A fixed tuning stream (``_tune_stream``) measured
+    # 17.3 (docs/PERF.md, "the 1.8x cliff").
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):

@@ -68,14 +68,69 @@ def cu_masked_stream(device: torch.device, cus: list[int]) -> torch.cuda.Externa
     return torch.cuda.ExternalStream(handle.value, device=device)
 
 
+_decoders: dict = {}
+_dec_lock = __import__("threading").Lock()
+
+
+def _hip_stream(device: torch.device, priority: int) -> torch.cuda.ExternalStream:
+    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipStreamCreateWithPriority(ctypes.byref(handle), ctypes.c_uint(1), ctypes.c_int(priority))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamCreateWithPriority failed: {rc}")
+    _keep.append(handle)
+    return torch.cuda.ExternalStream(handle.value, device=device)
+
+
+def decoder_streams(device: torch.device, priorities: dict) -> dict:
+    """The STT and LLM decoder streams, created ONCE per device, in a fixed
+    order, by whichever scheduler thread asks first.
+
+    HIP spreads a process's streams over a few hardware queues
+    (GPU_MAX_HW_QUEUES, 4 here) in creation order. Which queues the two
+    graph-replaying decoder streams share decides how the GPU interleaves
+    them, and measured end to end that is worth 11 vs 17 vs 19 utt/s
+    (docs/PERF.md, "the 1.8x cliff"). Pool streams (``torch.cuda.Stream()``)
+    made the placement depend on how many streams anything else drew first,
+    so these are dedicated HIP streams. ``LOQA_QSKEW="a,b"`` creates ``a``
+    spacer streams before the STT stream and ``b`` between it and the LLM
+    stream. Opt-in (set ``LOQA_QSKEW``): the four placements measured so far
+    gave 17.1 / 17.4 / 9.5 / 17.5 utt/s, while the default pool placement
+    measures 18.7-19.2."""
+    d = torch.device(device)
+    key = d.index if d.index is not None else torch.cuda.current_device()
+    with _dec_lock:
+        if key not in _decoders:
+            a, b = (int(t) for t in os.environ.get("LOQA_QSKEW", DEFAULT_QSKEW).split(","))
+            spacers = [_hip_stream(d, 0) for _ in range(a)]
+            stt = _hip_stream(d, priorities.get("stt", 0))
+            spacers += [_hip_stream(d, 0) for _ in range(b)]
+            llm = _hip_stream(d, priorities.get("llm", 0))
+            _decoders[key] = {"stt": stt, "llm": llm, "spacers": spacers}
+        return _decoders[key]
+
+
+DEFAULT_QSKEW = "0,0"
+_ROLE = {"LOQA_STT_CUS": "stt", "LOQA_LLM_CUS": "llm"}
+_PRIO: dict = {}
+
+
 def stream_for(device: torch.device, env_key: str, priority: int = 0):
     """The stream a worker thread should use: CU-masked when ``env_key`` is
-    set (e.g. ``LOQA_STT_CUS=0-63``), else a plain stream of ``priority``."""
+    set (e.g. ``LOQA_STT_CUS=0-63``), else the decoder's dedicated stream."""
     spec = os.environ.get(env_key, "")
     if spec:
         n = torch.cuda.get_device_properties(device).multi_processor_count
         return cu_masked_stream(device, parse_cu_spec(spec, n))
-    return torch.cuda.Stream(device, priority=priority)
+    role = _ROLE.get(env_key)
+    if role is None or not os.environ.get("LOQA_QSKEW"):
+        # default: PyTorch pool streams (the placement every number in
+        # docs/PERF.md was measured with; see decoder_streams for the caveat)
+        return torch.cuda.Stream(device, priority=priority)
+    _PRIO[role] = priority
+    prios = {"stt": _PRIO.get("stt", -1), "llm": _PRIO.get("llm", 0)}
+    return decoder_streams(device, prios)[role]
 
 
 def decode_cus(device: torch.device, cus_env: str, cap_env: str) -> int | None:
