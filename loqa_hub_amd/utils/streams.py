@@ -126,7 +126,11 @@ def stream_for(device: torch.device, env_key: str, priority: int = 0):
     role = _ROLE.get(env_key)
     if role is None or not os.environ.get("LOQA_QSKEW"):
         # default: PyTorch pool streams (the placement every number in
-        # docs/PERF.md was measured with; see decoder_streams for the caveat)
+        # docs/PERF.md was measured with; see decoder_streams for the caveat).
+        # LOQA_POOL_SKEW_STT / _LLM = n draws n pool streams first, moving this
+        # decoder n hardware queues along (placement search).
+        for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{(role or '').upper()}", "0") or 0)):
+            torch.cuda.Stream(device, priority=priority)
         return torch.cuda.Stream(device, priority=priority)
     _PRIO[role] = priority
     prios = {"stt": _PRIO.get("stt", -1), "llm": _PRIO.get("llm", 0)}
