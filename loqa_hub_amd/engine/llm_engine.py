@@ -551,8 +551,9 @@ class LLMEngine:
 
             def init():
                 if dev.type == "cuda":
+                    from ..utils.streams import pool_stream
                     torch.cuda.set_device(dev)
-                    torch.cuda.set_stream(torch.cuda.Stream(dev))
+                    torch.cuda.set_stream(pool_stream(dev, "prefill"))
             self._pf_pool = ThreadPoolExecutor(1, thread_name_prefix="llm-prefill", initializer=init)
         return self._pf_pool
 

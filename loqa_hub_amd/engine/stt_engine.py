@@ -590,7 +590,8 @@ class STTEngine:
             dev = self.device
 
             def init():
+                from ..utils.streams import pool_stream
                 torch.cuda.set_device(dev)
-                torch.cuda.set_stream(torch.cuda.Stream(dev))
+                torch.cuda.set_stream(pool_stream(dev, "encoder"))
             self._enc_pool = ThreadPoolExecutor(1, thread_name_prefix="stt-encoder", initializer=init)
         return self._enc_pool

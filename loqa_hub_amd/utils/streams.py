@@ -68,6 +68,15 @@ def cu_masked_stream(device: torch.device, cus: list[int]) -> torch.cuda.Externa
     return torch.cuda.ExternalStream(handle.value, device=device)
 
 
+def pool_stream(device: torch.device, role: str, priority: int = 0):
+    """A PyTorch pool stream for a worker thread, first drawing
+    ``LOQA_POOL_SKEW_<ROLE>`` extra pool streams (hardware-queue placement
+    search; see decoder_streams)."""
+    for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{role.upper()}", "0") or 0)):
+        torch.cuda.Stream(device, priority=priority)
+    return torch.cuda.Stream(device, priority=priority)
+
+
 _decoders: dict = {}
 _dec_lock = __import__("threading").Lock()
 
