@@ -8,9 +8,11 @@
 //                  conversion loop + WAV/HTTP round trip (audio_service.go:1048,
 //                  stt_client.go:365).
 //  * BlockPool   - paged KV-cache block allocator with per-sequence block tables,
-//                  reference counts and a hash-keyed prefix cache so prompts that
-//                  share the parser template prefix share KV blocks
-//                  (SURVEY §7.2 step 4).
+//                  reference counts and a prefix cache so prompts that share the
+//                  parser template prefix share KV blocks.
+//                  The cache is looked up by a chained hash but every hit is
+//                  verified against the block's stored token prefix, so a hash
+//                  collision can never hand out another prompt's KV.
 // Exposed through a flat C ABI (loaded with ctypes after torch, so the process
 // has exactly one HIP runtime).
 #include <hip/hip_runtime.h>
@@ -51,19 +53,48 @@ struct BlockPool {
   std::vector<int32_t> refcnt;
   std::deque<int32_t> free_list;
   std::unordered_map<int64_t, Seq> seqs;
-  // prefix cache: chained hash of full blocks -> block id (holds one reference)
-  std::unordered_map<uint64_t, int32_t> prefix;
-  std::unordered_map<int32_t, uint64_t> block_hash;
+  // prefix cache: chained hash of full blocks -> candidate block ids (each
+  // holds one reference); a cached block keeps the WHOLE token prefix it ends
+  // (tokens 0 .. its last token), compared on every hit
+  std::unordered_multimap<uint64_t, int32_t> prefix;
+  struct Cached {
+    uint64_t hash;
+    std::vector<int32_t> toks;
+  };
+  std::unordered_map<int32_t, Cached> cached;
+  uint64_t hash_mask = ~0ULL;  // tests narrow it to force collisions
   std::mutex mu;
+
+  // cached block whose stored prefix equals toks[0:n], or -1
+  int32_t lookup(uint64_t h, const int32_t* toks, int n) const {
+    auto range = prefix.equal_range(h);
+    for (auto it = range.first; it != range.second; ++it) {
+      const Cached& c = cached.at(it->second);
+      if ((int)c.toks.size() == n && std::memcmp(c.toks.data(), toks, sizeof(int32_t) * n) == 0)
+        return it->second;
+    }
+    return -1;
+  }
+  void uncache(int32_t b) {
+    auto c = cached.find(b);
+    if (c == cached.end()) return;
+    auto range = prefix.equal_range(c->second.hash);
+    for (auto it = range.first; it != range.second; ++it) {
+      if (it->second == b) {
+        prefix.erase(it);
+        break;
+      }
+    }
+    cached.erase(c);
+  }
 
   int32_t take() {
     if (free_list.empty()) {
       // evict an unreferenced cached prefix block
-      for (auto it = prefix.begin(); it != prefix.end(); ++it) {
-        if (refcnt[it->second] == 1) {
-          const int32_t b = it->second;
-          block_hash.erase(b);
-          prefix.erase(it);
+      for (auto it = cached.begin(); it != cached.end(); ++it) {
+        const int32_t b = it->first;
+        if (refcnt[b] == 1) {
+          uncache(b);
           refcnt[b] = 0;
           return take_fresh(b);
         }
@@ -202,12 +233,20 @@ void* loqa_pool_create(int num_blocks, int block_size) {
 
 void loqa_pool_destroy(void* h) { delete static_cast<BlockPool*>(h); }
 
+// Test hook: keep only the masked bits of the prefix hash (mask 0 makes every
+// block collide, so lookups must be decided by the stored tokens alone).
+void loqa_pool_debug_hash_mask(void* h, unsigned long long mask) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  p->hash_mask = mask;
+}
+
 int loqa_pool_free_blocks(void* h) {
   auto* p = static_cast<BlockPool*>(h);
   std::lock_guard<std::mutex> g(p->mu);
   int n = (int)p->free_list.size();
-  for (auto& kv : p->prefix)
-    if (p->refcnt[kv.second] == 1) ++n;
+  for (auto& kv : p->cached)
+    if (p->refcnt[kv.first] == 1) ++n;
   return n;
 }
 
@@ -222,11 +261,11 @@ long long loqa_pool_add_seq(void* h, long long seq_id, const int32_t* toks, int 
   uint64_t hsh = 0;
   const int bs = p->block_size;
   for (int i = 0; i + bs < ntok; i += bs) {  // keep >= 1 token to compute
-    hsh = mix_hash(hsh, toks + i, bs);
-    auto it = p->prefix.find(hsh);
-    if (it == p->prefix.end()) break;
-    p->refcnt[it->second]++;
-    sq.blocks.push_back(it->second);
+    hsh = mix_hash(hsh, toks + i, bs) & p->hash_mask;
+    const int32_t b = p->lookup(hsh, toks, i + bs);
+    if (b < 0) break;
+    p->refcnt[b]++;
+    sq.blocks.push_back(b);
     sq.len += bs;
   }
   p->seqs.emplace(seq_id, std::move(sq));
@@ -265,13 +304,12 @@ int loqa_pool_cache_prefix(void* h, long long seq_id, const int32_t* toks, int n
   const int bs = p->block_size;
   uint64_t hsh = 0;
   for (int i = 0, bi = 0; i + bs <= ntok && bi < (int)it->second.blocks.size(); i += bs, ++bi) {
-    hsh = mix_hash(hsh, toks + i, bs);
+    hsh = mix_hash(hsh, toks + i, bs) & p->hash_mask;
     const int32_t b = it->second.blocks[bi];
-    if (!p->prefix.count(hsh) && !p->block_hash.count(b)) {
-      p->prefix[hsh] = b;
-      p->block_hash[b] = hsh;
-      p->refcnt[b]++;  // the cache's own reference
-    }
+    if (p->cached.count(b) || p->lookup(hsh, toks, i + bs) >= 0) continue;
+    p->prefix.emplace(hsh, b);
+    p->cached.emplace(b, BlockPool::Cached{hsh, std::vector<int32_t>(toks, toks + i + bs)});
+    p->refcnt[b]++;  // the cache's own reference
   }
   return 0;
 }

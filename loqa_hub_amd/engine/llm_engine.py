@@ -30,6 +30,7 @@ import torch
 
 from .. import ops
 from ..models.configs import LlamaConfig
+from .batching import join_futures, plan_step
 from ..models.llama import LlamaModel, LlamaWeights, StepMeta, TPGroup
 from .grammar import GrammarState, GrammarTables
 from .kv_cache import PagedKVCache
@@ -110,7 +111,18 @@ class LLMEngine:
         self.fused_decode = fused_decode and self.weights.fused
         self.scratch = ops.FusedScratch(self.device)
         self.prefill_chunk = prefill_chunk
+        # token budget of one decode step: every live sequence feeds its sampled
+        # token plus a jump-forward literal, so without a cap 17+ sequences in a
+        # forced run would exceed the fused GEMMs' row limit (ops.MPADS);
+        # leftovers carry to the next step (batching.plan_step)
+        self.step_tokens = max(1, min(int(os.environ.get("LOQA_LLM_STEP_TOKENS", "64")),
+                                      ops.MPADS[-2]))
+        self._rr = 0
         self._graphs: dict[tuple[int, int], dict] = {}
+        # set once warmup_graphs() has captured every reachable bucket: from
+        # then on an uncaptured shape runs eagerly instead of capturing while
+        # the other worker threads issue HIP work
+        self._graphs_frozen = False
         self._next_id = 1
         self._on_done = None
         self._cells_lock = threading.Lock()
@@ -277,16 +289,21 @@ class LLMEngine:
         if not self.use_graphs:
             return 0
         n = 0
+        b_max = _bucket(max(1, self.max_seqs), self.SEQ_BUCKETS)
         for b in self.SEQ_BUCKETS:
-            if b > max(1, self.max_seqs):
+            if b > b_max:
                 break
-            t_max = ops.mpad_for(min(ops.MPADS[-2], b * self.max_decode_q))
+            t_min = ops.mpad_for(min(self.step_tokens, b // 2 + 1))   # T >= B > b/2
+            t_max = ops.mpad_for(min(self.step_tokens, b * self.max_decode_q))
             for t in ops.MPADS:
                 if t > t_max:
                     break
+                if t < t_min:
+                    continue
                 for c in range(self.CTX_BUCKET, self.max_seq_len + self.CTX_BUCKET, self.CTX_BUCKET):
                     self._decode_graph(b, t, min(c, self.max_seq_len))
                     n += 1
+        self._graphs_frozen = True
         return n
 
     # ------------------------------------------------------------ generate
@@ -381,16 +398,24 @@ class LLMEngine:
             self._sample_and_advance([r], nxt.cpu().numpy(), time.perf_counter())
 
     def decode_step(self, live: list[GenRequest]) -> None:
-        feeds, carry = [], []
-        for r in live:
+        """One decode step over (a budgeted subset of) ``live``: at most
+        ``step_tokens`` tokens in total and ``max_decode_q`` per sequence; a
+        sequence fed only part of its pending tokens carries the rest (its
+        logits this step are unused), one left out entirely waits a step."""
+        take = plan_step([len(r.feed) for r in live], self.step_tokens, self.max_decode_q,
+                         self._rr)
+        self._rr = (self._rr + self.step_tokens) % len(live) if len(live) > self.step_tokens else 0
+        step, feeds, carry = [], [], []
+        for r, n in zip(live, take):
+            if n == 0:
+                continue
             f = r.feed
-            if len(f) > self.max_decode_q:  # long forced run: feed it over two steps
-                feeds.append(f[: self.max_decode_q])
-                r.feed = f[self.max_decode_q:]
-                carry.append(True)
-            else:
-                feeds.append(f)
-                carry.append(False)
+            step.append(r)
+            feeds.append(f[:n])
+            carry.append(n < len(f))
+            if n < len(f):
+                r.feed = f[n:]
+        live = step
         t0 = time.perf_counter()
         B = len(live)
         T = sum(len(f) for f in feeds)
@@ -400,7 +425,12 @@ class LLMEngine:
             T_pad = ops.mpad_for(T)
             ctx = max(self.kv.pool.seq_len(r.seq_id) + len(f) for r, f in zip(live, feeds))
             C = min(self.max_seq_len, -(-ctx // self.CTX_BUCKET) * self.CTX_BUCKET)
-            g = self._decode_graph(B_pad, T_pad, C)
+            g = self._graphs.get((B_pad, T_pad, C))
+            if g is None and self._graphs_frozen:
+                g = False                 # uncaptured shape while serving: eager
+            elif g is None:
+                g = self._decode_graph(B_pad, T_pad, C)
+        if self.use_graphs and g is not False:
             hb = g["host"]
             self._meta(live, feeds, True, B_pad, T_pad, out=hb)
             hb["mask_rows"].fill(0)
@@ -456,6 +486,13 @@ class LLMEngine:
         if getattr(self, "_fatal", None) is not None:
             fut.set_exception(self._fatal)
             return fut
+        reqs = list(reqs)
+        cap = max(1, self.max_seqs)
+        if len(reqs) > cap:
+            # admission holds an inbox item until it fits under max_seqs: an
+            # oversize item would wait forever, so it goes in max_seqs chunks
+            return join_futures([self.submit_batch(reqs[i:i + cap], on_done)
+                                 for i in range(0, len(reqs), cap)], reqs)
         self._inbox.put((reqs, on_done, fut))
         return fut
 
@@ -482,31 +519,36 @@ class LLMEngine:
         # at the first step boundary after its prefill completed (the worker
         # synchronises on its first sampled token, so its KV writes are done)
         pending: list[tuple[list[GenRequest], Future]] = []
+        # inbox items not yet admitted: at most max_seqs sequences are live or
+        # prefilling at once (the KV pool and the captured graph buckets are
+        # sized for that many)
+        waiting: list[tuple] = []
+        cap = max(1, self.max_seqs)
         pf_pool = self._prefill_executor() if self.overlap_prefill else None
         while self._running:
-            idle = not live and not pending
+            idle = not live and not pending and not waiting
             items = [self._inbox.get()] if idle else []   # idle: block for work
             while True:
                 try:
                     items.append(self._inbox.get_nowait())
                 except queue.Empty:
                     break
-            new: list[GenRequest] = []
-            for it in items:
-                if it is None:
-                    continue
-                reqs, cb, fut = it
-                if not reqs:
-                    fut.set_result(reqs)
-                    continue
-                cell = [len(reqs), fut, reqs]
-                with self._cells_lock:
-                    cells[id(cell)] = cell
-                for r in reqs:
-                    r.on_done = self._completion(cb, cell, cells)
-                    self.submit(r)
-                new += reqs
+            waiting += [it for it in items if it is not None]
             try:
+                new: list[GenRequest] = []
+                active = len(live) + sum(len(r) for r, _ in pending)
+                while waiting and active + len(new) + len(waiting[0][0]) <= cap:
+                    reqs, cb, fut = waiting.pop(0)
+                    if not reqs:
+                        fut.set_result(reqs)
+                        continue
+                    cell = [len(reqs), fut, reqs]
+                    with self._cells_lock:
+                        cells[id(cell)] = cell
+                    for r in reqs:
+                        r.on_done = self._completion(cb, cell, cells)
+                        self.submit(r)
+                    new += reqs
                 if new:
                     if pf_pool is not None:
                         pending.append((new, pf_pool.submit(self._prefill_timed, new)))
@@ -530,15 +572,25 @@ class LLMEngine:
                     self.stats["decode_s"] += time.perf_counter() - t0
                     live = [r for r in live if not r.done]
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
+                # in-flight prefills still write KV into their sequences' blocks:
+                # let them finish before those blocks go back to the pool
+                wait([f for _, f in pending])
                 with self._cells_lock:
                     for cell in list(cells.values()):
                         if not cell[1].done():
                             cell[1].set_exception(e)
                         for r in cell[2]:
                             if not r.done:
-                                self.kv.pool.free_seq(r.seq_id)
+                                r.done = True
+                                try:
+                                    self.kv.pool.free_seq(r.seq_id)
+                                except KeyError:
+                                    pass        # never registered
                     cells.clear()
-                live, pending = [], []
+                for _, _, fut in waiting:
+                    if not fut.done():
+                        fut.set_exception(e)
+                live, pending, waiting = [], [], []
 
     def _prefill_timed(self, reqs: list[GenRequest]) -> None:
         t0 = time.perf_counter()

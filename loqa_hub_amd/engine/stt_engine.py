@@ -25,6 +25,7 @@ from .. import ops
 from ..models.configs import WhisperConfig
 from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused
 from ..utils.tracing import tracer
+from .batching import join_futures, plan_step
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
@@ -104,6 +105,12 @@ class STTEngine:
         self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
                                 device=self.device) for _ in range(cfg.dec_layers)]
         self._graphs: dict[tuple[int, int], dict] = {}
+        self._graphs_frozen = False     # see LLMEngine: no capture while serving
+        # token budget of one decoder step (each new sequence feeds the 4-token
+        # SOT prompt; 17+ simultaneous arrivals would exceed ops.MPADS rows)
+        self.step_tokens = max(len(self.sot), min(int(os.environ.get("LOQA_STT_STEP_TOKENS", "64")),
+                                                  ops.MPADS[-2]))
+        self._rr = 0
 
     # ------------------------------------------------------------ front end
     def upload(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
@@ -296,16 +303,21 @@ class STTEngine:
             return 0
         n = 0
         n_sot = len(self.sot)
+        b_max = next((b for b in self.SEQ_BUCKETS if b >= self.max_batch), self.SEQ_BUCKETS[-1])
         for b in self.SEQ_BUCKETS:
-            if b > self.max_batch:
+            if b > b_max:
                 break
-            t_max = ops.mpad_for(min(64, b * n_sot))
+            t_min = ops.mpad_for(min(self.step_tokens, b // 2 + 1))   # T >= B > b/2
+            t_max = ops.mpad_for(min(self.step_tokens, b * n_sot))
             for t in ops.MPADS:
                 if t > t_max:
                     break
+                if t < t_min:
+                    continue
                 for c in range(self.SPLIT_KEYS, self.cfg.n_text_ctx + self.SPLIT_KEYS, self.SPLIT_KEYS):
                     self._graph(b, t, min(c, self.cfg.n_text_ctx))
                     n += 1
+        self._graphs_frozen = True
         return n
 
     def _step(self, live: list[STTRequest]) -> np.ndarray:
@@ -315,9 +327,9 @@ class STTEngine:
         if self.fast_decode:
             B_pad = next((b for b in self.SEQ_BUCKETS if b >= B), B)
             T_pad = ops.mpad_for(T)
-            if self.use_graphs:
-                ctx = max(self.kv.pool.seq_len(r.seq_id) + len(r.feed) for r in live)
-                C = min(self.cfg.n_text_ctx, -(-ctx // self.SPLIT_KEYS) * self.SPLIT_KEYS)
+            ctx = max(self.kv.pool.seq_len(r.seq_id) + len(r.feed) for r in live)
+            C = min(self.cfg.n_text_ctx, -(-ctx // self.SPLIT_KEYS) * self.SPLIT_KEYS)
+            if self.use_graphs and ((B_pad, T_pad, C) in self._graphs or not self._graphs_frozen):
                 t0 = time.perf_counter()
                 g = self._graph(B_pad, T_pad, C)
                 self._host_meta(live, B_pad, T_pad, out=g["host"])
@@ -405,11 +417,25 @@ class STTEngine:
                 r.target = self.tok.encode(" " + r.transcript.strip())[: self.cfg.n_text_ctx - 8] + [self.eot]
 
     def _decode_once(self, live: list[STTRequest]) -> list[STTRequest]:
-        """One decoder step over ``live``; returns the requests that finished."""
+        """One decoder step over ``live`` (at most ``step_tokens`` tokens: a
+        sequence may sit the step out or feed only part of its SOT prompt, see
+        ``batching.plan_step``); returns the requests that finished."""
+        take = plan_step([len(r.feed) for r in live], self.step_tokens, len(self.sot), self._rr)
+        self._rr = (self._rr + self.step_tokens) % len(live) if len(live) > self.step_tokens else 0
+        step, rest = [], []
+        for r, n in zip(live, take):
+            if n:
+                step.append(r)
+                rest.append(r.feed[n:])
+                r.feed = r.feed[:n]
+        live = step
         nxt = self._step(live)
         self.stats["decode_steps"] += 1
         done = []
         for j, r in enumerate(live):
+            if rest[j]:            # part of the prompt still to feed: logits unused
+                r.feed = rest[j]
+                continue
             t = int(r.target[r.step]) if r.target is not None else int(nxt[j])
             r.tokens.append(t)
             r.step += 1
@@ -475,23 +501,8 @@ class STTEngine:
         if len(reqs) > self.max_batch:
             # admission needs a free slot for every request of an inbox item:
             # an oversize batch would wait forever, so it goes in max_batch chunks
-            parts = [self.submit_batch(reqs[i:i + self.max_batch], on_done)
-                     for i in range(0, len(reqs), self.max_batch)]
-            left = [len(parts)]
-            lock = threading.Lock()
-
-            def _part_done(f: Future) -> None:
-                with lock:
-                    left[0] -= 1
-                    if fut.done():
-                        return
-                    if f.exception() is not None:
-                        fut.set_exception(f.exception())
-                    elif left[0] == 0:
-                        fut.set_result(reqs)
-            for p in parts:
-                p.add_done_callback(_part_done)
-            return fut
+            return join_futures([self.submit_batch(reqs[i:i + self.max_batch], on_done)
+                                 for i in range(0, len(reqs), self.max_batch)], reqs)
         self._inbox.put((reqs, on_done, fut))
         return fut
 
@@ -574,6 +585,9 @@ class STTEngine:
                             cell[1].set_result(cell[2])
                     live = [r for r in live if r.t_done == 0.0]
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
+                # encoder jobs already submitted keep writing cross-attention K|V
+                # into their slots: let them finish before any slot is reused
+                wait([f for _, f in encoding])
                 for cell in list(cells.values()):
                     if not cell[1].done():
                         cell[1].set_exception(e)

@@ -113,6 +113,7 @@ _RUNTIME_SIGS = {
     "loqa_stager_release": ([c_void_p, c_int], None),
     "loqa_pool_create": ([c_int, c_int], c_void_p),
     "loqa_pool_destroy": ([c_void_p], None),
+    "loqa_pool_debug_hash_mask": ([c_void_p, ctypes.c_ulonglong], None),
     "loqa_pool_free_blocks": ([c_void_p], c_int),
     "loqa_pool_add_seq": ([c_void_p, c_ll, c_void_p, c_int], c_ll),
     "loqa_pool_append": ([c_void_p, c_ll, c_int, c_void_p], c_int),

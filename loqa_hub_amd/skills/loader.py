@@ -149,23 +149,43 @@ class ProcessSkill(SkillPlugin):
             stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL)
 
     async def call(self, method: str, params) -> dict | None:
+        """One request/reply. A timeout, a garbled or out-of-order reply, or a
+        cancelled call leaves the child's stdout in an unknown state (a late
+        reply would be read by the NEXT call), so the child is killed and
+        reaped and the next call respawns it."""
         async with self._io:
             if self._proc is None or self._proc.returncode is not None:
                 await self._spawn()
             rid = next(self._ids)
             msg = '{"id":%d,"method":%s,"params":%s}\n' % (rid, json.dumps(method),
                                                            gojson.dumps(params))
-            self._proc.stdin.write(msg.encode())
-            await self._proc.stdin.drain()
-            line = await asyncio.wait_for(self._proc.stdout.readline(), self.request_timeout)
-            if not line:
-                raise RuntimeError(f"skill process {self.manifest.id} exited")
-            resp = json.loads(line)
-            if resp.get("id") != rid:
-                raise RuntimeError("skill process protocol error: id mismatch")
+            try:
+                self._proc.stdin.write(msg.encode())
+                await self._proc.stdin.drain()
+                line = await asyncio.wait_for(self._proc.stdout.readline(), self.request_timeout)
+                if not line:
+                    raise RuntimeError(f"skill process {self.manifest.id} exited")
+                try:
+                    resp = json.loads(line)
+                except ValueError as e:
+                    raise RuntimeError(f"skill process protocol error: {e}") from e
+                if not isinstance(resp, dict) or resp.get("id") != rid:
+                    raise RuntimeError("skill process protocol error: id mismatch")
+            except BaseException:
+                await self._kill()
+                raise
             if resp.get("error"):
                 raise RuntimeError(str(resp["error"]))
             return resp.get("result")
+
+    async def _kill(self) -> None:
+        p, self._proc = self._proc, None
+        if p is not None and p.returncode is None:
+            try:
+                p.kill()
+            except ProcessLookupError:
+                pass
+            await p.wait()
 
     async def initialize(self, config: SkillConfig) -> None:
         self.config = config

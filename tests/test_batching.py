@@ -1,0 +1,113 @@
+"""Per-step token budget and admission limits of the continuous-batching
+schedulers (17+ sequences in a forced-literal run, or 33+ STT
+arrivals feeding their SOT prompt, used to exceed the fused GEMMs' row limit
+and fail every in-flight request)."""
+import numpy as np
+import torch
+
+from loqa_hub_amd.engine.batching import plan_step
+from loqa_hub_amd.engine.grammar import multi_command_schema
+from loqa_hub_amd.llm.commands import parse_multi_command_response
+
+
+def test_plan_step_budget_and_fairness():
+    # under budget: everyone gets their feed, capped at max_q
+    assert plan_step([1, 3, 20], 64, 8) == [1, 3, 8]
+    # over budget: one token each first, then top-ups in order
+    t = plan_step([8] * 10, 16, 8)
+    assert sum(t) == 16 and all(x >= 1 for x in t) and t[0] == 7
+    # more sequences than budget: a window of `budget` sequences, rotating
+    t0 = plan_step([1] * 10, 4, 8, start=0)
+    t1 = plan_step([1] * 10, 4, 8, start=4)
+    assert t0 == [1, 1, 1, 1, 0, 0, 0, 0, 0, 0] and t1 == [0, 0, 0, 0, 1, 1, 1, 1, 0, 0]
+    assert plan_step([], 8, 8) == []
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        lens = rng.integers(1, 30, rng.integers(1, 80)).tolist()
+        b, q = int(rng.integers(1, 65)), int(rng.integers(1, 17))
+        t = plan_step(lens, b, q, int(rng.integers(0, 100)))
+        assert sum(t) <= b and all(0 <= x <= min(n, q) for x, n in zip(t, lens))
+        assert sum(1 for x in t if x) == min(b, len(lens))
+
+
+def _wrap_steps(eng, name="decode_step"):
+    seen = {"max_live": 0, "max_tokens": 0}
+    orig = getattr(eng, name)
+
+    def step(live):
+        before = eng.stats.get("decode_tokens", 0)
+        seen["max_live"] = max(seen["max_live"], len(live))
+        out = orig(live)
+        seen["max_tokens"] = max(seen["max_tokens"], eng.stats.get("decode_tokens", 0) - before)
+        return out
+    setattr(eng, name, step)
+    return seen
+
+
+def test_llm_scheduler_64_seqs_long_forced_runs_cpu():
+    """max_seqs=64 (production HUB_MAX_BATCH), 80 submitted requests with
+    4-command schemas: admission holds the overflow, every step stays under
+    the token budget, and every request completes with valid JSON."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=64,
+                    max_seq_len=512, use_graphs=False)
+    assert eng.max_decode_q == 16 and eng.step_tokens == 64
+    seen = _wrap_steps(eng)
+    prompt = eng.tok.encode("turn on the lights and play music", bos=True)
+    n_cmds = [1 + i % 4 for i in range(80)]
+    reqs = [GenRequest(list(prompt), multi_command_schema(n)) for n in n_cmds]
+    try:
+        fut_a = eng.submit_batch(reqs[:70])     # oversize vs max_seqs: chunked
+        fut_b = eng.submit_batch(reqs[70:])
+        fut_a.result(timeout=600)
+        fut_b.result(timeout=600)
+    finally:
+        eng.stop()
+    assert seen["max_live"] <= 64
+    assert 0 < seen["max_tokens"] <= 64
+    for n, r in zip(n_cmds, reqs):
+        assert r.done and len(parse_multi_command_response(r.output, "x").commands) == n
+    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
+
+
+def test_llm_generate_small_budget_cpu():
+    """A budget below the live count: sequences sit steps out in turn."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=8,
+                    max_seq_len=512, use_graphs=False)
+    eng.step_tokens = 5
+    seen = _wrap_steps(eng)
+    reqs = [GenRequest(eng.tok.encode("dim the lights", bos=True), multi_command_schema(n))
+            for n in (1, 2, 3, 4, 2, 3, 1, 4)]
+    eng.generate(reqs)
+    assert seen["max_tokens"] <= 5
+    for n, r in zip((1, 2, 3, 4, 2, 3, 1, 4), reqs):
+        assert len(parse_multi_command_response(r.output, "x").commands) == n
+
+
+def test_stt_many_arrivals_under_budget_cpu():
+    """More arrivals than the budget allows SOT prompts for: some sit a step
+    out or feed part of the prompt; transcripts are unchanged."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    eng = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=16)
+    eng.step_tokens = 10
+    seen = {"max_tokens": 0}
+    orig = eng._step
+
+    def step(live):
+        seen["max_tokens"] = max(seen["max_tokens"], sum(len(r.feed) for r in live))
+        return orig(live)
+    eng._step = step
+    utts = make_batch(0, 12, [1, 2, 3])
+    reqs = [STTRequest(u.pcm, transcript=u.text) for u in utts]
+    try:
+        eng.submit_batch(reqs).result(timeout=600)
+    finally:
+        eng.stop()
+    assert seen["max_tokens"] <= 10
+    for r, u in zip(reqs, utts):
+        assert r.text == u.text

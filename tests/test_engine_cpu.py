@@ -129,6 +129,36 @@ def test_native_block_pool_matches():
     _exercise_pool(NativeBlockPool(64, 16))
 
 
+def test_native_prefix_cache_survives_hash_collisions():
+    """Every prefix hash forced to collide: hits must still be decided by the
+    stored tokens (a collision must never reuse another prompt's KV)."""
+    from loqa_hub_amd.engine.kv_cache import NativeBlockPool
+    from loqa_hub_amd.ops import _lib
+    try:
+        _lib.runtime()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native runtime not built: {e}")
+    pool = NativeBlockPool(64, 16)
+    pool.lib.loqa_pool_debug_hash_mask(pool.h, 0)
+    a = list(range(48))
+    b = list(range(100, 148))
+    for sid, toks in ((1, a), (2, b)):
+        assert pool.add_seq(sid, toks) == 0
+        pool.append(sid, len(toks))
+        pool.cache_prefix(sid, toks)
+    # same hash for every block of a and b: only exact token prefixes hit
+    assert pool.add_seq(3, b[:32] + [1]) == 32
+    assert pool.block_table(3)[:2] == pool.block_table(2)[:2]
+    assert pool.add_seq(4, a[:16] + b[16:32] + [1]) == 16     # block 2 differs -> stops
+    assert pool.block_table(4)[:1] == pool.block_table(1)[:1]
+    assert pool.add_seq(5, [7] * 40) == 0
+    for sid in range(1, 6):
+        pool.free_seq(sid)
+    # cached blocks are evicted (not leaked) when the pool runs dry
+    assert pool.add_seq(6, [5]) == 0
+    assert pool.append(6, 16 * 64) is not None
+
+
 def test_skinny_reference_and_shuffle():
     torch.manual_seed(0)
     N, K = 64, 256

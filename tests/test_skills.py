@@ -239,6 +239,48 @@ def test_process_skill(skills_root, tmp_path):
     run(go())
 
 
+SLOW_PROCESS_SKILL = textwrap.dedent('''\
+    #!{py}
+    import json, sys, time
+    for line in sys.stdin:
+        req = json.loads(line)
+        t = req["params"]["transcript"] if req["method"] == "handle_intent" else ""
+        if "slow" in t:
+            time.sleep(1.0)
+        res = {{"success": True, "message": "proc:" + t}}
+        sys.stdout.write(json.dumps({{"id": req["id"], "result": res}}) + "\\n")
+        sys.stdout.flush()
+''')
+
+
+def test_process_skill_recovers_after_timeout(skills_root, tmp_path):
+    """A timed-out call must not leave its late reply for the next call
+    (ADVICE r1: every later call would read the previous reply)."""
+    from loqa_hub_amd.skills.loader import ProcessSkill
+
+    d = skills_root / "slow"
+    d.mkdir()
+    (d / "skill.json").write_text(json.dumps(manifest("slow", mode="process")))
+    exe = d / "skill"
+    exe.write_text(SLOW_PROCESS_SKILL.format(py=sys.executable))
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+
+    async def go():
+        sk = ProcessSkill(SkillManifest.from_dict(manifest("slow", mode="process")), str(exe),
+                          str(d), request_timeout=0.3)
+        r = await sk.handle_intent(VoiceIntent(transcript="fast one"))
+        assert r.message == "proc:fast one"
+        first = sk._proc
+        with pytest.raises(asyncio.TimeoutError):
+            await sk.handle_intent(VoiceIntent(transcript="slow one"))
+        assert sk._proc is None and first.returncode is not None   # killed and reaped
+        for k in range(3):   # respawned; replies line up with their requests again
+            r = await sk.handle_intent(VoiceIntent(transcript=f"fast {k}"))
+            assert r.message == f"proc:fast {k}"
+        await sk.close()
+    run(go())
+
+
 def test_auto_load_all(skills_root, tmp_path):
     async def go():
         make_module_skill(skills_root, "a1")
