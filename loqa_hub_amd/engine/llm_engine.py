@@ -111,6 +111,11 @@ class LLMEngine:
         self.fused_decode = fused_decode and self.weights.fused
         self.scratch = ops.FusedScratch(self.device)
         self.prefill_chunk = prefill_chunk
+        # inline prefill: a new request whose uncached prompt tail is at most
+        # this many tokens skips the separate prefill pass and joins the decode
+        # batch directly, its tail fed max_decode_q tokens per step (it shares
+        # the decode steps' weight reads instead of a whole pass of its own)
+        self.inline_prefill = int(os.environ.get("LOQA_INLINE_PREFILL", "64"))
         # token budget of one decode step: every live sequence feeds its sampled
         # token plus a jump-forward literal, so without a cap 17+ sequences in a
         # forced run would exceed the fused GEMMs' row limit (ops.MPADS);
@@ -131,7 +136,7 @@ class LLMEngine:
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
-                      "host_post_s": 0.0}
+                      "host_post_s": 0.0, "replay_call_s": 0.0, "sched_s": 0.0}
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
@@ -331,6 +336,9 @@ class LLMEngine:
                 continue  # long forced run split across steps: logits of this step unused
             if r.t_first == 0.0:
                 r.t_first = now
+                if getattr(r, "inline", False):   # prompt fed through decode steps
+                    self.stats["prefill_tokens"] += r.inline   # type: ignore[attr-defined]
+                    self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
             r.token_times.append(now)
             r.steps += 1
             forced = r.grammar.advance(int(t))
@@ -439,9 +447,11 @@ class LLMEngine:
             g["d64"].copy_(g["h64"], non_blocking=True)
             t1 = time.perf_counter()
             g["graph"].replay()
+            t15 = time.perf_counter()
             nxt = g["out"][:B].cpu().numpy()
             t2 = time.perf_counter()
             self.stats["host_pre_s"] += t1 - t0
+            self.stats["replay_call_s"] += t15 - t1
             self.stats["gpu_wait_s"] += t2 - t1
         else:
             max_q, max_ctx, host = self._meta(live, feeds, True, B, ops.mpad_for(T))
@@ -463,6 +473,8 @@ class LLMEngine:
         every weight read of the decode steps."""
         if getattr(self, "_sched", None) is not None:
             return
+        from ..utils.gil import tune_switch_interval
+        tune_switch_interval()
         self._inbox: queue.Queue = queue.Queue()
         self._running = True
         self._sched = threading.Thread(target=self._schedule, args=(stream_priority,),
@@ -525,6 +537,7 @@ class LLMEngine:
         waiting: list[tuple] = []
         cap = max(1, self.max_seqs)
         pf_pool = self._prefill_executor() if self.overlap_prefill else None
+        t_end = 0.0
         while self._running:
             idle = not live and not pending and not waiting
             items = [self._inbox.get()] if idle else []   # idle: block for work
@@ -549,6 +562,12 @@ class LLMEngine:
                         r.on_done = self._completion(cb, cell, cells)
                         self.submit(r)
                     new += reqs
+                if new and self.inline_prefill > 0:
+                    inl = [r for r in new if len(r.feed) <= self.inline_prefill]
+                    for r in inl:
+                        r.inline = len(r.feed)   # type: ignore[attr-defined]
+                    live += inl
+                    new = [r for r in new if len(r.feed) > self.inline_prefill]
                 if new:
                     if pf_pool is not None:
                         pending.append((new, pf_pool.submit(self._prefill_timed, new)))
@@ -568,9 +587,14 @@ class LLMEngine:
                     pending = still
                 if live:
                     t0 = time.perf_counter()
+                    if t_end:
+                        self.stats["sched_s"] += t0 - t_end   # loop work between steps
                     self.decode_step(live)
-                    self.stats["decode_s"] += time.perf_counter() - t0
+                    t_end = time.perf_counter()
+                    self.stats["decode_s"] += t_end - t0
                     live = [r for r in live if not r.done]
+                else:
+                    t_end = 0.0
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
                 # in-flight prefills still write KV into their sequences' blocks:
                 # let them finish before those blocks go back to the pool

@@ -474,6 +474,8 @@ class STTEngine:
         so an utterance never waits for an earlier batch's decode to drain."""
         if getattr(self, "_sched", None) is not None:
             return
+        from ..utils.gil import tune_switch_interval
+        tune_switch_interval()
         self._inbox: queue.Queue = queue.Queue()
         self._running = True
         self._free_slots = list(range(self.max_batch))

@@ -31,6 +31,12 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if use_gpu:
+        sched = os.environ.get("LOQA_HIP_SCHEDULE")   # experiment: spin | yield | block
+        if sched:
+            import ctypes
+            flag = {"spin": 1, "yield": 2, "block": 4}[sched]
+            rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(flag)
+            print(f"hipSetDeviceFlags({sched}) -> {rc}", flush=True)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -49,6 +49,13 @@ def main(path, engine="llm"):
             by.setdefault(n, []).append((r[1] - r[0]) / 1e3)
     print(f"{engine}: {len(steps)} steps; median span {st.median(span):.1f} us, "
           f"summed kernel time {st.median(busy):.1f} us, {st.median([len(s) for s in steps]):.0f} launches")
+    # host turnaround: last kernel of a step -> first kernel of the next one
+    # (sampling read-back, grammar advance, metadata, graph launch)
+    gaps = [(b[0][0] - a[-1][1]) / 1e3 for a, b in zip(steps, steps[1:])]
+    gaps = [g for g in gaps if 0 <= g < 5000]
+    if gaps:
+        print(f"   step-to-step gap: median {st.median(gaps):.1f} us, p90 "
+              f"{sorted(gaps)[int(0.9 * (len(gaps) - 1))]:.1f} us")
     per = sorted(((sum(v) / len(steps), n, len(v) / len(steps), st.median(v)) for n, v in by.items()),
                  reverse=True)
     for tot, n, c, med in per[:12]:

@@ -111,3 +111,26 @@ def test_stt_many_arrivals_under_budget_cpu():
     assert seen["max_tokens"] <= 10
     for r, u in zip(reqs, utts):
         assert r.text == u.text
+
+
+def test_llm_inline_prefill_cpu(monkeypatch):
+    """Inline prefill (prompt tail fed through the decode steps) gives the same
+    greedy outputs as the separate prefill pass."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    outs = {}
+    for inline in ("0", "4096"):
+        monkeypatch.setenv("LOQA_INLINE_PREFILL", inline)
+        eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=8,
+                        max_seq_len=512, use_graphs=False)
+        assert eng.inline_prefill == int(inline)
+        texts = ["turn on the lights and play music", "dim the kitchen lights", "hello there"]
+        reqs = [GenRequest(eng.tok.encode(t, bos=True), multi_command_schema(n))
+                for t, n in zip(texts, (2, 1, 1))]
+        try:
+            eng.submit_batch(reqs).result(timeout=300)
+        finally:
+            eng.stop()
+        outs[inline] = [r.output for r in reqs]
+        assert eng.stats["prefill_tokens"] > 0
+    assert outs["0"] == outs["4096"]
