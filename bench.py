@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from loqa_hub_amd.engine.llm_engine import LLMEngine  # noqa: E402
 from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline, added_command_stats  # noqa: E402
 from loqa_hub_amd.engine.stt_engine import STTEngine  # noqa: E402
-from loqa_hub_amd.engine.synthetic import make_batch  # noqa: E402
+from loqa_hub_amd.engine.synthetic import make_batch, make_unique  # noqa: E402
 from loqa_hub_amd.messaging.nats_server import NATSServer  # noqa: E402
 from loqa_hub_amd.messaging.nats_service import NATSService  # noqa: E402
 from loqa_hub_amd.models.configs import llama_config, whisper_config  # noqa: E402
@@ -150,6 +150,19 @@ def main(argv=None) -> int:
             tasks.append(t)
         await asyncio.gather(*tasks)
 
+    # closed mode: every submission is a DISTINCT utterance (distinct
+    # transcript -> distinct prompt, so only the template text before the
+    # transcript can hit the prefix cache), drawn up front for the warmup and
+    # timed rounds; each stream's command count cycles through the mix
+    n_per_stream = args.warmup + args.steps
+    uniq = []
+    if args.mode == "closed":
+        counts = [mix[(ci + k) % len(mix)] for ci in range(B) for k in range(n_per_stream)]
+        uniq = make_unique(args.seed, counts, offset=info.rank * B * n_per_stream)
+
+    def next_utt(ci: int, k: int, record: bool):
+        return uniq[ci * n_per_stream + k + (args.warmup if record else 0)]
+
     async def run_closed(n: int, record: bool) -> None:
         """--mode closed (default): B concurrent relay streams per GPU, each a
         closed loop (its next utterance is sent when the previous one's reply
@@ -157,7 +170,7 @@ def main(argv=None) -> int:
         and join the running LLM decode batch (continuous batching)."""
         async def client(ci: int) -> None:
             for k in range(n):
-                u = mine[(ci + k) % len(mine)]
+                u = next_utt(ci, k, record)
                 j = PipelineJob(u.relay_id, f"req-{info.rank}-{ci}-{k}", u.pcm,
                                 transcript_hint=u.text)
                 await pipe.submit(j)
@@ -217,7 +230,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT, grammar-constrained LLM)",
+            "data": "synthetic speech-like PCM16, every utterance a distinct transcript (no repeated prompts) + random-init weights (teacher-forced STT, grammar-constrained LLM)",
             "config": {"model": f"{args.stt} + {args.llm}", "global_batch": info.world * B,
                        "seq_len": 1500, "parallelism": f"dp{info.world}",
                        "commands_mix": mix, "baseline_config": 4, "mode": args.mode,

@@ -239,6 +239,126 @@ extern "C" int loqa_shuffle_weight(const void* W, void* Wp, int N, int K, hipStr
 }
 
 // ============================================================================
+// x through LDS (XL): the mid-M form (Mpad 64 / 128: decode steps that carry a
+// chunked-prefill slice or long jump-forward runs). At M >= 64 the register
+// form above reads Mpad/16 KiB of activation fragments per 1 KiB weight
+// fragment, from L2, once per WAVE: at Mpad 64 the activation stream was 4x
+// the weight stream and the step took 2.2x the Mpad-16 time. In the XL form
+// the 4 waves of a workgroup own 4 row tiles over the SAME k range; each
+// U-k-step chunk of x is loaded once per workgroup (256 threads, 16-byte
+// pieces, prefetched into registers one chunk ahead) and written to LDS, and
+// every wave reads its MFMA B fragments from there (16 B per lane, rows padded
+// to XROW elements so a fragment read is bank-conflict free). Weights keep the
+// register ping-pong stream (one group of U k-steps in flight).
+constexpr int XROW = 40;   // LDS row: 32 k values + 8 pad (80 B: 16 lanes hit disjoint banks)
+
+template <int RT, int U>
+struct WFrag {
+  bf16x8 a[U][RT];
+};
+
+template <int RT, int U>
+__device__ __forceinline__ void load_w(WFrag<RT, U>& f, const bf16_t* wp, size_t tile_stride, int ks) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int i = 0; i < RT; ++i) f.a[u][i] = ldw(wp + (size_t)i * tile_stride + (size_t)(ks + u) * 512);
+}
+
+// one chunk of x: U k-steps x MP rows = MP * U * 4 pieces of 16 B
+template <int MP, int U>
+struct XRegs {
+  static constexpr int NP = (MP * U * 4) / 256;
+  uint4 v[NP];
+};
+
+template <int MP, int U>
+__device__ __forceinline__ void load_xc(XRegs<MP, U>& r, const bf16_t* x, long long ldx_, int ks) {
+#pragma unroll
+  for (int p = 0; p < XRegs<MP, U>::NP; ++p) {
+    const int idx = p * 256 + (int)threadIdx.x;
+    const int q = idx & 3, rest = idx >> 2;
+    const int row = rest % MP, u = rest / MP;
+    r.v[p] = *reinterpret_cast<const uint4*>(x + (size_t)row * ldx_ + (size_t)(ks + u) * 32 + q * 8);
+  }
+}
+
+template <int MP, int U>
+__device__ __forceinline__ void store_xc(const XRegs<MP, U>& r, bf16_t* xs) {
+#pragma unroll
+  for (int p = 0; p < XRegs<MP, U>::NP; ++p) {
+    const int idx = p * 256 + (int)threadIdx.x;
+    const int q = idx & 3, rest = idx >> 2;
+    const int row = rest % MP, u = rest / MP;
+    *reinterpret_cast<uint4*>(xs + (size_t)(u * MP + row) * XROW + q * 8) = r.v[p];
+  }
+}
+
+template <int RT, int MT, int U>
+__device__ __forceinline__ void mma_xl(const WFrag<RT, U>& f, float4v_ (&acc)[RT][MT], const bf16_t* xs,
+                                       int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    bf16x8 b[MT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(xs + (size_t)(u * MT * 16 + j * 16 + (lane & 15)) * XROW +
+                                              8 * (lane >> 4));
+#pragma unroll
+    for (int j = 0; j < MT; ++j)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(f.a[u][i], b[j], acc[i][j]);
+  }
+}
+
+// The XL stream. On entry chunk 0 of x (xr) and weight group 0 (f0) are in
+// flight, x issued first, so storing xr waits for x only. Each chunk: issue the
+// next chunk's x, then the next weight group (both unconditional, clamped to
+// the last chunk: no join point drains the prefetch, see stream_k), consume the
+// current chunk from LDS, then (barrier) overwrite LDS with the next chunk.
+template <int RT, int MT, int U>
+__device__ __forceinline__ void stream_k_xl(WFrag<RT, U>& f0, WFrag<RT, U>& f1, XRegs<MT * 16, U>& xr,
+                                            float4v_ (&acc)[RT][MT], const bf16_t* wp,
+                                            size_t tile_stride, const bf16_t* x, long long ldx_,
+                                            bf16_t* xs, int ks0, int ng, int lane) {
+  auto ks = [&](int g) { return ks0 + (g < ng ? g : ng - 1) * U; };
+  store_xc<MT * 16, U>(xr, xs);
+  lds_barrier();
+  int g = 0;
+  for (; g + 2 < ng; g += 2) {
+    load_xc<MT * 16, U>(xr, x, ldx_, ks(g + 1));
+    load_w(f1, wp, tile_stride, ks(g + 1));
+    __builtin_amdgcn_sched_barrier(0);
+    mma_xl(f0, acc, xs, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    store_xc<MT * 16, U>(xr, xs);
+    lds_barrier();
+    load_xc<MT * 16, U>(xr, x, ldx_, ks(g + 2));
+    load_w(f0, wp, tile_stride, ks(g + 2));
+    __builtin_amdgcn_sched_barrier(0);
+    mma_xl(f1, acc, xs, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    store_xc<MT * 16, U>(xr, xs);
+    lds_barrier();
+  }
+  if (g + 1 < ng) {
+    load_xc<MT * 16, U>(xr, x, ldx_, ks(g + 1));
+    load_w(f1, wp, tile_stride, ks(g + 1));
+    __builtin_amdgcn_sched_barrier(0);
+    mma_xl(f0, acc, xs, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    store_xc<MT * 16, U>(xr, xs);
+    lds_barrier();
+    mma_xl(f1, acc, xs, lane);
+  } else {
+    mma_xl(f0, acc, xs, lane);
+  }
+}
+
+// ============================================================================
 // Fused decode GEMMs: the skinny GEMM above with its follow-on op moved into
 // the epilogue and the preceding RMSNorm moved into the operand load, so a
 // Llama decode layer is 5 launches instead of 10:
@@ -273,7 +393,8 @@ struct FusedParams {
   const int* positions; const void* cs; void* q_out; void* kc; void* vc; const int* slots;
   int H, Hkv, D, blk;
   int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
-  int wr;                 // waves along the rows (1, or 4 with S == 1)
+  int wr;                 // waves along the rows (1, or 4 with S == 1; any S with xl)
+  int xl;                 // x through LDS (wr == 4; Mpad 64 / 128)
 };
 
 struct FusedArgs {
@@ -294,12 +415,17 @@ struct FusedArgs {
 // workgroup (L1 hits for the other 3) instead of once per wave, and no
 // cross-wave reduction is needed (measured on cold weights, M = 16: the
 // gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
-template <int RT, int MT, int U, int WR, int MODE, int NORM>
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   constexpr int WK = 4 / WR;                     // waves along K
   constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
   constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
+  static_assert(!XL || WR == 4, "XL needs the 4 waves along rows");
+  // XL + RoPE at MT 8: the RoPE cos/sin operands (RT * MT * 8 VGPRs) are
+  // loaded after the k loop instead of being held through it
+  constexpr bool EARLY_EPI = !(XL && MODE == EPI_ROPE && MT > 4);
   __shared__ __attribute__((aligned(16))) float smem[NSM];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   float4v_* red = reinterpret_cast<float4v_*>(smem);
   float* sred = smem;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -316,12 +442,19 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   // the first weight group is requested before the norm prologue: the row
   // statistics only scale the accumulator, so the stream need not wait for
   // them (the prologue's two L2 round trips then hide under the first fill)
-  Frag<RT, MT, U> f0, f1;
+  Frag<RT, MT, XL ? 1 : U> f0, f1;
+  WFrag<RT, XL ? U : 1> w0, w1;
+  XRegs<XL ? MT * 16 : 64, XL ? U : 1> xr;
   const int ng = kw / U;
   // (a k-start rotation per workgroup measured 5-10 % SLOWER on every shape:
   // the in-step x reuse across neighbouring workgroups in L2 matters more)
   const int rot = 0;
-  load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + rot * U);
+  if constexpr (XL) {
+    load_xc<MT * 16, U>(xr, a.x, a.ldx, ks0);      // x first: storing it waits for x only
+    load_w(w0, wp, tile_stride, ks0);
+  } else {
+    load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + rot * U);
+  }
 
   // Epilogue operands (residual tile, bias, LayerNorm column sums, RoPE
   // positions / cos-sin / cache slots) are requested now, by the epilogue
@@ -332,6 +465,31 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   float4 bvec[RT], cvec[RT];
   int eslot[MT];
   float2 ecs[RT][MT][4];
+  // RoPE epilogue operands: 16-row pair tiles, rows 0-7 = features c..c+7 of
+  // the first half, rows 8-15 = their RoPE partners c+D/2..; lanes (l>>4) & 1
+  // pick c's 4-row half
+  auto load_rope_ops = [&]() {
+    const int tph = a.D / 16, nq_t = a.H * tph, nk_t = a.Hkv * tph;
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = j * 16 + (lane & 15);
+      eslot[j] = a.slots[m];
+      if (a.cs) {
+        const int pos = a.positions[m];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const int pt = tile * RT + i;
+          if (pt < nq_t + nk_t) {
+            const int tt = pt >= nq_t ? pt - nq_t : pt;
+            const int c = (tt % tph) * 8 + 4 * ((lane >> 4) & 1);
+            const float2* e = a.cs + (size_t)pos * (a.D >> 1) + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ecs[i][j][r] = e[r];
+          }
+        }
+      }
+    }
+  };
 #pragma unroll
   for (int i = 0; i < RT; ++i) {
     bvec[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -365,29 +523,8 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         for (int i = 0; i < RT; ++i)
           rres[i][j] = *reinterpret_cast<const uint2*>(
               a.residual + (size_t)(j * 16 + (lane & 15)) * a.N + tile * (16 * RT) + i * 16 + nq);
-    } else if constexpr (MODE == EPI_ROPE) {
-      // 16-row pair tiles: rows 0-7 = features c..c+7 of the first half, rows
-      // 8-15 = their RoPE partners c+D/2..; lanes (l>>4) & 1 pick c's 4-row half
-      const int tph = a.D / 16, nq_t = a.H * tph, nk_t = a.Hkv * tph;
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int m = j * 16 + (lane & 15);
-        eslot[j] = a.slots[m];
-        if (a.cs) {
-          const int pos = a.positions[m];
-#pragma unroll
-          for (int i = 0; i < RT; ++i) {
-            const int pt = tile * RT + i;
-            if (pt < nq_t + nk_t) {
-              const int tt = pt >= nq_t ? pt - nq_t : pt;
-              const int c = (tt % tph) * 8 + 4 * ((lane >> 4) & 1);
-              const float2* e = a.cs + (size_t)pos * (a.D >> 1) + c;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ecs[i][j][r] = e[r];
-            }
-          }
-        }
-      }
+    } else if constexpr (MODE == EPI_ROPE && EARLY_EPI) {
+      load_rope_ops();
     }
   }
 
@@ -428,14 +565,14 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       }
       const float mean = ts / (float)a.K;
       const float var = fmaxf(tq / (float)a.K - mean * mean, 0.f);
-      sred[256 + threadIdx.x] = rsqrtf(var + a.eps);
-      sred[256 + 64 + threadIdx.x] = mean;
+      sred[768 + threadIdx.x] = rsqrtf(var + a.eps);   // [768, 896): up to Mpad 128 rows
+      sred[896 + threadIdx.x] = mean;
     }
     lds_barrier();
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
-      sc[j] = sred[256 + j * 16 + (lane & 15)];
-      mu[j] = sred[256 + 64 + j * 16 + (lane & 15)];
+      sc[j] = sred[768 + j * 16 + (lane & 15)];
+      mu[j] = sred[896 + j * 16 + (lane & 15)];
     }
     lds_barrier();
   }
@@ -445,7 +582,12 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (float4v_){0.f, 0.f, 0.f, 0.f};
-  stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, ng, rot);
+  if constexpr (XL) {
+    stream_k_xl(w0, w1, xr, acc, wp, tile_stride, a.x, a.ldx, xs, ks0, ng, lane);
+    if constexpr (MODE == EPI_ROPE && !EARLY_EPI) load_rope_ops();
+  } else {
+    stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, ng, rot);
+  }
 
   if constexpr (WK > 1) {
     // red[wr][wk - 1][i * MT + j][lane]
@@ -466,14 +608,16 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
           for (int q = 0; q < WK - 1; ++q) acc[i][j] += red[ridx(q, i * MT + j)];
     }
   }
-  if (WR == 1 && a.S > 1) {
+  if ((WR == 1 || XL) && a.S > 1) {
     // publish this split's partial (tile-contiguous slab, sc1 write-through),
     // take a ticket; the last arriver reduces with sc1 loads (no acquire fence:
-    // every handed-off byte is stored and loaded sc1, guide §6 Guideline 16)
+    // every handed-off byte is stored and loaded sc1, guide §6 Guideline 16).
+    // WR == 1: wave 0 holds the workgroup's tile; XL (WR == 4): every wave
+    // publishes and tickets its own tile.
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.part, 0, (int)((size_t)gridDim.x * a.S * RT * MT * 64 * 16), 0x00020000);
+        a.part, 0, (int)((size_t)gridDim.x * WR * a.S * RT * MT * 64 * 16), 0x00020000);
     const int slab0 = tile * a.S * RT * MT;
-    if (wave == 0) {
+    if (WR > 1 || wave == 0) {
 #pragma unroll
       for (int i = 0; i < RT; ++i)
 #pragma unroll
@@ -483,16 +627,27 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
               (((slab0 + s * RT * MT) + i * MT + j) * 64 + lane) * 16, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int t = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      if (t == a.S - 1)
-        __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sred[0] = (float)t;
+    if constexpr (WR > 1) {
+      int t = 0;
+      if (lane == 0) {
+        t = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == a.S - 1)
+          __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      t = __shfl(t, 0, 64);
+      if (t != a.S - 1) return;
+    } else {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add(&a.counters[tile], 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (t == a.S - 1)
+          __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sred[0] = (float)t;
+      }
+      __syncthreads();
+      if ((int)sred[0] != a.S - 1 || wave != 0) return;
     }
-    __syncthreads();
-    if ((int)sred[0] != a.S - 1 || wave != 0) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // fixed summation order (split 0..S-1) whichever block arrives last
     float4v_ tot[RT][MT];
@@ -721,6 +876,28 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
   }
 }
 
+// XL dispatch: Mpad 64 (MT 4) / 128 (MT 8), 4 waves along rows, any split-K.
+// Prefetch group = one LDS chunk: 4 k-steps, 2 when the VGPR budget is tight.
+template <int RT, int MT, int MODE, int NORM>
+static int launch_xl(const FusedArgs& a, hipStream_t st) {
+  dim3 grid(a.N / (16 * RT * 4), a.S);
+  const int kw = a.K / 32 / a.S;
+  constexpr int UA = (RT * MT >= 16) ? 2 : 4;
+  if (kw % UA == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, UA, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
+  else if (kw % 2 == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, int NORM>
+static int dispatch_xl(const FusedArgs& a, int rt, hipStream_t st) {
+  if (a.Mpad == 64) return rt == 2 ? launch_xl<2, 4, MODE, NORM>(a, st) : launch_xl<1, 4, MODE, NORM>(a, st);
+  return rt == 2 ? launch_xl<2, 8, MODE, NORM>(a, st) : launch_xl<1, 8, MODE, NORM>(a, st);
+}
+
 // rt: rows per output tile / 16 (1 or 2, every mode: the paired epilogues pair
 // rows inside each 16-row tile through a lane shuffle, so 16-row tiles give
 // twice the workgroups without a K split, i.e. without a reduction tail).
@@ -738,7 +915,15 @@ static int dispatch_fused(const FusedArgs& a, int rt, int wr, hipStream_t st) {
 }
 
 template <int MODE>
-static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, hipStream_t st) {
+static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, hipStream_t st) {
+  if (xl) {
+    switch (norm) {
+      case NORM_NONE: return dispatch_xl<MODE, NORM_NONE>(a, rt, st);
+      case NORM_RMS: return dispatch_xl<MODE, NORM_RMS>(a, rt, st);
+      case NORM_LN: return dispatch_xl<MODE, NORM_LN>(a, rt, st);
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   switch (norm) {
     case NORM_NONE: return dispatch_fused<MODE, NORM_NONE>(a, rt, wr, st);
     case NORM_RMS: return dispatch_fused<MODE, NORM_RMS>(a, rt, wr, st);
@@ -756,7 +941,10 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, hipStream
 // the residual epilogue are written per (16*rt)-row tile.
 extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   const int Mpad = p->Mpad, N = p->N, K = p->K, S = p->S;
-  if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 || (Mpad != 16 && Mpad != 32 && Mpad != 64))
+  if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 ||
+      (Mpad != 16 && Mpad != 32 && Mpad != 64 && !(Mpad == 128 && p->xl)))
+    return (int)hipErrorInvalidValue;
+  if (p->xl && (p->wr != 4 || Mpad < 64 || (p->rt != 1 && p->rt != 2) || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;
   if (S > 1 && (!p->part || !p->counters)) return (int)hipErrorInvalidValue;
   if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1)) return (int)hipErrorInvalidValue;
@@ -767,7 +955,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if (p->rt != 1 && p->rt != 2 && !(p->rt == 4 && Mpad == 64)) return (int)hipErrorInvalidValue;
   if (p->mode == EPI_RESID && (!p->residual || !p->rowsq_out)) return (int)hipErrorInvalidValue;
-  if (p->wr != 1 && (p->wr != 4 || S != 1 || N % (64 * p->rt)))
+  if (p->wr != 1 && (p->wr != 4 || (S != 1 && !p->xl) || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;
   FusedArgs a{(const bf16_t*)p->x, p->ldx, (const bf16_t*)p->Wp, p->part, N, K, S, Mpad,
               p->counters, p->rowsq_in, p->rowsum_in, p->rowstat_tiles, p->eps, p->colsum,
@@ -775,10 +963,10 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   switch (p->mode) {
-    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, st);
-    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, st);
-    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, p->rt, p->wr, st);
-    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, p->rt, p->wr, st);
+    case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, p->xl, st);
+    case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, p->xl, st);
+    case EPI_ROPE: return dispatch_norm<EPI_ROPE>(a, p->norm, p->rt, p->wr, p->xl, st);
+    case EPI_ACT: return dispatch_norm<EPI_ACT>(a, p->norm, p->rt, p->wr, p->xl, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -477,6 +477,7 @@ class LLMEngine:
         tune_switch_interval()
         self._inbox: queue.Queue = queue.Queue()
         self._running = True
+        stream_priority = int(os.environ.get("LOQA_LLM_PRIORITY", stream_priority))
         self._sched = threading.Thread(target=self._schedule, args=(stream_priority,),
                                        name="llm-scheduler", daemon=True)
         self._sched.start()

@@ -78,3 +78,24 @@ def make_utterance(seed: int, index: int, n_commands: int, relay_id: str | None 
 def make_batch(seed: int, n: int, commands_mix: list[int], offset: int = 0) -> list[SyntheticUtterance]:
     return [make_utterance(seed, offset + i, commands_mix[(offset + i) % len(commands_mix)])
             for i in range(n)]
+
+
+def make_unique(seed: int, counts: list[int], offset: int = 0,
+                seen: set[str] | None = None, max_tries: int = 64) -> list[SyntheticUtterance]:
+    """Utterances with ``counts[i]`` commands each, no two of which (here or in
+    ``seen``) share a transcript: every LLM prompt is then distinct, so the
+    prefix cache can only reuse the template text before the transcript, as
+    with real traffic (a cycled set of utterances would let whole prompts hit
+    the cache)."""
+    seen = set() if seen is None else seen
+    out = []
+    for i, nc in enumerate(counts):
+        for t in range(max_tries):
+            u = make_utterance(seed + 7919 * t, offset + i, nc)
+            if u.text not in seen:
+                break
+        else:
+            raise RuntimeError("could not draw a distinct utterance")
+        seen.add(u.text)
+        out.append(u)
+    return out

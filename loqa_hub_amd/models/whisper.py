@@ -88,11 +88,12 @@ class WhisperWeights:
                 ops.tune_skinny_splits(self.dec_p[0][k], mpads=(16, 32))
             ops.tune_skinny_splits(self.lm_head_p, mpads=(16, 32))
             F = self.dec_f[0]
-            ops.tune_fused(F["qkv"], "rope", heads=(cfg.n_heads, cfg.n_heads, cfg.head_dim))
-            ops.tune_fused(F["o"], "resid")
-            ops.tune_fused(F["xq"], "act")
-            ops.tune_fused(F["fc1"], "act", act="gelu")
-            ops.tune_fused(F["fc2"], "resid")
+            MP = (16, 32, 64)   # a Whisper decoder step never exceeds 64 tokens
+            ops.tune_fused(F["qkv"], "rope", heads=(cfg.n_heads, cfg.n_heads, cfg.head_dim), mpads=MP, xl=False)
+            ops.tune_fused(F["o"], "resid", mpads=MP, xl=False)
+            ops.tune_fused(F["xq"], "act", mpads=MP, xl=False)
+            ops.tune_fused(F["fc1"], "act", act="gelu", mpads=MP, xl=False)
+            ops.tune_fused(F["fc2"], "resid", mpads=MP, xl=False)
 
     @classmethod
     def from_tensors(cls, cfg: WhisperConfig, *, conv1_w, conv1_b, conv2_w, conv2_b, pos_enc, enc,

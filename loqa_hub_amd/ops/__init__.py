@@ -454,7 +454,7 @@ class contended_tuning:
 
 
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
-                      wr4: bool = False, fewest: bool = True) -> tuple[int, int, int]:
+                      wr4: bool = False, fewest: bool = True, xl: str = "no") -> tuple:
     """(split-K, tile rows / 16, waves along rows) for a fused-epilogue GEMM,
     measured: ``run(s, rt, wr, i)`` launches it on weight copy ``i`` (the graph
     cycles through ``ncopies`` copies so every call streams COLD weights, as a
@@ -463,7 +463,9 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
     The in-launch reduce adds a store-drain + ticket round trip to every
     workgroup's tail, so the best split is lower than the plain GEMM's; 16-row
     tiles (rt=1, residual / act epilogues only) double the workgroups without
-    any reduction; ``wr4`` adds the 4-waves-along-rows layout (S = 1 only).
+    any reduction; ``wr4`` adds the 4-waves-along-rows layout (S = 1 only). ``xl``: "no",
+    "also" (add the x-through-LDS layouts, any split) or "only" (Mpad 128).
+    Returns (split-K, rt, wr) or (split-K, rt, 4, 1) for an XL layout.
     ``key`` = (mode, N, K, Mpad)."""
     if key in _FSPLITS:
         return _FSPLITS[key]
@@ -472,9 +474,13 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
         _FSPLITS[key] = ov
         return ov
     N = key[1]
-    cands = [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
-    if wr4:
+    cands = [] if xl == "only" else \
+        [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
+    if wr4 and xl != "only":
         cands += [(1, rt, 4) for rt in rts if N % (64 * rt) == 0]
+    if xl != "no":
+        cands += [(s, rt, 4, 1) for rt in (1, 2) for s in SPLIT_CANDIDATES
+                  if K % (s * 128) == 0 and N % (64 * rt) == 0]
     # co-scheduling cap: the STT and LLM decoders run concurrently on their own
     # streams; a grid that fills every CU slot makes the other stream's small
     # latency-bound kernels wait for it to drain (measured: a 768-workgroup
@@ -495,11 +501,11 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
         # (fastest alone) and 11.0 for 224 4-wave 32-row workgroups.
         capped = cands[:1]
     cands = capped
-    best, best_t = (1, rts[-1], 1), float("inf")
+    best, best_t = cands[0] if xl == "only" else (1, rts[-1], 1), float("inf")
     n = max(1, ncopies)
     for c in cands:
         it = iter(range(1 << 30))
-        t = graph_time(lambda: run(*c, next(it) % n), max(reps, 2 * n))
+        t = graph_time(lambda: run(*c[:3], next(it) % n, *c[3:]), max(reps, 2 * n))
         if t < best_t * 0.98:
             best, best_t = c, t
     _FSPLITS[key] = best
@@ -968,8 +974,9 @@ class FusedLinear:
         self.N, self.K = w.shape
 
 
-def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none",
-               heads: tuple | None = None, cos_sin=None, prefill: bool = False) -> None:
+def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = "none",
+               heads: tuple | None = None, cos_sin=None, prefill: bool = False,
+               xl: bool = True) -> None:
     """Measure the split-K of one fused decode GEMM shape on dummy operands
     (``heads`` = (H, Hkv, D) for "rope"); before any graph capture.
     ``prefill``: Mpad 64 is the chunked prefill of compact weights (a whole
@@ -996,7 +1003,10 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
         else:
             c = wp.clone()
         copies.append(c)
+    xl_on = xl and os.environ.get("LOQA_TUNE_XL", "1") != "0"
     for Mpad in mpads:
+        if Mpad == 128 and not xl_on:
+            continue
         key = (mode, N, K, Mpad)
         if key in _FSPLITS:
             continue
@@ -1012,16 +1022,21 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64), norm=None, act: str = "none
             kw.update(act=act)
         elif mode == "rope":
             H, Hkv, D = heads
-            kc = torch.zeros(4, Hkv, 16, D, **bf)
+            kc = torch.zeros(max(4, Mpad // 16), Hkv, 16, D, **bf)   # one slot per row
             pos = torch.arange(Mpad, dtype=torch.int32, device=dev)
             kw.update(positions=pos, cos_sin=cos_sin, q_out=torch.empty(Mpad, H * D, **bf),
                       k_cache=kc, v_cache=torch.zeros_like(kc), slots=pos, n_heads=H, n_kv=Hkv,
                       head_dim=D)
         wide = Mpad <= 32 or prefill
         rts = (1, 2, 4) if (prefill and Mpad == 64) else (1, 2)
-        tune_fused_splits(key, lambda sp, rt, wr, i: skinny_fused(
-            x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, **kw), K, rts=rts,
-            ncopies=len(copies), wr4=wide, fewest=wide)
+        # XL layouts at Mpad 64 win in isolation but, as decode steps beside the
+        # Whisper decoder, took the pipeline from 17.6 to 10.3 utt/s (long-lived
+        # 4-wave workgroups: the co-scheduling cliff, docs/PERF.md): opt-in only
+        xl = "only" if Mpad == 128 else (
+            "also" if Mpad == 64 and xl_on and os.environ.get("LOQA_TUNE_XL64") == "1" else "no")
+        tune_fused_splits(key, lambda sp, rt, wr, i, xl_=0: skinny_fused(
+            x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, xl=xl_, **kw), K, rts=rts,
+            ncopies=len(copies), wr4=wide, fewest=wide, xl=xl)
     del copies
 
 
@@ -1037,8 +1052,10 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
                  residual: torch.Tensor | None = None, positions=None, cos_sin=None, q_out=None,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
-                 row_sums: bool = False, wr: int | None = None) -> torch.Tensor:
-    """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32 or 64.
+                 row_sums: bool = False, wr: int | None = None, xl: int | None = None) -> torch.Tensor:
+    """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32,
+    64 or 128 (``xl``: activations staged through LDS, 4 waves along rows,
+    required at Mpad 128; chosen by the tuner at 64).
 
     ``wp`` is a shuffled weight or a ``FusedLinear`` (which supplies the norm
     kind unless ``norm`` is given, the folded bias and the LayerNorm column
@@ -1061,10 +1078,15 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     nrm = _NORMS[norm]
     tuned = _FSPLITS.get((mode, N, K, Mpad))
     S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
-    rt = rt or (tuned[1] if tuned else 2)
+    rt = rt or (tuned[1] if tuned else (1 if Mpad == 128 else 2))
+    if xl is None:
+        xl = tuned[3] if (tuned and not splits and len(tuned) > 3) else int(Mpad == 128)
     if wr is None:
         wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
-    if wr != 1 and (S != 1 or N % (64 * rt)):
+    if xl:
+        wr = 4
+        rt = rt if rt in (1, 2) and N % (64 * rt) == 0 else 1
+    elif wr != 1 and (S != 1 or N % (64 * rt)):
         wr = 1
     if rowsq_tiles is None:
         rowsq_tiles = scratch.stat_tiles
@@ -1080,12 +1102,18 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
         return _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual,
                                  positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
                                  n_kv, head_dim, out, act, bias, colsum, row_sums, rt)
-    assert Mpad in (16, 32, 64) and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert Mpad in (16, 32, 64, 128) and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert Mpad != 128 or xl, "Mpad 128 needs the XL layout"
     assert ntiles <= scratch.counters.numel() and ntiles * Mpad <= scratch.rowsq.numel()
     if nrm == 2:
         assert colsum is not None and colsum.numel() == N
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.numel() == N and bias.is_contiguous()
+    if mode == "rope":   # the epilogue reads slots / positions for every padded row
+        assert slots.numel() >= Mpad and q_out.shape[0] >= Mpad and k_cache.is_contiguous()
+        assert cos_sin is None or positions.numel() >= Mpad
+    elif mode == "resid":
+        assert residual.shape[0] >= Mpad and residual.shape[1] == N
     part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device) if S > 1 else None
     blk = k_cache.shape[2] if k_cache is not None else 0
     p = FusedParams()
@@ -1103,7 +1131,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.positions, p.cs, p.q_out = ptr(positions), ptr(cos_sin), ptr(q_out)
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
-    p.rt, p.wr = rt, wr
+    p.rt, p.wr, p.xl = rt, wr, int(bool(xl))
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out

@@ -39,7 +39,7 @@ class FusedParams(ctypes.Structure):
         ("positions", c_void_p), ("cs", c_void_p), ("q_out", c_void_p), ("kc", c_void_p),
         ("vc", c_void_p), ("slots", c_void_p),
         ("H", c_int), ("Hkv", c_int), ("D", c_int), ("blk", c_int),
-        ("rt", c_int), ("wr", c_int),
+        ("rt", c_int), ("wr", c_int), ("xl", c_int),
     ]
 
 

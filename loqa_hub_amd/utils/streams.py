@@ -68,13 +68,62 @@ def cu_masked_stream(device: torch.device, cus: list[int]) -> torch.cuda.Externa
     return torch.cuda.ExternalStream(handle.value, device=device)
 
 
+# ---------------------------------------------------------------- pool slots
+# PyTorch hands out pool streams round-robin (32 per priority); HIP places a
+# process's streams on its few hardware queues by creation order, so a pool
+# stream's INDEX decides its hardware queue. Which queues the decoder streams
+# share is worth 11 vs 19 utt/s (docs/PERF.md, "the 1.8x cliff"), and before
+# this the index a decoder got depended on how many pool streams the tuner had
+# drawn first. ``pool_slot`` identifies a pool stream's index from its handle;
+# ``aligned_pool_stream`` draws streams until the next one has a given index.
+POOL_SIZE = 32
+_POOL_TABLES: dict = {}
+
+
+def _pool_table(device: torch.device, priority: int) -> list[int]:
+    d = torch.device(device)
+    key = (d.index if d.index is not None else torch.cuda.current_device(), priority)
+    tab = _POOL_TABLES.get(key)
+    if tab is None:
+        # one full cycle of the pool: the cursor ends where it started
+        tab = [torch.cuda.Stream(d, priority=priority).cuda_stream for _ in range(POOL_SIZE)]
+        _POOL_TABLES[key] = tab
+    return tab
+
+
+def pool_slot(stream, device: torch.device, priority: int) -> int:
+    tab = _pool_table(device, priority)
+    try:
+        return tab.index(stream.cuda_stream)
+    except ValueError:
+        return -1
+
+
+def aligned_pool_stream(device: torch.device, priority: int, slot: int):
+    """The pool stream with index ``slot`` (mod 32) of this priority's pool."""
+    tab = _pool_table(device, priority)
+    for _ in range(POOL_SIZE + 1):
+        st = torch.cuda.Stream(device, priority=priority)
+        if tab.index(st.cuda_stream) == slot % POOL_SIZE:
+            return st
+    raise RuntimeError("pool stream slot not found")
+
+
+def _log_slot(role: str, st, device, priority: int) -> None:
+    if os.environ.get("LOQA_LOG_STREAMS"):
+        print(f"[streams] {role}: priority {priority} pool slot {pool_slot(st, device, priority)}",
+              flush=True)
+
+
 def pool_stream(device: torch.device, role: str, priority: int = 0):
     """A PyTorch pool stream for a worker thread, first drawing
     ``LOQA_POOL_SKEW_<ROLE>`` extra pool streams (hardware-queue placement
     search; see decoder_streams)."""
     for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{role.upper()}", "0") or 0)):
         torch.cuda.Stream(device, priority=priority)
-    return torch.cuda.Stream(device, priority=priority)
+    st = torch.cuda.Stream(device, priority=priority)
+    _log_slot(role, st, device, priority)
+    return st
 
 
 _decoders: dict = {}
@@ -140,7 +189,9 @@ def stream_for(device: torch.device, env_key: str, priority: int = 0):
         # decoder n hardware queues along (placement search).
         for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{(role or '').upper()}", "0") or 0)):
             torch.cuda.Stream(device, priority=priority)
-        return torch.cuda.Stream(device, priority=priority)
+        st = torch.cuda.Stream(device, priority=priority)
+        _log_slot(role or env_key, st, device, priority)
+        return st
     _PRIO[role] = priority
     prios = {"stt": _PRIO.get("stt", -1), "llm": _PRIO.get("llm", 0)}
     return decoder_streams(device, prios)[role]

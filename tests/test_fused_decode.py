@@ -159,7 +159,65 @@ def test_fused_rows_per_wave_layout_gpu(mode, Mpad, rt):
             assert rel < 1e-2, (wr, rel)
 
 
-def _ln_case(dev, S=None, Mpad=16, rt=2):
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
+@pytest.mark.parametrize("Mpad,rt,S", [(64, 1, 1), (64, 2, 2), (128, 1, 1), (128, 1, 2),
+                                       (128, 2, 1), (128, 2, 4)])
+@pytest.mark.parametrize("norm", [None, "rms"])
+def test_fused_xl_layout_gpu(mode, Mpad, rt, S, norm):
+    """The x-through-LDS (XL) layout of the fused GEMM (Mpad 64 / 128, 4 waves
+    along rows, per-wave split-K tickets) against the fp32 CPU reference of
+    the same call, with and without the RMSNorm prologue."""
+    from loqa_hub_amd.ops import reference as ref
+    if norm and mode == "resid":
+        pytest.skip("no residual GEMM takes a norm prologue (it would rewrite the statistics it reads)")
+    torch.manual_seed(5)
+    K = 1024
+    H, Hkv, D = 8, 2, 64
+    N = {"resid": 512, "silu": 1024, "act": 512, "rope": (H + 2 * Hkv) * D}[mode]
+    x = torch.randn(Mpad, K).bfloat16()
+    w = (torch.randn(N, K) * 0.03).bfloat16()
+    if mode == "silu":
+        w = w[ref.perm_gate_up(N // 2)].contiguous()
+    elif mode == "rope":
+        w = w[ref.perm_rope_qkv(H, Hkv, D)].contiguous()
+    res0 = torch.randn(Mpad, N).bfloat16()
+    cs = ref.rope_cos_sin(D, 512, 10000.0)
+    tiles = 4
+    rowsq = torch.rand(tiles * Mpad) * 300 + 50
+
+    def run(dev):
+        wp = ops.shuffle_weight(w.to(dev))
+        scr = ops.FusedScratch(dev)
+        kw = dict(splits=S, wr=4, rt=rt, xl=1)
+        if norm:
+            scr.rowsq[: tiles * Mpad].copy_(rowsq.to(dev))
+            kw.update(norm=norm, rowsq_tiles=tiles)
+        xd = x.to(dev)
+        if mode == "resid":
+            res = res0.clone().to(dev)
+            ops.skinny_fused(xd, wp, "resid", scr, residual=res, **kw)
+            return [res.float().cpu(), scr.rowsq[: (N // (16 * rt)) * Mpad].float().cpu()]
+        if mode == "rope":
+            kc = torch.zeros(Mpad // 16, Hkv, 16, D, device=dev).bfloat16()
+            vc = torch.zeros_like(kc)
+            pos = (torch.arange(Mpad, dtype=torch.int32) * 3 + 5).to(dev)
+            slots = torch.arange(Mpad, dtype=torch.int32, device=dev)
+            q = torch.empty(Mpad, H * D, device=dev).bfloat16()
+            ops.skinny_fused(xd, wp, "rope", scr, positions=pos, cos_sin=cs.to(dev), q_out=q,
+                             k_cache=kc, v_cache=vc, slots=slots, n_heads=H, n_kv=Hkv,
+                             head_dim=D, **kw)
+            return [q.float().cpu(), kc.float().cpu(), vc.float().cpu()]
+        return [ops.skinny_fused(xd, wp, mode, scr, **kw).float().cpu()]
+
+    expect = run("cpu")
+    got = run("cuda")
+    for a, b in zip(got, expect):
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-6))
+        assert rel < 1e-2, rel
+
+
+def _ln_case(dev, S=None, Mpad=16, rt=2, xl=None):
     """LayerNorm-prologue GEMM (folded weight / shift / bias) with a GELU
     epilogue, against layernorm -> linear -> gelu in fp32."""
     torch.manual_seed(1)
@@ -172,7 +230,8 @@ def _ln_case(dev, S=None, Mpad=16, rt=2):
     lin = ops.FusedLinear(w, norm="ln", norm_w=g, norm_b=b, bias=bias)
     scr = ops.FusedScratch(dev)
     scr.seed_stats(x)
-    y = ops.skinny_fused(x, lin, "act", scr, splits=S, act="gelu", eps=1e-5, rowsq_tiles=1, rt=rt)
+    y = ops.skinny_fused(x, lin, "act", scr, splits=S, act="gelu", eps=1e-5, rowsq_tiles=1, rt=rt,
+                         xl=xl)
     h = torch.nn.functional.layer_norm(x.float(), (K,), g.float(), b.float(), 1e-5)
     expect = torch.nn.functional.gelu(h @ w.float().t() + bias.float())
     rel = float((y.float() - expect).norm() / expect.norm())
@@ -182,7 +241,7 @@ def _ln_case(dev, S=None, Mpad=16, rt=2):
     a = (torch.randn(Mpad, N, device=dev) * 0.5).bfloat16()
     wo = (torch.randn(K, N, device=dev) * 0.05).bfloat16()
     ops.skinny_fused(a, ops.FusedLinear(wo, bias=bias[:K]), "resid", scr,
-                     splits=S, residual=res, row_sums=True, rt=rt)
+                     splits=S, residual=res, row_sums=True, rt=rt, xl=xl)
     tiles = K // (16 * rt)
     assert scr.stat_tiles == tiles
     sm = scr.rowsum[: tiles * Mpad].view(tiles, Mpad).sum(0)
@@ -200,6 +259,12 @@ def test_fused_layernorm_act_cpu():
                                        (1, 16, 1), (2, 32, 1), (2, 64, 1)])
 def test_fused_layernorm_act_gpu(S, Mpad, rt):
     _ln_case("cuda", S, Mpad, rt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,Mpad,rt", [(1, 128, 1), (2, 128, 2), (1, 64, 1)])
+def test_fused_layernorm_act_xl_gpu(S, Mpad, rt):
+    _ln_case("cuda", S, Mpad, rt, xl=1)
 
 
 @pytest.mark.gpu
