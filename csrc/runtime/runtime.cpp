@@ -314,6 +314,65 @@ int loqa_pool_cache_prefix(void* h, long long seq_id, const int32_t* toks, int n
   return 0;
 }
 
+// One decode / prefill step's KV metadata in a single call (the per-sequence
+// seq_len / append / block_table round trips from Python cost ~50 us per
+// sequence per step on the scheduler's critical path). For the B sequences,
+// append n[i] tokens each and fill, for a padded step of T_pad tokens and
+// B_pad sequences: positions / slots (concatenated per sequence; padding rows
+// position 0, slot -1), cu_q [B_pad + 1] (padding sequences empty), ctx_lens
+// [B_pad], block_tables [B_pad][max_blocks] (zero padded) and, if lidx, the
+// index of each sequence's last token (lidx_len entries, rest 0).
+// Returns 0; -1 unknown sequence, -2 out of KV blocks, -3 shape overflow.
+int loqa_pool_step_meta(void* h, int B, const long long* seq_ids, const int* n, int B_pad, int T_pad,
+                        int max_blocks, int32_t* positions, int32_t* slots, int32_t* cu, int32_t* ctx,
+                        int32_t* bt, long long* lidx, int lidx_len) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  if (B > B_pad || (lidx && B > lidx_len)) return -3;
+  int T = 0;
+  for (int i = 0; i < B; ++i) T += n[i];
+  if (T > T_pad) return -3;
+  for (int i = 0; i < T_pad; ++i) {
+    positions[i] = 0;
+    slots[i] = -1;
+  }
+  std::memset(bt, 0, sizeof(int32_t) * (size_t)B_pad * max_blocks);
+  const int bs = p->block_size;
+  int off = 0;
+  cu[0] = 0;
+  for (int i = 0; i < B; ++i) {
+    auto it = p->seqs.find(seq_ids[i]);
+    if (it == p->seqs.end()) return -1;
+    Seq& sq = it->second;
+    for (int j = 0; j < n[i]; ++j) {
+      const long long pos = sq.len + j;
+      const int bi = (int)(pos / bs);
+      if (bi >= (int)sq.blocks.size()) {
+        const int32_t b = p->take();
+        if (b < 0) return -2;
+        sq.blocks.push_back(b);
+      }
+      positions[off + j] = (int32_t)pos;
+      slots[off + j] = sq.blocks[bi] * bs + (int)(pos % bs);
+    }
+    sq.len += n[i];
+    off += n[i];
+    cu[i + 1] = off;
+    ctx[i] = (int32_t)sq.len;
+    const int nb = (int)sq.blocks.size();
+    if (nb > max_blocks) return -3;
+    std::memcpy(bt + (size_t)i * max_blocks, sq.blocks.data(), sizeof(int32_t) * nb);
+    if (lidx) lidx[i] = off - 1;
+  }
+  for (int i = B; i < B_pad; ++i) {
+    cu[i + 1] = off;
+    ctx[i] = 0;
+  }
+  if (lidx)
+    for (int i = B; i < lidx_len; ++i) lidx[i] = 0;
+  return 0;
+}
+
 int loqa_pool_block_table(void* h, long long seq_id, int32_t* out, int max_blocks) {
   auto* p = static_cast<BlockPool*>(h);
   std::lock_guard<std::mutex> g(p->mu);

@@ -105,6 +105,40 @@ class PyBlockPool:
         for b in self.seqs.pop(seq_id)["blocks"]:
             self._release(b)
 
+    def step_meta(self, seq_ids, ns, B_pad, T_pad, max_blocks, positions, slots, cu, ctx, bt,
+                  lidx=None) -> int:
+        """Same contract as the native ``loqa_pool_step_meta``."""
+        if len(seq_ids) > B_pad or sum(ns) > T_pad or (lidx is not None and len(seq_ids) > len(lidx)):
+            return -3
+        positions[:T_pad] = 0
+        slots[:T_pad] = -1
+        bt[:B_pad] = 0
+        off = 0
+        cu[0] = 0
+        for i, (sid, n) in enumerate(zip(seq_ids, ns)):
+            if sid not in self.seqs:
+                return -1
+            start = self.seqs[sid]["len"]
+            sl = self.append(sid, n)
+            if sl is None:
+                return -2
+            positions[off:off + n] = range(start, start + n)
+            slots[off:off + n] = sl
+            off += n
+            cu[i + 1] = off
+            ctx[i] = start + n
+            tab = self.seqs[sid]["blocks"]
+            if len(tab) > max_blocks:
+                return -3
+            bt[i, :len(tab)] = tab
+            if lidx is not None:
+                lidx[i] = off - 1
+        cu[len(seq_ids) + 1:B_pad + 1] = off
+        ctx[len(seq_ids):B_pad] = 0
+        if lidx is not None:
+            lidx[len(seq_ids):] = 0
+        return 0
+
 
 class NativeBlockPool:
     def __init__(self, num_blocks: int, block_size: int):
@@ -155,6 +189,26 @@ class NativeBlockPool:
 
     def free_seq(self, seq_id: int) -> None:
         self.lib.loqa_pool_free_seq(self.h, seq_id)
+
+    def step_meta(self, seq_ids, ns, B_pad, T_pad, max_blocks, positions, slots, cu, ctx, bt,
+                  lidx=None) -> int:
+        """One call for a whole step's KV metadata (see runtime.cpp); the numpy
+        outputs must be C-contiguous int32 (``lidx`` int64)."""
+        ids = np.asarray(seq_ids, dtype=np.int64)
+        nn = np.asarray(ns, dtype=np.int32)
+        vp = ctypes.c_void_p
+        for a in (positions, slots, cu, ctx, bt):
+            assert a.dtype == np.int32 and a.flags.c_contiguous
+        if lidx is not None:
+            assert lidx.dtype == np.int64 and lidx.flags.c_contiguous
+        assert positions.size >= T_pad and slots.size >= T_pad and cu.size >= B_pad + 1
+        assert ctx.size >= B_pad and bt.size >= B_pad * max_blocks
+        return int(self.lib.loqa_pool_step_meta(
+            self.h, len(ids), ids.ctypes.data_as(vp), nn.ctypes.data_as(vp), B_pad, T_pad,
+            max_blocks, positions.ctypes.data_as(vp), slots.ctypes.data_as(vp),
+            cu.ctypes.data_as(vp), ctx.ctypes.data_as(vp), bt.ctypes.data_as(vp),
+            lidx.ctypes.data_as(vp) if lidx is not None else None,
+            len(lidx) if lidx is not None else 0))
 
 
 def make_block_pool(num_blocks: int, block_size: int, require_native: bool):

@@ -177,9 +177,7 @@ class STTEngine:
                    out: dict | None = None) -> tuple[int, dict]:
         T_enc = self.cfg.n_audio_ctx
         L = max(16, ops.mpad_for(B_pad))
-        if out is not None:  # preallocated pinned views (graph path)
-            for k, a in out.items():
-                a.fill(-1 if k == "slots" else 0)
+        if out is not None:  # preallocated pinned views (graph path), filled below
             tokens, positions, slots = out["tokens"], out["positions"], out["slots"]
             cu, ctx, bt = out["cu_q"], out["ctx_lens"], out["block_tables"]
             enc_starts, enc_lens, lidx = out["enc_starts"], out["enc_lens"], out["logit_idx"]
@@ -193,28 +191,22 @@ class STTEngine:
             enc_starts = np.zeros(B_pad, np.int32)
             enc_lens = np.zeros(B_pad, np.int32)
             lidx = np.zeros(L, np.int64)
-        off, max_q = 0, 1
-        pool = self.kv.pool
-        for j, r in enumerate(live):
-            f = r.feed
-            n = len(f)
-            start = pool.seq_len(r.seq_id)
-            sl = pool.append(r.seq_id, n)
-            if sl is None:
-                raise RuntimeError("STT KV cache exhausted")
-            tokens[off:off + n] = f
-            positions[off:off + n] = np.arange(start, start + n)
-            slots[off:off + n] = sl
-            off += n
-            cu[j + 1] = off
-            ctx[j] = start + n
-            tab = pool.block_table(r.seq_id)
-            bt[j, :len(tab)] = tab
-            enc_starts[j] = r.slot * T_enc
-            enc_lens[j] = T_enc
-            lidx[j] = off - 1
-            max_q = max(max_q, n)
-        cu[len(live) + 1:] = off
+        T = sum(len(r.feed) for r in live)
+        tokens.fill(0)
+        if T:
+            tokens[:T] = [t for r in live for t in r.feed]
+        rc = self.kv.pool.step_meta([r.seq_id for r in live], [len(r.feed) for r in live], B_pad,
+                                    T_pad, self.max_blocks, positions, slots, cu, ctx, bt, lidx)
+        if rc == -2:
+            raise RuntimeError("STT KV cache exhausted")
+        if rc != 0:
+            raise RuntimeError(f"step metadata failed ({rc})")
+        n = len(live)
+        enc_starts[:n] = [r.slot * T_enc for r in live]
+        enc_starts[n:] = 0
+        enc_lens[:n] = T_enc
+        enc_lens[n:] = 0
+        max_q = max([len(r.feed) for r in live] + [1])
         return max_q, {"tokens": tokens, "positions": positions, "slots": slots, "cu_q": cu,
                        "ctx_lens": ctx, "block_tables": bt, "enc_starts": enc_starts,
                        "enc_lens": enc_lens, "logit_idx": lidx}
@@ -531,7 +523,7 @@ class STTEngine:
         # the running decoder batch (an arrival's encode no longer stalls every
         # live transcription); requests join at the next step boundary after
         # their encoder output and cross-attention K|V are complete
-        enc_pool = self._encoder_executor() if self.is_gpu else None
+        enc_pool = self._encoder_executor() if (self.is_gpu and os.environ.get("LOQA_OVERLAP_ENCODER", "1") != "0") else None
         while self._running:
             idle = not live and not waiting and not encoding
             items = [self._inbox.get()] if idle else []

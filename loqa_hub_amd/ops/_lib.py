@@ -119,6 +119,8 @@ _RUNTIME_SIGS = {
     "loqa_pool_append": ([c_void_p, c_ll, c_int, c_void_p], c_int),
     "loqa_pool_cache_prefix": ([c_void_p, c_ll, c_void_p, c_int], c_int),
     "loqa_pool_block_table": ([c_void_p, c_ll, c_void_p, c_int], c_int),
+    "loqa_pool_step_meta": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int], c_int),
     "loqa_pool_seq_len": ([c_void_p, c_ll], c_ll),
     "loqa_pool_free_seq": ([c_void_p, c_ll], c_int),
 }

@@ -479,3 +479,36 @@ def test_llm_compact_weights_match_default_cpu():
         eng.generate(reqs)
         outs.append([r.output for r in reqs])
     assert outs[0] == outs[1]
+
+
+def test_step_meta_native_matches_python():
+    """One-call step metadata (native) against the Python twin."""
+    from loqa_hub_amd.engine.kv_cache import NativeBlockPool
+    from loqa_hub_amd.ops import _lib
+    try:
+        _lib.runtime()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip(f"native runtime not built: {e}")
+    rng = np.random.default_rng(0)
+    pools = [PyBlockPool(128, 16), NativeBlockPool(128, 16)]
+    for p in pools:
+        for sid in range(1, 6):
+            assert p.add_seq(sid, []) == 0
+    B_pad, T_pad, MB = 8, 32, 16
+    for step in range(12):
+        ids = [s for s in range(1, 6) if rng.random() < 0.8]
+        ns = [int(rng.integers(1, 5)) for _ in ids]
+        outs = []
+        for p in pools:
+            a = dict(positions=np.full(T_pad, 7, np.int32), slots=np.full(T_pad, 7, np.int32),
+                     cu=np.full(B_pad + 1, 7, np.int32), ctx=np.full(B_pad, 7, np.int32),
+                     bt=np.full((B_pad, MB), 7, np.int32), lidx=np.full(16, 7, np.int64))
+            assert p.step_meta(ids, ns, B_pad, T_pad, MB, a["positions"], a["slots"], a["cu"], a["ctx"],
+                               a["bt"], a["lidx"]) == 0
+            outs.append(a)
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[1][k]), (step, k)
+    # exhausted pool / unknown sequence
+    assert pools[1].step_meta([99], [1], B_pad, T_pad, MB, *[np.zeros(T_pad, np.int32)] * 2,
+                              np.zeros(B_pad + 1, np.int32), np.zeros(B_pad, np.int32),
+                              np.zeros((B_pad, MB), np.int32)) == -1
