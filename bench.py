@@ -201,9 +201,16 @@ def main(argv=None) -> int:
     if args.mode == "closed" and recs_local:
         step.records.append(gather_records(info, torch.tensor(recs_local, dtype=torch.float64)).cpu())
     stats = added_command_stats(all_jobs)
+    def _mean_ms(a, b):
+        v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
+        return round(float(np.mean(v)) * 1e3, 2) if v else None
     phase_ms = {
-        "stt": round(float(np.mean([(j.t["stt_done"] - j.t["start"]) for j in all_jobs])) * 1e3, 2)
-        if all_jobs else None,
+        "stt": _mean_ms("start", "stt_done"),
+        "stt_wait_encoder": _mean_ms("start", "enc0"),
+        "stt_encode": _mean_ms("enc0", "enc1"),
+        "stt_wait_decoder": _mean_ms("enc1", "dec0"),
+        "stt_decode": _mean_ms("dec0", "stt_done"),
+        "llm_total": _mean_ms("stt_done", "queue_done"),
         "llm_prefill": round((llm.stats["prefill_s"] - s0["prefill_s"]) / args.steps * 1e3, 2),
         "llm_decode": round((llm.stats["decode_s"] - s0["decode_s"]) / args.steps * 1e3, 2),
         "llm_decode_steps": (llm.stats["decode_steps"] - s0["decode_steps"]) / args.steps,

@@ -12,76 +12,76 @@
 #include <float.h>
 
 // ---------------------------------------------------------------- K14 SwiGLU
-// in: [T, 2F] = [gate | up], out: [T, F]
-__global__ void silu_mul_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
-                                int F, long long total_vec) {
-  const int fv = F >> 3;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long row = i / fv;
-    const int c = (int)(i - row * fv);
-    const uint4* g = reinterpret_cast<const uint4*>(in + row * 2 * F) + c;
-    const uint4* u = reinterpret_cast<const uint4*>(in + row * 2 * F + F) + c;
-    float a[8], b[8], o[8];
-    unpack8(*g, a);
-    unpack8(*u, b);
+// in: [T, 2F] = [gate | up], out: [T, F]. 2-D grid (x: 8-wide column vectors,
+// y: rows): one 16-byte vector per thread, no per-element 64-bit division (the
+// grid-stride form with `i / (F / 8)` ran at 0.8 TB/s on the 318 x 14336
+// prefill activations; these kernels are pure streams).
+__global__ __launch_bounds__(256) void silu_mul_kernel(const bf16_t* __restrict__ in,
+                                                      bf16_t* __restrict__ out, int F) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= (F >> 3)) return;
+  const size_t row = blockIdx.y;
+  const uint4 gv = reinterpret_cast<const uint4*>(in + row * 2 * F)[c];
+  const uint4 uv = reinterpret_cast<const uint4*>(in + row * 2 * F + F)[c];
+  float a[8], b[8], o[8];
+  unpack8(gv, a);
+  unpack8(uv, b);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
-    reinterpret_cast<uint4*>(out + row * F)[c] = pack8(o);
-  }
+  for (int j = 0; j < 8; ++j) o[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
+  reinterpret_cast<uint4*>(out + row * F)[c] = pack8(o);
 }
 
 extern "C" int loqa_silu_mul(const void* in, void* out, long long rows, int F, hipStream_t s) {
   if (F % 8 != 0 || rows <= 0) return (int)hipErrorInvalidValue;
-  const long long tv = rows * (F / 8);
-  const int threads = 256;
-  long long blocks = (tv + threads - 1) / threads;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(threads), 0, s,
-                     (const bf16_t*)in, (bf16_t*)out, F, tv);
+  for (long long r0 = 0; r0 < rows; r0 += 65535) {   // grid.y limit
+    const long long n = rows - r0 < 65535 ? rows - r0 : 65535;
+    dim3 grid((unsigned)((F / 8 + 255) / 256), (unsigned)n);
+    hipLaunchKernelGGL(silu_mul_kernel, grid, dim3(256), 0, s, (const bf16_t*)in + r0 * 2 * F,
+                       (bf16_t*)out + r0 * F, F);
+  }
   return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------ K6 bias+GELU(+pos)
-// x[T, F] <- gelu(x + bias) + pos[(t % pos_period), :]   (bias, pos optional)
-__global__ void gelu_bias_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ bias,
-                                 const bf16_t* __restrict__ pos, int F, int pos_period,
-                                 long long total_vec) {
-  const int fv = F >> 3;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total_vec;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long row = i / fv;
-    const int c = (int)(i - row * fv);
-    uint4* p = reinterpret_cast<uint4*>(x + row * F) + c;
-    float v[8];
-    unpack8(*p, v);
-    if (bias) {
-      float b[8];
-      unpack8(reinterpret_cast<const uint4*>(bias)[c], b);
+// x[T, F] <- gelu(x + bias) + pos[(t % pos_period), :]   (bias, pos optional);
+// 2-D grid as silu_mul
+__global__ __launch_bounds__(256) void gelu_bias_kernel(bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ bias,
+                                                       const bf16_t* __restrict__ pos, int F,
+                                                       int pos_period, long long row0) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= (F >> 3)) return;
+  const size_t row = (size_t)row0 + blockIdx.y;
+  uint4* p = reinterpret_cast<uint4*>(x + row * F) + c;
+  float v[8];
+  unpack8(*p, v);
+  if (bias) {
+    float b[8];
+    unpack8(reinterpret_cast<const uint4*>(bias)[c], b);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += b[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
-    if (pos) {
-      float q[8];
-      const long long prow = row % pos_period;
-      unpack8(reinterpret_cast<const uint4*>(pos + prow * F)[c], q);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += q[j];
-    }
-    *p = pack8(v);
+    for (int j = 0; j < 8; ++j) v[j] += b[j];
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+  if (pos) {
+    float q[8];
+    const size_t prow = row % (size_t)pos_period;
+    unpack8(reinterpret_cast<const uint4*>(pos + prow * F)[c], q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += q[j];
+  }
+  *p = pack8(v);
 }
 
 extern "C" int loqa_gelu_bias(void* x, const void* bias, const void* pos, long long rows, int F,
                               int pos_period, hipStream_t s) {
   if (F % 8 != 0 || rows <= 0 || (pos && pos_period <= 0)) return (int)hipErrorInvalidValue;
-  const long long tv = rows * (F / 8);
-  long long blocks = (tv + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(gelu_bias_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (bf16_t*)x,
-                     (const bf16_t*)bias, (const bf16_t*)pos, F, pos_period, tv);
+  for (long long r0 = 0; r0 < rows; r0 += 65535) {   // grid.y limit
+    const long long n = rows - r0 < 65535 ? rows - r0 : 65535;
+    dim3 grid((unsigned)((F / 8 + 255) / 256), (unsigned)n);
+    hipLaunchKernelGGL(gelu_bias_kernel, grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)bias,
+                       (const bf16_t*)pos, F, pos_period, r0);
+  }
   return (int)hipGetLastError();
 }
 
@@ -296,5 +296,77 @@ extern "C" int loqa_masked_argmax(const void* logits, int is_bf16, long long ld,
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(argmax_unpack_kernel, dim3((B + 63) / 64), dim3(64), 0, s, packed, B, out_idx);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------- pipelined decode: step I/O
+// A decode step graph exchanges its host data without copy-engine operations
+// between graphs (each H2D / D2H copy on the decode stream cost a copy-engine
+// hand-off of tens of microseconds between two back-to-back step graphs).
+// The host stages a step's metadata in pinned memory; the graph's first node
+// reads it zero-copy into the graph's device buffers, and its last node writes
+// the sampled tokens zero-copy into a pinned result ring. *ctr counts the step
+// graphs launched so far (advanced by the last node), so the staging slot
+// (ctr % 2) and result slot (ctr % nres) follow the host's launch order.
+__global__ __launch_bounds__(256) void step_fetch_kernel(int* __restrict__ d32,
+                                                        const int* __restrict__ h32, int n32,
+                                                        int stride32, long long* __restrict__ d64,
+                                                        const long long* __restrict__ h64, int n64,
+                                                        int stride64, const int* __restrict__ ctr,
+                                                        int T, int src_off,
+                                                        const int* __restrict__ last_tok) {
+  const int slot = ctr[0] & 1;
+  const int* src = h32 + (size_t)slot * stride32;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n32; i += gridDim.x * 256) {
+    int v = src[i];
+    if (i < T) {   // tokens: a staged src slot >= 0 takes that sequence's last sampled token
+      const int sl = src[src_off + i];
+      if (sl >= 0) v = last_tok[sl];
+    }
+    d32[i] = v;
+  }
+  const long long* src64 = h64 + (size_t)slot * stride64;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n64; i += gridDim.x * 256) d64[i] = src64[i];
+}
+
+__global__ __launch_bounds__(256) void step_publish_kernel(const int* __restrict__ out, int n,
+                                                          int* __restrict__ res, int stride,
+                                                          int nres, int* __restrict__ ctr,
+                                                          const int* __restrict__ row_slot,
+                                                          int* __restrict__ last_tok) {
+  const int c = ctr[0];
+  int* dst = res + (size_t)(c % nres) * stride;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int v = out[i];
+    dst[i] = v;
+    last_tok[row_slot[i]] = v;     // padding rows write the trash slot
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(ctr, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// T: token rows at the head of the staged int32 block; src_off: offset of the
+// per-token source-slot array in it (see LLMEngine._decode_graph).
+extern "C" int loqa_step_fetch(void* d32, const void* h32, int n32, int stride32, void* d64,
+                               const void* h64, int n64, int stride64, const int* ctr, int T,
+                               int src_off, const int* last_tok, hipStream_t s) {
+  if (n32 < 0 || n32 > stride32 || n64 < 0 || n64 > stride64 || src_off + T > n32)
+    return (int)hipErrorInvalidValue;
+  int blocks = (n32 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 16 ? 16 : blocks);
+  hipLaunchKernelGGL(step_fetch_kernel, dim3(blocks), dim3(256), 0, s, (int*)d32, (const int*)h32, n32,
+                     stride32, (long long*)d64, (const long long*)h64, n64, stride64, ctr, T, src_off,
+                     last_tok);
+  return (int)hipGetLastError();
+}
+
+extern "C" int loqa_step_publish(const int* out, int n, void* res, int stride, int nres, int* ctr,
+                                 const int* row_slot, int* last_tok, hipStream_t s) {
+  if (n < 0 || n > stride || nres < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(step_publish_kernel, dim3(1), dim3(256), 0, s, out, n, (int*)res, stride, nres, ctr,
+                     row_slot, last_tok);
   return (int)hipGetLastError();
 }

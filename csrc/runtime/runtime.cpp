@@ -391,6 +391,25 @@ long long loqa_pool_seq_len(void* h, long long seq_id) {
   return it == p->seqs.end() ? -1 : it->second.len;
 }
 
+// Roll a sequence back to its first new_len tokens (a discarded speculative
+// step of the pipelined decode): blocks past the new length go back to the
+// pool. Returns 0, -1 unknown sequence, -2 new_len beyond the sequence.
+int loqa_pool_truncate(void* h, long long seq_id, long long new_len) {
+  auto* p = static_cast<BlockPool*>(h);
+  std::lock_guard<std::mutex> g(p->mu);
+  auto it = p->seqs.find(seq_id);
+  if (it == p->seqs.end()) return -1;
+  Seq& sq = it->second;
+  if (new_len < 0 || new_len > sq.len) return -2;
+  const size_t keep = (size_t)((new_len + p->block_size - 1) / p->block_size);
+  while (sq.blocks.size() > keep) {
+    p->release(sq.blocks.back());
+    sq.blocks.pop_back();
+  }
+  sq.len = new_len;
+  return 0;
+}
+
 int loqa_pool_free_seq(void* h, long long seq_id) {
   auto* p = static_cast<BlockPool*>(h);
   std::lock_guard<std::mutex> g(p->mu);

@@ -113,6 +113,9 @@ class GrammarTables:
         rows.append(digits)
         self.ROW_FREE_OPEN = 2  # string body that may not close yet (min length)
         rows.append(safe)
+        # stand-ins for "some allowed token" in GrammarState.predict
+        self.generic_free = int(safe.nonzero()[0])
+        self.generic_digit = tok.token_id("0")
         self._rows = rows
         self._tries: dict[tuple, _Trie] = {}
         self._lit_cache: dict[str, list[int]] = {}
@@ -250,3 +253,37 @@ class GrammarState:
 
     def text(self) -> str:
         return self.t.tok.decode(self.emitted)
+
+    # ---- speculation support (pipelined decode, LLMEngine._pl_*)
+    def fork(self) -> "GrammarState":
+        """Cursor copy without the emitted text (segments / tries are shared)."""
+        g = GrammarState.__new__(GrammarState)
+        g.t, g.segs, g.i, g.node, g.count = self.t, self.segs, self.i, self.node, self.count
+        g.after_free, g.done, g.emitted, g.free_steps = self.after_free, self.done, [], 0
+        return g
+
+    def is_generic(self, tok: int) -> bool:
+        """Whether ``tok`` (about to be consumed) takes the path ``predict``
+        assumes: anything but a Free field's closing quote."""
+        return self.done or not (isinstance(self.segs[self.i], Free) and tok == self.t.quote)
+
+    def predict(self):
+        """(forced tokens, next mask row, done) after the NEXT sampled token,
+        for any generic token (see ``is_generic``), or None when the outcome
+        depends on which token is sampled (a Choice node with a non-terminal
+        child). The pipelined decode feeds these forced tokens before the
+        sampled token itself is known."""
+        if self.done:
+            return None
+        s = self.segs[self.i]
+        if isinstance(s, Choice):
+            if any(c.children for c in self.node.children.values()):
+                return None
+            tok = next(iter(self.node.children))
+        elif isinstance(s, Free):
+            tok = self.t.generic_free
+        else:
+            tok = self.t.generic_digit
+        f = self.fork()
+        forced = f.advance(tok)
+        return forced, f.mask_row(), f.done

@@ -105,6 +105,15 @@ class PyBlockPool:
         for b in self.seqs.pop(seq_id)["blocks"]:
             self._release(b)
 
+    def truncate(self, seq_id: int, new_len: int) -> None:
+        s = self.seqs[seq_id]
+        if not 0 <= new_len <= s["len"]:
+            raise ValueError("truncate beyond the sequence")
+        keep = -(-new_len // self.block_size)
+        while len(s["blocks"]) > keep:
+            self._release(s["blocks"].pop())
+        s["len"] = new_len
+
     def step_meta(self, seq_ids, ns, B_pad, T_pad, max_blocks, positions, slots, cu, ctx, bt,
                   lidx=None) -> int:
         """Same contract as the native ``loqa_pool_step_meta``."""
@@ -189,6 +198,13 @@ class NativeBlockPool:
 
     def free_seq(self, seq_id: int) -> None:
         self.lib.loqa_pool_free_seq(self.h, seq_id)
+
+    def truncate(self, seq_id: int, new_len: int) -> None:
+        rc = self.lib.loqa_pool_truncate(self.h, seq_id, new_len)
+        if rc == -1:
+            raise KeyError(seq_id)
+        if rc != 0:
+            raise ValueError("truncate beyond the sequence")
 
     def step_meta(self, seq_ids, ns, B_pad, T_pad, max_blocks, positions, slots, cu, ctx, bt,
                   lidx=None) -> int:

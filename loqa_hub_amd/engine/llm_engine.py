@@ -68,6 +68,7 @@ def _bucket(n: int, buckets: list[int]) -> int:
 
 class LLMEngine:
     SEQ_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128]
+    RES_SLOTS = 3       # result ring slots (>= steps in flight + 1)
 
     def __init__(self, cfg: LlamaConfig, device, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
@@ -124,6 +125,25 @@ class LLMEngine:
                                       ops.MPADS[-2]))
         self._rr = 0
         self._graphs: dict[tuple[int, int], dict] = {}
+        # pipelined decode (GPU graphs): last sampled token per sequence slot
+        # (+ one trash slot for padding rows), free sequence slots
+        self.last_tok = torch.zeros(max_seqs + 1, dtype=torch.int32, device=self.device)
+        self._free_seq_slots = list(range(max_seqs))
+        if self.use_graphs:
+            # step I/O without copy-engine operations between step graphs
+            # (elementwise.hip step_fetch / step_publish): a 2-slot pinned
+            # staging ring for step metadata, a 3-slot pinned result ring, and
+            # a device counter of launched step graphs that picks the slots
+            b_max = _bucket(max(1, max_seqs), self.SEQ_BUCKETS)
+            self._n32_max = 4 * ops.MPADS[-1] + 4 * b_max + 1 + b_max * self.max_blocks
+            self._n64_max = max(16, b_max)
+            self._stage32 = torch.zeros(2, self._n32_max, dtype=torch.int32).pin_memory()
+            self._stage64 = torch.zeros(2, self._n64_max, dtype=torch.int64).pin_memory()
+            self._res_ring = torch.zeros(self.RES_SLOTS, 256, dtype=torch.int32).pin_memory()
+            self._step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._step_no = 0
+        self.pipelined = self.use_graphs and os.environ.get("LOQA_LLM_PIPELINE", "1") != "0"
+        self._pl = None
         # set once warmup_graphs() has captured every reachable bucket: from
         # then on an uncaptured shape runs eagerly instead of capturing while
         # the other worker threads issue HIP work
@@ -242,41 +262,92 @@ class LLMEngine:
         g = self._graphs.get(key)
         if g is not None:
             return g
-        # all int32 metadata lives in ONE device buffer (one H2D copy per step)
-        # mirrored by ONE pinned host buffer; logit_idx (int64) has its own pair
+        # all int32 metadata lives in ONE device buffer, int64 logit rows in a
+        # second; the graph's first node fills both from the pinned staging ring
         shapes = {"tokens": (T_pad,), "positions": (T_pad,), "slots": (T_pad,),
                   "cu_q": (B_pad + 1,), "ctx_lens": (B_pad,),
-                  "block_tables": (B_pad, self.max_blocks), "mask_rows": (B_pad,)}
+                  "block_tables": (B_pad, self.max_blocks), "mask_rows": (B_pad,),
+                  "src": (T_pad,), "row_slot": (B_pad,)}
         n32 = sum(int(np.prod(v)) for v in shapes.values())
         L = max(16, B_pad)
+        assert n32 <= self._n32_max and L <= self._n64_max and B_pad <= 256
         d32 = torch.zeros(n32, dtype=torch.int32, device=self.device)
-        h32 = torch.zeros(n32, dtype=torch.int32).pin_memory()
         d64 = torch.zeros(L, dtype=torch.int64, device=self.device)
-        h64 = torch.zeros(L, dtype=torch.int64).pin_memory()
-        dev, host, off = {}, {}, 0
-        hn = h32.numpy()
+        dev, off = {}, 0
         for k, shp in shapes.items():
             n = int(np.prod(shp))
             dev[k] = d32[off:off + n].view(*shp)
-            host[k] = hn[off:off + n].reshape(shp)
             off += n
         dev["slots"].fill_(-1)
-        dev["logit_idx"], host["logit_idx"] = d64, h64.numpy()
+        dev["src"].fill_(-1)
+        dev["row_slot"].fill_(self.max_seqs)
+        dev["logit_idx"] = d64
         meta = self._build_meta(dev, self.max_decode_q, ctx, True)
-        # warm up (allocator + kernels) on a side stream, then capture
+        # warm up (allocator + kernels) on a side stream, then capture; the
+        # warm-up runs the body only (the I/O nodes would advance the counter)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            out = self._forward_sample(meta, dev["mask_rows"])
+            out = self._step_body(meta, dev)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
+        k = ops._lib.kernels()
         # thread-local capture: the other GPU worker thread keeps running
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            out = self._forward_sample(meta, dev["mask_rows"])
-        g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
-             "h64": h64, "d64": d64}
+            st = ops._lib.stream_ptr(d32)
+            src_off = dev["src"].data_ptr() // 4 - d32.data_ptr() // 4
+            ops._lib.check(k.loqa_step_fetch(
+                ops._lib.ptr(d32), self._stage32.data_ptr(), n32, self._n32_max, ops._lib.ptr(d64),
+                self._stage64.data_ptr(), L, self._n64_max, ops._lib.ptr(self._step_ctr), T_pad,
+                src_off, ops._lib.ptr(self.last_tok), st), "step_fetch")
+            out = self._step_body(meta, dev, device_io=True)
+            ops._lib.check(k.loqa_step_publish(
+                ops._lib.ptr(out), B_pad, self._res_ring.data_ptr(), self._res_ring.shape[1],
+                self.RES_SLOTS, ops._lib.ptr(self._step_ctr), ops._lib.ptr(dev["row_slot"]),
+                ops._lib.ptr(self.last_tok), st), "step_publish")
+        g = {"graph": graph, "dev": dev, "out": out, "shapes": shapes, "n32": n32, "L": L}
         self._graphs[key] = g
         return g
+
+    def _stage(self, g: dict) -> dict:
+        """Numpy views of the staging slot of the NEXT step graph launch, in
+        graph ``g``'s metadata layout."""
+        slot = self._step_no % 2
+        hn, out, off = self._stage32[slot].numpy(), {}, 0
+        for k, shp in g["shapes"].items():
+            n = int(np.prod(shp))
+            out[k] = hn[off:off + n].reshape(shp)
+            off += n
+        out["logit_idx"] = self._stage64[slot].numpy()[: g["L"]]
+        return out
+
+    def _replay(self, g: dict) -> int:
+        """Launch a step graph whose staging slot is filled; returns the result
+        ring slot its sampled tokens will land in."""
+        rslot = self._step_no % self.RES_SLOTS
+        g["graph"].replay()
+        self._step_no += 1
+        return rslot
+
+    def _step_body(self, meta: StepMeta, dev: dict, device_io: bool = False) -> torch.Tensor:
+        """One captured decode step: tokens whose ``src`` >= 0 are taken from
+        the device-resident last sampled token of that sequence slot (the
+        pipelined decode launches a step before the host has seen the previous
+        step's tokens), then forward + masked argmax, then each row's sampled
+        token is stored under its sequence slot (``row_slot``; padding rows
+        write a trash slot). ``device_io``: the graph's fetch / publish nodes
+        do the gather and the store (LLMEngine._decode_graph)."""
+        if device_io:
+            return self._forward_sample(meta, dev["mask_rows"])
+        src = dev["src"]
+        tok = torch.where(src >= 0, self.last_tok[src.clamp(min=0).long()], dev["tokens"])
+        meta = StepMeta(tokens=tok, positions=meta.positions, slots=meta.slots, cu_q=meta.cu_q,
+                        ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
+                        logit_idx=meta.logit_idx, max_q=meta.max_q, max_ctx=meta.max_ctx,
+                        decode=meta.decode)
+        out = self._forward_sample(meta, dev["mask_rows"])
+        self.last_tok.index_copy_(0, dev["row_slot"].long(), out[: dev["row_slot"].numel()])
+        return out
 
     def warmup_graphs(self) -> int:
         """Capture every decode-step graph bucket up front (sequence x token x
@@ -321,34 +392,45 @@ class LLMEngine:
         req._prompt_full = list(req.prompt) + req.grammar.emitted  # type: ignore[attr-defined]
         return req
 
+    def _commit(self, r: GenRequest, t: int, now: float) -> list[int]:
+        """Consume one sampled token of ``r``: grammar advance, streaming hook,
+        completion. Returns the forced tokens that follow it."""
+        if r.t_first == 0.0:
+            r.t_first = now
+            if getattr(r, "inline", False):   # prompt fed through decode steps
+                self.stats["prefill_tokens"] += r.inline   # type: ignore[attr-defined]
+                self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
+        r.token_times.append(now)
+        r.steps += 1
+        forced = r.grammar.advance(int(t))
+        self.stats["sampled_tokens"] += 1
+        self.stats["forced_tokens"] += len(forced)
+        if r.on_tokens is not None:
+            r.on_tokens([int(t)] + forced)
+        if r.grammar.done:
+            r.done = True
+            r.t_done = now
+            r.output = r.grammar.text()
+            r.feed = []
+            if self._pl is not None:
+                self._pl.release(r)
+            if r.on_done is not None:
+                r.on_done(r)
+            elif self._on_done is not None:
+                self._on_done(r)
+        else:
+            r.feed = [int(t)] + forced
+        return forced
+
+    def _bucket_seqs(self, B: int) -> int:
+        return _bucket(B, self.SEQ_BUCKETS)
+
     def _sample_and_advance(self, live: list[GenRequest], nxt: np.ndarray, now: float,
                             carry: list[bool] | None = None) -> None:
         for i, (r, t) in enumerate(zip(live, nxt.tolist())):
             if carry is not None and carry[i]:
                 continue  # long forced run split across steps: logits of this step unused
-            if r.t_first == 0.0:
-                r.t_first = now
-                if getattr(r, "inline", False):   # prompt fed through decode steps
-                    self.stats["prefill_tokens"] += r.inline   # type: ignore[attr-defined]
-                    self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
-            r.token_times.append(now)
-            r.steps += 1
-            forced = r.grammar.advance(int(t))
-            self.stats["sampled_tokens"] += 1
-            self.stats["forced_tokens"] += len(forced)
-            if r.on_tokens is not None:
-                r.on_tokens([int(t)] + forced)
-            if r.grammar.done:
-                r.done = True
-                r.t_done = now
-                r.output = r.grammar.text()
-                r.feed = []
-                if r.on_done is not None:
-                    r.on_done(r)
-                elif self._on_done is not None:
-                    self._on_done(r)
-            else:
-                r.feed = [int(t)] + forced
+            self._commit(r, int(t), now)
 
     def prefill(self, reqs: list[GenRequest]) -> None:
         """Run the prompts (chunked) and sample each sequence's first token."""
@@ -431,16 +513,17 @@ class LLMEngine:
             elif g is None:
                 g = self._decode_graph(B_pad, T_pad, C)
         if self.use_graphs and g is not False:
-            hb = g["host"]
+            hb = self._stage(g)
             self._meta(live, feeds, True, B_pad, T_pad, out=hb)
             hb["mask_rows"].fill(0)
             hb["mask_rows"][:B] = rows
-            g["d32"].copy_(g["h32"], non_blocking=True)
-            g["d64"].copy_(g["h64"], non_blocking=True)
+            hb["src"].fill(-1)
+            hb["row_slot"].fill(self.max_seqs)
             t1 = time.perf_counter()
-            g["graph"].replay()
+            rslot = self._replay(g)
             t15 = time.perf_counter()
-            nxt = g["out"][:B].cpu().numpy()
+            torch.cuda.current_stream(self.device).synchronize()
+            nxt = self._res_ring[rslot, :B].numpy().copy()
             t2 = time.perf_counter()
             self.stats["host_pre_s"] += t1 - t0
             self.stats["replay_call_s"] += t15 - t1
@@ -530,6 +613,10 @@ class LLMEngine:
         waiting: list[tuple] = []
         cap = max(1, self.max_seqs)
         pf_pool = self._prefill_executor() if self.overlap_prefill else None
+        if self.pipelined:
+            from .llm_pipeline import DecodePipeline
+            self._pl = DecodePipeline(self)
+        pl = self._pl
         t_end = 0.0
         while self._running:
             idle = not live and not pending and not waiting
@@ -559,6 +646,8 @@ class LLMEngine:
                     inl = [r for r in new if len(r.feed) <= self.inline_prefill]
                     for r in inl:
                         r.inline = len(r.feed)   # type: ignore[attr-defined]
+                        if pl is not None:
+                            pl.admit(r)
                     live += inl
                     new = [r for r in new if len(r.feed) > self.inline_prefill]
                 if new:
@@ -566,7 +655,11 @@ class LLMEngine:
                         pending.append((new, pf_pool.submit(self._prefill_timed, new)))
                     else:
                         self._prefill_timed(new)
-                        live += [r for r in new if not r.done]
+                        joined = [r for r in new if not r.done]
+                        if pl is not None:
+                            for r in joined:
+                                pl.admit(r)
+                        live += joined
                 if pending:
                     if not live:   # nothing to decode: wait for a prefill (or new work)
                         wait([f for _, f in pending], timeout=0.002, return_when=FIRST_COMPLETED)
@@ -574,7 +667,11 @@ class LLMEngine:
                     for reqs, f in pending:
                         if f.done():
                             f.result()                     # re-raise a prefill failure
-                            live += [r for r in reqs if not r.done]
+                            joined = [r for r in reqs if not r.done]
+                            if pl is not None:
+                                for r in joined:
+                                    pl.admit(r)
+                            live += joined
                         else:
                             still.append((reqs, f))
                     pending = still
@@ -582,16 +679,24 @@ class LLMEngine:
                     t0 = time.perf_counter()
                     if t_end:
                         self.stats["sched_s"] += t0 - t_end   # loop work between steps
-                    self.decode_step(live)
+                    if pl is not None:
+                        pl.pump(live)
+                    else:
+                        self.decode_step(live)
                     t_end = time.perf_counter()
                     self.stats["decode_s"] += t_end - t0
                     live = [r for r in live if not r.done]
+                    if not live and pl is not None:
+                        pl.drain()          # speculative steps of finished sequences
                 else:
                     t_end = 0.0
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
-                # in-flight prefills still write KV into their sequences' blocks:
-                # let them finish before those blocks go back to the pool
+                # in-flight prefills / pipelined steps still write KV into their
+                # sequences' blocks: let them finish before the blocks go back
                 wait([f for _, f in pending])
+                if pl is not None:
+                    pl.abort()
+                    self._free_seq_slots = list(range(self.max_seqs))
                 with self._cells_lock:
                     for cell in list(cells.values()):
                         if not cell[1].done():
@@ -620,9 +725,14 @@ class LLMEngine:
 
             def init():
                 if dev.type == "cuda":
-                    from ..utils.streams import pool_stream
+                    from ..utils.streams import cu_masked_stream, parse_cu_spec, pool_stream
                     torch.cuda.set_device(dev)
-                    torch.cuda.set_stream(pool_stream(dev, "prefill"))
+                    spec = os.environ.get("LOQA_PREFILL_CUS", "")
+                    if spec:   # experiment: confine the overlapped prefill to a CU subset
+                        n = torch.cuda.get_device_properties(dev).multi_processor_count
+                        torch.cuda.set_stream(cu_masked_stream(dev, parse_cu_spec(spec, n)))
+                    else:
+                        torch.cuda.set_stream(pool_stream(dev, "prefill"))
             self._pf_pool = ThreadPoolExecutor(1, thread_name_prefix="llm-prefill", initializer=init)
         return self._pf_pool
 

@@ -111,6 +111,8 @@ class VoicePipeline:
     def _stt_post(self, j: PipelineJob, r: STTRequest) -> None:
         j.raw_text, j.rms = r.text, r.rms
         j.t["stt_done"] = time.perf_counter()
+        if r.t_enc0:
+            j.t["enc0"], j.t["enc1"], j.t["dec0"] = r.t_enc0, r.t_enc1, r.t_dec0
         fi = faults()
         if fi and fi.active("stt_error"):
             j.stt_failed, j.error = True, "stt: injected fault"

@@ -44,6 +44,9 @@ class STTRequest:
     tokens: list[int] = field(default_factory=list)
     seq_id: int = -1
     t_done: float = 0.0
+    t_enc0: float = 0.0               # encoder start / end, decoder start (perf_counter)
+    t_enc1: float = 0.0
+    t_dec0: float = 0.0
     # decoder state (engine-owned)
     slot: int = -1                    # cross-attention K|V slot (encoder rows)
     target: list[int] | None = None
@@ -381,6 +384,7 @@ class STTEngine:
         once that work is complete (the RMS read-back synchronises)."""
         tr = tracer()
         dev = self.device if self.is_gpu else None
+        t_enc0 = time.perf_counter()
         with tr.span("h2d", dev, batch=len(reqs)):
             audio, sumsq = self.upload(reqs, device_pcm)
         t0 = time.perf_counter()
@@ -390,7 +394,10 @@ class STTEngine:
         ss = sumsq.cpu().numpy()
         if self.is_gpu:
             torch.cuda.current_stream(self.device).synchronize()
-        self.stats["encode_s"] += time.perf_counter() - t0
+        t1 = time.perf_counter()
+        self.stats["encode_s"] += t1 - t0
+        for r in reqs:
+            r.t_enc0, r.t_enc1 = t_enc0, t1
         for i, (r, sl) in enumerate(zip(reqs, slots)):
             n = max(1, min(len(r.pcm), N_SAMPLES))
             r.sumsq = float(ss[i])
@@ -399,7 +406,9 @@ class STTEngine:
 
     def _start_decode(self, reqs: list[STTRequest]) -> None:
         """Decoder sequences for encoded requests (scheduler thread)."""
+        now = time.perf_counter()
         for r in reqs:
+            r.t_dec0 = now
             r.seq_id = self._next
             self._next += 1
             self.kv.pool.add_seq(r.seq_id, [])

@@ -89,6 +89,10 @@ _KERNEL_SIGS = {
                            c_int, c_float, ctypes.c_uint, c_void_p],
     "loqa_slab_silu_mul": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "loqa_step_fetch": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                        c_int, c_int, c_void_p, c_void_p],
+    "loqa_step_publish": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                          c_void_p],
 }
 
 # (argtypes, restype) of the custom all-reduce entry points (in the kernels library)
@@ -123,6 +127,7 @@ _RUNTIME_SIGS = {
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int], c_int),
     "loqa_pool_seq_len": ([c_void_p, c_ll], c_ll),
     "loqa_pool_free_seq": ([c_void_p, c_ll], c_int),
+    "loqa_pool_truncate": ([c_void_p, c_ll, c_ll], c_int),
 }
 
 

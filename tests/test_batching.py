@@ -134,3 +134,42 @@ def test_llm_inline_prefill_cpu(monkeypatch):
         outs[inline] = [r.output for r in reqs]
         assert eng.stats["prefill_tokens"] > 0
     assert outs["0"] == outs["4096"]
+
+
+def _run_sched(pipelined: bool, mispredict: float = 0.0):
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=6,
+                    max_seq_len=512, use_graphs=False)
+    eng.pipelined = pipelined
+    texts = ["turn on the lights and play music", "dim the kitchen lights", "hello there",
+             "turn off the tv then lock the door", "what time is it", "play music"]
+    reqs = [GenRequest(eng.tok.encode(t, bos=True), multi_command_schema(n))
+            for t, n in zip(texts, (2, 1, 1, 3, 1, 4))]
+    try:
+        eng.start()
+        if pipelined:
+            import time as _t
+            while eng._pl is None:
+                _t.sleep(0.01)
+            eng._pl.force_mispredict = mispredict
+        eng.submit_batch(reqs[:3]).result(timeout=300)
+        eng.submit_batch(reqs[3:]).result(timeout=300)
+    finally:
+        eng.stop()
+    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
+    return [r.output for r in reqs], eng
+
+
+def test_llm_pipelined_decode_matches_cpu():
+    """Two steps in flight with device-fed tokens and predicted jump-forward
+    literals: same greedy outputs as the synchronous loop, also when
+    predictions are forced to fail (discard + KV rollback + re-feed)."""
+    ref, _ = _run_sched(False)
+    got, eng = _run_sched(True)
+    assert got == ref
+    assert eng._pl.stats["pl_spec"] > 0 and eng._pl.stats["pl_steps"] > 0
+    got2, eng2 = _run_sched(True, mispredict=0.35)
+    assert got2 == ref
+    assert eng2._pl.stats["pl_discard"] > 0
+    assert sorted(eng2._free_seq_slots) == list(range(6))

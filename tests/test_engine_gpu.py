@@ -36,6 +36,45 @@ def test_llm_graphs_match_eager():
         assert len(json.loads(x.output)["commands"]) == n
 
 
+def _sched_outputs(eng, n_list, mispredict=0.0):
+    tok = eng.tok
+    reqs = [GenRequest(tok.encode(f"Voice command: turn on the lights {i}", bos=True),
+                       multi_command_schema(n, min_response_tokens=3)) for i, n in enumerate(n_list)]
+    eng.warmup_graphs()
+    eng.start()
+    try:
+        if eng.pipelined:
+            import time as _t
+            while eng._pl is None:
+                _t.sleep(0.01)
+            eng._pl.force_mispredict = mispredict
+        eng.submit_batch(reqs[:3]).result(timeout=120)
+        eng.submit_batch(reqs[3:]).result(timeout=120)
+    finally:
+        eng.stop()
+    return [r.output for r in reqs]
+
+
+def test_llm_pipelined_decode_gpu():
+    """Two graph-replayed steps in flight (device-fed tokens, zero-copy step
+    I/O rings): same tokens as the synchronous graph loop, with and without
+    forced prediction failures (discard + KV rollback)."""
+    cfg = llama_config("test-tiny")
+    n_list = [1, 2, 3, 4, 2, 1]
+    a = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
+    a.pipelined = False
+    ref = _sched_outputs(a, n_list)
+    b = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
+    assert b.pipelined
+    assert _sched_outputs(b, n_list) == ref
+    assert b.stats["pl_spec"] > 0
+    c = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
+    assert _sched_outputs(c, n_list, mispredict=0.3) == ref
+    assert c.stats["pl_discard"] > 0
+    for o, n in zip(ref, n_list):
+        assert len(json.loads(o)["commands"]) == n
+
+
 def test_llm_gpu_matches_cpu_reference_first_tokens():
     cfg = llama_config("test-tiny")
     g = LLMEngine(cfg, "cuda", max_seqs=4, use_graphs=False)
