@@ -3,6 +3,9 @@
 // One kernel family covers every attention in the hub:
 //   * PREFILL mode  - 128 query rows of ONE head per workgroup (Whisper encoder,
 //                     Llama prompt prefill, VITS text encoder). Causal or not.
+//                     Served by attn_prefill2_kernel below (8 waves, key range
+//                     split between two wave groups); LOQA_ATTN_V1=1 selects
+//                     the original 4-wave attn_fwd_kernel.
 //   * GROUPED mode  - all query heads of ONE kv head x a few query tokens per
 //                     workgroup (decode / jump-forward extend, GQA), with
 //                     split-K over the context and a separate combine kernel.
@@ -23,12 +26,14 @@
 // LDS rows are padded (K: +16 B, V: +64 B) so that both the b128 row reads and
 // the tr_b16 reads are bank-conflict free (guide §2, G4).
 #include "common.h"
+#include <cstdlib>
 
 #define ATT_THREADS 256
 #define ATT_WAVES 4
 #define KV_TILE 64
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct AttnParams {
   const bf16_t* q;
@@ -307,6 +312,275 @@ __global__ __launch_bounds__(ATT_THREADS, QR == 2 ? 2 : 1) void attn_fwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// PREFILL / ENCODER attention, split-KV inside the workgroup.
+//
+// The 4-wave prefill kernel above gives one workgroup 128-256 query rows of one
+// head, so a Whisper encoder pass at batch 1 (1500 frames x 20 heads) is 120
+// workgroups on a 256-CU chip with ONE wave per SIMD: the softmax VALU, the
+// K/V staging and the MFMAs of that wave serialize (measured 107 us per layer,
+// ~110 TFLOP/s). Here a workgroup is 8 waves over 128 query rows: waves 0-3
+// take the first half of the key tiles, waves 4-7 the second half (same query
+// rows, same lane layout), so every CU holds two waves per SIMD whose MFMA and
+// VALU phases overlap, and the grid doubles. Each half streams its K/V tiles
+// through registers into its own double-buffered LDS ring (guide T14: issue the
+// global loads of tile i+1 before computing tile i, write them to LDS after) -
+// one barrier per tile, no drain. The halves merge their (m, l, O) through LDS
+// at the end. Softmax work per score: max on raw scores, one fma + exp2 (scale
+// folded), masking only on the tail / causal-diagonal tiles (wave-uniform test).
+template <int D>
+struct AttnSmem2 {
+  bf16_t k[2][2][KV_TILE][D + 8];   // [half][stage]
+  bf16_t v[2][2][KV_TILE][D + 32];
+};
+
+template <int D, bool PAGED>
+__global__ __launch_bounds__(512, 1) void attn_prefill2_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) AttnSmem2<D> sm;
+  constexpr int NS = D / 16, NDT = D / 32, CH = D / 8;
+  constexpr int NC = KV_TILE * CH / 256;      // 16-byte chunks per thread per operand
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int half = wave >> 2, w4 = wave & 3;
+  const int th = threadIdx.x & 255;
+  const int h = lane >> 5;
+  int bx, by, bz;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int n = gx * gy * gridDim.z;
+    const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int logical = xcd_remap(lin, n);
+    bx = logical % gx;
+    by = (logical / gx) % gy;
+    bz = logical / (gx * gy);
+  }
+  const int b = bz;
+  const int q0 = p.cu_q[b];
+  const int qlen = p.cu_q[b + 1] - q0;
+  int k0 = 0, klen;
+  if (PAGED) {
+    klen = p.ctx_lens[b];
+  } else {
+    k0 = p.cu_k[b];
+    klen = p.ctx_lens ? p.ctx_lens[b] : p.cu_k[b + 1] - k0;
+  }
+  const int head = by, kvh = head / (p.Hq / p.Hkv);
+  const int row_lo = bx * 128;
+  if (row_lo >= qlen) return;                               // whole workgroup: uniform
+  const int row_hi = min(qlen - 1, row_lo + 127);
+  const int qi = row_lo + w4 * 32 + (lane & 31);
+  const bool row_valid = qi < qlen;
+  const int qpos_lo = klen - qlen + row_lo + w4 * 32;       // wave's first / last query position
+  const int qpos_hi = qpos_lo + 31;
+  int kend = klen;
+  if (p.causal) kend = min(kend, klen - qlen + row_hi + 1);
+  const int ntiles = kend > 0 ? (kend + KV_TILE - 1) / KV_TILE : 0;
+  const int n0 = (ntiles + 1) >> 1;
+  const int my_t0 = half ? n0 : 0;
+  const int my_n = half ? ntiles - n0 : n0;
+
+  bf16x8 qf[NS];
+  {
+    const bf16_t* qrow = p.q + (size_t)(q0 + (row_valid ? qi : 0)) * p.q_stride + (size_t)head * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4 v = row_valid ? *reinterpret_cast<const uint4*>(qrow + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      qf[s] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+  float16v acc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+  const float sl2 = p.scale_log2;
+
+  const int* btab = PAGED ? p.block_tables + (size_t)b * p.max_blocks : nullptr;
+  // Loads are unconditional (rows past kend re-read the last key - finite
+  // values whose scores are masked to -inf, so P = 0 exactly; a half past its
+  // last tile re-reads a valid tile): a load under a branch makes hipcc fall
+  // back to vmcnt(0) at the first MFMA, serialising the prefetch.
+#define ATT2_ROW_OFF(KT, i, key_, cc_)                                                \
+    const int c = th + (i) * 256;                                                     \
+    const int kr = c / CH, cc_ = (c - kr * CH) * 8;                                   \
+    const int key_ = min((KT) + kr, kend - 1);                                        \
+    size_t off;                                                                       \
+    if (PAGED) {                                                                      \
+      const int bi = key_ / p.blk, bo = key_ - bi * p.blk;                            \
+      off = (((size_t)btab[bi] * p.Hkv + kvh) * p.blk + bo) * D + cc_;                \
+    } else {                                                                          \
+      off = (size_t)(k0 + key_) * p.kv_stride + (size_t)kvh * D + cc_;                \
+    }
+#define ATT2_LOAD1(SRC, KT, R)                                                        \
+  _Pragma("clang loop unroll(full)") for (int i = 0; i < NC; ++i) {                   \
+    ATT2_ROW_OFF(KT, i, key, cc)                                                      \
+    R[i] = *reinterpret_cast<const u32x4*>(SRC + off);                                \
+  }
+#define ATT2_STORE1(DST, R)                                                           \
+  _Pragma("clang loop unroll(full)") for (int i = 0; i < NC; ++i) {                   \
+    const int c = th + i * 256;                                                       \
+    const int kr = c / CH, cc = (c - kr * CH) * 8;                                    \
+    *reinterpret_cast<u32x4*>(&DST[kr][cc]) = R[i];                                   \
+  }
+  // S^T = K Q^T for the tile in K stage KST (two 32-key halves; the query is
+  // this lane's column)
+#define ATT2_QK(KST, ST)                                                              \
+  {                                                                                   \
+    const bf16_t(*ks_)[D + 8] = sm.k[half][KST];                                      \
+    _Pragma("unroll") for (int t = 0; t < 2; ++t) {                                   \
+      _Pragma("unroll") for (int j = 0; j < 16; ++j) ST[t][j] = 0.f;                  \
+      _Pragma("unroll") for (int s = 0; s < NS; ++s) {                                \
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&ks_[32 * t + (lane & 31)][16 * s + 8 * h]); \
+        ST[t] = mfma32(a, qf[s], ST[t]);                                              \
+      }                                                                               \
+    }                                                                                 \
+  }
+
+  // online softmax of the scores ST of the tile at key KT, then O^T += V^T P^T
+  // with V from V stage VST
+  auto softmax_pv = [&](float16v (&st)[2], int vst, int kt) __attribute__((always_inline)) {
+    // masking only where a key can be invalid for this wave (wave-uniform test)
+    if (kt + KV_TILE > kend || (p.causal && kt + KV_TILE - 1 > qpos_lo)) {
+      const int lim = (p.causal ? min(kend, klen - qlen + qi + 1) : kend) - kt - 4 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (32 * t + (j & 3) + 8 * (j >> 2) >= lim) st[t][j] = -INFINITY;
+    }
+    float mx = st[0][0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, st[0][j]);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = fmaxf(mx, st[1][j]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * sl2);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          pf[t][s2][j] = (__bf16)__builtin_amdgcn_exp2f(fmaf(st[t][8 * s2 + j], sl2, -m_new));
+    // row sums on the matrix core (ones . P^T: every output row is the sum
+    // over the tile's 64 keys of the bf16 P that also feeds O), which has
+    // slack here, instead of 32 VALU adds + a cross-lane exchange
+    {
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+      float16v ls = {};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) ls = mfma32(ones, pf[t][s2], ls);
+      l_run = l_run * alpha + ls[0];
+    }
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    const bf16_t(*vt_s)[D + 32] = sm.v[half][vst];
+    const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int c0 = 32 * dt + 16 * (g & 1) + 4 * (li & 3);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int kb = 32 * t + 16 * s2 + 4 * h + (li >> 2);
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(&vt_s[kb][c0]));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(&vt_s[kb + 8][c0]));
+          short8 a8;
+          a8[0] = lo[0]; a8[1] = lo[1]; a8[2] = lo[2]; a8[3] = lo[3];
+          a8[4] = hi[0]; a8[5] = hi[1]; a8[6] = hi[2]; a8[7] = hi[3];
+          acc[dt] = mfma32(*reinterpret_cast<bf16x8*>(&a8), pf[t][s2], acc[dt]);
+        }
+    }
+  };
+#define ATT2_BARRIER()                                                                \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
+  __builtin_amdgcn_s_barrier();                                                       \
+  asm volatile("" ::: "memory");
+
+  // two K/V stages; tile i+1 is loaded to registers while tile i is computed
+  if (ntiles > 0) {
+    const int kt0 = min(my_t0, ntiles - 1) * KV_TILE;
+    u32x4 kreg[NC], vreg[NC];   // native vectors: HIP's uint4 struct copies stay in scratch
+    ATT2_LOAD1(p.k, kt0, kreg)
+    ATT2_LOAD1(p.v, kt0, vreg)
+    ATT2_STORE1(sm.k[half][0], kreg)
+    ATT2_STORE1(sm.v[half][0], vreg)
+  }
+  for (int it = 0; it < n0; ++it) {
+    const int stage = it & 1;
+    const int kt = (my_t0 + it) * KV_TILE;
+    const int ktn = min(my_t0 + it + 1, ntiles - 1) * KV_TILE;   // next tile (clamped)
+    u32x4 kreg[NC], vreg[NC];
+    ATT2_LOAD1(p.k, ktn, kreg)                       // lands during this tile's math
+    ATT2_LOAD1(p.v, ktn, vreg)
+    ATT2_BARRIER()                                   // stage `stage` written by every wave
+    if (it < my_n && !(p.causal && kt > qpos_hi)) {
+      float16v st[2];
+      ATT2_QK(stage, st)
+      softmax_pv(st, stage, kt);
+    }
+    // that stage was last read before this tile's barrier; past a half's last
+    // tile the write is never read
+    ATT2_STORE1(sm.k[half][stage ^ 1], kreg)
+    ATT2_STORE1(sm.v[half][stage ^ 1], vreg)
+  }
+#undef ATT2_ROW_OFF
+#undef ATT2_LOAD1
+#undef ATT2_STORE1
+#undef ATT2_QK
+#undef ATT2_BARRIER
+
+  // ---- merge the two halves: waves 4-7 hand (m, l, O) to waves 0-3 through LDS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();                        // every wave done with the K/V rings
+  asm volatile("" ::: "memory");
+  float* xo = reinterpret_cast<float*>(&sm);           // [4 waves][NDT * 16][64 lanes]
+  float* xml = xo + 4 * NDT * 16 * 64;                 // [4 waves][2][64 lanes]
+  if (half) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xo[(w4 * NDT * 16 + dt * 16 + j) * 64 + lane] = acc[dt][j];
+    xml[(w4 * 2) * 64 + lane] = m_run;
+    xml[(w4 * 2 + 1) * 64 + lane] = l_run;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (half || !row_valid) return;
+  const float m1 = xml[(w4 * 2) * 64 + lane], l1 = xml[(w4 * 2 + 1) * 64 + lane];
+  const float m = fmaxf(m_run, m1);
+  const float a0 = exp2f(m_run - m), a1 = exp2f(m1 - m);
+  const float l = l_run * a0 + l1 * a1;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const float s0 = a0 * inv, s1 = a1 * inv;
+  bf16_t* orow = p.o + (size_t)(q0 + qi) * p.o_stride + (size_t)head * D;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        o[r] = acc[dt][4 * g4 + r] * s0 + xo[(w4 * NDT * 16 + dt * 16 + 4 * g4 + r) * 64 + lane] * s1;
+      *reinterpret_cast<uint2*>(orow + d0) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+    }
+}
+
 // Combine split-K partials: one workgroup of D threads per (token, head).
 __global__ void attn_combine_kernel(const float* __restrict__ part_o,
                                     const float* __restrict__ part_ml, bf16_t* __restrict__ o,
@@ -331,6 +605,12 @@ static int launch_attn(const AttnParams& p, int B, int max_q, hipStream_t s) {
   dim3 grid;
   // QR = 2 (64 query rows per wave) where it pays: D = 64 prefill / encoder
   constexpr int QR = (!GROUPED && D == 64) ? 2 : 1;
+  static const bool v1 = getenv("LOQA_ATTN_V1") != nullptr;
+  if (!GROUPED && !v1) {
+    grid = dim3((max_q + 127) / 128, p.Hq, B);
+    hipLaunchKernelGGL((attn_prefill2_kernel<D, PAGED>), grid, dim3(512), 0, s, p);
+    return (int)hipGetLastError();
+  }
   if (GROUPED)
     grid = dim3(p.num_splits, p.Hkv, B);
   else
