@@ -609,6 +609,9 @@ class STTEngine:
             def init():
                 from ..utils.streams import pool_stream
                 torch.cuda.set_device(dev)
-                torch.cuda.set_stream(pool_stream(dev, "encoder"))
+                # LOQA_ENCODER_PRIORITY=-1: the encoder's workgroups are
+                # dispatched ahead of the decoders' (placement experiment)
+                prio = int(os.environ.get("LOQA_ENCODER_PRIORITY", "0"))
+                torch.cuda.set_stream(pool_stream(dev, "encoder", prio))
             self._enc_pool = ThreadPoolExecutor(1, thread_name_prefix="stt-encoder", initializer=init)
         return self._enc_pool
