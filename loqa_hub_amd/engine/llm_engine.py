@@ -159,10 +159,17 @@ class LLMEngine:
         # hipBLASLt GEMMs slowed every concurrent decode step (4.1 -> 4.6 ms) and
         # the Whisper decoder: 18.3-18.5 vs 17.9-18.0 utt/s serialised.
         self.overlap_prefill = self.is_gpu and os.environ.get("LOQA_OVERLAP_PREFILL", "0") == "1"
+        # mixed steps (LOQA_MIXED_PREFILL=1): a serialised prefill also feeds
+        # every live sequence's next token. Opt-in: in the 8-stream bench it
+        # saves the prefill's wait behind in-flight steps but the pipeline
+        # drain costs as much (LLM thread time 10.51 vs 10.50 s, 19.0 vs
+        # 19.1 utt/s; docs/PERF.md)
+        self.mixed_prefill = (os.environ.get("LOQA_MIXED_PREFILL", "0") == "1"
+                              and not getattr(self.weights, "compact", False))
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
-                      "host_post_s": 0.0, "replay_call_s": 0.0, "sched_s": 0.0}
+                      "host_post_s": 0.0, "replay_call_s": 0.0, "sched_s": 0.0, "mixed_riders": 0}
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
@@ -432,10 +439,18 @@ class LLMEngine:
                 continue  # long forced run split across steps: logits of this step unused
             self._commit(r, int(t), now)
 
-    def prefill(self, reqs: list[GenRequest]) -> None:
-        """Run the prompts (chunked) and sample each sequence's first token."""
+    def prefill(self, reqs: list[GenRequest], riders: list[GenRequest] | None = None) -> None:
+        """Run the prompts (chunked) and sample each sequence's first token.
+
+        ``riders``: live decoding sequences whose next feed (``feed``: the
+        sampled token plus any forced literal) joins the FIRST chunk - a mixed
+        step. The prefill's GEMMs are compute-bound at ~300 rows, so the extra
+        rows cost little, and each rider advances by one sampled token without
+        a decode step of its own (one whole weight pass saved per prefill)."""
         if getattr(self.weights, "compact", False):
+            assert not riders, "mixed steps need the hipBLASLt prefill path"
             return self._prefill_fused(reqs)
+        riders = [r for r in (riders or []) if r.feed and not r.done]
         i = 0
         while i < len(reqs):
             batch, T = [], 0
@@ -443,6 +458,12 @@ class LLMEngine:
                 batch.append(reqs[i])
                 T += len(reqs[i].feed)
                 i += 1
+            n_new = len(batch)
+            if riders:
+                batch += riders
+                self.stats["mixed_riders"] += len(riders)
+                self.stats["decode_tokens"] += sum(len(r.feed) for r in riders)
+                riders = []
             feeds = [r.feed for r in batch]
             max_q, max_ctx, host = self._meta(batch, feeds, decode=False)
             rows = np.array([r.grammar.mask_row() for r in batch], np.int32)
@@ -451,7 +472,7 @@ class LLMEngine:
             meta = self._build_meta(dev, max_q, max_ctx, False)
             nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
             self.stats["prefill_tokens"] += T
-            for r in batch:
+            for r in batch[:n_new]:
                 self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
             self._sample_and_advance(batch, nxt, time.perf_counter())
 
@@ -654,7 +675,24 @@ class LLMEngine:
                     if pf_pool is not None:
                         pending.append((new, pf_pool.submit(self._prefill_timed, new)))
                     else:
-                        self._prefill_timed(new)
+                        riders: list[GenRequest] = []
+                        if self.mixed_prefill and live:
+                            # mixed step: the live sequences' next feeds ride
+                            # along on the prefill pass (their in-flight
+                            # pipelined steps are retired first)
+                            if pl is not None:
+                                pl.drain()
+                                riders = [r for r in live if not r.done and r.pl_host]
+                                for r in riders:
+                                    r.feed, r.pl_host = list(r.pl_host), []
+                            else:
+                                riders = [r for r in live if not r.done and r.feed]
+                        self._prefill_timed(new, riders)
+                        if pl is not None:
+                            for r in riders:
+                                if not r.done:
+                                    r.pl_host = list(r.feed)
+                        live = [r for r in live if not r.done]
                         joined = [r for r in new if not r.done]
                         if pl is not None:
                             for r in joined:
@@ -714,9 +752,9 @@ class LLMEngine:
                         fut.set_exception(e)
                 live, pending, waiting = [], [], []
 
-    def _prefill_timed(self, reqs: list[GenRequest]) -> None:
+    def _prefill_timed(self, reqs: list[GenRequest], riders: list[GenRequest] | None = None) -> None:
         t0 = time.perf_counter()
-        self.prefill(reqs)
+        self.prefill(reqs, riders)
         self.stats["prefill_s"] += time.perf_counter() - t0
 
     def _prefill_executor(self) -> ThreadPoolExecutor:
