@@ -89,15 +89,16 @@ def main(argv=None) -> int:
         args.stt, args.llm = "test-whisper", "test-tiny"
     info = pdist.init_distributed(prefer_gpu=not args.cpu_smoke)
     dev = info.device
+
     if dev.type == "cuda":
         torch.backends.cuda.matmul.allow_tf32 = False
 
     # event bus: embedded NATS broker on rank 0, every rank connects
     port = start_broker()[0] if info.rank == 0 else 0
     if info.world > 1:
-        obj = [port]
-        torch.distributed.broadcast_object_list(obj, src=0)
-        port = obj[0]
+        # through the rendezvous store: the first RCCL collective waits until
+        # the pipeline's own streams are in use (parallel/dist.py)
+        port = int(pdist.store_exchange(info, "loqa_nats_port", str(port)))
     loop = asyncio.new_event_loop()
     nats = NATSService(f"nats://127.0.0.1:{port}")
     loop.run_until_complete(nats.connect())

@@ -46,11 +46,31 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         backend = "nccl" if use_gpu else "gloo"
-        kw = {"device_id": device} if use_gpu else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        # no device_id: the RCCL communicator (and its streams) is created at
+        # the first collective, not here. HIP hands its few hardware queues to
+        # streams in first-use order, and which queues the two decoder streams
+        # share moves the pipeline between ~11 and ~19 utt/s (docs/PERF.md, "the
+        # 1.8x cliff"); a communicator used before the engines' streams would
+        # shift every one of them. Callers exchange startup data through the
+        # rendezvous store (``store_exchange``) and issue the first collective
+        # once the serving streams are in use.
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
     elif dist.is_initialized():
         backend = dist.get_backend()
     return DistInfo(rank, local, world, device, backend)
+
+
+def store_exchange(info: DistInfo, key: str, value: str | None = None, timeout_s: float = 300.0) -> str:
+    """Rank 0 publishes ``value`` under ``key`` in the rendezvous (TCP) store;
+    every rank returns it. No GPU collective (see init_distributed)."""
+    if info.world == 1:
+        return value or ""
+    import datetime
+    store = dist.distributed_c10d._get_default_store()
+    if info.rank == 0:
+        store.set(key, value or "")
+    store.wait([key], datetime.timedelta(seconds=timeout_s))
+    return store.get(key).decode()
 
 
 def barrier(info: DistInfo) -> None:
