@@ -75,6 +75,40 @@ def test_llm_pipelined_decode_gpu():
         assert len(json.loads(o)["commands"]) == n
 
 
+def test_llm_mixed_prefill_gpu(monkeypatch):
+    """Mixed steps on the GPU (the live sequences' feeds ride on a prefill pass
+    through hipBLASLt GEMMs and the split-KV prefill attention, after a drain
+    of the pipelined steps): every request completes with valid output and the
+    expected command count, the KV pool and sequence slots are all returned."""
+    import time as _t
+    monkeypatch.setenv("LOQA_MIXED_PREFILL", "1")
+    monkeypatch.setenv("LOQA_INLINE_PREFILL", "0")
+    cfg = llama_config("test-tiny")
+    eng = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
+    assert eng.mixed_prefill and eng.pipelined
+    n_list = [2, 3, 1, 4, 2, 1]
+    tok = eng.tok
+    reqs = [GenRequest(tok.encode(f"Voice command: turn on the lights {i}", bos=True),
+                       multi_command_schema(n, min_response_tokens=3)) for i, n in enumerate(n_list)]
+    eng.warmup_graphs()
+    eng.start()
+    try:
+        fa = eng.submit_batch(reqs[:3])
+        t0 = _t.time()
+        while not all(r.t_first for r in reqs[:3]) and _t.time() - t0 < 60:
+            _t.sleep(0.001)
+        fb = eng.submit_batch(reqs[3:])
+        fa.result(timeout=120)
+        fb.result(timeout=120)
+    finally:
+        eng.stop()
+    assert eng.stats["mixed_riders"] > 0
+    for r, n in zip(reqs, n_list):
+        assert len(json.loads(r.output)["commands"]) == n
+    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
+    assert sorted(eng._free_seq_slots) == list(range(8))
+
+
 def test_llm_gpu_matches_cpu_reference_first_tokens():
     cfg = llama_config("test-tiny")
     g = LLMEngine(cfg, "cuda", max_seqs=4, use_graphs=False)

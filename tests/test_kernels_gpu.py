@@ -429,3 +429,21 @@ def test_relpos_attention_and_expand():
     assert _rel(z, ref.expand_sample(stats, cum, flen, F, 0.0)) < 1e-2
     zn = ops.expand_sample(torch.zeros_like(stats), cum, flen, F, 1.0, seed=7)[0].float()
     assert abs(zn.mean().item()) < 0.05 and abs(zn.std().item() - 1.0) < 0.05
+
+
+@pytest.mark.parametrize("D,H,Hkv,lens,causal", [
+    (128, 32, 8, [1100, 3, 640, 1], True),      # long GQA prefill, decode-like rows
+    (64, 20, 20, [1500, 1500, 1500], False),     # Whisper encoder, batch 3
+    (64, 6, 6, [65, 127, 129, 64], False),       # tile-boundary lengths (odd/one tile per half)
+])
+def test_attention_prefill2_shapes(D, H, Hkv, lens, causal):
+    """Split-KV prefill attention: key-tile counts odd / even / one (the second
+    wave group idle), lengths at the 64-key tile and 128-row boundaries."""
+    T = sum(lens)
+    q = torch.randn(T, H * D, device=DEV, dtype=torch.bfloat16)
+    kv = torch.randn(T, 2 * Hkv * D, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int32, device=DEV)
+    k, v = kv[:, : Hkv * D], kv[:, Hkv * D:]
+    o = ops.attention(q, k, v, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=causal, max_q=max(lens), cu_k=cu)
+    orf = ref.attention(q, k, v, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=causal, cu_k=cu)
+    assert _rel(o, orf) < 2e-2
