@@ -920,7 +920,9 @@ class FusedScratch:
     row statistics (sums of squares, sums) handed from the residual epilogues to
     the next GEMM's norm prologue."""
 
-    def __init__(self, device, max_tiles: int = 8192, max_rows: int = 32):
+    def __init__(self, device, max_tiles: int = 8192, max_rows: int = 128):
+        # max_rows = the largest Mpad (128): the 70B gate|up at Mpad 128 has
+        # 3584 row tiles x 128 rows of statistics
         self.counters = torch.zeros(max_tiles, dtype=torch.int32, device=device)
         self.rowsq = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
         self.rowsum = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)

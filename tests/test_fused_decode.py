@@ -306,3 +306,12 @@ def test_whisper_fused_decode_matches_fast_gpu():
     for a, b in zip(outs["fused"], outs["fast"]):
         rel = float((a - b).norm() / b.norm())
         assert rel < 2e-2, rel
+
+
+def test_fused_scratch_holds_70b_mpad128():
+    """Row statistics for the largest decode GEMM at the largest Mpad: the 70B
+    gate|up (N = 57344) at Mpad 128 with 16-row tiles (config 5's tuner runs
+    it)."""
+    scr = ops.FusedScratch(torch.device("cpu"))
+    ntiles = 57344 // 16
+    assert ntiles <= scr.counters.numel() and ntiles * 128 <= scr.rowsq.numel()
