@@ -219,3 +219,55 @@ def test_stt_continuous_batching_gpu():
     eng.stop()
     for got, want in zip(a + b, solo):
         assert got.tokens == want.tokens
+
+
+def test_hub_server_gpu_end_to_end(tmp_path):
+    """The composed hub with the ON-DEVICE processor: a relay streams audio over
+    real gRPC, the arbitration winner goes through the GPU pipeline (Whisper-
+    tiny encoder + decoder graphs, constrained Llama decode), the reply comes
+    back on the stream, and the voice event lands in SQLite and /api."""
+    import asyncio
+    import urllib.request
+
+    grpc = pytest.importorskip("grpc")
+    from loqa_hub_amd import config as cfgmod
+    from loqa_hub_amd.server import HubServer, build_gpu_processor
+    from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
+
+    def pcm(n=16000):
+        t = np.arange(n) / 16000.0
+        return (6000 * np.sin(2 * np.pi * 220 * t) * (1 + 0.5 * np.sin(2 * np.pi * 3 * t))).astype("<i2").tobytes()
+
+    async def relay(relay_id):
+        yield AudioChunk(relay_id=relay_id, audio_data=pcm(), sample_rate=16000, is_wake_word=True)
+        for i in range(2):
+            await asyncio.sleep(0.01)
+            yield AudioChunk(relay_id=relay_id, audio_data=pcm(), sample_rate=16000,
+                             is_end_of_speech=i == 1)
+
+    def http_get(url):
+        with urllib.request.urlopen(url, timeout=20) as r:
+            return r.status, r.read().decode()
+
+    async def go():
+        cfg = cfgmod.load({"LOQA_DB_PATH": str(tmp_path / "hub.db"), "NATS_URL": "embedded",
+                           "ARBITRATION_WINDOW_DURATION": "50ms", "HUB_STT_MODEL": "whisper-tiny",
+                           "HUB_LLM_MODEL": "test-tiny", "HUB_MAX_BATCH": "4"})
+        srv = HubServer(cfg, skills_dir=str(tmp_path / "skills"),
+                        skills_config_store=str(tmp_path / "skillcfg"))
+        await srv._connect_nats()
+        srv.processor = await asyncio.to_thread(build_gpu_processor, cfg, srv.nats, "cuda:0")
+        await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
+        try:
+            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
+                got = [r async for r in stream_audio_stub(ch)(relay("kitchen-relay"))]
+            last = got[-1]
+            assert last.command in ("voice_command_success", "no_speech", "error",
+                                    "confirmation_needed")
+            assert last.transcription is not None
+            base = f"http://127.0.0.1:{srv.http_port}"
+            st, body = await asyncio.to_thread(http_get, base + "/api/metrics")
+            assert st == 200 and "loqa_audio_processed_total 1.0" in body
+        finally:
+            await srv.stop()
+    asyncio.run(go())
