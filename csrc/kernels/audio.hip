@@ -37,7 +37,14 @@ __device__ __forceinline__ void atomic_max_float(float* addr, float v) {
 
 // audio: [B, n_samples] f32;  window: [400];  cosb/sinb: [400, 224];
 // filt: [n_mels, 201];  out: [B, n_mels, n_frames] f32 (log10 mel);  gmax: [B]
-__global__ __launch_bounds__(256) void logmel_kernel(
+//
+// 8 waves: wave w < 7 owns DFT bin tile w (32 bins) for the workgroup's 32
+// frames, then waves 0..3 own one 32-mel tile each. Every MFMA chain is split
+// into two independent accumulator pairs (even / odd k-steps) and the DFT basis
+// for 16 k-steps is loaded before its MFMAs, so a wave is neither one
+// dependent MFMA chain nor one global load per k-step (the 4-wave form, two bin
+// tiles per wave, measured ~370 us per 30-s utterance).
+__global__ __launch_bounds__(512) void logmel_kernel(
     const float* __restrict__ audio, int n_samples, const float* __restrict__ window,
     const float* __restrict__ cosb, const float* __restrict__ sinb,
     const float* __restrict__ filt, int n_mels, float* __restrict__ out, int n_frames,
@@ -62,42 +69,63 @@ __global__ __launch_bounds__(256) void logmel_kernel(
     (&power[0][0])[i] = 0.f;
   __syncthreads();
 
-  // 2. power spectrum: wave w handles bin tiles w, w+4
-  for (int bt = wave; bt < BIN_TILES; bt += 4) {
-    f16v re, im;
+  // 2. power spectrum: wave w handles bin tile w
+  if (wave < BIN_TILES) {
+    f16v re0, im0, re1, im1;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) { re[j] = 0.f; im[j] = 0.f; }
-    const int bin = bt * 32 + lo;
-#pragma unroll 4
-    for (int k = 0; k < NFFT; k += 2) {
-      const float a = frames[lo][k + hi];          // A[frame i][k]
-      const float bc = cosb[(k + hi) * BASIS_LD + bin];  // B[k][bin]
-      const float bs = sinb[(k + hi) * BASIS_LD + bin];
-      re = mfma_f32(a, bc, re);
-      im = mfma_f32(a, bs, im);
+    for (int j = 0; j < 16; ++j) { re0[j] = 0.f; im0[j] = 0.f; re1[j] = 0.f; im1[j] = 0.f; }
+    const int bin = wave * 32 + lo;
+    const float* cb = cosb + hi * BASIS_LD + bin;
+    const float* sb = sinb + hi * BASIS_LD + bin;
+    // NFFT = 400 = 12 x 32 + 16: blocks of 16 k-steps (32 taps) then a tail of 8
+    int k = 0;
+    for (; k + 32 <= NFFT; k += 32) {
+      float bc[16], bs[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        bc[u] = cb[(size_t)(k + 2 * u) * BASIS_LD];
+        bs[u] = sb[(size_t)(k + 2 * u) * BASIS_LD];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u += 2) {
+        const float a0 = frames[lo][k + 2 * u + hi], a1 = frames[lo][k + 2 * u + 2 + hi];
+        re0 = mfma_f32(a0, bc[u], re0);
+        im0 = mfma_f32(a0, bs[u], im0);
+        re1 = mfma_f32(a1, bc[u + 1], re1);
+        im1 = mfma_f32(a1, bs[u + 1], im1);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (NFFT % 32) / 2; ++u) {
+      const float a = frames[lo][k + 2 * u + hi];
+      re0 = mfma_f32(a, cb[(size_t)(k + 2 * u) * BASIS_LD], re0);
+      im0 = mfma_f32(a, sb[(size_t)(k + 2 * u) * BASIS_LD], im0);
     }
     // C layout: col = lane&31 (bin), row = (j&3) + 8*(j>>2) + 4*hi (frame)
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int fr = (j & 3) + 8 * (j >> 2) + 4 * hi;
-      if (bin < NBINS) power[fr][bin] = re[j] * re[j] + im[j] * im[j];
+      const float r = re0[j] + re1[j], im = im0[j] + im1[j];
+      if (bin < NBINS) power[fr][bin] = r * r + im * im;
     }
   }
   __syncthreads();
 
   // 3. mel projection: wave w -> mel tile w (32 mels), K = 202 (power col 201 = 0)
   float wmax = -FLT_MAX;
-  for (int mt = wave; mt * 32 < n_mels; mt += 4) {
-    f16v acc;
+  if (wave * 32 < n_mels) {
+    f16v acc0, acc1;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-    const int mel = mt * 32 + lo;
+    for (int j = 0; j < 16; ++j) { acc0[j] = 0.f; acc1[j] = 0.f; }
+    const int mel = wave * 32 + lo;
     const bool mv = mel < n_mels;
-#pragma unroll 4
-    for (int k = 0; k < NBINS + 1; k += 2) {
-      const float a = power[lo][k + hi];
-      const float bf = (mv && k + hi < NBINS) ? filt[mel * NBINS + k + hi] : 0.f;
-      acc = mfma_f32(a, bf, acc);
+    const float* fr_ = filt + (size_t)(mv ? mel : 0) * NBINS;
+#pragma unroll 2
+    for (int k = 0; k < NBINS + 1; k += 4) {    // 202 = 50 x 4 + 2
+      const float f0v = (mv && k + hi < NBINS) ? fr_[k + hi] : 0.f;
+      const float f1v = (mv && k + 2 + hi < NBINS && k + 2 < NBINS + 1) ? fr_[k + 2 + hi] : 0.f;
+      acc0 = mfma_f32(power[lo][k + hi], f0v, acc0);
+      if (k + 2 < NBINS + 1) acc1 = mfma_f32(power[lo][k + 2 + hi], f1v, acc1);
     }
     if (mv) {
       float* orow = out + ((size_t)b * n_mels + mel) * n_frames;
@@ -105,7 +133,7 @@ __global__ __launch_bounds__(256) void logmel_kernel(
       for (int j = 0; j < 16; ++j) {
         const int fr = f0 + (j & 3) + 8 * (j >> 2) + 4 * hi;
         if (fr < n_frames) {
-          const float lv = log10f(fmaxf(acc[j], 1e-10f));
+          const float lv = log10f(fmaxf(acc0[j] + acc1[j], 1e-10f));
           orow[fr] = lv;
           wmax = fmaxf(wmax, lv);
         }
@@ -141,7 +169,7 @@ extern "C" int loqa_log_mel(const float* audio, int B, int n_samples, const floa
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(fill_kernel, dim3((B + 255) / 256), dim3(256), 0, s, gmax, B, -FLT_MAX);
   dim3 grid((n_frames + FRAMES_PER_WG - 1) / FRAMES_PER_WG, B);
-  hipLaunchKernelGGL(logmel_kernel, grid, dim3(256), 0, s, audio, n_samples, window, cosb, sinb,
+  hipLaunchKernelGGL(logmel_kernel, grid, dim3(512), 0, s, audio, n_samples, window, cosb, sinb,
                      filt, n_mels, work, n_frames, gmax);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

@@ -57,4 +57,11 @@ res["pf_rmsnorm_res_318x4096"] = (round(us, 1), round(318 * 4096 * 2 * 4 / us / 
 ss = [torch.randn(318, 28672, **bf) for _ in range(NC)]
 us = dtime(lambda i: ops.silu_mul(ss[i % NC]))
 res["pf_silu_mul_318x28672"] = (round(us, 1), round(318 * 28672 * 2 * 1.5 / us / 1e6, 2))
+# Whisper-large-v3 log-mel of one / four 30-s windows (f32 MFMA DFT + mel GEMM)
+from loqa_hub_amd.ops.reference import MelConstants  # noqa: E402
+mc = MelConstants.create(128)
+for B in (1, 4):
+    au = [torch.randn(B, 480000, device=dev) * 0.1 for _ in range(NC)]
+    us = dtime(lambda i: ops.log_mel(au[i % NC], mc), n=8)
+    res[f"log_mel_B{B}"] = (round(us, 1), 0.0)
 print(json.dumps({k: {"us": v[0], "TBps": v[1]} for k, v in res.items()}))
