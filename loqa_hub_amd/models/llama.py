@@ -339,9 +339,13 @@ class LlamaModel:
         cfg, w = self.cfg, self.w
         H, Hkv, D, d = w.h, w.hkv, cfg.head_dim, cfg.d_model
         Mpad = meta.tokens.numel()
-        residual = self.embed(meta.tokens).contiguous()
-        # layer 0's RMSNorm row scale: one partial sum of squares per row
-        scratch.seed_stats(residual, sums=False)
+        # embedding + layer 0's RMSNorm row scale (one partial sum of squares per
+        # row) in one launch
+        if ops.FUSED_EMBED and w.tp.world == 1 and meta.tokens.dtype == torch.int32:
+            residual = ops.embed_stats(meta.tokens, w.embed, scratch)
+        else:
+            residual = self.embed(meta.tokens).contiguous()
+            scratch.seed_stats(residual, sums=False)
         num_splits, split_keys = ops.decode_attn_splits(meta.max_ctx, meta.ctx_lens.numel() * Hkv,
                                                         split_keys, getattr(w, "max_wgs", None))
         q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
@@ -364,8 +368,10 @@ class LlamaModel:
             a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
                                  eps=cfg.norm_eps)
             ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
-        sel = residual.index_select(0, meta.logit_idx).contiguous()
-        hf = ops.rmsnorm(sel, w.final_norm, cfg.norm_eps)
+        if ops.FUSED_EMBED:
+            hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
+        else:
+            hf = ops.rmsnorm(residual.index_select(0, meta.logit_idx), w.final_norm, cfg.norm_eps)
         return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -304,8 +304,12 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
     d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
     enc_splits = (cfg.n_audio_ctx + cross_split_keys - 1) // cross_split_keys
     Mpad = tokens.numel()
-    residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
-    scratch.seed_stats(residual)
+    if ops.FUSED_EMBED:
+        residual = ops.embed_stats(tokens, w.tok_embed, scratch, positions=positions,
+                                   pos_embed=w.dec_pos, sums=True)
+    else:
+        residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
+        scratch.seed_stats(residual)
     q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
     for i, F in enumerate(w.dec_f):
         ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5, positions=positions, q_out=q,
@@ -324,8 +328,10 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
         ops.skinny_fused(a, F["xo"], "resid", scratch, residual=residual, row_sums=True)
         m = ops.skinny_fused(residual, F["fc1"], "act", scratch, act="gelu", eps=1e-5)
         ops.skinny_fused(m, F["fc2"], "resid", scratch, residual=residual, row_sums=True)
-    sel = residual.index_select(0, logit_idx).contiguous()
-    hf = ops.layernorm(sel, w.dec_ln_w, w.dec_ln_b, 1e-5)
+    if ops.FUSED_EMBED:
+        hf = ops.layernorm(residual, w.dec_ln_w, w.dec_ln_b, 1e-5, row_idx=logit_idx)
+    else:
+        hf = ops.layernorm(residual.index_select(0, logit_idx), w.dec_ln_w, w.dec_ln_b, 1e-5)
     return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
 

@@ -37,38 +37,56 @@ def _bf16_contig(t: torch.Tensor, name: str) -> None:
 
 
 # --------------------------------------------------------------------- norms
-def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float,
-            residual: torch.Tensor | None = None) -> torch.Tensor:
-    """y = rmsnorm(x [+ residual]) * w; if residual is given it is updated in place
-    to x + residual (the fused pre-norm residual stream)."""
-    if not _gpu(x):
-        return ref.rmsnorm(x, w, eps, residual)
+def _norm_rows(x: torch.Tensor, residual, row_idx) -> tuple[int, int]:
     d = x.shape[-1]
-    rows = x.numel() // d
+    if row_idx is not None:
+        # gathered rows: y[i] = norm(x[row_idx[i]]); no residual update then
+        assert residual is None and x.dim() == 2
+        assert row_idx.dtype == torch.int64 and row_idx.is_contiguous()
+        return row_idx.numel(), d
+    return x.numel() // d, d
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float,
+            residual: torch.Tensor | None = None,
+            row_idx: torch.Tensor | None = None) -> torch.Tensor:
+    """y = rmsnorm(x [+ residual]) * w; if residual is given it is updated in place
+    to x + residual (the fused pre-norm residual stream). ``row_idx`` (int64)
+    normalises only rows x[row_idx] (the decode step's logit rows) in the same
+    launch."""
+    if not _gpu(x):
+        if row_idx is not None:
+            x = x.index_select(0, row_idx.long())
+        return ref.rmsnorm(x, w, eps, residual)
+    rows, d = _norm_rows(x, residual, row_idx)
     _bf16_contig(x, "x"); _bf16_contig(w, "w")
     if residual is not None:
         _bf16_contig(residual, "residual")
         assert residual.shape == x.shape
     assert w.numel() == d
-    y = torch.empty_like(x)
+    y = torch.empty((rows, d) if row_idx is not None else x.shape, dtype=x.dtype, device=x.device)
     check(kernels().loqa_rmsnorm(ptr(x), ptr(residual), ptr(w), ptr(y), rows, d, eps,
-                                 stream_ptr(x)), "rmsnorm")
+                                 ptr(row_idx), stream_ptr(x)), "rmsnorm")
     return y
 
 
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
-              residual: torch.Tensor | None = None) -> torch.Tensor:
+              residual: torch.Tensor | None = None,
+              row_idx: torch.Tensor | None = None) -> torch.Tensor:
+    """y = layernorm(x [+ residual]) * w + b; ``residual`` / ``row_idx`` as in
+    :func:`rmsnorm`."""
     if not _gpu(x):
+        if row_idx is not None:
+            x = x.index_select(0, row_idx.long())
         return ref.layernorm(x, w, b, eps, residual)
-    d = x.shape[-1]
-    rows = x.numel() // d
+    rows, d = _norm_rows(x, residual, row_idx)
     _bf16_contig(x, "x"); _bf16_contig(w, "w"); _bf16_contig(b, "b")
     if residual is not None:
         _bf16_contig(residual, "residual")
         assert residual.shape == x.shape
-    y = torch.empty_like(x)
+    y = torch.empty((rows, d) if row_idx is not None else x.shape, dtype=x.dtype, device=x.device)
     check(kernels().loqa_layernorm(ptr(x), ptr(residual), ptr(w), ptr(b), ptr(y), rows, d, eps,
-                                   stream_ptr(x)), "layernorm")
+                                   ptr(row_idx), stream_ptr(x)), "layernorm")
     return y
 
 
@@ -358,6 +376,9 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 
 _FSPLITS: dict = {}
 MAX_DECODE_WGS = int(os.environ.get("LOQA_MAX_DECODE_WGS", "256"))
+# fused-GEMM decode steps: embedding + layer-0 row statistics in one launch and
+# the final norm gathering its logit rows itself (0: the unfused torch ops)
+FUSED_EMBED = os.environ.get("LOQA_FUSED_EMBED", "1") != "0"
 _CAP = [MAX_DECODE_WGS]   # active co-scheduling cap while tuning (see decode_cap)
 
 
@@ -719,6 +740,37 @@ def embed_pos(tokens: torch.Tensor, positions: torch.Tensor, tok_embed: torch.Te
                                                   device=tok_embed.device)
     check(kernels().loqa_embed_pos(ptr(tokens), ptr(positions), ptr(tok_embed), ptr(pos_embed),
                                    ptr(out), rows, d, stream_ptr(tok_embed)), "embed_pos")
+    return out
+
+
+def embed_stats(tokens: torch.Tensor, tok_embed: torch.Tensor, scratch: "FusedScratch",
+                positions: torch.Tensor | None = None, pos_embed: torch.Tensor | None = None,
+                sums: bool = False) -> torch.Tensor:
+    """Decode-step input of the fused-GEMM path in one launch: the embedded rows
+    tok_embed[tokens] (+ pos_embed[positions]) [rows, d] bf16, with their row
+    sums of squares (and sums) written to ``scratch`` as ONE partial tile for
+    layer 0's norm prologue (what ``scratch.seed_stats`` computes)."""
+    rows, d = tokens.numel(), tok_embed.shape[1]
+    if not _gpu(tok_embed):
+        x = tok_embed[tokens.long()]
+        if pos_embed is not None:
+            x = (x.float() + pos_embed[positions.long()].float()).to(torch.bfloat16)
+        scratch.seed_stats(x, sums=sums)
+        return x
+    assert tokens.dtype == torch.int32 and tokens.is_contiguous()
+    _bf16_contig(tok_embed, "tok_embed")
+    if pos_embed is not None:
+        assert positions is not None and positions.dtype == torch.int32
+        assert positions.numel() == rows and positions.is_contiguous()
+        _bf16_contig(pos_embed, "pos_embed")
+        assert pos_embed.shape[1] == d
+    assert rows <= scratch.rowsq.numel()
+    out = torch.empty(rows, d, dtype=torch.bfloat16, device=tok_embed.device)
+    check(kernels().loqa_embed_stats(ptr(tokens), ptr(positions if pos_embed is not None else None),
+                                     ptr(tok_embed), ptr(pos_embed), ptr(out), ptr(scratch.rowsq),
+                                     ptr(scratch.rowsum) if sums else None, rows, d,
+                                     stream_ptr(tok_embed)), "embed_stats")
+    scratch.stat_tiles = 1
     return out
 
 

@@ -44,9 +44,10 @@ class FusedParams(ctypes.Structure):
 
 
 _KERNEL_SIGS = {
-    "loqa_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "loqa_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p,
+                     c_void_p],
     "loqa_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
-                       c_void_p],
+                       c_void_p, c_void_p],
     "loqa_silu_mul": [c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "loqa_gelu_bias": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_void_p],
     "loqa_rope_kv_append": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -79,6 +80,8 @@ _KERNEL_SIGS = {
     "loqa_slab_bias_act": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                            c_void_p],
     "loqa_embed_pos": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "loqa_embed_stats": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_int, c_int, c_void_p],
     "loqa_conv1d": [c_void_p, c_ll, c_int, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p,
                     c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,

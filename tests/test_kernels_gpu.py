@@ -50,6 +50,45 @@ def test_layernorm(d):
     assert _rel(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("kind,d", [("rms", 4096), ("ln", 1280), ("rms", 384)])
+def test_norm_row_gather(kind, d):
+    """Norm of gathered rows (the decode step's final norm of its logit rows)
+    against index_select + the fp32 reference."""
+    x = torch.randn(40, d, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).bfloat16()
+    b = torch.randn(d, device=DEV).bfloat16()
+    idx = torch.tensor([39, 0, 7, 7, 21], device=DEV, dtype=torch.int64)
+    sel = x.index_select(0, idx)
+    if kind == "rms":
+        y, yr = ops.rmsnorm(x, w, 1e-5, row_idx=idx), ref.rmsnorm(sel, w, 1e-5)
+    else:
+        y, yr = ops.layernorm(x, w, b, 1e-5, row_idx=idx), ref.layernorm(sel, w, b, 1e-5)
+    assert y.shape == (5, d)
+    assert _rel(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("d,with_pos,sums", [(4096, False, False), (1280, True, True),
+                                             (384, True, True)])
+def test_embed_stats(d, with_pos, sums):
+    """Fused embedding + layer-0 row statistics vs embedding + seed_stats."""
+    V, P, rows = 1000, 448, 48
+    te = torch.randn(V, d, device=DEV, dtype=torch.bfloat16)
+    pe = torch.randn(P, d, device=DEV, dtype=torch.bfloat16) if with_pos else None
+    tok = torch.randint(0, V, (rows,), device=DEV, dtype=torch.int32)
+    pos = torch.randint(0, P, (rows,), device=DEV, dtype=torch.int32) if with_pos else None
+    s1, s2 = ops.FusedScratch(DEV), ops.FusedScratch(DEV)
+    out = ops.embed_stats(tok, te, s1, positions=pos, pos_embed=pe, sums=sums)
+    xr = te[tok.long()]
+    if with_pos:
+        xr = (xr.float() + pe[pos.long()].float()).bfloat16()
+    assert torch.equal(out, xr)
+    s2.seed_stats(xr, sums=sums)
+    assert s1.stat_tiles == 1
+    torch.testing.assert_close(s1.rowsq[:rows], s2.rowsq[:rows], rtol=1e-5, atol=1e-3)
+    if sums:
+        torch.testing.assert_close(s1.rowsum[:rows], s2.rowsum[:rows], rtol=1e-4, atol=1e-3)
+
+
 def test_silu_mul_and_gelu():
     x = torch.randn(77, 2 * 1408, device=DEV, dtype=torch.bfloat16)
     assert _rel(ops.silu_mul(x), ref.silu_mul(x)) < 1e-2
