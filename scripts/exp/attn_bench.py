@@ -13,7 +13,7 @@ bf = dict(dtype=torch.bfloat16, device=dev)
 res = {}
 L = 32
 
-for B, ctx in ((6, 400), (6, 900)):
+for B, ctx in ((6, 400), (8, 600), (6, 900)):
     Hkv, G, D, blk = 8, 4, 128, 16
     H = Hkv * G
     nb_seq = (ctx + blk - 1) // blk
@@ -25,7 +25,7 @@ for B, ctx in ((6, 400), (6, 900)):
     cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
     cl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
     ws = ops.AttnWorkspace(dev, 64, H, D, 16)
-    for sk in (128, 256, 512, 1024):
+    for sk in (128, 256, 384, 512, 1024):
         ns = -(-ctx // sk)
         it = iter(range(1 << 30))
 

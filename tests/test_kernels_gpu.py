@@ -182,9 +182,12 @@ def test_attention_prefill_paged_with_prefix(G, D):
     assert _rel(o, orf) < 2e-2
 
 
+@pytest.mark.parametrize("split_keys", [128, 256, 512])
 @pytest.mark.parametrize("qlens,G,splits", [([1, 1, 1, 1], 4, 4), ([3, 1, 7, 2], 4, 2),
                                             ([1, 1], 1, 1), ([16, 5], 8, 3)])
-def test_attention_grouped_paged(qlens, G, splits):
+def test_attention_grouped_paged(qlens, G, splits, split_keys):
+    """Paged GQA decode attention; split_keys 128 / 256 / 512 run the 4- and
+    8-wave kernels (one pass, several passes, one split or several)."""
     D, Hkv, blk = 128, 2, 16
     H = Hkv * G
     ctx = [700, 65, 300, 1][: len(qlens)]
@@ -195,8 +198,7 @@ def test_attention_grouped_paged(qlens, G, splits):
     q = torch.randn(sum(qlens), H * D, device=DEV, dtype=torch.bfloat16)
     cu = torch.tensor([0] + list(np.cumsum(qlens)), dtype=torch.int32, device=DEV)
     cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
-    ws = ops.AttnWorkspace(DEV, 64, H, D, 4)
-    split_keys = 256
+    ws = ops.AttnWorkspace(DEV, 64, H, D, 8)
 
     def run():
         return ops.attention(q, kc, vc, cu, n_heads=H, n_kv=Hkv, head_dim=D, causal=True,
@@ -212,8 +214,10 @@ def test_attention_grouped_paged(qlens, G, splits):
     assert int(ws.counters.abs().sum()) == 0
 
 
-def test_attention_grouped_cross_starts():
-    """Whisper cross-attention: subset of utterances addressed by start/len."""
+@pytest.mark.parametrize("split_keys", [128, 256, 512, 1536])
+def test_attention_grouped_cross_starts(split_keys):
+    """Whisper cross-attention: subset of utterances addressed by start/len
+    (4 / 8 / 16-wave workgroups, 12 / 6 / 3 / 1 splits)."""
     D, H, T = 64, 6, 1500
     enc = torch.randn(4 * T, 2 * H * D, device=DEV, dtype=torch.bfloat16)
     live = [0, 2, 3]
@@ -221,9 +225,10 @@ def test_attention_grouped_cross_starts():
     cu = torch.arange(len(live) + 1, dtype=torch.int32, device=DEV)
     starts = torch.tensor([i * T for i in live], dtype=torch.int32, device=DEV)
     lens = torch.full((len(live),), T, dtype=torch.int32, device=DEV)
-    ws = ops.AttnWorkspace(DEV, 64, H, D, 8)
+    ws = ops.AttnWorkspace(DEV, 64, H, D, 12)
     o = ops.attention(q, enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D, causal=False, max_q=1,
-                      cu_k=starts, ctx_lens=lens, grouped=True, split_keys=256, num_splits=6, workspace=ws)
+                      cu_k=starts, ctx_lens=lens, grouped=True, split_keys=split_keys,
+                      num_splits=-(-T // split_keys), workspace=ws)
     orf = ref.attention(q, enc, enc[:, H * D:], cu, n_heads=H, n_kv=H, head_dim=D, causal=False,
                         cu_k=starts, ctx_lens=lens)
     assert _rel(o, orf) < 2e-2
