@@ -23,7 +23,8 @@ import torch
 
 from .. import ops
 from ..models.configs import WhisperConfig
-from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused
+from ..models.whisper import (WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused,
+                              decode_step_mega)
 from ..utils.tracing import tracer
 from .batching import join_futures, plan_step
 from .kv_cache import PagedKVCache
@@ -107,6 +108,12 @@ class STTEngine:
         # utterances, written in place each batch (graph-captured steps read it)
         self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
                                 device=self.device) for _ in range(cfg.dec_layers)]
+        # persistent one-launch decoder step for 16-row steps (ops.WhisperMega)
+        self.mega = None
+        if (self.fused and self.is_gpu and os.environ.get("LOQA_STT_MEGA", "0") == "1"
+                and cfg.head_dim == 64 and cfg.d_model % 128 == 0 and cfg.d_model <= 1280):
+            self.mega = ops.WhisperMega(self.model.w, self.kv.k, self.kv.v, self.xkv,
+                                        max_seqs=ops.WhisperMega.ROWS)
         self._graphs: dict[tuple[int, int], dict] = {}
         self._graphs_frozen = False     # see LLMEngine: no capture while serving
         # token budget of one decoder step (each new sequence feeds the 4-token
@@ -235,6 +242,12 @@ class STTEngine:
 
     def _fast_forward(self, dev: dict, max_q: int, B_pad: int, ctx: int | None = None) -> torch.Tensor:
         ns = self._self_splits(ctx)
+        if (self.mega is not None and dev["tokens"].numel() == ops.WhisperMega.ROWS
+                and B_pad <= self.mega.max_seqs):
+            logits = decode_step_mega(self.model, dev["tokens"], dev["positions"], dev["slots"],
+                                      dev["cu_q"], dev["ctx_lens"], dev["block_tables"],
+                                      dev["enc_starts"], dev["enc_lens"], dev["logit_idx"], self.mega)
+            return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
         if self.fused and dev["tokens"].numel() <= 64:
             logits = decode_step_fused(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                        dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,

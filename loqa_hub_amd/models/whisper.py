@@ -335,6 +335,22 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
     return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
 
+def decode_step_mega(model: "WhisperModel", tokens: torch.Tensor, positions: torch.Tensor,
+                     slots: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor,
+                     block_tables: torch.Tensor, enc_starts: torch.Tensor, enc_lens: torch.Tensor,
+                     logit_idx: torch.Tensor, mega) -> torch.Tensor:
+    """Decoder step with every layer in ONE persistent launch
+    (``ops.whisper_mega``): embedding -> 32 x (qkv, self-attention, o, xq,
+    cross-attention, xo, fc1, fc2) as a dependency-ordered work list -> final
+    LayerNorm of the logit rows -> vocab GEMM. 16 token rows (Mpad 16); same
+    metadata contract as ``decode_step_fused``."""
+    w = model.w
+    residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
+    ops.whisper_mega(mega, residual, slots, cu_q, ctx_lens, block_tables, enc_starts, enc_lens)
+    hf = ops.layernorm(residual, w.dec_ln_w, w.dec_ln_b, 1e-5, row_idx=logit_idx)
+    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
+
+
 def pad_or_trim(audio: np.ndarray, n: int = 480000) -> np.ndarray:
     if len(audio) >= n:
         return audio[:n]

@@ -1235,3 +1235,77 @@ def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, pos
     ref.rope_kv_append(qkv, positions, cos_sin, k_cache, v_cache, slots, H, Hkv, D)
     q_out.copy_(qkv[:, : H * D])
     return q_out
+
+
+# ------------------------------------------- Whisper decoder: one persistent launch
+class WhisperMega:
+    """State of the persistent Whisper decoder-step kernel
+    (``csrc/kernels/whisper_mega.hip``): the per-layer pointer table, the
+    inter-phase activation buffers, the split partials and the per-step sync
+    words. Built once per engine; every buffer is fixed so a captured graph
+    replays against it. Token rows per step: ``ROWS`` (Mpad 16)."""
+    ROWS = 16
+    XSK = 256          # cross-attention keys per split (kernel constant)
+
+    def __init__(self, w, k_cache: torch.Tensor, v_cache: torch.Tensor, xkv: list[torch.Tensor],
+                 max_seqs: int, grid: int | None = None):
+        cfg = w.cfg
+        d, H, D, F = cfg.d_model, cfg.n_heads, cfg.head_dim, w.dec[0]["fc1"].shape[0]
+        assert D == 64 and H * D == d and d % 128 == 0 and d <= 1280 and F % 128 == 0
+        dev = k_cache.device
+        self.d, self.H, self.F, self.L = d, H, F, cfg.dec_layers
+        self.nsplit = (cfg.n_audio_ctx + self.XSK - 1) // self.XSK
+        self.max_seqs = max_seqs
+        self.blk = k_cache.shape[3]
+        self.kv_bytes = k_cache[0].numel() * 2
+        assert self.kv_bytes < 2 ** 31
+        rows = []
+        for i, (L, P) in enumerate(zip(w.dec, w.dec_p)):
+            rows.append([P[k].data_ptr() for k in ("wqkv", "wo", "xq", "xo", "fc1", "fc2")]
+                        + [L[k].data_ptr() for k in ("bqkv", "bo", "xq_b", "xo_b", "fc1_b", "fc2_b")]
+                        + [L[k].data_ptr() for k in ("ln1_w", "ln1_b", "lnx_w", "lnx_b", "ln2_w", "ln2_b")]
+                        + [k_cache[i].data_ptr(), v_cache[i].data_ptr(), xkv[i].data_ptr()])
+        self._keep = (w, k_cache, v_cache, xkv)       # the table points into these
+        self.table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        R = self.ROWS
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.qb = torch.zeros(R, d, **bf)
+        self.ab = torch.zeros(R, d, **bf)
+        self.xqb = torch.zeros(R, d, **bf)
+        self.mb = torch.zeros(R, F, **bf)
+        self.part = torch.zeros(max_seqs * H * self.nsplit * R * 66, dtype=torch.float32, device=dev)
+        self.sync = torch.zeros(self.L * 8 + max_seqs * H + 1, dtype=torch.int32, device=dev)
+        self.grid = grid or int(os.environ.get("LOQA_STT_MEGA_WGS", "256"))
+        self.eps = 1e-5
+        self.scale_log2 = (1.0 / math.sqrt(D)) * 1.4426950408889634
+
+    def error(self) -> int:
+        """Non-zero when a step's bounded dependency wait expired (host read)."""
+        return int(self.sync[-1].item())
+
+
+def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: torch.Tensor,
+                 ctx_lens: torch.Tensor, block_tables: torch.Tensor, enc_starts: torch.Tensor,
+                 enc_lens: torch.Tensor) -> torch.Tensor:
+    """All decoder layers of one Whisper step on the residual rows ``x``
+    [16, d] bf16 (embedded tokens in, pre-final-LayerNorm residual out), in one
+    launch. Metadata as for the fused path (``STTEngine._host_meta``)."""
+    from ._lib import WhisperMegaParams
+    B = cu_q.numel() - 1
+    R = m.ROWS
+    assert x.is_cuda and x.shape == (R, m.d) and x.dtype == torch.bfloat16 and x.is_contiguous()
+    assert slots.numel() == R and 0 < B <= m.max_seqs
+    for t in (slots, cu_q, ctx_lens, block_tables, enc_starts, enc_lens):
+        assert t.dtype == torch.int32 and t.is_contiguous() and t.is_cuda
+    p = WhisperMegaParams()
+    p.layers, p.L = ptr(m.table), m.L
+    p.x, p.qb, p.ab, p.xqb, p.mb = ptr(x), ptr(m.qb), ptr(m.ab), ptr(m.xqb), ptr(m.mb)
+    p.part, p.sync = ptr(m.part), ptr(m.sync)
+    p.slots, p.cu_q, p.ctx_lens, p.block_tables = ptr(slots), ptr(cu_q), ptr(ctx_lens), ptr(block_tables)
+    p.max_blocks, p.blk = block_tables.shape[1], m.blk
+    p.enc_starts, p.enc_lens = ptr(enc_starts), ptr(enc_lens)
+    p.B, p.d, p.H, p.ffn, p.nsplit = B, m.d, m.H, m.F, m.nsplit
+    p.kv_bytes, p.eps, p.scale_log2 = m.kv_bytes, m.eps, m.scale_log2
+    p.dbg = ptr(m.dbg) if getattr(m, "dbg", None) is not None else None
+    check(kernels().loqa_whisper_mega(ctypes.byref(p), m.grid, stream_ptr(x)), "whisper_mega")
+    return x
