@@ -5,8 +5,6 @@ import torch
 
 
 def _run(cfg_name: str, mode: str, steps: int = 3, n_seq: int = 3):
-    import os
-    os.environ["LOQA_STT_MEGA"] = "1"
     from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
     from loqa_hub_amd.engine.synthetic import make_batch
     from loqa_hub_amd.models.configs import whisper_config
@@ -47,9 +45,10 @@ def _run(cfg_name: str, mode: str, steps: int = 3, n_seq: int = 3):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg_name", ["test-whisper", "whisper-base", "whisper-large-v3"])
-def test_whisper_mega_matches_fused_gpu(cfg_name):
+def test_whisper_mega_matches_fused_gpu(cfg_name, monkeypatch):
     """Logits of three decoder steps (a 4-token SOT prefill step, then single
     tokens) agree with the fused-epilogue path."""
+    monkeypatch.setenv("LOQA_STT_MEGA", "1")
     a = _run(cfg_name, "mega")
     b = _run(cfg_name, "fused")
     for x, y in zip(a, b):
