@@ -16,6 +16,7 @@ from loqa_hub_amd.models.configs import whisper_config  # noqa: E402
 from loqa_hub_amd.models.whisper import decode_step_fused, decode_step_mega  # noqa: E402
 
 dev = torch.device("cuda", 0)
+os.environ["LOQA_STT_MEGA"] = "1"
 cfg = whisper_config(os.environ.get("MODEL", "whisper-large-v3"))
 eng = STTEngine(cfg, dev, seed=0, max_batch=8, use_graphs=False)
 grids = [int(g) for g in os.environ.get("GRIDS", "256").split(",")]
