@@ -44,6 +44,22 @@ from loqa_hub_amd.parallel.dp_router import gather_records, scatter_pcm, slot_le
 BASELINE_MS_PER_ADDED_COMMAND = 200.0
 
 
+def spawn_broker() -> tuple[int, "subprocess.Popen"]:
+    """NATS broker in its own process (as nats-server is in a deployment): the
+    serving process's GIL carries no broker work, which matters most on rank 0
+    of a DP run, where every rank publishes. Started before anything touches
+    the GPU; it exits when our end of its stdin closes."""
+    import subprocess
+    p = subprocess.Popen([sys.executable, "-m", "loqa_hub_amd.messaging.nats_server"],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True,
+                         cwd=os.path.dirname(os.path.abspath(__file__)))
+    line = p.stdout.readline().split()
+    if len(line) != 2 or line[0] != "port":
+        p.kill()
+        raise RuntimeError(f"NATS broker did not start: {line}")
+    return int(line[1]), p
+
+
 def start_broker() -> tuple[int, threading.Thread]:
     ready = threading.Event()
     box = {}
@@ -87,14 +103,21 @@ def main(argv=None) -> int:
 
     if args.cpu_smoke:
         args.stt, args.llm = "test-whisper", "test-tiny"
+    # event bus: one NATS broker for the node (rank 0 starts it), every rank
+    # connects; a separate process unless LOQA_BENCH_BROKER=thread
+    broker = None
+    port = 0
+    if int(os.environ.get("RANK", "0")) == 0:
+        if os.environ.get("LOQA_BENCH_BROKER", "process") == "process":
+            port, broker = spawn_broker()
+        else:
+            port = start_broker()[0]
     info = pdist.init_distributed(prefer_gpu=not args.cpu_smoke)
     dev = info.device
 
     if dev.type == "cuda":
         torch.backends.cuda.matmul.allow_tf32 = False
 
-    # event bus: embedded NATS broker on rank 0, every rank connects
-    port = start_broker()[0] if info.rank == 0 else 0
     if info.world > 1:
         # through the rendezvous store: the first RCCL collective waits until
         # the pipeline's own streams are in use (parallel/dist.py)
@@ -260,6 +283,9 @@ def main(argv=None) -> int:
         print(json.dumps(out), flush=True)
     loop.run_until_complete(nats.close())
     pdist.shutdown(info)
+    if broker is not None:
+        broker.stdin.close()
+        broker.wait(timeout=10)
     return 0
 
 

@@ -113,9 +113,20 @@ class GrammarTables:
         rows.append(digits)
         self.ROW_FREE_OPEN = 2  # string body that may not close yet (min length)
         rows.append(safe)
+        # two digits in one token ("95"): a Digits field with >= 2 digits left
+        # samples one of these instead of two single digits (one decode step)
+        digits2 = torch.zeros(V, dtype=torch.bool)
+        for t in range(tok.n_special, tok.n_real):
+            s2 = tok.token_text(t)
+            if len(s2) == 2 and s2.isdigit():
+                digits2[t] = True
+        self.ROW_DIGIT2 = 3 if bool(digits2.any()) else -1
+        if self.ROW_DIGIT2 >= 0:
+            rows.append(digits2)
         # stand-ins for "some allowed token" in GrammarState.predict
         self.generic_free = int(safe.nonzero()[0])
         self.generic_digit = tok.token_id("0")
+        self.generic_digit2 = int(digits2.nonzero()[0]) if self.ROW_DIGIT2 >= 0 else -1
         self._rows = rows
         self._tries: dict[tuple, _Trie] = {}
         self._lit_cache: dict[str, list[int]] = {}
@@ -213,6 +224,11 @@ class GrammarState:
             return self.node.row
         if isinstance(s, Free):
             return self.t.ROW_FREE if self.count >= s.min_tokens else self.t.ROW_FREE_OPEN
+        return self._digit_row(s)
+
+    def _digit_row(self, s: "Digits") -> int:
+        if s.n - self.count >= 2 and self.t.ROW_DIGIT2 >= 0:
+            return self.t.ROW_DIGIT2
         return self.t.ROW_DIGIT
 
     def advance(self, tok: int) -> list[int]:
@@ -244,8 +260,8 @@ class GrammarState:
                 self.emitted.append(self.t.quote)
                 return forced + self._run_forced()
             return forced
-        # Digits
-        self.count += 1
+        # Digits: one or two digits per token
+        self.count += max(1, len(self.t.tok.token_text(tok)))
         if self.count >= s.n:
             self.i += 1
             forced = self._run_forced()
@@ -283,7 +299,8 @@ class GrammarState:
         elif isinstance(s, Free):
             tok = self.t.generic_free
         else:
-            tok = self.t.generic_digit
+            tok = (self.t.generic_digit2 if self._digit_row(s) == self.t.ROW_DIGIT2
+                   else self.t.generic_digit)
         f = self.fork()
         forced = f.advance(tok)
         return forced, f.mask_row(), f.done

@@ -89,6 +89,10 @@ class SyntheticTokenizer:
             add(" " + w)
             add(w.capitalize())
             add(" " + w.capitalize())
+        # every two-digit number is one token, as in Llama-3's BPE (digits are
+        # pre-split into runs of up to three); appended last so earlier ids stay
+        for n in range(100):
+            add(f"{n:02d}")
         if len(strings) > vocab_size:
             raise ValueError(f"vocab_size {vocab_size} too small for the synthetic tokenizer")
         self.n_real = len(strings)

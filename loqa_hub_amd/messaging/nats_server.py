@@ -127,3 +127,31 @@ class NATSServer:
             self.msgs_routed += 1
         except Exception:
             pass
+
+
+def main(argv=None) -> int:
+    """Stand-alone broker process: ``python -m loqa_hub_amd.messaging.nats_server
+    [--port P]`` prints ``port <n>`` once listening and exits when its stdin
+    closes (so it never outlives the process that started it)."""
+    import argparse
+    import sys
+    import threading
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    args = ap.parse_args(argv)
+    loop = asyncio.new_event_loop()
+    srv = loop.run_until_complete(NATSServer(args.host, args.port).start())
+    print(f"port {srv.port}", flush=True)
+
+    def watch_stdin():
+        sys.stdin.read()                      # EOF: the parent is gone
+        loop.call_soon_threadsafe(loop.stop)
+
+    threading.Thread(target=watch_stdin, daemon=True).start()
+    loop.run_forever()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -70,10 +70,18 @@ def test_grammar_min_length_and_digits():
     st.advance(tok.token_id("y"))
     assert st.mask_row() == tables.ROW_FREE
     st.advance(tables.quote)
-    assert st.mask_row() == tables.ROW_DIGIT
-    st.advance(tok.token_id("4"))
-    st.advance(tok.token_id("2"))
+    # two digits in one token (Llama-3 BPE keeps numbers <= 999 whole)
+    assert st.mask_row() == tables.ROW_DIGIT2
+    assert bool(tables.allowed(st.mask_row())[tok.token_id("42")])
+    assert not bool(tables.allowed(st.mask_row())[tok.token_id("4")])
+    st.advance(tok.token_id("42"))
     assert st.done and json.loads(st.text()) == {"a": "xy", "d": 0.42}
+    # a single-digit field still samples from the one-digit row
+    st = GrammarState(tables, [Lit("0."), Digits(1)])
+    st.start()
+    assert st.mask_row() == tables.ROW_DIGIT
+    st.advance(tok.token_id("7"))
+    assert st.done and st.text() == "0.7"
     # choice trie: forced completion once the prefix is unique
     st = GrammarState(tables, [Lit('"'), Choice("c", ["turn_on", "turn_off"]), Lit('"')])
     st.start()
