@@ -16,6 +16,7 @@ Layout is MI355X-first rather than HF-module-first:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -242,6 +243,19 @@ class LlamaWeights:
         return n * 2
 
 
+PREFILL_DOWN_SPLITS = int(os.environ.get("LOQA_PREFILL_DOWN_SPLITS", "8"))
+
+
+def _splitk_slabs(a: torch.Tensor, w: torch.Tensor, S: int) -> torch.Tensor:
+    """a [T, K] @ w[N, K]^T as S split-K f32 slabs [S, T, N] (strided views, one
+    batched GEMM); the consumer (``ops.slab_rmsnorm``) sums them."""
+    T, K = a.shape
+    N = w.shape[0]
+    xs = a.view(T, S, K // S).transpose(0, 1)           # [S, T, K/S]
+    ws = w.view(N, S, K // S).permute(1, 2, 0)          # [S, K/S, N]
+    return torch.bmm(xs, ws, out_dtype=torch.float32)
+
+
 class LlamaModel:
     def __init__(self, w: LlamaWeights):
         self.w = w
@@ -269,9 +283,20 @@ class LlamaModel:
         h = ops.rmsnorm(x, w.layers[0]["attn_norm"], cfg.norm_eps)
         split_keys = 256
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
+        # down projection as split-K f32 slabs summed by the next norm (one
+        # strided-batched GEMM: hipBLASLt's best down tile count at ~300 rows
+        # leaves most CUs idle, PERF.md)
+        S_down = PREFILL_DOWN_SPLITS
+        if not (S_down > 0 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 128
+                and w.f % S_down == 0):
+            S_down = 0
+        part = None
         for li, L in enumerate(w.layers):
             if li > 0:
-                h = ops.rmsnorm(mlp_out, L["attn_norm"], cfg.norm_eps, residual=residual)
+                if part is not None:
+                    h = ops.slab_rmsnorm(part, residual, L["attn_norm"], cfg.norm_eps)
+                else:
+                    h = ops.rmsnorm(mlp_out, L["attn_norm"], cfg.norm_eps, residual=residual)
             qkv = ops.linear(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
@@ -284,7 +309,13 @@ class LlamaModel:
             o = tp.all_reduce_(ops.linear(attn, L["wo"]))
             h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             gu = ops.linear(h, L["w_gate_up"])
+            if S_down:
+                part = _splitk_slabs(ops.silu_mul(gu), L["w_down"], S_down)
+                continue
             mlp_out = tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["w_down"]))
+        if part is not None:
+            return ops.slab_rmsnorm(part, residual, w.final_norm, cfg.norm_eps,
+                                    row_idx=meta.logit_idx, write_residual=False)
         sel_res = residual.index_select(0, meta.logit_idx)
         sel_mlp = mlp_out.index_select(0, meta.logit_idx)
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,

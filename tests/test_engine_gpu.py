@@ -271,3 +271,25 @@ def test_hub_server_gpu_end_to_end(tmp_path):
         finally:
             await srv.stop()
     asyncio.run(go())
+
+
+def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
+    """Prefill with the down projection as split-K f32 slabs summed by the next
+    norm (models/llama.py ``_splitk_slabs`` + ``ops.slab_rmsnorm``) vs the plain
+    hipBLASLt GEMM + rmsnorm: final hidden rows of a 300-token prompt agree."""
+    from loqa_hub_amd.models import llama as llama_mod
+    cfg = llama_config("tinyllama")
+    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(0)
+    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
+    r = GenRequest(toks, multi_command_schema(1))
+    eng.submit(r)
+    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
+    dev = eng._to_device(host)
+    meta = eng._build_meta(dev, max_q, max_ctx, False)
+    outs = {}
+    for S in (8, 0):
+        monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", S)
+        outs[S] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
+    rel = float((outs[8] - outs[0]).norm() / outs[0].norm())
+    assert torch.isfinite(outs[8]).all() and rel < 2e-2, rel
