@@ -1,0 +1,150 @@
+// Prefill-shaped GEMM (M ~ 100-512 token rows): Y = X W^T for the Llama
+// projections at one parser prompt (PERF.md "prefill GEMMs").
+//
+// At M ~ 318 hipBLASLt's tiles cover too few CUs for the N = 4096 projections
+// (o, down) and its large-N tiles re-read weights; both run at 30-50% of the
+// HBM / MFMA roofline. Here the weights are streamed exactly once, in the
+// MFMA-fragment order of ops.shuffle_weight (the decode copies: 1 KiB contiguous
+// per wave load), and the activation rows stay on chip:
+//   workgroup = 4 waves x FT feature tiles of 16 (128 features) x RB row tiles
+//               of 16 (160 rows) x one K range (split-K S);
+//   per K chunk of 128: the 160 x 128 activation block is staged once in LDS
+//   (register double-buffered: the next chunk's rows and weight fragments are
+//   in flight while this chunk's MFMAs run), every wave multiplies its
+//   weight fragments against all RB row tiles (v_mfma_f32_16x16x32_bf16, A =
+//   weights, B = rows, each LDS fragment feeds FT MFMAs).
+// Output: bf16 Y [M, N], or f32 split-K slabs [S, M, N] that the consumer
+// (slab_rmsnorm / slab_rope_append) sums in a fixed order.
+#include "common.h"
+
+#define PG_FT 2            // feature tiles per wave
+#define PG_RB 10           // row tiles per workgroup
+#define PG_KC 128          // K per LDS chunk (4 k-steps)
+#define PG_PAD 8
+
+typedef unsigned u32x4p __attribute__((ext_vector_type(4)));
+typedef float f4p __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4p pg_ldw(const bf16_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4p*>(p));
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_prefill_kernel(
+    const bf16_t* __restrict__ X, int M, int K, const bf16_t* __restrict__ Wp, int N, int S,
+    bf16_t* __restrict__ Y, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) bf16_t xs[PG_RB * 16][PG_KC + PG_PAD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NT = 4 * PG_FT * 16;                 // features per workgroup
+  const int nslices = N / NT;
+  // XCD-aware order: the row blocks of one feature slice run back to back on
+  // the same XCD, so the second reads the weights from L2
+  const int mblocks = (M + PG_RB * 16 - 1) / (PG_RB * 16);
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int mb = wg % mblocks;
+  const int rest = wg / mblocks;
+  const int slice = rest % nslices;
+  const int s = rest / nslices;
+  if (s >= S) return;
+  const int KS = K >> 5;
+  const int Ks = K / S;                          // multiple of PG_KC (host-checked)
+  const int k0 = s * Ks;
+  const int m0 = mb * PG_RB * 16;
+  const int nchunks = Ks / PG_KC;
+  const int tile0 = slice * (NT / 16) + wave * PG_FT;
+
+  // activation staging: 160 rows x 128 k = 2560 16-byte pieces, 10 per thread
+  u32x4p xr[10];
+  auto load_x = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c >> 4, col = (c & 15) * 8;
+      const int m = m0 + row;
+      xr[i] = m < M ? *reinterpret_cast<const u32x4p*>(X + (size_t)m * K + kc + col) : u32x4p{0, 0, 0, 0};
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int row = c >> 4, col = (c & 15) * 8;
+      *reinterpret_cast<u32x4p*>(&xs[row][col]) = xr[i];
+    }
+  };
+  // weight fragments of one chunk: FT tiles x 4 k-steps
+  u32x4p wf[PG_FT][4], wn[PG_FT][4];
+  auto load_w = [&](int kc, u32x4p (&w)[PG_FT][4]) {
+    const int ks0 = kc >> 5;
+#pragma unroll
+    for (int f = 0; f < PG_FT; ++f)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        w[f][u] = pg_ldw(Wp + ((size_t)(tile0 + f) * KS + ks0 + u) * 512 + lane * 8);
+  };
+  f4p acc[PG_RB][PG_FT];
+#pragma unroll
+  for (int r = 0; r < PG_RB; ++r)
+#pragma unroll
+    for (int f = 0; f < PG_FT; ++f) acc[r][f] = f4p{0.f, 0.f, 0.f, 0.f};
+
+  load_w(k0, wf);
+  load_x(k0);
+  store_x();
+  __syncthreads();
+  const int t = lane & 15, kq = 8 * (lane >> 4);
+  for (int c = 0; c < nchunks; ++c) {
+    const int kc = k0 + c * PG_KC;
+    const bool more = c + 1 < nchunks;
+    const int kn = more ? kc + PG_KC : kc;      // clamped: unconditional loads
+    load_x(kn);
+    load_w(kn, wn);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int r = 0; r < PG_RB; ++r) {
+        const u32x4p b = *reinterpret_cast<const u32x4p*>(&xs[r * 16 + t][u * 32 + kq]);
+#pragma unroll
+        for (int f = 0; f < PG_FT; ++f)
+          acc[r][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[f][u]),
+                                                              __builtin_bit_cast(bf16x8, b), acc[r][f], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (more) store_x();
+#pragma unroll
+    for (int f = 0; f < PG_FT; ++f)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wf[f][u] = wn[f][u];
+    __syncthreads();
+  }
+  // epilogue: lane holds features (lane>>4)*4 + j of tile, token lane & 15
+#pragma unroll
+  for (int r = 0; r < PG_RB; ++r) {
+    const int m = m0 + r * 16 + t;
+    if (m >= M) continue;
+#pragma unroll
+    for (int f = 0; f < PG_FT; ++f) {
+      const int n = (tile0 + f) * 16 + (lane >> 4) * 4;
+      if (part) {
+        *reinterpret_cast<f4p*>(part + ((size_t)s * M + m) * N + n) = acc[r][f];
+      } else {
+        *reinterpret_cast<uint2*>(Y + (size_t)m * N + n) =
+            make_uint2(pack_bf16x2(acc[r][f][0], acc[r][f][1]), pack_bf16x2(acc[r][f][2], acc[r][f][3]));
+      }
+    }
+  }
+}
+
+// X [M, K] bf16 row-major; Wp = shuffle_weight(W [N, K]); S split-K ranges.
+// part != nullptr: f32 slabs [S, M, N]; else Y [M, N] bf16 (S must be 1).
+extern "C" int loqa_gemm_prefill(const void* X, int M, int K, const void* Wp, int N, int S, void* Y,
+                                 float* part, hipStream_t st) {
+  const int NT = 4 * PG_FT * 16;
+  if (M <= 0 || N % NT || S < 1 || K % (S * PG_KC) || (!part && S != 1) || (!part && !Y))
+    return (int)hipErrorInvalidValue;
+  const int mblocks = (M + PG_RB * 16 - 1) / (PG_RB * 16);
+  const int grid = mblocks * (N / NT) * S;
+  hipLaunchKernelGGL(gemm_prefill_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)X, M, K,
+                     (const bf16_t*)Wp, N, S, (bf16_t*)Y, part);
+  return (int)hipGetLastError();
+}

@@ -1309,3 +1309,30 @@ def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: tor
     p.dbg = ptr(m.dbg) if getattr(m, "dbg", None) is not None else None
     check(kernels().loqa_whisper_mega(ctypes.byref(p), m.grid, stream_ptr(x)), "whisper_mega")
     return x
+
+
+# ------------------------------------------------------------- prefill GEMM
+PREFILL_GEMM_NT = 128     # features per workgroup (kernel constant)
+
+
+def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, slabs: bool = False) -> torch.Tensor:
+    """x [M, K] bf16 @ W^T for ~100-512 rows with W given pre-shuffled
+    (``shuffle_weight``), weights streamed once (``csrc/kernels/gemm_prefill.hip``).
+    ``slabs``: f32 split-K partials [S, M, N] (summed by a slab consumer),
+    else bf16 [M, N] (S = 1)."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    assert wp.shape[1] * 32 == K
+    if not _gpu(x):
+        part = ref.skinny_gemm(x, wp, splits)
+        return part if slabs else part.sum(0).to(torch.bfloat16)
+    _bf16_contig(x, "x")
+    assert N % PREFILL_GEMM_NT == 0 and K % (splits * 128) == 0 and (slabs or splits == 1)
+    if slabs:
+        out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+        rc = kernels().loqa_gemm_prefill(ptr(x), M, K, ptr(wp), N, splits, None, ptr(out), stream_ptr(x))
+    else:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        rc = kernels().loqa_gemm_prefill(ptr(x), M, K, ptr(wp), N, 1, ptr(out), None, stream_ptr(x))
+    check(rc, "gemm_prefill")
+    return out

@@ -110,6 +110,7 @@ _KERNEL_SIGS = {
     "loqa_step_fetch": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p, c_void_p],
     "loqa_whisper_mega": [c_void_p, c_int, c_void_p],
+    "loqa_gemm_prefill": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "loqa_step_publish": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                           c_void_p],
 }
