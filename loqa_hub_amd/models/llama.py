@@ -244,6 +244,7 @@ class LlamaWeights:
 
 
 PREFILL_DOWN_SPLITS = int(os.environ.get("LOQA_PREFILL_DOWN_SPLITS", "8"))
+PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
 
 
 def _splitk_slabs(a: torch.Tensor, w: torch.Tensor, S: int) -> torch.Tensor:
@@ -290,6 +291,9 @@ class LlamaModel:
         if not (S_down > 0 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 128
                 and w.f % S_down == 0):
             S_down = 0
+        S_o = PREFILL_O_SPLITS if (S_down and PREFILL_O_SPLITS > 0 and hasattr(w, "decode_layers")
+                                   and (H * D) % (PREFILL_O_SPLITS * 128) == 0
+                                   and cfg.d_model % ops.PREFILL_GEMM_NT == 0) else 0
         part = None
         for li, L in enumerate(w.layers):
             if li > 0:
@@ -306,8 +310,14 @@ class LlamaModel:
                                  grouped=meta.decode, split_keys=split_keys,
                                  num_splits=num_splits if meta.decode else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
-            o = tp.all_reduce_(ops.linear(attn, L["wo"]))
-            h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
+            if S_o:
+                # o projection on the weight-streaming prefill GEMM (decode copy
+                # of wo), split-K f32 slabs summed by the norm
+                part_o = ops.prefill_gemm(attn, w.decode_layers[li]["wo"], S_o, slabs=True)
+                h = ops.slab_rmsnorm(part_o, residual, L["mlp_norm"], cfg.norm_eps)
+            else:
+                o = tp.all_reduce_(ops.linear(attn, L["wo"]))
+                h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             gu = ops.linear(h, L["w_gate_up"])
             if S_down:
                 part = _splitk_slabs(ops.silu_mul(gu), L["w_down"], S_down)

@@ -274,9 +274,10 @@ def test_hub_server_gpu_end_to_end(tmp_path):
 
 
 def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
-    """Prefill with the down projection as split-K f32 slabs summed by the next
-    norm (models/llama.py ``_splitk_slabs`` + ``ops.slab_rmsnorm``) vs the plain
-    hipBLASLt GEMM + rmsnorm: final hidden rows of a 300-token prompt agree."""
+    """Prefill with the down projection as split-K f32 slabs and the o
+    projection on the weight-streaming prefill GEMM, both summed by the next
+    norm (``ops.slab_rmsnorm``), vs plain hipBLASLt GEMMs + rmsnorm: final
+    hidden rows of a 300-token prompt agree."""
     from loqa_hub_amd.models import llama as llama_mod
     cfg = llama_config("tinyllama")
     eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
@@ -288,8 +289,12 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     dev = eng._to_device(host)
     meta = eng._build_meta(dev, max_q, max_ctx, False)
     outs = {}
-    for S in (8, 0):
+    for S in (8, 0):   # 8: split-K down + o on the prefill GEMM (4 slabs); 0: hipBLASLt
         monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", S)
+        monkeypatch.setattr(llama_mod, "PREFILL_O_SPLITS", 4 if S else 0)
         outs[S] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
     rel = float((outs[8] - outs[0]).norm() / outs[0].norm())
-    assert torch.isfinite(outs[8]).all() and rel < 2e-2, rel
+    # the slab paths skip two bf16 roundings per layer (f32 sums feed the
+    # norm); over 22 random-weight layers that drifts ~2% - a layout or
+    # indexing error would be O(1)
+    assert torch.isfinite(outs[8]).all() and rel < 4e-2, rel
