@@ -1278,6 +1278,9 @@ class WhisperMega:
         self.grid = grid or int(os.environ.get("LOQA_STT_MEGA_WGS", "256"))
         self.eps = 1e-5
         self.scale_log2 = (1.0 / math.sqrt(D)) * 1.4426950408889634
+        # optional int64 [items * 5] buffer: per-item s_memrealtime stamps
+        # (scripts/exp/whisper_mega_bench.py)
+        self.dbg: torch.Tensor | None = None
 
     def error(self) -> int:
         """Non-zero when a step's bounded dependency wait expired (host read)."""
@@ -1306,7 +1309,7 @@ def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: tor
     p.enc_starts, p.enc_lens = ptr(enc_starts), ptr(enc_lens)
     p.B, p.d, p.H, p.ffn, p.nsplit = B, m.d, m.H, m.F, m.nsplit
     p.kv_bytes, p.eps, p.scale_log2 = m.kv_bytes, m.eps, m.scale_log2
-    p.dbg = ptr(m.dbg) if getattr(m, "dbg", None) is not None else None
+    p.dbg = ptr(m.dbg)
     check(kernels().loqa_whisper_mega(ctypes.byref(p), m.grid, stream_ptr(x)), "whisper_mega")
     return x
 
