@@ -245,6 +245,18 @@ def test_bench_cpu_smoke_dp2_gloo():
     assert out["config"]["global_batch"] == 4 and out["queue_success_rate"] == 1.0
 
 
+def test_bench_cpu_smoke_dp4_gloo():
+    """Four ranks (the driver runs 1/2/4/8): one NATS broker process for the
+    node, every rank publishes to it, records are all-gathered to rank 0."""
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+                "4", "--master-addr", "127.0.0.1", "--master-port", "29563", "bench.py",
+                "--cpu-smoke", "--gpus", "4", "--steps", "1", "--warmup", "0",
+                "--batch-per-gpu", "2"])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["config"]["global_batch"] == 8 and out["queue_success_rate"] == 1.0
+    assert out["command_count_match_rate"] == 1.0
+
+
 def test_whisper_fast_decode_matches_eager_cpu():
     """The skinny-GEMM/slab decode path equals the eager reference decoder
     (first step with the 4 SOT tokens and a follow-up 1-token step)."""
