@@ -346,12 +346,22 @@ class STTEngine:
                 t1 = time.perf_counter()
                 g["graph"].replay()
                 out = g["out"][:B].cpu().numpy()
+                if self.mega is not None and T_pad == ops.WhisperMega.ROWS:
+                    self._check_mega()
                 self.stats["host_pre_s"] += t1 - t0
                 self.stats["gpu_wait_s"] += time.perf_counter() - t1
                 return out
             max_q, host = self._host_meta(live, B_pad, T_pad)
             return self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
         return self._eager_step(live)
+
+    def _check_mega(self) -> None:
+        """Every 32nd one-launch step, read the kernel's error word: an expired
+        (bounded) dependency wait means that step's outputs are garbage, so
+        the scheduler fails the batch loudly instead of serving them."""
+        self._mega_steps = getattr(self, "_mega_steps", 0) + 1
+        if self._mega_steps % 32 == 0 and self.mega.error():
+            raise RuntimeError("whisper_mega: a dependency wait expired (kernel error flag set)")
 
     def _eager_step(self, live: list[STTRequest]) -> np.ndarray:
         """Reference decode path (hipBLASLt GEMMs, eager launches)."""
