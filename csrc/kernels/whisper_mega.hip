@@ -64,7 +64,7 @@ struct MegaParams {
   bf16_t* xqb;           // [MP, d] cross-attention queries
   bf16_t* mb;            // [MP, ffn] GELU activations
   float* part;           // [B, H, nsplit, MP, 66] cross-attention split partials
-  int* sync;             // [L * NPH] done counters | [B * H] tickets | err  (zeroed per step)
+  int* sync;             // err (sticky) | [L * NPH] done counters | [B * H] tickets (zeroed per step)
   const int* slots;      // [MP] cache slot per token row (-1: padding)
   const int* cu_q;       // [B + 1]
   const int* ctx_lens;   // [B]
@@ -380,7 +380,7 @@ __device__ void attn_item(const MegaParams& p, MegaSmem& sm, const MegaLayer& Lw
   }
   if (nsplit == 1) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int* tk = p.sync + p.L * NPH + b * p.H + h;
+  int* tk = p.sync + 1 + p.L * NPH + b * p.H + h;
   int t = 0;
   if (lane == 0) {
     t = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -420,8 +420,8 @@ __global__ __launch_bounds__(256, 1) void whisper_mega_kernel(MegaParams p) {
 #pragma unroll
   for (int i = 0; i < NPH; ++i) C += n[i];
   const int total = C * p.L;
-  int* done = p.sync;
-  int* err = p.sync + p.L * NPH + p.B * p.H;
+  int* err = p.sync;
+  int* done = p.sync + 1;
   const int d = p.d;
   for (int it = blockIdx.x; it < total; it += gridDim.x) {
     const int l = it / C;
@@ -497,8 +497,9 @@ extern "C" int loqa_whisper_mega(const MegaParams* hp, int grid, hipStream_t s) 
   if (p.L <= 0 || p.B <= 0 || p.H * HD != p.d || p.d % 128 || p.d > 1280 || p.ffn % 128 ||
       p.ffn > 4 * 1280 || p.nsplit < 1 || p.blk <= 0 || grid <= 0 || !p.sync || !p.layers)
     return (int)hipErrorInvalidValue;
-  const size_t sync_bytes = (size_t)(p.L * NPH + p.B * p.H + 1) * sizeof(int);
-  hipError_t e = hipMemsetAsync(p.sync, 0, sync_bytes, s);
+  // counters and tickets restart every step; the error word stays set
+  const size_t sync_bytes = (size_t)(p.L * NPH + p.B * p.H) * sizeof(int);
+  hipError_t e = hipMemsetAsync(p.sync + 1, 0, sync_bytes, s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(whisper_mega_kernel, dim3(grid), dim3(256), 0, s, p);
   return (int)hipGetLastError();

@@ -356,9 +356,9 @@ class STTEngine:
         return self._eager_step(live)
 
     def _check_mega(self) -> None:
-        """Every 32nd one-launch step, read the kernel's error word: an expired
-        (bounded) dependency wait means that step's outputs are garbage, so
-        the scheduler fails the batch loudly instead of serving them."""
+        """Every 32nd one-launch step, read the kernel's sticky error word: an
+        expired (bounded) dependency wait means outputs since then are garbage,
+        so the scheduler fails the batch loudly instead of serving them."""
         self._mega_steps = getattr(self, "_mega_steps", 0) + 1
         if self._mega_steps % 32 == 0 and self.mega.error():
             raise RuntimeError("whisper_mega: a dependency wait expired (kernel error flag set)")

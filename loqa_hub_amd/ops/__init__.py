@@ -1283,8 +1283,9 @@ class WhisperMega:
         self.dbg: torch.Tensor | None = None
 
     def error(self) -> int:
-        """Non-zero when a step's bounded dependency wait expired (host read)."""
-        return int(self.sync[-1].item())
+        """Non-zero once any step's bounded dependency wait expired (sticky:
+        the per-step reset leaves word 0 alone; host read)."""
+        return int(self.sync[0].item())
 
 
 def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: torch.Tensor,
