@@ -21,15 +21,19 @@
 #include "common.h"
 
 #define CAR_MAX_WORLD 8
-#define CAR_BLOCKS 32
-#define CAR_SPIN_LIMIT (1 << 26)
+#define CAR_BLOCKS 32          // blocks of the one-/two-shot kernels
+#define CAR_MAX_BLOCKS 64      // flag rows (the residual kernel may use up to 64 blocks)
+// bounded waits (~several seconds); once any wait of this rank timed out the
+// sticky error word makes every later wait give up at once, so a diverged TP
+// group fails fast instead of spinning out every remaining collective
+#define CAR_SPIN_LIMIT (1 << 22)
 
 #define CAR_TWOSHOT_MIN_BYTES (512 << 10)
 
 struct CarSignals {
-  unsigned start[CAR_BLOCKS][CAR_MAX_WORLD];
-  unsigned end[CAR_BLOCKS][CAR_MAX_WORLD];
-  unsigned mid[CAR_BLOCKS][CAR_MAX_WORLD];     // two-shot: reduce-scatter -> all-gather
+  unsigned start[CAR_MAX_BLOCKS][CAR_MAX_WORLD];
+  unsigned end[CAR_MAX_BLOCKS][CAR_MAX_WORLD];
+  unsigned mid[CAR_MAX_BLOCKS][CAR_MAX_WORLD];     // two-shot: reduce-scatter -> all-gather
   unsigned epoch;
   unsigned done;
   unsigned error;
@@ -63,8 +67,10 @@ __device__ bool car_barrier(CarPeers peers, int rank, int world, int which, int 
     CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
     const unsigned* f = which == 0 ? &me->start[blk][threadIdx.x]
                         : which == 1 ? &me->end[blk][threadIdx.x] : &me->mid[blk][threadIdx.x];
-    unsigned spins = 0;
-    while (ld_sys(f) != e) {
+    unsigned spins = ld_sys(&me->error) ? CAR_SPIN_LIMIT : 0u;
+    // epochs only grow, and a peer is at most one call ahead (it cannot pass
+    // the next barrier before this rank arrives there): wait for >= e
+    while ((int)(ld_sys(f) - e) < 0) {
       if (++spins > CAR_SPIN_LIMIT) {
         st_sys(&me->error, 1u);
         ok = false;
@@ -182,28 +188,249 @@ __global__ __launch_bounds__(256) void car_twoshot_kernel(CarPeers peers, const 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tensor-parallel decode step collectives (models/llama.py forward_decode_fused
+// at tp > 1). The row-parallel o / down GEMMs write their f32 partial sums
+// straight into this rank's IPC input buffer (ops.skinny_fused "act" epilogue
+// with f32 output, out = CustomAllReduce.inbuf); one kernel then sums every
+// rank's partial into the replicated residual and emits the row statistics
+// the next fused GEMM's norm prologue reads - the all-reduce IS the residual
+// epilogue.
+//
+// No end barrier: the o and down projections alternate between two sets of
+// input / result / statistics buffers (and the argmax exchange has its own),
+// so a buffer is rewritten only after some LATER call's start barrier, which
+// no peer passes before it finished reading the earlier contents (every call
+// is a kernel boundary on each rank's stream).
+//
+// Peer data is read with system-coherent buffer loads (sc0 | sc1: straight
+// from the owner's memory, never a stale L2 line); the buffers live in the
+// uncached region, so the GEMM's stores are in memory when its kernel ends.
+#define CAR_KEY_ROWS 256      // rows of the argmax exchange
+#define CAR_SYS 17            // buffer-op cache policy: sc0 | sc1 (system coherent)
+
+typedef unsigned car_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t car_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// start barrier of block `blk` only (the data was written by earlier kernels)
+__device__ __forceinline__ bool car_arrive_wait(const CarPeers& peers, int rank, int world, int blk,
+                                                unsigned e) {
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < world; ++q)
+      st_sys(&reinterpret_cast<CarSignals*>(peers.base[q])->start[blk][rank], e);
+  }
+  bool ok = true;
+  if (threadIdx.x < world) {
+    CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
+    const unsigned* f = &me->start[blk][threadIdx.x];
+    unsigned spins = ld_sys(&me->error) ? CAR_SPIN_LIMIT : 0u;
+    while ((int)(ld_sys(f) - e) < 0) {
+      if (++spins > CAR_SPIN_LIMIT) {
+        st_sys(&me->error, 1u);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return __syncthreads_and(ok);
+}
+
+__device__ __forceinline__ void car_epoch_done(CarSignals* me, unsigned e, int nblk) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned d = __hip_atomic_fetch_add(&me->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (unsigned)nblk - 1) {
+      st_sys(&me->done, 0u);
+      st_sys(&me->epoch, e);
+    }
+  }
+}
+
+// Residual all-reduce of the TP decode step, reduce-scatter + all-gather:
+//   phase 1: rank r owns the column slice [r * d/W, (r+1) * d/W). Its block b
+//            sums, for sub-slice b of that, residual + every rank's f32 partial
+//            (system-coherent loads, fixed rank order), rounds to bf16 ONCE,
+//            writes the result into its local residual and its IPC result
+//            buffer, and the sub-slice's row sums of squares into its IPC stats;
+//   phase 2: after a second barrier, it copies sub-slice b of every other
+//            rank's owned slice (bf16 results) and stats tiles.
+// Bytes read per rank: Mpad * d * 4 (f32 slices) + (W-1)/W * Mpad * d * 2,
+// vs W * Mpad * d * 2 for a one-shot bf16 sum - and f32 partials keep the
+// numerics of the single-GPU residual epilogue (one rounding).
+// rowsq_out gets W * nblk tiles: tile q * nblk + b = rank q's sub-slice b.
+__global__ __launch_bounds__(256) void car_resid_kernel(CarPeers peers, long long in_off, long long res_off,
+                                                        long long st_off, bf16_t* __restrict__ residual,
+                                                        float* __restrict__ rowsq_out, int Mpad, int d,
+                                                        int rank, int world) {
+  CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
+  const unsigned e = ld_sys(&me->epoch) + 1;
+  const int blk = blockIdx.x, nblk = gridDim.x;
+  const int owned = d / world, cw = owned / nblk;     // columns per rank / per block
+  const int c0 = rank * owned + blk * cw;
+  const unsigned in_bytes = (unsigned)((size_t)Mpad * d * 4), res_bytes = (unsigned)((size_t)Mpad * d * 2);
+  const unsigned st_bytes = (unsigned)((size_t)nblk * Mpad * 4);
+  bool ok = car_arrive_wait(peers, rank, world, blk, e);
+  if (ok) {
+    const int vpr = cw >> 2;                           // f32x4 vectors per row
+    const int rpp = 256 / vpr, r0 = threadIdx.x / vpr, cv = threadIdx.x % vpr;
+    bf16_t* rmine = reinterpret_cast<bf16_t*>(peers.base[rank] + res_off);
+    float* smine = reinterpret_cast<float*>(peers.base[rank] + st_off);
+    for (int m0 = 0; m0 < Mpad; m0 += rpp) {
+      const int m = m0 + r0;
+      const bool act = r0 < rpp && m < Mpad;
+      float sq = 0.f;
+      if (act) {
+        const size_t el = (size_t)m * d + c0 + cv * 4;
+        const uint2 rv = *reinterpret_cast<const uint2*>(residual + el);
+        float acc[4] = {bf2f(rv.x & 0xffff), bf2f(rv.x >> 16), bf2f(rv.y & 0xffff), bf2f(rv.y >> 16)};
+        car_u32x4 v[CAR_MAX_WORLD];
+#pragma unroll
+        for (int q = 0; q < CAR_MAX_WORLD; ++q)
+          if (q < world)
+            v[q] = __builtin_amdgcn_raw_buffer_load_b128(car_rsrc(peers.base[q] + in_off, in_bytes),
+                                                         (unsigned)(el * 4), 0, CAR_SYS);
+#pragma unroll
+        for (int q = 0; q < CAR_MAX_WORLD; ++q) {
+          if (q >= world) break;
+          acc[0] += __uint_as_float(v[q].x); acc[1] += __uint_as_float(v[q].y);
+          acc[2] += __uint_as_float(v[q].z); acc[3] += __uint_as_float(v[q].w);
+        }
+        uint2 o;
+        o.x = pack_bf16x2(acc[0], acc[1]);
+        o.y = pack_bf16x2(acc[2], acc[3]);
+        *reinterpret_cast<uint2*>(residual + el) = o;
+        *reinterpret_cast<uint2*>(rmine + el) = o;
+        const float h0 = bf2f(o.x & 0xffff), h1 = bf2f(o.x >> 16), h2 = bf2f(o.y & 0xffff), h3 = bf2f(o.y >> 16);
+        sq = h0 * h0 + h1 * h1 + h2 * h2 + h3 * h3;
+      }
+      for (int o = 1; o < vpr; o <<= 1) sq += __shfl_xor(sq, o, 64);
+      if (cv == 0 && act) {
+        smine[(size_t)blk * Mpad + m] = sq;
+        rowsq_out[((size_t)rank * nblk + blk) * Mpad + m] = sq;
+      }
+    }
+    // phase 2: publish (release at system scope, as car_barrier), then gather
+    // every other rank's rounded sub-slice b and its statistics
+    ok = car_barrier(peers, rank, world, 2, blk, e);
+    if (ok) {
+      const int vb = cw >> 3;                          // bf16x8 vectors per row of a sub-slice
+      for (int q = 0; q < world; ++q) {
+        if (q == rank) continue;
+        const int cq = q * owned + blk * cw;
+        const auto rr = car_rsrc(peers.base[q] + res_off, res_bytes);
+        for (int t = threadIdx.x; t < Mpad * vb; t += 256) {
+          const int m = t / vb, c = t - m * vb;
+          const size_t el = (size_t)m * d + cq + c * 8;
+          const car_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rr, (unsigned)(el * 2), 0, CAR_SYS);
+          *reinterpret_cast<uint4*>(residual + el) = uint4{v.x, v.y, v.z, v.w};
+        }
+        const auto rs = car_rsrc(peers.base[q] + st_off, st_bytes);
+        for (int m = threadIdx.x; m < Mpad; m += 256)
+          rowsq_out[((size_t)q * nblk + blk) * Mpad + m] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rs, (unsigned)(((size_t)blk * Mpad + m) * 4), 0, CAR_SYS));
+      }
+    }
+  }
+  car_epoch_done(me, e, nblk);
+}
+
+// Vocab-parallel masked argmax combine: every rank publishes one
+// 64-bit record per row - [63:49] epoch, [48:17] order-preserving bits of the
+// row's best local logit, [16:0] 2^17-1 - global token id (larger = smaller id,
+// so ties go to the lowest id) - and every rank takes the max over ranks. The
+// record carries its own epoch, so no separate flag or fence is needed.
+__device__ __forceinline__ unsigned long long car_ld64_sys(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void car_argmax_kernel(CarPeers peers, long long key_off,
+                                                         const float* __restrict__ logits, long long ld,
+                                                         const int* __restrict__ idx, int B, int lo,
+                                                         int* __restrict__ out, int rank, int world) {
+  CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
+  const unsigned e = ld_sys(&me->epoch) + 1;
+  const unsigned long long tag = (unsigned long long)(e & 0x7fffu) << 49;
+  // every row is rewritten each call (rows >= B as "nothing"), so a stale
+  // record is always from an earlier call with a different 15-bit epoch
+  for (int b = threadIdx.x; b < CAR_KEY_ROWS; b += blockDim.x) {
+    const int i = b < B ? idx[b] : -1;
+    unsigned long long key = 0;   // nothing allowed on this shard
+    if (i >= 0) {
+      const unsigned u = __float_as_uint(logits[(size_t)b * ld + i]);
+      const unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      key = ((unsigned long long)ord << 17) | (unsigned long long)(0x1ffffu - (unsigned)(i + lo));
+    }
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(peers.base[rank] + key_off) + b;
+    __hip_atomic_store(dst, tag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  bool ok = true;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    unsigned long long best = 0;
+    for (int q = 0; q < world; ++q) {
+      const unsigned long long* src =
+          reinterpret_cast<const unsigned long long*>(peers.base[q] + key_off) + b;
+      unsigned long long v;
+      unsigned spins = ld_sys(&me->error) ? CAR_SPIN_LIMIT : 0u;
+      while (((v = car_ld64_sys(src)) >> 49) != (e & 0x7fffu)) {
+        if (++spins > CAR_SPIN_LIMIT) {
+          st_sys(&me->error, 1u);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) break;
+      const unsigned long long k = v & ((1ull << 49) - 1);
+      best = k > best ? k : best;
+    }
+    out[b] = (!ok || best == 0) ? -1 : (int)(0x1ffffu - (unsigned)(best & 0x1ffffu));
+  }
+  car_epoch_done(me, e, 1);
+}
+
 struct CarHandle {
   int rank, world;
-  size_t bytes, slot_bytes;
+  size_t bytes, slot_bytes, in_bytes;
   char* local;
   CarPeers peers;
   bool opened[CAR_MAX_WORLD];
 };
 
-extern "C" void* loqa_car_create(int rank, int world, long long slot_bytes) {
-  if (world < 1 || world > CAR_MAX_WORLD || rank < 0 || rank >= world || slot_bytes % 16)
+// region: [signals][slot 0][slot 1][f32 input 0][f32 input 1][bf16 result 0]
+// [bf16 result 1][stats 0][stats 1][argmax keys]; in_bytes = one f32 input
+#define CAR_ST_BYTES (CAR_MAX_BLOCKS * 128 * 4)
+static size_t car_in_off(const CarHandle* h, int which) {
+  return sizeof(CarSignals) + 2 * h->slot_bytes + (size_t)which * h->in_bytes;
+}
+static size_t car_res_off(const CarHandle* h, int which) {
+  return car_in_off(h, 2) + (size_t)which * (h->in_bytes / 2);
+}
+static size_t car_st_off(const CarHandle* h, int which) {
+  return car_res_off(h, 2) + (size_t)which * CAR_ST_BYTES;
+}
+static size_t car_key_off(const CarHandle* h) { return car_st_off(h, 2); }
+
+extern "C" void* loqa_car_create(int rank, int world, long long slot_bytes, long long in_bytes) {
+  if (world < 1 || world > CAR_MAX_WORLD || rank < 0 || rank >= world || slot_bytes % 16 ||
+      in_bytes % 512 || in_bytes < 0)
     return nullptr;
   CarHandle* h = new CarHandle();
   h->rank = rank;
   h->world = world;
   h->slot_bytes = (size_t)slot_bytes;
-  h->bytes = sizeof(CarSignals) + 2 * (size_t)slot_bytes;
+  h->in_bytes = (size_t)in_bytes;
+  h->bytes = car_key_off(h) + CAR_KEY_ROWS * 8;
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&h->local), h->bytes, hipDeviceMallocUncached) !=
       hipSuccess) {
     delete h;
     return nullptr;
   }
   hipMemset(h->local, 0, sizeof(CarSignals));
+  hipMemset(h->local + car_key_off(h), 0, CAR_KEY_ROWS * 8);
   hipDeviceSynchronize();
   for (int q = 0; q < CAR_MAX_WORLD; ++q) {
     h->peers.base[q] = nullptr;
@@ -250,6 +477,47 @@ extern "C" int loqa_car_allreduce(void* hp, const void* in, void* out, long long
                : (is_f32 ? car_oneshot_kernel<true> : car_oneshot_kernel<false>);
   hipLaunchKernelGGL(k, dim3(CAR_BLOCKS), dim3(256), 0, s, h->peers, in, out, nbytes, h->rank,
                      h->world, (long long)h->slot_bytes);
+  return (int)hipGetLastError();
+}
+
+// this rank's TP f32 input buffer `which` (0 / 1): the row-parallel GEMM's output
+extern "C" void* loqa_car_inbuf(void* hp, int which) {
+  CarHandle* h = static_cast<CarHandle*>(hp);
+  if (which < 0 || which > 1 || h->in_bytes == 0) return nullptr;
+  return h->local + car_in_off(h, which);
+}
+
+// residual [Mpad, d] += sum over ranks of f32 input buffer `which` ([Mpad, d]);
+// row sums of squares -> rowsq_out [world * nblk, Mpad]. d / world / nblk
+// columns per block: a multiple of 8, at most 256 (<= 64 f32x4 lanes per row).
+extern "C" int loqa_car_resid(void* hp, int which, void* residual, float* rowsq_out, int Mpad, int d,
+                              int nblk, hipStream_t s) {
+  CarHandle* h = static_cast<CarHandle*>(hp);
+  if (which < 0 || which > 1 || nblk < 1 || nblk > CAR_MAX_BLOCKS || d % (h->world * nblk) ||
+      Mpad < 1 || Mpad > 128)
+    return (int)hipErrorInvalidValue;
+  const int cw = d / h->world / nblk, vpr = cw / 4;
+  if (cw % 8 || vpr > 64 || (vpr & (vpr - 1)) || (size_t)Mpad * d * 4 > h->in_bytes)
+    return (int)hipErrorInvalidValue;
+  for (int q = 0; q < h->world; ++q)
+    if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(car_resid_kernel, dim3(nblk), dim3(256), 0, s, h->peers,
+                     (long long)car_in_off(h, which), (long long)car_res_off(h, which),
+                     (long long)car_st_off(h, which), (bf16_t*)residual, rowsq_out, Mpad, d, h->rank,
+                     h->world);
+  return (int)hipGetLastError();
+}
+
+// out[b] = global argmax over ranks of (logits[b, idx[b]], idx[b] + lo); -1 if
+// no rank allowed any token. idx: this rank's masked argmax (-1 = none).
+extern "C" int loqa_car_argmax(void* hp, const float* logits, long long ld, const int* idx, int B,
+                               int lo, int* out, hipStream_t s) {
+  CarHandle* h = static_cast<CarHandle*>(hp);
+  if (B < 1 || B > CAR_KEY_ROWS || lo < 0) return (int)hipErrorInvalidValue;
+  for (int q = 0; q < h->world; ++q)
+    if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(car_argmax_kernel, dim3(1), dim3(256), 0, s, h->peers, (long long)car_key_off(h),
+                     logits, ld, idx, B, lo, out, h->rank, h->world);
   return (int)hipGetLastError();
 }
 

@@ -344,7 +344,10 @@ __global__ __launch_bounds__(256) void step_publish_kernel(const int* __restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence_system();
-    __hip_atomic_store(ctr, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // wrap at 2 * nres (a common multiple of the 2 staging slots and the nres
+    // result slots; the host's step number wraps the same way), so the counter
+    // never overflows on a long-running hub
+    __hip_atomic_store(ctr, (c + 1) % (2 * nres), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -368,5 +371,45 @@ extern "C" int loqa_step_publish(const int* out, int n, void* res, int stride, i
   if (n < 0 || n > stride || nres < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(step_publish_kernel, dim3(1), dim3(256), 0, s, out, n, (int*)res, stride, nres, ctr,
                      row_slot, last_tok);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based random init (seeded random-init weights): element
+// (r, c) of a [rows, cols] block at (row0, col0) of a conceptual [*, ld] tensor
+// gets scale * (u0 + u1 + u2 + u3 - 2) with u_k = fmix32(4 * idx + k + s) / 2^32
+// (Irwin-Hall(4): mean 0, variance 1/3 - the caller folds sqrt(3) into scale),
+// idx = (row0 + r) * ld + col0 + c. Any shard of a tensor is generated on its
+// own, with exactly the values of the unsharded tensor (tensor-parallel ranks
+// build their slices without materialising the full model). Integer hashing and
+// exact f32 sums: bitwise equal to the CPU path (ops.reference.init_uniform4).
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+
+__global__ __launch_bounds__(256) void init_uniform4_kernel(bf16_t* __restrict__ out, long long rows,
+                                                            int cols, long long ld, long long row0,
+                                                            long long col0, uint32_t s, float scale) {
+  const long long n = rows * cols;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long r = i / cols, c = i - r * cols;
+    const uint32_t idx = (uint32_t)((row0 + r) * ld + col0 + c);
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += (float)(fmix32(idx * 4u + (uint32_t)k + s) >> 8) * (1.0f / 16777216.0f);
+    out[i] = f2bf((acc - 2.0f) * scale);
+  }
+}
+
+extern "C" int loqa_init_uniform4(void* out, long long rows, int cols, long long ld, long long row0,
+                                  long long col0, unsigned s, float scale, hipStream_t st) {
+  if (rows < 0 || cols < 0 || col0 + cols > ld) return (int)hipErrorInvalidValue;
+  const long long n = rows * cols;
+  if (n == 0) return 0;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(init_uniform4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (bf16_t*)out, rows,
+                     cols, ld, row0, col0, (uint32_t)s, scale);
   return (int)hipGetLastError();
 }

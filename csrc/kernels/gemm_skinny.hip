@@ -827,6 +827,21 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       }
     }
   } else if constexpr (MODE == EPI_ACT) {
+    if (a.act == 2) {
+      // f32 output (tensor-parallel partial sums: the all-reduce adds them in
+      // f32 before the one bf16 rounding of the residual, as the single-GPU
+      // residual epilogue does)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int m = j * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.out) + (size_t)m * a.ldo +
+                                     tile * (16 * RT) + i * 16 + nq) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < MT; ++j) {
       const int m = j * 16 + (lane & 15);

@@ -150,6 +150,9 @@ class LLMEngine:
         self._graphs_frozen = False
         self._next_id = 1
         self._on_done = None
+        # tensor parallel: the lock-step control ring (parallel/tp_control.py);
+        # rank 0 publishes each scheduler iteration's arrivals, followers replay
+        self.tp_ctl = None
         self._cells_lock = threading.Lock()
         # prefill placement (continuous-batching scheduler). Serialised (default):
         # the scheduler runs a step's new prompts on the decode stream between
@@ -158,7 +161,16 @@ class LLMEngine:
         # decode steps. With distinct ~320-token prompts the overlapped prefill's
         # hipBLASLt GEMMs slowed every concurrent decode step (4.1 -> 4.6 ms) and
         # the Whisper decoder: 18.3-18.5 vs 17.9-18.0 utt/s serialised.
-        self.overlap_prefill = self.is_gpu and os.environ.get("LOQA_OVERLAP_PREFILL", "0") == "1"
+        # Tensor parallel: every collective must be issued in the same order on
+        # every rank, so prefill stays on the decode stream (no overlap).
+        self.overlap_prefill = (self.is_gpu and self.tp.world == 1
+                                and os.environ.get("LOQA_OVERLAP_PREFILL", "0") == "1")
+        if self.overlap_prefill and self.pipelined:
+            # a pipelined step still in flight writes KV blocks that completion /
+            # misprediction already returned to the pool; only the decode stream's
+            # own order makes that safe, and an overlapped prefill on another
+            # stream could be handed those blocks - the two are exclusive
+            self.pipelined = False
         # mixed steps (LOQA_MIXED_PREFILL=1): a serialised prefill also feeds
         # every live sequence's next token. Opt-in: in the 8-stream bench it
         # saves the prefill's wait behind in-flight steps but the pipeline
@@ -237,14 +249,21 @@ class LLMEngine:
         return self._tp_argmax(logits, mask_rows)
 
     def _tp_argmax(self, logits: torch.Tensor, mask_rows: torch.Tensor) -> torch.Tensor:
-        """Vocab-parallel masked argmax: local (max, idx) then all_gather (D5)."""
-        import torch.distributed as dist
+        """Vocab-parallel masked argmax (D5): this rank's masked argmax over its
+        vocab slice, then one combine - the custom all-reduce's argmax kernel
+        on GPUs (one 64-bit record per row and rank), all_gather otherwise."""
         V = self.weights.v
         lo = self.tp.rank * V
-        W = self.masks.shape[1]
-        w0 = lo // 32
-        local_mask = self.masks[:, w0:w0 + (V + 31) // 32].contiguous()
-        idx = ops.masked_argmax(logits, local_mask, mask_rows)
+        if getattr(self, "_local_mask", None) is None:
+            assert lo % 32 == 0, "vocab shard must start on a mask word"
+            w0 = lo // 32
+            self._local_mask = self.masks[:, w0:w0 + (V + 31) // 32].contiguous()
+        idx = ops.masked_argmax(logits, self._local_mask, mask_rows)
+        if self.tp.car is not None and logits.is_cuda:
+            if logits.dtype != torch.float32:
+                logits = logits.float()
+            return self.tp.car.argmax(logits, idx, lo)
+        import torch.distributed as dist
         val = logits.float().gather(1, idx.clamp(min=0).long()[:, None])[:, 0]
         val = torch.where(idx >= 0, val, torch.full_like(val, -float("inf")))
         pair = torch.stack([val, (idx + lo).float()], dim=1)  # idx < 2^24 exact in fp32
@@ -333,7 +352,8 @@ class LLMEngine:
         ring slot its sampled tokens will land in."""
         rslot = self._step_no % self.RES_SLOTS
         g["graph"].replay()
-        self._step_no += 1
+        # wraps like the device counter (step_publish): 2 staging x RES_SLOTS
+        self._step_no = (self._step_no + 1) % (2 * self.RES_SLOTS)
         return rslot
 
     def _step_body(self, meta: StepMeta, dev: dict, device_io: bool = False) -> torch.Tensor:
@@ -641,12 +661,9 @@ class LLMEngine:
         t_end = 0.0
         while self._running:
             idle = not live and not pending and not waiting
-            items = [self._inbox.get()] if idle else []   # idle: block for work
-            while True:
-                try:
-                    items.append(self._inbox.get_nowait())
-                except queue.Empty:
-                    break
+            items = self._next_items(idle)
+            if items is None:          # TP follower: the leader stopped
+                break
             waiting += [it for it in items if it is not None]
             try:
                 new: list[GenRequest] = []
@@ -751,6 +768,44 @@ class LLMEngine:
                     if not fut.done():
                         fut.set_exception(e)
                 live, pending, waiting = [], [], []
+
+        if self.tp_ctl is not None and self.tp_ctl.leader:
+            self.tp_ctl.publish([], stop=True)
+
+    def _next_items(self, idle: bool) -> list | None:
+        """This scheduler iteration's new inbox items (blocking when idle).
+        TP leader: also publishes them; TP follower: replays the leader's
+        record instead of reading an inbox (None once the leader stopped)."""
+        ctl = self.tp_ctl
+        if ctl is None or ctl.leader:
+            items = [self._inbox.get()] if idle else []   # idle: block for work
+            while True:
+                try:
+                    items.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            if ctl is not None:
+                ctl.publish([[(r.prompt, r.schema) for r in it[0]] for it in items if it is not None])
+            return items
+        while True:
+            rec, stop = ctl.recv(timeout_s=0.5)
+            if stop:
+                self._running = False
+                return None
+            if rec is not None:
+                break
+        self.stats["tp_records"] = self.stats.get("tp_records", 0) + 1
+        return [([GenRequest(list(p), sch) for p, sch in batch], None, Future()) for batch in rec]
+
+    def follow(self, stream_priority: int = 0) -> None:
+        """TP follower rank: run the scheduler on the calling thread, replaying
+        the leader's iterations until it stops."""
+        assert self.tp_ctl is not None and not self.tp_ctl.leader
+        from ..utils.gil import tune_switch_interval
+        tune_switch_interval()
+        self._inbox = queue.Queue()
+        self._running = True
+        self._schedule(int(os.environ.get("LOQA_LLM_PRIORITY", stream_priority)))
 
     def _prefill_timed(self, reqs: list[GenRequest], riders: list[GenRequest] | None = None) -> None:
         t0 = time.perf_counter()

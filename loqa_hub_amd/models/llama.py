@@ -42,7 +42,13 @@ class StepMeta:
 
 
 class TPGroup:
-    """Tensor-parallel context; world 1 = no-op."""
+    """Tensor-parallel context; world 1 = no-op.
+
+    On GPUs every collective of a TP decode step is a custom IPC kernel
+    (``parallel/custom_allreduce.py``): the row-parallel o / down all-reduce fused
+    with the residual add and the next norm's row statistics, and the
+    vocab-parallel argmax combine. On the CPU (gloo) the same step runs through
+    ``dist`` collectives, which is what the CPU test tier exercises."""
 
     def __init__(self, rank: int = 0, world: int = 1, group=None, allreduce=None):
         self.rank, self.world, self.group = rank, world, group
@@ -60,6 +66,11 @@ class TPGroup:
             ar = CustomAllReduce(group)
         return cls(rank, world, group, ar)
 
+    @property
+    def car(self):
+        """The custom all-reduce (None: dist collectives)."""
+        return self._allreduce
+
     def all_reduce_(self, x: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return x
@@ -69,6 +80,27 @@ class TPGroup:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def partial_out(self, which: int, rows: int, cols: int, device):
+        """Where a row-parallel GEMM writes its f32 partial (the IPC input
+        buffer on GPUs, a plain tensor for the dist path)."""
+        if self._allreduce is not None:
+            return self._allreduce.inbuf(which, rows, cols)
+        return torch.empty(rows, cols, dtype=torch.float32, device=device)
+
+    def resid_epilogue(self, which: int, partial, residual: torch.Tensor, scratch) -> None:
+        """residual += sum over ranks of ``partial``; the row sums of squares
+        of the new residual go to ``scratch`` for the next norm prologue."""
+        if self._allreduce is not None:
+            nb = self._allreduce.resid_blocks(residual.shape[1])
+            self._allreduce.resid(which, residual, scratch.rowsq, nb)
+            scratch.stat_tiles = self.world * nb
+            return
+        import torch.distributed as dist
+        p = partial.float()
+        dist.all_reduce(p, group=self.group)
+        residual.copy_((residual.float() + p).to(torch.bfloat16))
+        scratch.seed_stats(residual, sums=False)
+
 
 class LlamaWeights:
     def __init__(self, cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0,
@@ -77,48 +109,58 @@ class LlamaWeights:
         self.cfg, self.tp = cfg, tp
         # compact: ONE copy of every projection, in the fused decode layout
         # (prefill then runs through the fused GEMMs in <= 64-token chunks).
-        # Llama-3-70B bf16 (141 GB) fits one 288 GB MI355X this way; the
-        # default keeps row-major copies for hipBLASLt prefill as well.
+        # Llama-3-70B bf16 (141 GB) fits one 288 GB MI355X this way, and a
+        # TP=8 shard (17.6 GB) fits eight ranks sharing one GPU; the default
+        # keeps row-major copies for hipBLASLt prefill as well.
         self.compact = compact
-        assert not compact or tp.world == 1, "compact weights are single-GPU"
         assert cfg.n_heads % tp.world == 0 and cfg.n_kv_heads % tp.world == 0
         assert cfg.ffn_dim % tp.world == 0 and cfg.vocab_size % tp.world == 0
         self.h = cfg.n_heads // tp.world
         self.hkv = cfg.n_kv_heads // tp.world
         self.f = cfg.ffn_dim // tp.world
         self.v = cfg.vocab_size // tp.world
-        d, D = cfg.d_model, cfg.head_dim
-        g = torch.Generator(device=device)
-        g.manual_seed(seed * 1000003 + 17 + tp.rank)  # shards differ; replicas (same rank) identical
+        d, D, r = cfg.d_model, cfg.head_dim, tp.rank
+        H, Hkv, F, V = cfg.n_heads, cfg.n_kv_heads, cfg.ffn_dim, cfg.vocab_size
 
-        def rnd(*shape, std=0.02):
-            t = torch.empty(*shape, dtype=dtype, device=device)
-            t.normal_(0.0, std, generator=g)
-            return t
+        # Counter-based init (ops.init_normal): every tensor is a function of
+        # (seed, layer, name, global index), so a TP rank generates exactly its
+        # Megatron slice of the SAME model the single-GPU engine builds -
+        # column-parallel q/k/v, gate/up and vocab rows, row-parallel o / down
+        # columns - and TP=N is comparable token for token with TP=1.
+        def rnd(key, rows, cols, *, ld=None, row0=0, col0=0):
+            return ops.init_normal(rows, cols, seed=seed, key=key, ld=ld, row0=row0, col0=col0,
+                                   device=device).to(dtype)
 
         def ones(n):
             return torch.ones(n, dtype=dtype, device=device)
 
-        # std 0.02 everywhere keeps activations O(1) through random layers
-        self.embed = rnd(self.v, d)
+        # the embedding table is replicated on every TP rank (2.1 GB for the
+        # 128k x 8192 table - cheap in 288 GB of HBM), so a decode step's
+        # embedding needs no all-reduce; the lm_head stays vocab-parallel
+        self.embed = rnd(("embed",), V, d)
         self.layers = []
         if compact:
             self.decode_layers = []
-        for _ in range(cfg.n_layers):
+        for li in range(cfg.n_layers):
             L = {
                 "attn_norm": ones(d),
-                "wqkv": rnd((self.h + 2 * self.hkv) * D, d),
-                "wo": rnd(d, self.h * D),
+                "wqkv": torch.cat([rnd((li, "q"), self.h * D, d, row0=r * self.h * D),
+                                   rnd((li, "k"), self.hkv * D, d, row0=r * self.hkv * D),
+                                   rnd((li, "v"), self.hkv * D, d, row0=r * self.hkv * D)]),
+                "wo": rnd((li, "o"), d, self.h * D, ld=H * D, col0=r * self.h * D),
                 "mlp_norm": ones(d),
-                "w_gate_up": rnd(2 * self.f, d),
-                "w_down": rnd(d, self.f),
+                "w_gate_up": torch.cat([rnd((li, "gate"), self.f, d, row0=r * self.f),
+                                        rnd((li, "up"), self.f, d, row0=r * self.f)]),
+                "w_down": rnd((li, "down"), d, self.f, ld=F, col0=r * self.f),
             }
             if compact:   # convert layer by layer: peak = one layer's row-major copy
                 self.decode_layers.append(self._compact_layer(L))
                 L = {"attn_norm": L["attn_norm"], "mlp_norm": L["mlp_norm"]}
             self.layers.append(L)
         self.final_norm = ones(d)
-        self.lm_head = self.embed if cfg.tie_embeddings else rnd(self.v, d)
+        vs = slice(r * self.v, (r + 1) * self.v)
+        self.lm_head = self.embed[vs] if cfg.tie_embeddings else \
+            rnd(("lm_head",), self.v, d, row0=r * self.v)
         self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
         self._finalize()
 
@@ -178,10 +220,8 @@ class LlamaWeights:
 
     def _add_fused_copies(self) -> None:
         """Row-permuted decode copies for the fused-epilogue GEMMs (RoPE pairs /
-        gate-up pairs share a 32-row tile); single-GPU only."""
-        self.fused = self.tp.world == 1
-        if not self.fused:
-            return
+        gate-up pairs share a 32-row tile); TP ranks permute their own slices."""
+        self.fused = True
         from ..ops import reference as _ref
         pq = _ref.perm_rope_qkv(self.h, self.hkv, self.cfg.head_dim).to(self.embed.device)
         pg = _ref.perm_gate_up(self.f).to(self.embed.device)
@@ -199,8 +239,11 @@ class LlamaWeights:
         ops.tune_fused(P["wqkv_f"], "rope", norm="rms", heads=(self.h, self.hkv, D),
                        cos_sin=self.cos_sin, prefill=pf)
         ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms", prefill=pf)
-        ops.tune_fused(P["wo"], "resid", prefill=pf)
-        ops.tune_fused(P["w_down"], "resid", prefill=pf)
+        # TP: the row-parallel projections emit bf16 partials ("act" epilogue)
+        # that the all-reduce kernel adds to the residual stream
+        mode = "resid" if self.tp.world == 1 else "act"
+        ops.tune_fused(P["wo"], mode, prefill=pf)
+        ops.tune_fused(P["w_down"], mode, prefill=pf)
 
     @classmethod
     def shard(cls, full: "LlamaWeights", tp: TPGroup) -> "LlamaWeights":
@@ -217,7 +260,8 @@ class LlamaWeights:
         H, Hkv, F = cfg.n_heads, cfg.n_kv_heads, cfg.ffn_dim
         qs, ks = slice(r * self.h * D, (r + 1) * self.h * D), slice(r * self.hkv * D, (r + 1) * self.hkv * D)
         fs, vs = slice(r * self.f, (r + 1) * self.f), slice(r * self.v, (r + 1) * self.v)
-        self.embed = full.embed[vs].contiguous()
+        self.compact = False
+        self.embed = full.embed          # replicated (see __init__)
         self.layers = []
         for L in full.layers:
             w = L["wqkv"]
@@ -231,7 +275,7 @@ class LlamaWeights:
                 "w_gate_up": torch.cat([gu[:F][fs], gu[F:][fs]]).contiguous(),
                 "w_down": L["w_down"][:, fs].contiguous()})
         self.final_norm = full.final_norm
-        self.lm_head = self.embed if cfg.tie_embeddings else full.lm_head[vs].contiguous()
+        self.lm_head = (full.embed if cfg.tie_embeddings else full.lm_head)[vs].contiguous()
         self.cos_sin = full.cos_sin
         self._finalize()
         return self
@@ -264,7 +308,7 @@ class LlamaModel:
 
     def embed(self, tokens: torch.Tensor) -> torch.Tensor:
         tp = self.w.tp
-        if tp.world == 1:
+        if tp.world == 1 or self.w.embed.shape[0] == self.cfg.vocab_size:   # replicated table
             return torch.nn.functional.embedding(tokens.long(), self.w.embed)
         lo = tp.rank * self.w.v
         local = tokens.long() - lo
@@ -375,14 +419,16 @@ class LlamaModel:
         """Decode step with the fused-epilogue GEMMs (5 launches per layer):
         qkv (RMSNorm prologue, RoPE + KV append epilogue) -> attention ->
         o (residual + row sum-of-squares epilogue) -> gate|up (RMSNorm prologue,
-        SwiGLU epilogue) -> down (residual + row sum-of-squares). Single GPU,
-        Mpad 16 / 32. Same numerics as ``forward_decode``."""
-        cfg, w = self.cfg, self.w
+        SwiGLU epilogue) -> down (residual + row sum-of-squares); Mpad 16 / 32 /
+        64. Same numerics as ``forward_decode``. Tensor parallel:
+        o and down emit bf16 partials and the residual all-reduce kernel adds
+        them (7 launches per layer); the logits are this rank's vocab slice."""
+        cfg, w, tp = self.cfg, self.w, self.w.tp
         H, Hkv, D, d = w.h, w.hkv, cfg.head_dim, cfg.d_model
         Mpad = meta.tokens.numel()
         # embedding + layer 0's RMSNorm row scale (one partial sum of squares per
-        # row) in one launch
-        if ops.FUSED_EMBED and w.tp.world == 1 and meta.tokens.dtype == torch.int32:
+        # row) in one launch (TP ranks hold the whole table)
+        if ops.FUSED_EMBED and w.embed.shape[0] == cfg.vocab_size and meta.tokens.dtype == torch.int32:
             residual = ops.embed_stats(meta.tokens, w.embed, scratch)
         else:
             residual = self.embed(meta.tokens).contiguous()
@@ -405,10 +451,22 @@ class LlamaModel:
                                  block_tables=meta.block_tables, grouped=grouped,
                                  split_keys=split_keys, num_splits=num_splits if grouped else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
-            ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
+            if tp.world == 1:
+                ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
+            else:
+                # row-parallel o: f32 partial into the all-reduce input buffer,
+                # then ONE kernel sums the ranks into the residual + row stats
+                po = tp.partial_out(0, Mpad, d, residual.device)
+                ops.skinny_fused(attn, P["wo"], "act", scratch, out=po, act="f32")
+                tp.resid_epilogue(0, po, residual, scratch)
             a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
                                  eps=cfg.norm_eps)
-            ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
+            if tp.world == 1:
+                ops.skinny_fused(a, P["w_down"], "resid", scratch, residual=residual)
+            else:
+                pd = tp.partial_out(1, Mpad, d, residual.device)
+                ops.skinny_fused(a, P["w_down"], "act", scratch, out=pd, act="f32")
+                tp.resid_epilogue(1, pd, residual, scratch)
         if ops.FUSED_EMBED:
             hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
         else:

@@ -325,6 +325,35 @@ def im2col_k3(x: torch.Tensor, strides: tuple[int, int, int], B: int, C: int, L:
     return cols
 
 
+def tensor_seed(seed: int, *key) -> int:
+    """uint32 stream id of one weight tensor of a seeded random init (stable
+    across processes and Python versions: no ``hash()``)."""
+    h = (seed * 0x9E3779B1 + 0x7F4A7C15) & 0xFFFFFFFF
+    for k in key:
+        for ch in str(k).encode():
+            h = ((h ^ ch) * 0x01000193) & 0xFFFFFFFF
+        h = ((h ^ 0xFF) * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+def init_normal(rows: int, cols: int, *, seed: int, key: tuple, std: float = 0.02,
+                ld: int | None = None, row0: int = 0, col0: int = 0, device="cpu") -> torch.Tensor:
+    """Seeded random-init block [rows, cols] bf16 of a conceptual [*, ld] tensor
+    at (row0, col0): zero mean, standard deviation ``std`` (Irwin-Hall(4), a
+    near-normal with bounded tails). A shard generated on its own holds
+    exactly the values of the unsharded tensor, on the GPU and the CPU alike."""
+    ld = cols if ld is None else ld
+    s = tensor_seed(seed, *key)
+    scale = float(torch.tensor(std * math.sqrt(3.0), dtype=torch.float32))
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return ref.init_uniform4(rows, cols, ld, row0, col0, s, scale).to(dev)
+    out = torch.empty(rows, cols, dtype=torch.bfloat16, device=dev)
+    check(kernels().loqa_init_uniform4(ptr(out), rows, cols, ld, row0, col0, s, scale,
+                                       stream_ptr(out)), "init_uniform4")
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     """Plain GEMM: hipBLASLt via torch on the GPU."""
     return torch.nn.functional.linear(x, w, b)
@@ -992,7 +1021,7 @@ class FusedScratch:
 
 _FUSED_MODES = {"silu": 1, "resid": 2, "rope": 3, "act": 4}
 _NORMS = {None: 0, False: 0, True: 1, "rms": 1, "ln": 2}
-_ACTS = {"none": 0, "gelu": 1}
+_ACTS = {"none": 0, "gelu": 1, "f32": 2}   # "f32": no activation, f32 output
 
 
 class FusedLinear:
@@ -1151,7 +1180,8 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     if mode == "silu" and out is None:
         out = torch.empty(Mpad, N // 2, dtype=torch.bfloat16, device=x.device)
     elif mode == "act" and out is None:
-        out = torch.empty(Mpad, N, dtype=torch.bfloat16, device=x.device)
+        out = torch.empty(Mpad, N, dtype=torch.float32 if act == "f32" else torch.bfloat16,
+                          device=x.device)
     if not _gpu(x):
         return _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual,
                                  positions, cos_sin, q_out, k_cache, v_cache, slots, n_heads,
@@ -1163,6 +1193,9 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
         assert colsum is not None and colsum.numel() == N
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.numel() == N and bias.is_contiguous()
+    if mode == "act":
+        assert out.dtype == (torch.float32 if act == "f32" else torch.bfloat16)
+        assert out.stride(0) % 4 == 0 and out.shape[0] >= Mpad and out.shape[1] >= N
     if mode == "rope":   # the epilogue reads slots / positions for every padded row
         assert slots.numel() >= Mpad and q_out.shape[0] >= Mpad and k_cache.is_contiguous()
         assert cos_sin is None or positions.numel() >= Mpad
@@ -1215,6 +1248,9 @@ def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, pos
         out.copy_(ref.silu_mul(y.to(torch.bfloat16)))
         return out
     if mode == "act":
+        if act == "f32":
+            out.copy_(y)
+            return out
         yb = y.to(torch.bfloat16)
         if act == "gelu":
             yb = torch.nn.functional.gelu(yb.float()).to(torch.bfloat16)

@@ -111,13 +111,17 @@ _KERNEL_SIGS = {
                         c_int, c_int, c_void_p, c_void_p],
     "loqa_whisper_mega": [c_void_p, c_int, c_void_p],
     "loqa_gemm_prefill": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "loqa_init_uniform4": [c_void_p, c_ll, c_int, c_ll, c_ll, c_ll, ctypes.c_uint, c_float, c_void_p],
     "loqa_step_publish": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                           c_void_p],
 }
 
 # (argtypes, restype) of the custom all-reduce entry points (in the kernels library)
 _CAR_SIGS = {
-    "loqa_car_create": ([c_int, c_int, c_ll], c_void_p),
+    "loqa_car_create": ([c_int, c_int, c_ll, c_ll], c_void_p),
+    "loqa_car_inbuf": ([c_void_p, c_int], c_void_p),
+    "loqa_car_resid": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "loqa_car_argmax": ([c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
     "loqa_car_handle": ([c_void_p, c_void_p], c_int),
     "loqa_car_handle_size": ([], c_int),
     "loqa_car_open": ([c_void_p, c_void_p], c_int),
@@ -148,6 +152,11 @@ _RUNTIME_SIGS = {
     "loqa_pool_seq_len": ([c_void_p, c_ll], c_ll),
     "loqa_pool_free_seq": ([c_void_p, c_ll], c_int),
     "loqa_pool_truncate": ([c_void_p, c_ll, c_ll], c_int),
+    "loqa_tpctl_open": ([ctypes.c_char_p, c_int, c_int, c_int, c_ll], c_void_p),
+    "loqa_tpctl_unlink": ([c_void_p], None),
+    "loqa_tpctl_publish": ([c_void_p, c_void_p, c_ll, c_int, c_ll], c_int),
+    "loqa_tpctl_recv": ([c_void_p, c_void_p, c_ll, ctypes.POINTER(c_int), c_ll], c_ll),
+    "loqa_tpctl_close": ([c_void_p], None),
 }
 
 

@@ -468,3 +468,27 @@ def fused_row_scale(rowsq_in, eps, K):
     """RMSNorm row scale 1/rms from per-tile partial sums of squares [tiles, Mpad]."""
     tot = rowsq_in.float().sum(0)  # [Mpad]
     return torch.rsqrt(tot / K + eps)
+
+
+def _fmix32(h: torch.Tensor) -> torch.Tensor:
+    m = 0xFFFFFFFF
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & m
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & m
+    return h ^ (h >> 16)
+
+
+def init_uniform4(rows: int, cols: int, ld: int, row0: int, col0: int, s: int,
+                  scale: float) -> torch.Tensor:
+    """CPU twin of elementwise.hip ``init_uniform4_kernel``: bf16 [rows, cols],
+    element (r, c) = scale * (sum_k fmix32(4 idx + k + s) / 2^32 - 2) with
+    idx = (row0 + r) * ld + col0 + c (uint32 arithmetic, exact f32 sums)."""
+    r = torch.arange(rows, dtype=torch.int64)[:, None] + row0
+    c = torch.arange(cols, dtype=torch.int64)[None, :] + col0
+    idx = (r * ld + c) & 0xFFFFFFFF
+    acc = torch.zeros(rows, cols, dtype=torch.float32)
+    for k in range(4):
+        h = _fmix32((idx * 4 + k + s) & 0xFFFFFFFF)
+        acc += (h >> 8).to(torch.float32) * (1.0 / 16777216.0)
+    return ((acc - 2.0) * torch.tensor(scale, dtype=torch.float32)).to(torch.bfloat16)
