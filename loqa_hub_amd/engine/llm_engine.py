@@ -383,6 +383,12 @@ class LLMEngine:
         first-time capture would stall that step by tens of ms."""
         if not self.use_graphs:
             return 0
+        if self.tp.world > 1:
+            # the captures' warm-up runs collectives: every rank must arrive
+            # here before any of them spins on a peer (the leader's STT warm-up
+            # can take longer than a bounded collective wait)
+            import torch.distributed as dist
+            dist.barrier(group=self.tp.group)
         n = 0
         b_max = _bucket(max(1, self.max_seqs), self.SEQ_BUCKETS)
         for b in self.SEQ_BUCKETS:

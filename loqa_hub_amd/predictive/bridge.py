@@ -11,7 +11,9 @@ Classification failures fall back to streaming-only.
 
 MI355X-first differences:
 * the classification comes from an already-parsed command when the caller has
-  one (the constrained GPU decode), so the bridge adds no LLM pass;
+  one (the constrained GPU decode), so the bridge adds no LLM pass; with
+  ``streamed`` (that decode's streaming result) the streaming-only strategy
+  monitors it instead of starting a second, streaming parse;
 * streaming-only sessions monitor the real streaming result (completion or
   error) instead of simulating a 10 s completion (:345-436).
 """
@@ -85,9 +87,10 @@ class StreamingPredictiveBridge:
         self.active: dict[str, BridgeSession] = {}
         self.metrics = BridgeMetrics()
 
-    async def process_voice_command(self, transcript: str,
-                                    parsed: Command | None = None) -> BridgeSession:
+    async def process_voice_command(self, transcript: str, parsed: Command | None = None,
+                                    streamed=None) -> BridgeSession:
         s = BridgeSession(generate_session_id(), transcript)
+        s.streaming_result = streamed
         self.active[s.session_id] = s
         try:
             s.classification = (self.classifier.classify_parsed(parsed) if parsed is not None
@@ -136,8 +139,9 @@ class StreamingPredictiveBridge:
     async def _streaming_only(self, s: BridgeSession, fallback: bool = False) -> BridgeSession:
         s.streaming_active, s.prediction_active = True, False
         try:
-            s.streaming_result = await self.streaming_parser.parse_command_streaming(
-                s.user_transcript)
+            if s.streaming_result is None:
+                s.streaming_result = await self.streaming_parser.parse_command_streaming(
+                    s.user_transcript)
         except Exception as e:
             self._cleanup(s.session_id)
             raise RuntimeError(("fallback streaming failed: " if fallback else

@@ -37,27 +37,88 @@ from .transport.audio_service import AudioService
 log = logging.getLogger("loqa.server")
 
 
-def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None):
-    """On-device STT -> constrained intent decode -> queue (one GPU)."""
+def build_tts(cfg: Config, device: str = "cuda:0"):
+    """The reply voice (``audio_service.go:180-195``) from ``HUB_TTS_BACKEND``:
+    ``gpu`` -> on-device VITS (``HUB_TTS_MODEL``) on the serving GPU,
+    ``http`` / ``openai`` -> the OpenAI-compatible client (``TTS_URL``; its
+    connection is tested in ``HubServer.start`` with the reference's
+    fallback rule), ``none`` -> text-only replies."""
+    b = cfg.gpu.tts_backend
+    if b == "none":
+        return None
+    if b == "gpu":
+        from .engine.tts_engine import VitsTTSEngine
+        from .models.configs import vits_config
+        return VitsTTSEngine(vits_config(cfg.gpu.tts_model), device, seed=cfg.gpu.seed)
+    if b in ("http", "openai"):
+        from .llm.tts import OpenAITTSClient
+        return OpenAITTSClient(cfg.tts)
+    raise ValueError(f"unknown HUB_TTS_BACKEND {b!r} (gpu | http | none)")
+
+
+def build_bridge(skills_manager=None, tts=None, fallback_parser=None):
+    """The streaming-predictive bridge and its stack (``audio_service.go:345-405``):
+    classifier + reliability tracker, predictive engine and async execution
+    pipeline over the skill manager (the hub's skills, the reference's
+    always-failing adapter when there are none), status manager speaking
+    through ``tts``. On the GPU path the classification and the streaming
+    result both come from the one constrained decode, so ``fallback_parser``
+    only serves callers without a parse."""
+    from .predictive.async_execution import AsyncExecutionPipeline
+    from .predictive.bridge import StreamingPredictiveBridge
+    from .predictive.classifier import CommandClassifier
+    from .predictive.engine import PredictiveResponseEngine
+    from .predictive.reliability import DeviceReliabilityTracker
+    from .predictive.skill_adapter import NullSkillManager, SkillManagerAdapter
+    from .predictive.status_manager import StatusManager
+    from .streaming.parser import StreamingCommandParser
+    adapter = SkillManagerAdapter(skills_manager) if skills_manager is not None else NullSkillManager()
+    rel = DeviceReliabilityTracker()
+    clf = CommandClassifier(fallback_parser, rel)
+    engine = PredictiveResponseEngine(adapter, clf, rel)
+    return StreamingPredictiveBridge(StreamingCommandParser(None, fallback_parser, enabled=False),
+                                     engine, StatusManager(tts), clf,
+                                     AsyncExecutionPipeline(adapter))
+
+
+def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, skills=None,
+                        llm=None, bridge: bool = True):
+    """On-device STT -> constrained intent decode -> queue (one GPU), the
+    bridge on that decode, and the reply voice (``tts``: "auto" builds it from
+    ``HUB_TTS_BACKEND``). ``llm``: a prebuilt engine (the tensor-parallel
+    leader, ``parallel/tp_serving.py``). Speech is progressive (phrases from
+    the live decode) when ``STREAMING_ENABLED``."""
     from .engine.llm_engine import LLMEngine
     from .engine.pipeline import VoicePipeline
     from .engine.stt_engine import STTEngine
     from .models.configs import llama_config, whisper_config
+    from .streaming.components import tts_options_from
     from .transport.voice_processor import GPUVoiceProcessor
     g = cfg.gpu
     scfg, lcfg = whisper_config(g.stt_model), llama_config(g.llm_model)
     sw = lw = None
-    if g.stt_checkpoint or g.llm_checkpoint:
+    if g.stt_checkpoint or (g.llm_checkpoint and llm is None):
         from .models import loader
         sw = loader.load_whisper(scfg, g.stt_checkpoint, device) if g.stt_checkpoint else None
-        lw = loader.load_llama(lcfg, g.llm_checkpoint, device) if g.llm_checkpoint else None
+        lw = loader.load_llama(lcfg, g.llm_checkpoint, device) if (g.llm_checkpoint and llm is None) \
+            else None
     stt = STTEngine(scfg, device, seed=g.seed, max_batch=g.max_batch, use_graphs=g.use_graphs,
                     weights=sw)
-    llm = LLMEngine(lcfg, device, seed=g.seed, max_seqs=g.max_batch, weights=lw,
-                    max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs)
+    if llm is None:
+        llm = LLMEngine(lcfg, device, seed=g.seed, max_seqs=g.max_batch, weights=lw,
+                        max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs)
+    if tts == "auto":
+        tts = build_tts(cfg, device)
     pipe = VoicePipeline(stt, llm, nats)
     pipe.warmup()
-    return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64))
+    sc = cfg.streaming
+    return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64),
+                             bridge=build_bridge(skills, tts) if bridge else None,
+                             bridge_timeout=cfg.arbitration.bridge_timeout,
+                             progressive=sc.enabled, tts_options=tts_options_from(cfg),
+                             tts_format=cfg.tts.response_format,
+                             max_buffer_time=sc.max_buffer_time,
+                             max_tokens_per_phrase=sc.max_tokens_per_phrase)
 
 
 async def build_dp_processor(cfg: Config, n_gpus: int):
@@ -85,7 +146,7 @@ async def build_service_processor(cfg: Config, nats, tts=None):
 class HubServer:
     def __init__(self, cfg: Config, *, processor=None, nats: NATSService | None = None,
                  streaming=None, skills_dir: str = "./skills",
-                 skills_config_store: str = "./data/skills"):
+                 skills_config_store: str = "./data/skills", transcript_hints=None):
         self.cfg = cfg
         self.database = Database(cfg.server.db_path)
         self.events = VoiceEventsStore(self.database)
@@ -101,6 +162,7 @@ class HubServer:
         self.http_port = 0
         self.grpc_port = 0
         self._embedded_broker = None
+        self.transcript_hints = transcript_hints     # synthetic load only (AudioService)
 
     # ------------------------------------------------------------------ wiring
     def app(self) -> web.Application:
@@ -130,6 +192,24 @@ class HubServer:
             except Exception as e:  # noqa: BLE001 - hub keeps serving without the bus
                 log.warning("Cannot connect to NATS: %s (events will not be published)", e)
 
+    async def _check_tts(self) -> None:
+        """The reference tests the TTS service at start-up and, with
+        ``TTS_FALLBACK_ENABLED``, keeps serving text-only if it is down
+        (``audio_service.go:182-195``)."""
+        tts = getattr(self.processor, "tts", None)
+        test = getattr(tts, "test_connection", None)
+        if test is None:
+            return
+        try:
+            await test()
+        except Exception as e:  # noqa: BLE001
+            if not self.cfg.tts.fallback_enabled:
+                raise RuntimeError(f"failed to connect to TTS service: {e}") from e
+            log.warning("TTS service unavailable, continuing without speech: %s", e)
+            self.processor.tts = None
+            if hasattr(self.processor, "progressive"):
+                self.processor.progressive = False
+
     async def start(self, host: str | None = None, http_port: int | None = None,
                     grpc_port: int | None = None) -> None:
         import grpc
@@ -139,11 +219,15 @@ class HubServer:
         await self.skills.register_plugin(LightsSkill())
         await self.skills.start()
         publisher = AudioStreamPublisher(self.nats.conn) if self.nats and self.nats.conn else None
+        if hasattr(self.processor, "attach_publisher"):
+            self.processor.attach_publisher(publisher)   # progressive per-phrase speech
+        await self._check_tts()
         a = self.cfg.arbitration
         self.audio_service = AudioService(
             self.processor, window_duration=a.window, scope=a.scope, relay_groups=a.relay_groups,
             end_of_speech_wait=a.end_of_speech_wait, events_store=self.events,
-            audio_publisher=publisher, confirmation_enabled=a.confirmation_enabled)
+            audio_publisher=publisher, confirmation_enabled=a.confirmation_enabled,
+            transcript_hints=self.transcript_hints)
         host = host if host is not None else self.cfg.server.host
         self.grpc_server = grpc.aio.server()
         add_audio_service(self.grpc_server, self.audio_service)
@@ -160,6 +244,9 @@ class HubServer:
         log.info("HTTP server listening on :%d", self.http_port)
 
     async def stop(self) -> None:
+        stop = getattr(self.processor, "close", None)
+        if stop is not None:
+            await stop()
         if self.grpc_server is not None:
             await self.grpc_server.stop(1.0)
         if self.http_runner is not None:

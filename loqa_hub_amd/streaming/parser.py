@@ -259,16 +259,8 @@ class StreamingCommandParser:
             res.close_outputs()
 
     def _fallback_result(self, cmd: Command) -> StreamingResult:
-        res = StreamingResult()
-        now = time.monotonic()
-        for ch in (res.visual_tokens, res.audio_phrases, res.token_stream):
-            ch.try_put(cmd.response)
-        res.final_command.try_put(cmd)
-        m = res.metrics
-        m.first_token_time = m.first_phrase_time = m.completion_time = now
-        m.token_count = m.phrase_count = 1
-        res.close_outputs()
-        return res
+        return completed_result(cmd)
+
 
     async def test_streaming_connection(self, timeout: float = 10.0) -> None:
         if not self.enabled:
@@ -296,3 +288,19 @@ class StreamingCommandParser:
             raise RuntimeError("streaming test timeout") from None
         finally:
             res.cancel()
+
+
+def completed_result(cmd: Command) -> StreamingResult:
+    """A finished streaming result carrying one already-parsed command (the
+    disabled-streaming fallback, :422-454, and the shared GPU decode that the
+    bridge monitors instead of a second parse)."""
+    res = StreamingResult()
+    now = time.monotonic()
+    for ch in (res.visual_tokens, res.audio_phrases, res.token_stream):
+        ch.try_put(cmd.response)
+    res.final_command.try_put(cmd)
+    m = res.metrics
+    m.first_token_time = m.first_phrase_time = m.completion_time = now
+    m.token_count = m.phrase_count = 1
+    res.close_outputs()
+    return res

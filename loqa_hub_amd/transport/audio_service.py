@@ -65,10 +65,16 @@ class RelayStream:
     end_of_speech: asyncio.Event = field(default_factory=asyncio.Event)
     result: asyncio.Future | None = None
     request_id: str = ""
+    # the relay's raw PCM16-LE bytes, wake word + speech, as received (the GPU
+    # path stages these; the float samples exist only for RMS / other backends)
+    pcm: bytearray = field(default_factory=bytearray)
 
     def full_audio(self) -> np.ndarray:
         parts = [self.wake_word_signal] + list(self.speech_audio)
         return np.concatenate(parts) if parts else np.zeros(0, np.float32)
+
+    def full_pcm16(self) -> np.ndarray:
+        return np.frombuffer(bytes(self.pcm), dtype="<i2")
 
 
 @dataclass
@@ -95,6 +101,10 @@ class UtteranceResult:
     confidence: float = 0.0
     entities: dict[str, str] = field(default_factory=dict)
     error: str = ""
+    audio_sample_rate: int = 0        # 0: the reference's guess (16 kHz, mp3 22.05 kHz)
+    audio_published: bool = False     # progressive speech already sent every phrase on NATS
+    strategy: str = ""                # streaming-predictive bridge strategy
+    metrics: dict = field(default_factory=dict)
 
 
 class VoiceProcessor(Protocol):
@@ -120,7 +130,8 @@ class AudioService:
     def __init__(self, processor: VoiceProcessor | None = None, *, window_duration: float = 0.300,
                  scope: str = "global", relay_groups: dict[str, str] | None = None,
                  end_of_speech_wait: float = 5.0, result_timeout: float = 30.0,
-                 events_store=None, audio_publisher=None, confirmation_enabled: bool = False):
+                 events_store=None, audio_publisher=None, confirmation_enabled: bool = False,
+                 transcript_hints=None):
         self.processor = processor
         self.arbitration_window_duration = window_duration
         self.scope = scope
@@ -130,6 +141,10 @@ class AudioService:
         self.events_store = events_store
         self.audio_publisher = audio_publisher
         self.confirmation_enabled = confirmation_enabled
+        # synthetic load only (bench --mode hub, tests): relay id -> the
+        # utterance's known transcript, which teacher-forces the random-init
+        # Whisper decoder; real relays never have one
+        self.transcript_hints = transcript_hints
         self.windows: dict[str, ArbitrationWindow] = {}
         self.active_streams: dict[str, RelayStream] = {}
         self.stats = {"windows": 0, "arbitrations": 0, "cancelled": 0, "processed": 0, "late": 0}
@@ -253,8 +268,14 @@ class AudioService:
             res = UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                   error="no voice processor configured")
         else:
+            kw = {}
+            if getattr(self.processor, "takes_pcm16", False):
+                kw["pcm16"] = rs.full_pcm16()
+            hint = self.transcript_hints(rs.relay_id) if self.transcript_hints else None
+            if hint:
+                kw["transcript_hint"] = hint
             try:
-                res = await self.processor.process(rs.relay_id, request_id, audio, 16000)
+                res = await self.processor.process(rs.relay_id, request_id, audio, 16000, **kw)
             except Exception as e:  # processor failure -> spoken error
                 log.exception("voice processing failed for relay %s", rs.relay_id)
                 res = UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
@@ -277,12 +298,12 @@ class AudioService:
         return res
 
     async def _deliver_audio(self, relay_id: str, res: UtteranceResult) -> None:
-        if not res.audio:
+        if not res.audio or res.audio_published:
             return
         if self.audio_publisher is None:
             log.warning("NATS audio publisher not available, skipping response to relay %s", relay_id)
             return
-        sr = 22050 if res.audio_format == "mp3" else 16000
+        sr = res.audio_sample_rate or (22050 if res.audio_format == "mp3" else 16000)
         try:
             await self.audio_publisher.stream_audio_to_relay(
                 relay_id, res.audio, res.audio_format, sr,
@@ -313,8 +334,9 @@ class AudioService:
                     relay_id = chunk.relay_id
                 hublog.log_audio_processing(relay_id, "received", bytes=len(chunk.audio_data),
                                             wake_word=chunk.is_wake_word)
+                data = chunk.audio_data
                 if chunk.is_wake_word:
-                    wake.append(bytes_to_float32_array(chunk.audio_data))
+                    wake.append(bytes_to_float32_array(data))
                     key = self.window_key(relay_id)
                     w = self.windows.get(key)
                     if w is None:
@@ -326,11 +348,13 @@ class AudioService:
                     rs = self.active_streams.get(relay_id)
                     if rs is not None:
                         rs.wake_word_signal = np.concatenate(wake)
+                        rs.pcm += data[: len(data) & ~1]
                         rs.request_id = request_id
                 else:
                     rs = self.active_streams.get(relay_id)
                     if rs is not None and rs.status != RelayStatus.CANCELLED:
-                        rs.speech_audio.append(bytes_to_float32_array(chunk.audio_data))
+                        rs.speech_audio.append(bytes_to_float32_array(data))
+                        rs.pcm += data[: len(data) & ~1]
                 if chunk.is_end_of_speech:
                     hublog.log_audio_processing(relay_id, "end_of_speech_detected")
                     if not self.is_relay_active(relay_id):

@@ -6,10 +6,16 @@ first command's response as the spoken reply, TTS over HTTP, NATS delivery.
 Two interchangeable implementations:
 
 * ``GPUVoiceProcessor`` - the MI355X path. Concurrent arbitration winners are
-  micro-batched (``batch_window``, ``max_batch``) into ONE ``VoicePipeline``
-  call: batched Whisper STT, one grammar-constrained multi-command decode per
-  utterance, the command queue with rollback + NATS publish per utterance as
-  soon as its own decode finishes, then batched TTS of the replies.
+  micro-batched into the ``VoicePipeline`` (continuous-batching Whisper STT,
+  ONE grammar-constrained multi-command decode per utterance, the command
+  queue with rollback + NATS publish as soon as its own decode finishes). The
+  streaming-predictive bridge is fed that decode's parse (no second LLM pass)
+  and decides the strategy / instant ack exactly as the reference's does. The
+  reply is spoken by the on-GPU VITS engine (or the OpenAI-compatible
+  client): progressively from the live decode when streaming is enabled
+  (``streaming/progressive.py``: the reply field's phrases are synthesised and
+  published on ``audio.<relay>`` while the decode runs), else as one file after
+  it.
 * ``ServiceVoiceProcessor`` - the reference's external-service path
   (BASELINE config 1): an STT client (``stt_client.py``), a ``CommandParser``
   over any ``LLMBackend`` (Ollama), optional bridge, optional TTS client.
@@ -48,8 +54,8 @@ def _result_from(text: str, mc: MultiCommand | None, queue_ok: bool | None,
         return UtteranceResult(transcription=text, success=False, command="error",
                                response_text=MSG_NO_COMMANDS)
     first = mc.commands[0]
-    reply = mc.combined_response if mc.is_multi and mc.combined_response else first.response
-    res = UtteranceResult(transcription=text, response_text=reply,
+    # the first command's response, as the reference (audio_service.go:687-689)
+    res = UtteranceResult(transcription=text, response_text=first.response or mc.combined_response,
                           intents=[c.intent for c in mc.commands],
                           confidence=first.confidence, entities=dict(first.entities),
                           success=queue_ok is not False)
@@ -59,50 +65,130 @@ def _result_from(text: str, mc: MultiCommand | None, queue_ok: bool | None,
 
 
 class GPUVoiceProcessor:
-    def __init__(self, pipeline, *, tts=None, batch_window: float = 0.005, max_batch: int = 8,
-                 tts_format: str = "wav"):
+    takes_pcm16 = True      # AudioService hands over the relay's raw PCM16 samples
+
+    def __init__(self, pipeline, *, tts=None, bridge=None, progressive: bool = False,
+                 speech_pipeline=None, batch_window: float = 0.005, max_batch: int = 8,
+                 tts_format: str = "wav", tts_options=None, bridge_timeout: float = 2.0,
+                 max_buffer_time: float = 2.0, max_tokens_per_phrase: int = 50):
         self.pipeline = pipeline
         self.tts = tts
+        self.bridge = bridge
+        self.bridge_timeout = bridge_timeout
         self.tts_format = tts_format
+        self.tts_options = tts_options
+        self.progressive = progressive and tts is not None
+        if self.progressive and speech_pipeline is None:
+            from ..streaming.audio_pipeline import StreamingAudioPipeline
+            speech_pipeline = StreamingAudioPipeline(tts, tts_options)
+        self.speech_pipeline = speech_pipeline
+        self.max_buffer_time, self.max_tokens_per_phrase = max_buffer_time, max_tokens_per_phrase
+        self.publisher = None           # NATS audio publisher (HubServer.start attaches it)
         pipeline.batch_window, pipeline.max_batch = batch_window, max_batch
-        self.stats = {"utterances": 0, "errors": 0}
+        self.stats = {"utterances": 0, "errors": 0, "bridge_sessions": 0, "bridge_ack": 0, "bridge_fallback": 0,
+                      "progressive": 0, "first_audio_ms_sum": 0.0, "first_audio_n": 0}
+
+    def attach_publisher(self, publisher) -> None:
+        self.publisher = publisher
+
+    async def close(self) -> None:
+        """Stop the engines' scheduler threads (a TP leader also releases its
+        followers)."""
+        await asyncio.to_thread(self.pipeline.llm.stop)
+        stop = getattr(self.pipeline.stt, "stop", None)
+        if stop is not None:
+            await asyncio.to_thread(stop)
 
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
-                      sample_rate: int, transcript_hint: str | None = None) -> UtteranceResult:
+                      sample_rate: int, transcript_hint: str | None = None,
+                      pcm16: np.ndarray | None = None) -> UtteranceResult:
         """``transcript_hint``: synthetic-traffic ground truth that teacher-forces
-        the (random-init) Whisper decoder; real relays never pass it. Concurrent
-        calls are micro-batched by the pipeline (STT batch, continuous LLM batch)."""
+        the (random-init) Whisper decoder; real relays never pass it. ``pcm16``:
+        the relay's raw samples (skips the float round trip). Concurrent calls
+        are micro-batched by the pipeline (STT batch, continuous LLM batch)."""
         from ..engine.pipeline import PipelineJob
-        j = PipelineJob(relay_id, request_id, float_to_pcm16(audio), transcript_hint)
+        pcm = pcm16 if pcm16 is not None else float_to_pcm16(audio)
+        j = PipelineJob(relay_id, request_id, pcm, transcript_hint)
+        speech = None
+        if self.progressive:
+            from ..streaming.progressive import ProgressiveSpeech
+            speech = ProgressiveSpeech(relay_id, self.pipeline.llm.tok, self.speech_pipeline,
+                                       self.publisher, max_buffer_time=self.max_buffer_time,
+                                       max_tokens_per_phrase=self.max_tokens_per_phrase)
+            j.on_tokens = speech.on_tokens
         try:
             await self.pipeline.submit(j)
         except Exception as e:  # noqa: BLE001
             log.exception("GPU pipeline failed")
             self.stats["errors"] += 1
+            if speech is not None:
+                await speech.finish()
             return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                    error=str(e))
         self.stats["utterances"] += 1
         if j.stt_failed:
+            if speech is not None:
+                await speech.finish()
             return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                    error=j.error)
         text = j.transcription.text if j.transcription else ""
         ok = None if j.queue is None else j.queue.success
         r = _result_from(text, j.multi, ok, j.transcription)
-        if self.tts is not None:
+        r.metrics = {"t": dict(j.t)}
+        if self.bridge is not None and r.success and j.multi is not None and j.multi.commands:
+            await self._bridge(r, j, ack=speech is None)
+        if speech is not None:
+            audio_b, sr = await speech.finish(r.response_text)
+            r.audio, r.audio_format, r.audio_sample_rate = audio_b, "wav", sr
+            r.audio_published = self.publisher is not None and speech.published > 0
+            if sr:
+                r.audio_duration = max(0, len(audio_b) - 44) / 2 / sr
+            m = speech.metrics()
+            r.metrics["speech"] = m
+            self.stats["progressive"] += 1
+            if m["first_audio_ms"] is not None:
+                self.stats["first_audio_ms_sum"] += m["first_audio_ms"]
+                self.stats["first_audio_n"] += 1
+        elif self.tts is not None:
             await self._speak([r])
         return r
 
+    async def _bridge(self, r: UtteranceResult, j, ack: bool) -> None:
+        """The streaming-predictive bridge on the shared decode: classification
+        from the parsed first command, the decode itself as the streaming
+        result. Its instant ack replaces the reply when speech is not already
+        streaming from the decode (the reference answers with the ack,
+        audio_service.go:641-656)."""
+        from ..streaming.parser import completed_result
+        first = j.multi.commands[0]
+        try:
+            sess = await asyncio.wait_for(
+                self.bridge.process_voice_command(r.transcription, parsed=first,
+                                                  streamed=completed_result(first)),
+                self.bridge_timeout)
+        except Exception as e:  # noqa: BLE001
+            self.stats["bridge_fallback"] += 1
+            log.info("bridge fallback: %s", e)
+            return
+        r.strategy = sess.strategy
+        self.stats["bridge_sessions"] += 1
+        if sess.predictive_response is not None:
+            self.stats["bridge_ack"] += 1
+            if ack:
+                r.response_text = sess.predictive_response.immediate_ack
+
     async def _speak(self, results: list[UtteranceResult]) -> None:
         from ..llm.tts import TTSOptions
-        opts = TTSOptions(response_format=self.tts_format)
+        opts = self.tts_options or TTSOptions(response_format=self.tts_format)
 
         async def one(r: UtteranceResult):
             if not r.response_text:
                 return
             try:
                 t = await self.tts.synthesize(r.response_text, opts)
-                r.audio, r.audio_format = t.audio, self.tts_format
+                r.audio, r.audio_format = t.audio, opts.response_format or self.tts_format
                 if t.sample_rate:
+                    r.audio_sample_rate = t.sample_rate
                     r.audio_duration = len(t.audio) / 2 / t.sample_rate
             except Exception as e:  # noqa: BLE001
                 log.warning("TTS failed: %s", e)

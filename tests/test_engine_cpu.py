@@ -483,22 +483,48 @@ def test_pipeline_continuous_stt_cpu():
 
 def test_llm_compact_weights_match_default_cpu():
     """Compact single-copy weights (fused layout only, chunked fused prefill)
-    produce the same constrained output as the default two-copy layout."""
+    compute the same model as the default two-copy layout: the logits of the
+    prompt's last position agree (the paths round to bf16 at different points,
+    so a sampled near-tie may flip later on), and the constrained outputs are
+    valid with the same structure."""
+    import json
+
     from loqa_hub_amd.engine.grammar import multi_command_schema
     from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
     from loqa_hub_amd.models.configs import llama_config
     cfg = llama_config("test-tiny")
-    outs = []
+    outs, logits = [], []
+    prompt = list(range(10, 10 + 70))
     for compact in (False, True):
         eng = LLMEngine(cfg, torch.device("cpu"), seed=4, max_seqs=4, max_seq_len=512,
                         use_graphs=False, compact=compact)
         if compact:
             assert "wqkv" not in eng.weights.layers[0] and "wqkv_f" in eng.weights.decode_layers[0]
+        r = GenRequest(prompt, [])
+        r.seq_id = eng._next_id
+        eng._next_id += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+        if compact:      # 64-token chunks through the fused decode step
+            for c0 in range(0, len(prompt), 64):
+                chunk = prompt[c0:c0 + 64]
+                max_q, max_ctx, host = eng._meta([r], [chunk], True, 1, 128 if len(chunk) > 64 else 64)
+                meta = eng._build_meta(eng._to_device(host), max_q, max_ctx, True)
+                lg = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws,
+                                                    eng.scratch)[:1]
+        else:
+            max_q, max_ctx, host = eng._meta([r], [prompt], decode=False)
+            meta = eng._build_meta(eng._to_device(host), max_q, max_ctx, False)
+            lg = eng.model.logits(eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws))
+        eng.kv.pool.free_seq(r.seq_id)
+        logits.append(lg.float())
         reqs = [GenRequest(list(range(10, 10 + 70 + 9 * i)), multi_command_schema(2, min_response_tokens=2))
                 for i in range(2)]
         eng.generate(reqs)
-        outs.append([r.output for r in reqs])
-    assert outs[0] == outs[1]
+        outs.append([json.loads(r.output) for r in reqs])
+    err = (logits[0] - logits[1]).abs().max().item()
+    assert err <= 0.02 * logits[0].abs().max().item(), err
+    for a, b in zip(*outs):
+        assert len(a["commands"]) == len(b["commands"]) == 2
 
 
 def test_step_meta_native_matches_python():

@@ -221,56 +221,32 @@ def test_stt_continuous_batching_gpu():
         assert got.tokens == want.tokens
 
 
-def test_hub_server_gpu_end_to_end(tmp_path):
+@pytest.mark.parametrize("streaming", [True, False])
+def test_hub_server_gpu_served(tmp_path, streaming):
     """The composed hub with the ON-DEVICE processor: a relay streams audio over
     real gRPC, the arbitration winner goes through the GPU pipeline (Whisper-
-    tiny encoder + decoder graphs, constrained Llama decode), the reply comes
-    back on the stream, and the voice event lands in SQLite and /api."""
-    import asyncio
-    import urllib.request
+    tiny encoder + decoder graphs, constrained Llama decode, command queue on
+    NATS), the bridge runs on that decode, the reply is spoken by on-GPU VITS -
+    progressively, phrase by phrase, when streaming is enabled - and published
+    on NATS audio.<relay>; the voice event lands in SQLite and /api."""
+    import base64
 
-    grpc = pytest.importorskip("grpc")
-    from loqa_hub_amd import config as cfgmod
-    from loqa_hub_amd.server import HubServer, build_gpu_processor
-    from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
-
-    def pcm(n=16000):
-        t = np.arange(n) / 16000.0
-        return (6000 * np.sin(2 * np.pi * 220 * t) * (1 + 0.5 * np.sin(2 * np.pi * 3 * t))).astype("<i2").tobytes()
-
-    async def relay(relay_id):
-        yield AudioChunk(relay_id=relay_id, audio_data=pcm(), sample_rate=16000, is_wake_word=True)
-        for i in range(2):
-            await asyncio.sleep(0.01)
-            yield AudioChunk(relay_id=relay_id, audio_data=pcm(), sample_rate=16000,
-                             is_end_of_speech=i == 1)
-
-    def http_get(url):
-        with urllib.request.urlopen(url, timeout=20) as r:
-            return r.status, r.read().decode()
-
-    async def go():
-        cfg = cfgmod.load({"LOQA_DB_PATH": str(tmp_path / "hub.db"), "NATS_URL": "embedded",
-                           "ARBITRATION_WINDOW_DURATION": "50ms", "HUB_STT_MODEL": "whisper-tiny",
-                           "HUB_LLM_MODEL": "test-tiny", "HUB_MAX_BATCH": "4"})
-        srv = HubServer(cfg, skills_dir=str(tmp_path / "skills"),
-                        skills_config_store=str(tmp_path / "skillcfg"))
-        await srv._connect_nats()
-        srv.processor = await asyncio.to_thread(build_gpu_processor, cfg, srv.nats, "cuda:0")
-        await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
-        try:
-            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
-                got = [r async for r in stream_audio_stub(ch)(relay("kitchen-relay"))]
-            last = got[-1]
-            assert last.command in ("voice_command_success", "no_speech", "error",
-                                    "confirmation_needed")
-            assert last.transcription is not None
-            base = f"http://127.0.0.1:{srv.http_port}"
-            st, body = await asyncio.to_thread(http_get, base + "/api/metrics")
-            assert st == 200 and "loqa_audio_processed_total 1.0" in body
-        finally:
-            await srv.stop()
-    asyncio.run(go())
+    from loqa_hub_amd.engine.grammar import INTENTS
+    from tests.test_hub_served import _served
+    got, audio, cmds, events, stats, metrics = _served(
+        tmp_path, "cuda:0", streaming=streaming, llm="test-tiny", stt="whisper-tiny",
+        tts_model="test-vits")
+    last = got[-1]
+    assert last.command == "voice_command_success" and last.success
+    assert last.transcription == "turn on the kitchen lights and then play some jazz"
+    assert len(cmds) == 2
+    assert audio and all(base64.b64decode(m["audio_data"])[:4] == b"RIFF" for m in audio)
+    ev = events[0]
+    assert ev["transcription"] == last.transcription and ev["intent"] in INTENTS
+    assert ev["intent"] == cmds[0]["intent"]
+    if streaming:
+        assert stats["progressive"] == 1 and stats["first_audio_n"] == 1
+    assert "loqa_audio_processed_total 1.0" in metrics
 
 
 def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
@@ -298,3 +274,64 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     # norm); over 22 random-weight layers that drifts ~2% - a layout or
     # indexing error would be O(1)
     assert torch.isfinite(outs[8]).all() and rel < 4e-2, rel
+
+
+def _to_cpu(obj, seen=None):
+    """Deep copy of a weights object with every tensor on the CPU."""
+    import copy
+    if torch.is_tensor(obj):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    if hasattr(obj, "__dict__") and not isinstance(obj, type) and \
+            not getattr(type(obj), "__dataclass_params__", None):
+        c = copy.copy(obj)
+        c.__dict__ = {k: _to_cpu(v) for k, v in obj.__dict__.items()}
+        return c
+    return obj       # configs (frozen dataclasses), scalars
+
+
+def test_vits_gpu_matches_fp32_reference():
+    """Full VITS on the HIP kernels vs the fp32 PyTorch reference (ops/reference.py
+    path on the CPU) with the SAME weights, stage by stage: text encoder
+    statistics, durations, the reverse flow and the HiFi-GAN waveform."""
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    from loqa_hub_amd.models.vits import VitsModel, VitsWeights, text_to_ids
+    cfg = VITS_CONFIGS["test-vits"]
+    gw = VitsWeights(cfg, "cuda", seed=3)
+    gm, cm = VitsModel(gw), VitsModel(_to_cpu(gw))
+    texts = ["Turning on the kitchen lights.", "Playing some jazz now."]
+    ids = [text_to_ids(t, cfg.n_symbols) for t in texts]
+    T = max(len(i) for i in ids)
+    arr = torch.zeros(len(ids), T, dtype=torch.int64)
+    for b, i in enumerate(ids):
+        arr[b, :len(i)] = torch.tensor(i)
+    lens = torch.tensor([len(i) for i in ids], dtype=torch.int32)
+
+    def rel(a, b):
+        a, b = a.float().cpu(), b.float().cpu()
+        return float((a - b).norm() / b.norm().clamp_min(1e-6))
+    with torch.inference_mode():
+        sg, xg = gm.encode_text(arr.cuda(), lens.cuda())
+        sc, xc = cm.encode_text(arr, lens)
+        assert rel(sg, sc) < 3e-2 and rel(xg, xc) < 3e-2, (rel(sg, sc), rel(xg, xc))
+        dg, dc = gm.durations(xg, lens.cuda(), 1.0).cpu(), cm.durations(xc, lens, 1.0)
+        assert (dg == dc).float().mean() >= 0.9
+        # the same latent through the reverse flow and the vocoder on both paths
+        cum = torch.cumsum(dc, dim=1, dtype=torch.int32)
+        flen = cum[:, -1].contiguous()
+        F = int(flen.max())
+        z = torch.randn(len(ids), F, cfg.inter_channels, generator=torch.Generator().manual_seed(0))
+        z = (z * 0.5).to(torch.bfloat16)
+        zg, zc = gm.flow_reverse(z.cuda(), flen.cuda()), cm.flow_reverse(z, flen)
+        assert rel(zg, zc) < 5e-2, rel(zg, zc)
+        hop = 1
+        for r in cfg.upsample_rates:
+            hop *= r
+        pg = gm.decode(zc.cuda(), (flen * hop).to(torch.int32).cuda()).float().cpu()
+        pc = cm.decode(zc, (flen * hop).to(torch.int32)).float()
+        assert pg.shape == pc.shape
+        assert rel(pg, pc) < 0.1, rel(pg, pc)
+        assert pc.abs().mean() > 50

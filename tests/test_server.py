@@ -83,7 +83,8 @@ def test_hub_server_end_to_end(tmp_path):
                 got = [r async for r in stream_audio_stub(ch)(relay("kitchen-relay"))]
             last = got[-1]
             assert last.success and last.transcription == "turn on the lights and turn off the fan"
-            assert last.response_text == "Turning on the lights and turning off the fan"
+            # the first command's response, as audio_service.go:687-689
+            assert last.response_text == "Lights on"
             st, body = await asyncio.to_thread(http_get, base + "/api/voice-events")
             ev = json.loads(body)
             assert ev["total"] == 1 and ev["events"][0]["relay_id"] == "kitchen-relay"
