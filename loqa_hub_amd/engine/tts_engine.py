@@ -12,6 +12,7 @@ import asyncio
 import io
 import struct
 import threading
+import time
 
 import numpy as np
 import torch
@@ -41,7 +42,7 @@ class VitsTTSEngine:
         self._flusher: asyncio.Task | None = None
         self._gpu_lock = threading.Lock()
         self._seed = seed
-        self.stats = {"batches": 0, "phrases": 0, "samples": 0}
+        self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0}
 
     # ---------------------------------------------------------------- batch
     def synthesize_batch(self, texts: list[str], speeds: list[float] | None = None
@@ -57,10 +58,12 @@ class VitsTTSEngine:
         # one length scale per batch (the engine groups by speed upstream)
         ls = 1.0 / max(1e-3, float(np.mean(speeds)))
         with self._gpu_lock, torch.inference_mode():
+            t0 = time.perf_counter()
             self._seed += 1
             pcm, n = self.model.synthesize(torch.from_numpy(arr).to(self.device), lens,
                                            seed=self._seed, length_scale=ls)
             pcm, n = pcm.cpu().numpy(), n.cpu().numpy()
+            self.stats["gpu_s"] += time.perf_counter() - t0   # launch to result on the host
         self.stats["batches"] += 1
         self.stats["phrases"] += len(texts)
         self.stats["samples"] += int(n.sum())

@@ -9,12 +9,19 @@
               decode; first-token latency, streamed tokens/s, ms per added
               command; every 4th utterance runs with NATS publishes failing
               at random (p = 0.5) so the queue's rollback path executes.
-  --config 5  Whisper-large-v3 + Llama-3-70B + VITS TTS of every reply, on ONE
-              GPU at TP=1: compact single-copy weights (fused decode layout,
-              chunked fused prefill), so 70B bf16 = 141 GB fits in 288 GB
-              HBM3E (the TP=8 path is exercised by tests/test_tp.py): 8
-              closed-loop streams, utterances/s, ms per added command, TTS
-              time per reply.
+  --config 5  Whisper-large-v3 + Llama-3-70B + progressive VITS speech of every
+              reply. --tp 1: ONE GPU, compact single-copy weights (fused
+              decode layout, chunked fused prefill: 70B bf16 = 141 GB fits in
+              288 GB HBM3E). --tp N: the config's own layout, one process per
+              GPU under torchrun (rank 0: hub pipeline + TP leader, ranks
+              1..N-1: followers; parallel/tp_serving.py):
+                torchrun --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+                  --master-port 29533 scripts/bench_configs.py --config 5 --tp 8
+              --share-gpu N rehearses that layout with N ranks on cuda:0 (a
+              1-GPU box: correct, not a timing of the xGMI links). 8 closed-loop
+              streams, utterances/s, ms per added command, first-phrase audio
+              latency (phrases are spoken while the decode runs) and the TTS
+              share of the wall time.
 
 Synthetic speech-like audio, random-init weights (teacher-forced STT,
 grammar-constrained LLM) as in bench.py. Prints one JSON line per config.
@@ -71,16 +78,51 @@ def _lat(jobs, key="queue_done"):
     return [(j.t[key] - j.t["start"]) * 1e3 for j in jobs if key in j.t]
 
 
-def config_2_or_5(cfg_id: int, args, dev, nats) -> dict:
+def _progressive_loop(pipe, utts, streams: int, per_stream: int, tts):
+    """Closed-loop clients whose replies are spoken progressively from the
+    live decode (streaming/progressive.py) - the config-5 serving path."""
+    from loqa_hub_amd.streaming.audio_pipeline import StreamingAudioPipeline
+    from loqa_hub_amd.streaming.progressive import ProgressiveSpeech
+    speech_pipe = StreamingAudioPipeline(tts)
+    jobs, speech = [], []
+
+    async def client(ci):
+        for k in range(per_stream):
+            u = utts[(ci * per_stream + k) % len(utts)]
+            j = PipelineJob(u.relay_id, f"c{ci}-{k}", u.pcm, transcript_hint=u.text)
+            sp = ProgressiveSpeech(u.relay_id, pipe.llm.tok, speech_pipe, None)
+            j.on_tokens = sp.on_tokens
+            j.t["start"] = sp.t_start = time.perf_counter()
+            await pipe.submit(j)
+            await sp.finish(j.multi.commands[0].response if j.multi and j.multi.commands else "")
+            j.t["tts_done"] = time.perf_counter()
+            jobs.append(j)
+            speech.append(sp)
+
+    async def main():
+        t0 = time.perf_counter()
+        await asyncio.gather(*[client(c) for c in range(streams)])
+        return time.perf_counter() - t0
+    wall = asyncio.get_event_loop().run_until_complete(main())
+    return jobs, wall, speech
+
+
+def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
     if cfg_id == 2:
         stt_name, llm_name, streams = "whisper-base", "tinyllama", 1
     else:
         stt_name, llm_name, streams = "whisper-large-v3", "llama3-70b", 8
     t0 = time.perf_counter()
     stt = STTEngine(whisper_config(stt_name), dev, seed=0, max_batch=8)
-    # 70B at TP=1: one weight copy in the fused decode layout (141 GB)
-    llm = LLMEngine(llama_config(llm_name), dev, seed=0, max_seqs=8, max_seq_len=1024,
-                    compact=llm_name == "llama3-70b")
+    tp = tp_info.world if tp_info is not None else 1
+    if tp > 1:
+        from loqa_hub_amd.parallel.tp_serving import build_tp_llm
+        llm = build_tp_llm(llama_config(llm_name), tp_info, seed=0, max_seqs=8, max_seq_len=1024,
+                           compact=args.compact)
+    else:
+        # 70B at TP=1: one weight copy in the fused decode layout (141 GB)
+        llm = LLMEngine(llama_config(llm_name), dev, seed=0, max_seqs=8, max_seq_len=1024,
+                        compact=llm_name == "llama3-70b")
     pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=8)
     pipe.warmup()
     tts = None
@@ -89,17 +131,25 @@ def config_2_or_5(cfg_id: int, args, dev, nats) -> dict:
         tts = VitsTTSEngine(vits_config("vits-ljs"), dev, seed=0)
     init_s = time.perf_counter() - t0
     utts = make_batch(0, 16, [1, 2, 3, 4])
-    _closed_loop(pipe, utts, streams, args.warmup, tts)           # warm-up
-    s0 = dict(llm.stats)
-    per_stream = args.per_stream * (4 if streams == 1 else 1)
-    jobs, wall, tts_s = _closed_loop(pipe, utts, streams, per_stream, tts)
+    speech = []
+    if tts is not None:
+        _progressive_loop(pipe, utts, streams, args.warmup, tts)          # warm-up
+        s0, t0s = dict(llm.stats), dict(tts.stats)
+        per_stream = args.per_stream
+        jobs, wall, speech = _progressive_loop(pipe, utts, streams, per_stream, tts)
+    else:
+        _closed_loop(pipe, utts, streams, args.warmup)           # warm-up
+        s0 = dict(llm.stats)
+        per_stream = args.per_stream * (4 if streams == 1 else 1)
+        jobs, wall, _ = _closed_loop(pipe, utts, streams, per_stream)
     st = added_command_stats(jobs)
     lat = _lat(jobs, "tts_done" if tts is not None else "queue_done")
     stt_ms = [(j.t["stt_done"] - j.t["start"]) * 1e3 for j in jobs]
     steps = llm.stats["decode_steps"] - s0["decode_steps"]
-    return {
+    out = {
         "config": cfg_id, "model": f"{stt_name} + {llm_name}" + (" + vits-ljs" if tts else ""),
-        "n_gpus": 1, "tp": 1, "streams": streams, "utterances": len(jobs), "dtype": "bf16",
+        "n_gpus": tp, "tp": tp, "streams": streams, "utterances": len(jobs), "dtype": "bf16",
+        "share_gpu": bool(args.share_gpu),
         "utterances_per_s": round(len(jobs) / wall, 3),
         "latency_ms_p50": round(float(np.median(lat)), 1),
         "latency_ms_p90": round(float(np.percentile(lat, 90)), 1),
@@ -108,12 +158,30 @@ def config_2_or_5(cfg_id: int, args, dev, nats) -> dict:
         else round(st["e2e_marginal_ms_per_added_command"], 2),
         "ms_per_added_command_ref_equiv": st["ref_equiv_ms_per_added_command"],
         "llm_ms_per_decode_step": round((llm.stats["decode_s"] - s0["decode_s"]) / max(1, steps) * 1e3, 3),
-        "tts_ms_mean": round(float(np.mean(tts_s)) * 1e3, 1) if tts_s else None,
         "command_count_match": float(np.mean([j.n_commands == j.n_expected for j in jobs])),
         "init_s": round(init_s, 1),
         "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v) for k, v in ops._FSPLITS.items()},
         "data": "synthetic speech-like PCM16 + random-init weights (teacher-forced STT)",
     }
+    if speech:
+        fa = [sp.t_first_audio - sp.t_start for sp in speech if sp.t_first_audio]
+        before = [sp.t_first_audio < j.t["llm_done"] for sp, j in zip(speech, jobs)
+                  if sp.t_first_audio and "llm_done" in j.t]
+        tts_s = tts.stats.get("gpu_s", 0.0) - t0s.get("gpu_s", 0.0)
+        out.update({
+            "first_phrase_audio_ms_p50": round(float(np.median(fa)) * 1e3, 1) if fa else None,
+            "first_phrase_audio_ms_p90": round(float(np.percentile(fa, 90)) * 1e3, 1) if fa else None,
+            "first_audio_before_decode_done": round(float(np.mean(before)), 3) if before else None,
+            "phrases_per_reply": round(float(np.mean([len(sp.chunks) for sp in speech])), 2),
+            "tts_batches": tts.stats["batches"] - t0s["batches"],
+            "tts_share_of_wall": round(tts_s / wall, 4),
+        })
+    if tp > 1:
+        llm.stop()
+        car = llm.tp.car
+        out["tp_collective_calls"] = car.calls if car is not None else None
+        out["tp_collective_error"] = bool(car.error()) if car is not None else None
+    return out
 
 
 def config_3(args, dev, nats) -> dict:
@@ -169,12 +237,66 @@ def config_3(args, dev, nats) -> dict:
     }
 
 
+def _tp_rank_main(args) -> int:
+    """Rank body of ``--config 5 --tp N`` (torchrun or --share-gpu)."""
+    from loqa_hub_amd.parallel.tp_serving import init_tp, run_follower
+    info = init_tp(args.tp)
+    if args.share_gpu:
+        info.device = torch.device("cuda", 0)
+        torch.cuda.set_device(0)
+    if info.rank != 0:
+        from loqa_hub_amd.parallel.tp_serving import build_tp_llm
+        eng = build_tp_llm(llama_config("llama3-70b"), info, seed=0, max_seqs=8, max_seq_len=1024,
+                           compact=args.compact)
+        run_follower(eng)
+        return 0
+    from loqa_hub_amd.messaging.nats_server import NATSServer
+    from loqa_hub_amd.messaging.nats_service import NATSService
+    loop = asyncio.new_event_loop()
+    asyncio.set_event_loop(loop)
+    srv = loop.run_until_complete(NATSServer("127.0.0.1", 0).start())
+    nats = NATSService(srv.url)
+    loop.run_until_complete(nats.connect())
+    res = config_2_or_5(5, args, info.device, nats, tp_info=info)
+    print(json.dumps(res), flush=True)
+    loop.run_until_complete(nats.close())
+    loop.run_until_complete(srv.stop())
+    return 0
+
+
+def _share_gpu_worker(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + argv
+    main()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--config", type=int, nargs="+", default=[2, 3])
     ap.add_argument("--per-stream", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=1, help="config 5: tensor-parallel degree")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="TP ranks share cuda:0 (spawned here when not under torchrun)")
+    ap.add_argument("--compact", action="store_true",
+                    help="TP: single-copy fused weights (needed when ranks share a GPU)")
     args = ap.parse_args()
+    if args.tp > 1:
+        if args.config != [5]:
+            ap.error("--tp applies to --config 5 only")
+        if args.share_gpu and "WORLD_SIZE" not in os.environ:
+            # spawn the ranks before this process touches the GPU
+            import socket
+
+            import torch.multiprocessing as mp
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            mp.start_processes(_share_gpu_worker, args=(args.tp, port, sys.argv[1:]),
+                               nprocs=args.tp, join=True, start_method="spawn")
+            return 0
+        return _tp_rank_main(args)
     from loqa_hub_amd.messaging.nats_server import NATSServer
     from loqa_hub_amd.messaging.nats_service import NATSService
     dev = torch.device("cuda", 0)
