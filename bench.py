@@ -15,6 +15,18 @@ One step = every rank processes its batch of B utterances end to end:
 Prints ONE JSON line (rank 0). ``value`` = utterances/s over all GPUs;
 ms-per-added-command (both BASELINE.md definitions) is reported alongside.
 Random-init weights, synthetic speech-like audio (no network / checkpoints).
+
+Modes: ``closed`` (default, the headline): B closed-loop streams per GPU
+submit straight into the voice pipeline. ``hub``: the SERVED path - a
+``HubServer`` per GPU with B simulated relays streaming PCM16 chunks over
+real gRPC, per-relay-group arbitration (window ``--window-ms``; the
+reference's is 300 ms), the GPU voice processor, voice-event writes to
+SQLite and the command queue on NATS. ``batch``: lockstep batches of B.
+
+``--gpus N`` must match the launch: under torchrun WORLD_SIZE must equal N
+(else exit 2); without torchrun and N > 1 the bench launches
+``torch.distributed.run`` itself (before touching the GPU) and exits with its
+status.
 """
 from __future__ import annotations
 
@@ -77,6 +89,42 @@ def start_broker() -> tuple[int, threading.Thread]:
     return box["port"], t
 
 
+async def _start_hub(args, pipe, nats_port: int, info):
+    """The served hub of --mode hub on this rank's GPU pipeline."""
+    import tempfile
+
+    from loqa_hub_amd import config as cfgmod
+    from loqa_hub_amd.server import HubServer, build_bridge
+    from loqa_hub_amd.transport.voice_processor import GPUVoiceProcessor
+    db = os.path.join(tempfile.mkdtemp(prefix="loqa-bench-"), "hub.db")
+    cfg = cfgmod.load({"LOQA_DB_PATH": db, "NATS_URL": f"nats://127.0.0.1:{nats_port}",
+                       "ARBITRATION_SCOPE": "per_relay_group",
+                       "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms"})
+    hints: dict[str, str] = {}
+    srv = HubServer(cfg, skills_dir=os.path.join(os.path.dirname(db), "skills"),
+                    skills_config_store=os.path.join(os.path.dirname(db), "skillcfg"),
+                    transcript_hints=hints.get)
+    await srv._connect_nats()
+    srv.processor = GPUVoiceProcessor(pipe, max_batch=pipe.max_batch,
+                                      bridge=build_bridge(srv.skills), batch_window=0.002)
+    await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
+    return srv, hints
+
+
+def relaunch(n: int, argv: list[str]) -> int:
+    """``--gpus N`` without torchrun: run this bench under torch.distributed.run
+    with N ranks (a child process; nothing here has touched the GPU)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+           *argv]
+    return subprocess.call(cmd)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,9 +139,12 @@ def main(argv=None) -> int:
     ap.add_argument("--mix", default="1,2,3,4", help="commands per utterance, cycled")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--mode", choices=["closed", "batch"], default="closed",
+    ap.add_argument("--mode", choices=["closed", "hub", "batch"], default="closed",
                     help="closed: B concurrent closed-loop streams per GPU (continuous batching); "
+                         "hub: B simulated relays per GPU over gRPC into the served hub; "
                          "batch: lockstep batches of B")
+    ap.add_argument("--window-ms", type=float, default=300.0,
+                    help="--mode hub: arbitration window (the reference's 300 ms)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="--mode batch: batches in flight (2: next batch's STT overlaps the decode)")
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
@@ -101,6 +152,13 @@ def main(argv=None) -> int:
                     help="HIP stream priority of the STT worker (-1 high, 0 normal)")
     args = ap.parse_args(argv)
 
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return relaunch(args.gpus, sys.argv[1:] if argv is None else list(argv))
+    if int(world_env or "1") != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: launch one rank per "
+              f"GPU (torchrun --nproc-per-node {args.gpus})", file=sys.stderr)
+        return 2
     if args.cpu_smoke:
         args.stt, args.llm = "test-whisper", "test-tiny"
     # event bus: one NATS broker for the node (rank 0 starts it), every rank
@@ -180,7 +238,7 @@ def main(argv=None) -> int:
     # timed rounds; each stream's command count cycles through the mix
     n_per_stream = args.warmup + args.steps
     uniq = []
-    if args.mode == "closed":
+    if args.mode in ("closed", "hub"):
         counts = [mix[(ci + k) % len(mix)] for ci in range(B) for k in range(n_per_stream)]
         uniq = make_unique(args.seed, counts, offset=info.rank * B * n_per_stream)
 
@@ -207,7 +265,48 @@ def main(argv=None) -> int:
 
     recs_local: list[list[float]] = []
 
+    hub = None
+    if args.mode == "hub":
+        hub = loop.run_until_complete(_start_hub(args, pipe, port, info))
+
+    async def run_hub(n: int, record: bool) -> None:
+        """--mode hub: B relays per GPU, each a closed loop of gRPC StreamAudio
+        calls (wake-word chunk, 100 ms speech chunks, end of speech) into the
+        served hub; latency = first chunk sent -> response received."""
+        import grpc
+
+        from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
+        srv, hints = hub
+
+        async def client(ci: int, ch) -> None:
+            call = stream_audio_stub(ch)
+            for k in range(n):
+                u = next_utt(ci, k, record)
+                relay = f"relay-{info.rank}-{ci}"
+                hints[relay] = u.text
+                data = np.ascontiguousarray(u.pcm, dtype="<i2").tobytes()
+                wake, rest = data[:9600], data[9600:]
+                step_b = 3200
+
+                async def chunks():
+                    yield AudioChunk(relay_id=relay, audio_data=wake, sample_rate=16000,
+                                     is_wake_word=True)
+                    for o in range(0, max(len(rest), 1), step_b):
+                        yield AudioChunk(relay_id=relay, audio_data=rest[o:o + step_b],
+                                         sample_rate=16000,
+                                         is_end_of_speech=o + step_b >= len(rest))
+                t_s = time.perf_counter()
+                got = [r async for r in call(chunks())]
+                lat = (time.perf_counter() - t_s) * 1e3
+                ok = bool(got) and got[-1].success
+                if record:
+                    recs_local.append([u.n_commands, u.n_commands, float(ok), lat])
+        async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
+            await asyncio.gather(*[client(ci, ch) for ci in range(B)])
+
     def run(n: int, record: bool):
+        if args.mode == "hub":
+            return run_hub(n, record)
         return run_closed(n, record) if args.mode == "closed" else run_batches(n, record)
 
     loop.run_until_complete(run(args.warmup, False))
@@ -222,9 +321,22 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
 
-    if args.mode == "closed" and recs_local:
+    if args.mode in ("closed", "hub") and recs_local:
         step.records.append(gather_records(info, torch.tensor(recs_local, dtype=torch.float64)).cpu())
     stats = added_command_stats(all_jobs)
+    hub_stats = None
+    if hub is not None:
+        # served path: per-utterance latency at the relay vs its command count
+        r = np.array(recs_local, dtype=np.float64)
+        slope = float(np.polyfit(r[:, 0], r[:, 3], 1)[0]) if len(set(r[:, 0])) >= 2 else None
+        stats["e2e_marginal_ms_per_added_command"] = slope
+        srv = hub[0]
+        from loqa_hub_amd.storage.voice_events_store import ListOptions
+        hub_stats = {"voice_events": srv.events.count(ListOptions()),
+                     "audio_service": dict(srv.audio_service.stats),
+                     "processor": dict(srv.processor.stats),
+                     "latency_ms_p50": round(float(np.median(r[:, 3])), 1),
+                     "window_ms": args.window_ms}
     def _mean_ms(a, b):
         v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
         return round(float(np.mean(v)) * 1e3, 2) if v else None
@@ -276,11 +388,14 @@ def main(argv=None) -> int:
             "phase_ms_per_step": phase_ms,
             "llm_stats": llm.stats,
             "stt_stats": stt.stats,
+            "hub": hub_stats,
             "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v)
                                   for k, v in __import__("loqa_hub_amd.ops", fromlist=["_FSPLITS"])._FSPLITS.items()},
             "init_s": round(t_init, 2),
         }
         print(json.dumps(out), flush=True)
+    if hub is not None:
+        loop.run_until_complete(hub[0].stop())
     loop.run_until_complete(nats.close())
     pdist.shutdown(info)
     if broker is not None:

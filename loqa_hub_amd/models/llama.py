@@ -177,7 +177,7 @@ class LlamaWeights:
     def _finalize(self) -> None:
         """Derived decode copies + split-K tuning (after the base tensors exist)."""
         if getattr(self, "compact", False):
-            self.lm_head_p = ops.shuffle_weight(self.lm_head)
+            self.lm_head_p = self._shuffle_lm_head()
             if not self.cfg.tie_embeddings:
                 del self.lm_head          # only the shuffled copy is read
             self.fused = True
@@ -191,12 +191,22 @@ class LlamaWeights:
         self.decode_layers = [{k: ops.shuffle_weight(L[k])
                                for k in ("wqkv", "wo", "w_gate_up", "w_down")}
                               for L in self.layers]
-        self.lm_head_p = ops.shuffle_weight(self.lm_head)
+        self.lm_head_p = self._shuffle_lm_head()
         self._add_fused_copies()
         if self.embed.device.type == "cuda":
             for k in ("wqkv", "wo", "w_gate_up", "w_down"):
                 ops.tune_skinny_splits(self.decode_layers[0][k])
             ops.tune_skinny_splits(self.lm_head_p)
+
+    def _shuffle_lm_head(self):
+        """Decode copy of the (vocab-shard) lm_head, rows zero-padded to a
+        multiple of 64 (the skinny GEMM's 64-row tiles at Mpad 64/128; a TP=8
+        Llama-3 shard has 16032 rows); ``LlamaModel`` slices the padding off."""
+        w = self.lm_head
+        pad = -w.shape[0] % 64
+        if pad:
+            w = torch.cat([w, torch.zeros(pad, w.shape[1], dtype=w.dtype, device=w.device)])
+        return ops.shuffle_weight(w.contiguous())
 
     @classmethod
     def from_tensors(cls, cfg: LlamaConfig, device, *, embed, layers: list[dict], final_norm,
@@ -411,7 +421,8 @@ class LlamaModel:
             tp.all_reduce_(down)
         hf = ops.slab_rmsnorm(down, residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx,
                               write_residual=False)
-        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
+        return ops.skinny_gemm(hf, w.lm_head_p, 1,
+                               max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
 
     def forward_decode_fused(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
                              attn_ws: ops.AttnWorkspace | None, scratch: ops.FusedScratch,
@@ -471,7 +482,8 @@ class LlamaModel:
             hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
         else:
             hf = ops.rmsnorm(residual.index_select(0, meta.logit_idx), w.final_norm, cfg.norm_eps)
-        return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
+        return ops.skinny_gemm(hf, w.lm_head_p, 1,
+                               max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """Local vocab shard logits [B, V/tp] (bf16)."""

@@ -257,6 +257,32 @@ def test_bench_cpu_smoke_dp4_gloo():
     assert out["command_count_match_rate"] == 1.0
 
 
+def test_bench_gpus_guard():
+    """--gpus must match the launch: a torchrun job of the wrong size exits 2;
+    without torchrun, --gpus 2 relaunches the bench under torch.distributed.run."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, "bench.py", "--cpu-smoke", "--gpus", "2", "--steps", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--cpu-smoke", "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--batch-per-gpu", "2"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+
+
+def test_bench_cpu_smoke_hub_mode():
+    """--mode hub: relays over gRPC into the served hub (arbitration, bridge,
+    voice events) on the same pipeline."""
+    out = _run([sys.executable, "bench.py", "--cpu-smoke", "--mode", "hub", "--steps", "1",
+                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "10"])
+    assert out["config"]["mode"] == "hub" and out["queue_success_rate"] == 1.0
+    assert out["hub"]["voice_events"] == 2 and out["hub"]["audio_service"]["processed"] == 2
+
+
 def test_whisper_fast_decode_matches_eager_cpu():
     """The skinny-GEMM/slab decode path equals the eager reference decoder
     (first step with the 4 SOT tokens and a follow-up 1-token step)."""
