@@ -43,6 +43,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from loqa_hub_amd import ops  # noqa: E402
 from loqa_hub_amd.engine.llm_engine import LLMEngine  # noqa: E402
 from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline, added_command_stats  # noqa: E402
 from loqa_hub_amd.engine.stt_engine import STTEngine  # noqa: E402
@@ -362,7 +363,8 @@ def main(argv=None) -> int:
     ref = pdist.max_over_ranks(info, ref if ref is not None else -1.0)
     if info.is_main:
         out = {
-            "metric": "utterances_per_sec (multi-command utterances; ms per added command reported alongside)",
+            "metric": ("utterances_per_sec (multi-command utterances; ms per added command "
+                       "reported alongside)"),
             "value": round(value, 3),
             "unit": "utterances/s",
             "n_gpus": info.world,
@@ -373,7 +375,9 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic speech-like PCM16, every utterance a distinct transcript (no repeated prompts) + random-init weights (teacher-forced STT, grammar-constrained LLM)",
+            "data": ("synthetic speech-like PCM16, every utterance a distinct transcript (no "
+                     "repeated prompts) + random-init weights (teacher-forced STT, "
+                     "grammar-constrained LLM)"),
             "config": {"model": f"{args.stt} + {args.llm}", "global_batch": info.world * B,
                        "seq_len": 1500, "parallelism": f"dp{info.world}",
                        "commands_mix": mix, "baseline_config": 4, "mode": args.mode,
@@ -382,7 +386,8 @@ def main(argv=None) -> int:
             "ms_per_added_command_e2e_marginal": None if e2e < 0 else round(e2e, 3),
             "ms_per_added_command_ref_equiv": None if ref < 0 else round(ref, 4),
             "baseline_ms_per_added_command": BASELINE_MS_PER_ADDED_COMMAND,
-            "added_command_speedup_vs_baseline": None if e2e <= 0 else round(BASELINE_MS_PER_ADDED_COMMAND / e2e, 3),
+            "added_command_speedup_vs_baseline": (None if e2e <= 0 else
+                                                  round(BASELINE_MS_PER_ADDED_COMMAND / e2e, 3)),
             "queue_success_rate": round(ok, 4),
             "command_count_match_rate": round(cmd_match, 4),
             "phase_ms_per_step": phase_ms,
@@ -390,7 +395,7 @@ def main(argv=None) -> int:
             "stt_stats": stt.stats,
             "hub": hub_stats,
             "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v)
-                                  for k, v in __import__("loqa_hub_amd.ops", fromlist=["_FSPLITS"])._FSPLITS.items()},
+                                  for k, v in ops._FSPLITS.items()},
             "init_s": round(t_init, 2),
         }
         print(json.dumps(out), flush=True)

@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <random>
 #include <thread>
+#include <unistd.h>
+#include <cstring>
 #include <vector>
 
 extern "C" {
@@ -21,6 +23,11 @@ int loqa_pool_cache_prefix(void* h, long long seq_id, const int32_t* toks, int n
 int loqa_pool_block_table(void* h, long long seq_id, int32_t* out, int max_blocks);
 long long loqa_pool_seq_len(void* h, long long seq_id);
 int loqa_pool_free_seq(void* h, long long seq_id);
+void* loqa_tpctl_open(const char* name, int rank, int world, int nslots, long long slot_bytes);
+void loqa_tpctl_unlink(void* h);
+int loqa_tpctl_publish(void* h, const void* data, long long n, int stop, long long timeout_us);
+long long loqa_tpctl_recv(void* h, void* buf, long long cap, int* stop, long long timeout_us);
+void loqa_tpctl_close(void* h);
 }
 
 int main() {
@@ -64,5 +71,50 @@ int main() {
   }
   loqa_pool_destroy(pool);
   std::printf("pool_stress: %d errors\n", errors.load());
+
+  // TP lock-step control ring: one leader thread publishes records of varying
+  // size (some larger than a slot: continuation chunks) through a ring of 4
+  // slots, three follower threads must see every record, in order, intact.
+  {
+    const int W = 4, RECS = 3000, SLOT = 256;
+    char name[64];
+    std::snprintf(name, sizeof name, "/loqa_tpctl_stress_%d", (int)getpid());
+    void* lead = loqa_tpctl_open(name, 0, W, 4, SLOT);
+    if (!lead) { std::printf("tpctl: open failed\n"); return 1; }
+    std::vector<void*> fol(W, nullptr);
+    for (int r = 1; r < W; ++r) fol[r] = loqa_tpctl_open(name, r, W, 4, SLOT);
+    loqa_tpctl_unlink(lead);
+    std::atomic<int> ring_errors{0};
+    auto payload = [](int i, std::vector<unsigned char>& v) {
+      v.resize((size_t)((i * 37) % 900));
+      for (size_t k = 0; k < v.size(); ++k) v[k] = (unsigned char)(i * 31 + k);
+    };
+    std::vector<std::thread> fs;
+    for (int r = 1; r < W; ++r)
+      fs.emplace_back([&, r] {
+        std::vector<unsigned char> buf(4096), want;
+        for (int i = 0;; ++i) {
+          int stop = 0;
+          const long long n = loqa_tpctl_recv(fol[r], buf.data(), (long long)buf.size(), &stop,
+                                              10000000);
+          if (n < 0) { ++ring_errors; return; }
+          if (stop) { if (i != RECS) ++ring_errors; return; }
+          payload(i, want);
+          if ((size_t)n != want.size() || (n && std::memcmp(buf.data(), want.data(), want.size())))
+            ++ring_errors;
+        }
+      });
+    std::vector<unsigned char> v;
+    for (int i = 0; i < RECS; ++i) {
+      payload(i, v);
+      if (loqa_tpctl_publish(lead, v.data(), (long long)v.size(), 0, 10000000) != 0) ++ring_errors;
+    }
+    loqa_tpctl_publish(lead, nullptr, 0, 1, 10000000);
+    for (auto& t : fs) t.join();
+    for (int r = 1; r < W; ++r) loqa_tpctl_close(fol[r]);
+    loqa_tpctl_close(lead);
+    std::printf("tpctl_stress: %d errors\n", ring_errors.load());
+    errors += ring_errors.load();
+  }
   return errors.load() == 0 ? 0 : 1;
 }

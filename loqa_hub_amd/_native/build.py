@@ -104,7 +104,7 @@ def build_sanitized(kind: str = "address,undefined", out_dir: str | None = None)
         raise RuntimeError("no host C++ compiler")
     cmd = [cxx, "-std=c++17", "-O1", "-g", f"-fsanitize={kind}", "-fno-omit-frame-pointer",
            "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-Wno-unused-result",
-           os.path.join(CSRC, "runtime", "runtime.cpp"),
+           os.path.join(CSRC, "runtime", "runtime.cpp"), os.path.join(CSRC, "runtime", "tp_control.cpp"),
            os.path.join(CSRC, "runtime", "tests", "pool_stress.cpp"),
            "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath,/opt/rocm/lib", "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)

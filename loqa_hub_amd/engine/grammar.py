@@ -166,7 +166,8 @@ class GrammarTables:
 
     def mask_table(self, device=None) -> torch.Tensor:
         device = device or self.device
-        if self._gpu is None or self._gpu.shape[0] != len(self._rows) or self._gpu.device != torch.device(device or "cpu"):
+        want = torch.device(device or "cpu")
+        if self._gpu is None or self._gpu.shape[0] != len(self._rows) or self._gpu.device != want:
             self._gpu = pack_mask(torch.stack(self._rows)).to(device or "cpu")
         return self._gpu
 

@@ -99,7 +99,8 @@ class STTEngine:
         self.use_graphs = use_graphs and self.is_gpu and fast_decode
         self.self_splits = (cfg.n_text_ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS
         # cross-attention keys per split (the workspace holds n_audio_ctx / 128 splits)
-        self.cross_split_keys = max(self.SPLIT_KEYS, int(os.environ.get("LOQA_XATTN_SPLIT_KEYS", "256")) // 32 * 32)
+        self.cross_split_keys = max(self.SPLIT_KEYS,
+                                    int(os.environ.get("LOQA_XATTN_SPLIT_KEYS", "256")) // 32 * 32)
         if fast_decode and self.is_gpu:
             self.ws = ops.AttnWorkspace(self.device, 128, cfg.n_heads, cfg.head_dim,
                                         max(self.self_splits, (cfg.n_audio_ctx + self.SPLIT_KEYS - 1)
@@ -555,7 +556,8 @@ class STTEngine:
         # the running decoder batch (an arrival's encode no longer stalls every
         # live transcription); requests join at the next step boundary after
         # their encoder output and cross-attention K|V are complete
-        enc_pool = self._encoder_executor() if (self.is_gpu and os.environ.get("LOQA_OVERLAP_ENCODER", "1") != "0") else None
+        overlap = self.is_gpu and os.environ.get("LOQA_OVERLAP_ENCODER", "1") != "0"
+        enc_pool = self._encoder_executor() if overlap else None
         while self._running:
             idle = not live and not waiting and not encoding
             items = [self._inbox.get()] if idle else []

@@ -121,7 +121,8 @@ class NATSServer:
             self._deliver(c, sid, subj, reply, payload)
 
     def _deliver(self, c: _Client, sid: str, subj: str, reply: str | None, payload: bytes) -> None:
-        hdr = f"MSG {subj} {sid} {reply} {len(payload)}\r\n" if reply else f"MSG {subj} {sid} {len(payload)}\r\n"
+        hdr = (f"MSG {subj} {sid} {reply} {len(payload)}\r\n" if reply
+               else f"MSG {subj} {sid} {len(payload)}\r\n")
         try:
             c.w.write(hdr.encode() + payload + b"\r\n")
             self.msgs_routed += 1

@@ -89,7 +89,8 @@ class WhisperWeights:
             ops.tune_skinny_splits(self.lm_head_p, mpads=(16, 32))
             F = self.dec_f[0]
             MP = (16, 32, 64)   # a Whisper decoder step never exceeds 64 tokens
-            ops.tune_fused(F["qkv"], "rope", heads=(cfg.n_heads, cfg.n_heads, cfg.head_dim), mpads=MP, xl=False)
+            ops.tune_fused(F["qkv"], "rope", heads=(cfg.n_heads, cfg.n_heads, cfg.head_dim), mpads=MP,
+                           xl=False)
             ops.tune_fused(F["o"], "resid", mpads=MP, xl=False)
             ops.tune_fused(F["xq"], "act", mpads=MP, xl=False)
             ops.tune_fused(F["fc1"], "act", act="gelu", mpads=MP, xl=False)

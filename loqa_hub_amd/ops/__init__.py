@@ -1144,7 +1144,8 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     kind unless ``norm`` is given, the folded bias and the LayerNorm column
     sums). ``norm`` True/"rms":
     RMSNorm, "ln": LayerNorm; the row statistics come from ``rowsq_tiles``
-    partial tiles in ``scratch`` (default: what the last residual epilogue wrote) (the norm weight is folded into the weight).
+    partial tiles in ``scratch`` (default: what the last residual epilogue wrote); the norm
+    weight is folded into the weight.
     mode "silu": returns bf16 [Mpad, N/2] (weights in ``perm_gate_up`` order);
     "resid": residual += x W^T (+ bias) in place, writes per-tile row sums of
     squares (and row sums with ``row_sums``);

@@ -158,7 +158,9 @@ class AudioService:
     @property
     def arbitration_window(self) -> ArbitrationWindow | None:
         """The global window (reference field name); None when idle."""
-        return self.windows.get("global") if self.scope == "global" else next(iter(self.windows.values()), None)
+        if self.scope == "global":
+            return self.windows.get("global")
+        return next(iter(self.windows.values()), None)
 
     def start_arbitration_window(self, relay_id: str, stream=None) -> ArbitrationWindow:
         key = self.window_key(relay_id)

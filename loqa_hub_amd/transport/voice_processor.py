@@ -85,7 +85,8 @@ class GPUVoiceProcessor:
         self.max_buffer_time, self.max_tokens_per_phrase = max_buffer_time, max_tokens_per_phrase
         self.publisher = None           # NATS audio publisher (HubServer.start attaches it)
         pipeline.batch_window, pipeline.max_batch = batch_window, max_batch
-        self.stats = {"utterances": 0, "errors": 0, "bridge_sessions": 0, "bridge_ack": 0, "bridge_fallback": 0,
+        self.stats = {"utterances": 0, "errors": 0, "bridge_sessions": 0, "bridge_ack": 0,
+                      "bridge_fallback": 0,
                       "progressive": 0, "first_audio_ms_sum": 0.0, "first_audio_n": 0}
 
     def attach_publisher(self, publisher) -> None:

@@ -33,7 +33,8 @@ def go_float(f: float) -> str:
     if mant.endswith(".0"):
         mant = mant[:-2]
     e = int(exp)
-    return f"{mant}e{'-' if e < 0 else '+'}{abs(e):02d}" if abs(e) < 10 else f"{mant}e{'-' if e < 0 else '+'}{abs(e)}"
+    sign = "-" if e < 0 else "+"
+    return f"{mant}e{sign}{abs(e):02d}"
 
 
 def _esc(s: str) -> str:

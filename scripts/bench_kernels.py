@@ -301,7 +301,8 @@ def slab_bench():
         part = torch.randn(S, M, d, device=dev)
         res = torch.randn(M, d, device=dev, dtype=torch.bfloat16)
         w = torch.ones(d, device=dev, dtype=torch.bfloat16)
-        emit(kernel="slab_rmsnorm", M=M, d=d, S=S, us=round(timeit(lambda: ops.slab_rmsnorm(part, res, w, 1e-5)), 2))
+        emit(kernel="slab_rmsnorm", M=M, d=d, S=S,
+             us=round(timeit(lambda: ops.slab_rmsnorm(part, res, w, 1e-5)), 2))
     part = torch.randn(1, 16, 2 * 14336, device=dev)
     emit(kernel="slab_silu_mul", M=16, F=14336, S=1, us=round(timeit(lambda: ops.slab_silu_mul(part)), 2))
     x = torch.randn(16, 4096, device=dev, dtype=torch.bfloat16)

@@ -25,7 +25,8 @@ def main(paths):
         for d, cs in per.items():
             for c, v in cs.items():
                 vals[names[d]][c].append(v)
-    print(f"{'kernel':60s} {'MFMA busy %':>11s} {'bf16 TF/s':>9s} {'LDS confl':>9s} {'HBM TB/s':>8s} {'us':>8s}")
+    print(f"{'kernel':60s} {'MFMA busy %':>11s} {'bf16 TF/s':>9s} {'LDS confl':>9s} "
+          f"{'HBM TB/s':>8s} {'us':>8s}")
     for k, cs in vals.items():
         med = {c: st.median(v) for c, v in cs.items()}
         # the dispatch's own timestamps give its duration (GRBM_GUI_ACTIVE is
@@ -33,7 +34,8 @@ def main(paths):
         secs = med.get("_dur_s")
         out = [k]
         mfma = med.get("SQ_VALU_MFMA_BUSY_CYCLES")
-        out.append(f"{100 * mfma / (secs * 2.4e9 * SIMDS):11.1f}" if mfma is not None and secs else f"{'-':>11s}")
+        out.append(f"{100 * mfma / (secs * 2.4e9 * SIMDS):11.1f}" if mfma is not None and secs
+                   else f"{'-':>11s}")
         mops = med.get("SQ_INSTS_VALU_MFMA_MOPS_BF16")
         out.append(f"{mops * 512 / secs / 1e12:9.1f}" if mops is not None and secs else f"{'-':>9s}")
         bc, act = med.get("SQ_LDS_BANK_CONFLICT"), med.get("SQ_LDS_IDX_ACTIVE")

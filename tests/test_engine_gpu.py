@@ -115,7 +115,8 @@ def test_llm_gpu_matches_cpu_reference_first_tokens():
     from loqa_hub_amd.models.llama import LlamaWeights
     c = LLMEngine(cfg, "cpu", max_seqs=4)
     # same weights on both
-    c.weights.__dict__.update({k: (v.cpu() if torch.is_tensor(v) else v) for k, v in g.weights.__dict__.items()})
+    c.weights.__dict__.update({k: (v.cpu() if torch.is_tensor(v) else v)
+                               for k, v in g.weights.__dict__.items()})
     c.weights.layers = [{k: t.cpu() for k, t in L.items()} for L in g.weights.layers]
     c.weights.decode_layers = [{k: t.cpu() for k, t in L.items()} for L in g.weights.decode_layers]
     c.weights.cos_sin = g.weights.cos_sin.cpu()

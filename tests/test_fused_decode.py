@@ -2,7 +2,6 @@
 row-sumsq / SwiGLU epilogues; in-launch split-K reduce) against the unfused
 skinny-GEMM + slab-consumer path, on the CPU (reference semantics of the
 weight permutations) and on the GPU (the HIP kernels)."""
-import numpy as np
 import pytest
 import torch
 

@@ -411,9 +411,9 @@ def test_llama_decode_fast_path_matches_generic():
 
 
 # ------------------------------------------------------------------ VITS kernels
-@pytest.mark.parametrize("Cin,Cout,K,dil,act,pre", [(192, 192, 5, 1, None, None), (64, 32, 7, 3, "relu", 0.1),
-                                                   (512, 256, 3, 1, "tanh", None), (32, 1, 7, 1, "tanh", 0.01),
-                                                   (192, 384, 5, 1, "gated", None)])
+@pytest.mark.parametrize("Cin,Cout,K,dil,act,pre", [
+    (192, 192, 5, 1, None, None), (64, 32, 7, 3, "relu", 0.1), (512, 256, 3, 1, "tanh", None),
+    (32, 1, 7, 1, "tanh", 0.01), (192, 384, 5, 1, "gated", None)])
 def test_conv1d_mfma(Cin, Cout, K, dil, act, pre):
     B, T = 2, 300
     w = torch.randn(Cout, Cin, K, device=DEV) * (Cin * K) ** -0.5

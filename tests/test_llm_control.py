@@ -14,7 +14,7 @@ from loqa_hub_amd.llm.command_queue import (CommandQueue, combined_response,
 from loqa_hub_amd.llm.commands import (Command, MultiCommand, ParseError, create_combined_command,
                                        detect_compound_utterance, parse_multi_command_response,
                                        parse_response, split_compound_utterance)
-from loqa_hub_amd.llm.http import MockHTTPClient, create_mock_ollama
+from loqa_hub_amd.llm.http import create_mock_ollama
 from loqa_hub_amd.llm.prompts import build_multi_command_prompt, build_prompt
 from loqa_hub_amd.llm.transcriber import estimate_confidence, post_process_transcription
 

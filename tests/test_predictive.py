@@ -1,6 +1,5 @@
 """Predictive subsystem (C25-C29); tables follow ``predictive_response_test.go``."""
 import asyncio
-import json
 
 import pytest
 

@@ -1,7 +1,6 @@
 """Skills subsystem (C32-C36) and the /api/skills surface (C11)."""
 import asyncio
 import json
-import os
 import stat
 import sys
 import textwrap

@@ -5,6 +5,7 @@ row-parallel O / down with all-reduce, vocab-parallel masked argmax)."""
 import json
 import os
 import socket
+import sys
 
 import pytest
 import torch
@@ -134,6 +135,12 @@ def _lockstep_worker(rank, world, port, out_dir):
         eng.tp_ctl.close()
     finally:
         dist.destroy_process_group()
+    # the gloo process group used from the engine's scheduler thread
+    # occasionally aborts in its C++ teardown at interpreter exit ("terminate
+    # called without an active exception", after both ranks returned and wrote
+    # their results): end the worker process here instead
+    sys.stdout.flush()
+    os._exit(0)
 
 
 def test_tp_lockstep_scheduler_matches_single(tmp_path):
