@@ -59,6 +59,7 @@ class STTRequest:
 class STTEngine:
     SEQ_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128]
     SPLIT_KEYS = 128
+    RES_SLOTS = 3       # result ring slots (>= steps in flight + 1)
 
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
                  block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
@@ -122,6 +123,25 @@ class STTEngine:
         self.step_tokens = max(len(self.sot), min(int(os.environ.get("LOQA_STT_STEP_TOKENS", "64")),
                                                   ops.MPADS[-2]))
         self._rr = 0
+        if self.use_graphs:
+            # step I/O without copy-engine operations between step graphs (as the
+            # LLM engine: elementwise.hip step_fetch / step_publish): a 2-slot
+            # pinned staging ring for the step metadata, a result ring, a device
+            # counter of launched step graphs, and the last token of every
+            # cross-attention slot (+ a trash slot) for device-fed greedy steps
+            b_max = next((b for b in self.SEQ_BUCKETS if b >= max_batch), self.SEQ_BUCKETS[-1])
+            self._n32_max = 4 * ops.MPADS[-1] + 6 * b_max + 1 + b_max * self.max_blocks
+            self._n64_max = max(16, ops.mpad_for(min(b_max, ops.MPADS[-1])))
+            self._stage32 = torch.zeros(2, self._n32_max, dtype=torch.int32).pin_memory()
+            self._stage64 = torch.zeros(2, self._n64_max, dtype=torch.int64).pin_memory()
+            self._res_ring = torch.zeros(self.RES_SLOTS, 256, dtype=torch.int32).pin_memory()
+            self._step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self._step_no = 0
+            self.last_tok = torch.zeros(max_batch + 1, dtype=torch.int32, device=self.device)
+        # two decoder steps in flight (the host prepares step j+1 while step j
+        # runs); LOQA_STT_PIPELINE=0: one synchronous step at a time
+        self.pipelined = self.use_graphs and os.environ.get("LOQA_STT_PIPELINE", "1") != "0" \
+            and self.mega is None
 
     # ------------------------------------------------------------ front end
     def upload(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
@@ -266,7 +286,10 @@ class STTEngine:
     def _graph(self, B_pad: int, T_pad: int, ctx: int) -> dict:
         """Captured decode step for (sequence bucket, token bucket, context
         bucket): the attention grid is sized for the bucket's context, so no
-        workgroups are spent on splits past the longest sequence."""
+        workgroups are spent on splits past the longest sequence. The graph's
+        first node fills the step metadata from the pinned staging ring (taking
+        a greedy sequence's fed token from ``last_tok`` on the device), its last
+        node publishes the sampled tokens to the pinned result ring."""
         key = (B_pad, T_pad, ctx)
         g = self._graphs.get(key)
         if g is not None:
@@ -274,22 +297,21 @@ class STTEngine:
         shapes = {"tokens": (T_pad,), "positions": (T_pad,), "slots": (T_pad,),
                   "cu_q": (B_pad + 1,), "ctx_lens": (B_pad,),
                   "block_tables": (B_pad, self.max_blocks), "enc_starts": (B_pad,),
-                  "enc_lens": (B_pad,)}
+                  "enc_lens": (B_pad,), "src": (T_pad,), "row_slot": (B_pad,)}
         n32 = sum(int(np.prod(v)) for v in shapes.values())
         L = max(16, ops.mpad_for(B_pad))
+        assert n32 <= self._n32_max and L <= self._n64_max and B_pad <= 256
         d32 = torch.zeros(n32, dtype=torch.int32, device=self.device)
-        h32 = torch.zeros(n32, dtype=torch.int32).pin_memory()
         d64 = torch.zeros(L, dtype=torch.int64, device=self.device)
-        h64 = torch.zeros(L, dtype=torch.int64).pin_memory()
-        dev, host, off = {}, {}, 0
-        hn = h32.numpy()
+        dev, off = {}, 0
         for k, shp in shapes.items():
             n = int(np.prod(shp))
             dev[k] = d32[off:off + n].view(*shp)
-            host[k] = hn[off:off + n].reshape(shp)
             off += n
         dev["slots"].fill_(-1)
-        dev["logit_idx"], host["logit_idx"] = d64, h64.numpy()
+        dev["src"].fill_(-1)
+        dev["row_slot"].fill_(self.max_batch)
+        dev["logit_idx"] = d64
         max_q = max(1, min(len(self.sot), T_pad))
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -297,13 +319,43 @@ class STTEngine:
             self._fast_forward(dev, max_q, B_pad, ctx)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
+        k = ops._lib.kernels()
+        lib = ops._lib
         # thread-local capture: the other GPU worker thread keeps running
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+            st = lib.stream_ptr(d32)
+            src_off = dev["src"].data_ptr() // 4 - d32.data_ptr() // 4
+            lib.check(k.loqa_step_fetch(
+                lib.ptr(d32), self._stage32.data_ptr(), n32, self._n32_max, lib.ptr(d64),
+                self._stage64.data_ptr(), L, self._n64_max, lib.ptr(self._step_ctr), T_pad, src_off,
+                lib.ptr(self.last_tok), st), "step_fetch")
             out = self._fast_forward(dev, max_q, B_pad, ctx)
-        g = {"graph": graph, "dev": dev, "out": out, "host": host, "h32": h32, "d32": d32,
-             "h64": h64, "d64": d64}
+            lib.check(k.loqa_step_publish(
+                lib.ptr(out), B_pad, self._res_ring.data_ptr(), self._res_ring.shape[1],
+                self.RES_SLOTS, lib.ptr(self._step_ctr), lib.ptr(dev["row_slot"]),
+                lib.ptr(self.last_tok), st), "step_publish")
+        g = {"graph": graph, "dev": dev, "out": out, "shapes": shapes, "n32": n32, "L": L}
         self._graphs[key] = g
         return g
+
+    def _stage(self, g: dict) -> dict:
+        """Numpy views of the staging slot of the NEXT step-graph launch."""
+        slot = self._step_no % 2
+        hn, out, off = self._stage32[slot].numpy(), {}, 0
+        for k, shp in g["shapes"].items():
+            n = int(np.prod(shp))
+            out[k] = hn[off:off + n].reshape(shp)
+            off += n
+        out["logit_idx"] = self._stage64[slot].numpy()[: g["L"]]
+        return out
+
+    def _replay(self, g: dict) -> int:
+        """Launch a step graph whose staging slot is filled; returns the result
+        ring slot its tokens land in."""
+        rslot = self._step_no % self.RES_SLOTS
+        g["graph"].replay()
+        self._step_no = (self._step_no + 1) % (2 * self.RES_SLOTS)   # wraps as the device counter
+        return rslot
 
     def warmup_graphs(self) -> int:
         """Capture every decoder-step graph bucket up front (see
@@ -341,12 +393,14 @@ class STTEngine:
             if self.use_graphs and ((B_pad, T_pad, C) in self._graphs or not self._graphs_frozen):
                 t0 = time.perf_counter()
                 g = self._graph(B_pad, T_pad, C)
-                self._host_meta(live, B_pad, T_pad, out=g["host"])
-                g["d32"].copy_(g["h32"], non_blocking=True)
-                g["d64"].copy_(g["h64"], non_blocking=True)
+                hb = self._stage(g)
+                self._host_meta(live, B_pad, T_pad, out=hb)
+                hb["src"].fill(-1)
+                hb["row_slot"].fill(self.max_batch)
                 t1 = time.perf_counter()
-                g["graph"].replay()
-                out = g["out"][:B].cpu().numpy()
+                rslot = self._replay(g)
+                torch.cuda.current_stream(self.device).synchronize()
+                out = self._res_ring[rslot, :B].numpy().copy()
                 if self.mega is not None and T_pad == ops.WhisperMega.ROWS:
                     self._check_mega()
                 self.stats["host_pre_s"] += t1 - t0
@@ -466,14 +520,17 @@ class STTEngine:
             r.step += 1
             if t == self.eot or len(r.tokens) >= r.max_new_tokens or \
                     (r.target is not None and r.step >= len(r.target)):
-                r.t_done = time.perf_counter()
-                r.text = self.tok.decode([x for x in r.tokens if x != self.eot]).strip()
-                self.kv.pool.free_seq(r.seq_id)
-                self.stats["utterances"] += 1
-                done.append(r)
+                done.append(self._finish(r))
             else:
                 r.feed = [t]
         return done
+
+    def _finish(self, r: STTRequest) -> STTRequest:
+        r.t_done = time.perf_counter()
+        r.text = self.tok.decode([x for x in r.tokens if x != self.eot]).strip()
+        self.kv.pool.free_seq(r.seq_id)
+        self.stats["utterances"] += 1
+        return r
 
     def transcribe(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
                    ) -> list[STTRequest]:
@@ -558,6 +615,10 @@ class STTEngine:
         # their encoder output and cross-attention K|V are complete
         overlap = self.is_gpu and os.environ.get("LOQA_OVERLAP_ENCODER", "1") != "0"
         enc_pool = self._encoder_executor() if overlap else None
+        pl = None
+        if self.pipelined:
+            from .stt_pipeline import STTPipeline
+            pl = STTPipeline(self)
         while self._running:
             idle = not live and not waiting and not encoding
             items = [self._inbox.get()] if idle else []
@@ -587,6 +648,9 @@ class STTEngine:
                         encoding.append((new, enc_pool.submit(self._encode, new, slots)))
                     else:
                         self._admit(new, slots)
+                        if pl is not None:
+                            for r in new:
+                                pl.admit(r)
                         live += new
                 if encoding:
                     if not live:
@@ -596,12 +660,16 @@ class STTEngine:
                         if f.done():
                             f.result()
                             self._start_decode(reqs)
+                            if pl is not None:
+                                for r in reqs:
+                                    pl.admit(r)
                             live += reqs
                         else:
                             still.append((reqs, f))
                     encoding = still
                 if live:
-                    for r in self._decode_once(live):
+                    finished = pl.pump(live) if pl is not None else self._decode_once(live)
+                    for r in finished:
                         self._free_slots.append(r.slot)
                         self._free_slots.sort()
                         cell = r.on_done
@@ -616,6 +684,8 @@ class STTEngine:
                 # encoder jobs already submitted keep writing cross-attention K|V
                 # into their slots: let them finish before any slot is reused
                 wait([f for _, f in encoding])
+                if pl is not None:
+                    pl.abort()
                 for cell in list(cells.values()):
                     if not cell[1].done():
                         cell[1].set_exception(e)

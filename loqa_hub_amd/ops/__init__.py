@@ -382,7 +382,7 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
     grid balance across the 256 CUs the dominant effect, and it depends on the
     shape, so it is measured rather than modelled. Run before graph capture."""
     N, K = wp.shape[0] * 16, wp.shape[1] * 32
-    if not _gpu(wp):
+    if not _gpu(wp) or NO_TUNE:
         return {}
     out = {}
     for Mpad in mpads:
@@ -405,6 +405,10 @@ def tune_skinny_splits(wp: torch.Tensor, mpads=MPADS, reps: int = 8) -> dict:
 
 _FSPLITS: dict = {}
 MAX_DECODE_WGS = int(os.environ.get("LOQA_MAX_DECODE_WGS", "256"))
+# LOQA_NO_TUNE=1: skip every split-K / layout measurement and use the
+# heuristic defaults (processes sharing one GPU - e.g. a TP rehearsal on a
+# 1-GPU box - cannot time anything meaningful, and the timing dominates start-up)
+NO_TUNE = os.environ.get("LOQA_NO_TUNE", "0") == "1"
 # fused-GEMM decode steps: embedding + layer-0 row statistics in one launch and
 # the final norm gathering its logit rows itself (0: the unfused torch ops)
 FUSED_EMBED = os.environ.get("LOQA_FUSED_EMBED", "1") != "0"
@@ -1069,7 +1073,7 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = 
     decoder, where those long-lived workgroups slow the pipeline."""
     lin = wp if isinstance(wp, FusedLinear) else None
     w = lin.wp if lin is not None else wp
-    if not _gpu(w):
+    if not _gpu(w) or NO_TUNE:
         return
     dev = w.device
     N, K = w.shape[0] * 16, w.shape[1] * 32

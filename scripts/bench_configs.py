@@ -237,10 +237,24 @@ def config_3(args, dev, nats) -> dict:
     }
 
 
+def _heartbeat(tag: str, every: float = 20.0) -> None:
+    """Progress line every ``every`` seconds (long start-ups stay visibly alive)."""
+    import threading
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print(f"[{tag}] alive {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def _tp_rank_main(args) -> int:
     """Rank body of ``--config 5 --tp N`` (torchrun or --share-gpu)."""
     from loqa_hub_amd.parallel.tp_serving import init_tp, run_follower
     info = init_tp(args.tp)
+    if info.rank == 0:
+        _heartbeat("tp leader")
     if args.share_gpu:
         info.device = torch.device("cuda", 0)
         torch.cuda.set_device(0)
@@ -266,7 +280,8 @@ def _tp_rank_main(args) -> int:
 
 def _share_gpu_worker(rank, world, port, argv):
     os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      LOQA_NO_TUNE="1")   # ranks sharing one GPU cannot time anything
     sys.argv = [sys.argv[0]] + argv
     main()
 
@@ -293,6 +308,7 @@ def main() -> int:
             with socket.socket() as sk:
                 sk.bind(("127.0.0.1", 0))
                 port = sk.getsockname()[1]
+            os.environ["LOQA_NO_TUNE"] = "1"     # inherited by the spawned ranks
             mp.start_processes(_share_gpu_worker, args=(args.tp, port, sys.argv[1:]),
                                nprocs=args.tp, join=True, start_method="spawn")
             return 0
