@@ -195,6 +195,39 @@ extern "C" int loqa_pcm16_f32_sumsq(const void* pcm, float* out, const long long
   return (int)hipGetLastError();
 }
 
+// Padded variant: segment s lands in row s of out [nseg, ld] (the Whisper
+// front end's 30 s window), zero beyond the segment - one launch instead of a
+// zero-fill plus a copy per utterance.
+__global__ void pcm16_f32_pad_kernel(const int16_t* __restrict__ pcm, float* __restrict__ out,
+                                     const long long* __restrict__ offsets, float* __restrict__ sumsq,
+                                     long long ld) {
+  __shared__ float scratch[4];
+  const int seg = blockIdx.y;
+  const long long beg = offsets[seg], len = min(offsets[seg + 1] - beg, ld);
+  const long long c0 = (long long)blockIdx.x * PCM_CHUNK;
+  const long long c1 = min(ld, c0 + PCM_CHUNK);
+  float* row = out + (size_t)seg * ld;
+  float acc = 0.f;
+  for (long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+    const float f = i < len ? (float)pcm[beg + i] * (1.0f / 32767.0f) : 0.f;
+    row[i] = f;
+    acc += f * f;
+  }
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0 && c0 < len) atomicAdd(sumsq + seg, acc);
+}
+
+extern "C" int loqa_pcm16_f32_pad(const void* pcm, float* out, const long long* offsets, float* sumsq,
+                                  int nseg, long long ld, hipStream_t s) {
+  if (nseg <= 0 || ld <= 0) return nseg < 0 || ld < 0 ? (int)hipErrorInvalidValue : 0;
+  hipError_t e = hipMemsetAsync(sumsq, 0, sizeof(float) * nseg, s);
+  if (e != hipSuccess) return (int)e;
+  const long long chunks = (ld + PCM_CHUNK - 1) / PCM_CHUNK;
+  hipLaunchKernelGGL(pcm16_f32_pad_kernel, dim3((unsigned)chunks, nseg), dim3(256), 0, s,
+                     (const int16_t*)pcm, out, offsets, sumsq, ld);
+  return (int)hipGetLastError();
+}
+
 // --------------------------------------------------- K15 grammar-masked argmax
 // logits: [B, V] (bf16 if is_bf16 else f32), row stride ld elements.
 // mask: [*, W] uint32 bitmask (bit v%32 of word v/32 = token v allowed), or null;

@@ -37,6 +37,7 @@ class PipelineJob:
     request_id: str
     pcm: np.ndarray
     transcript_hint: str | None = None     # synthetic ground truth (teacher forcing)
+    staged: object = None                  # pinned PCM slot with the samples (relay path)
     on_tokens: object = None               # streaming hook: called with each step's token ids
     # results
     transcription: TranscriptionResult | None = None
@@ -103,7 +104,7 @@ class VoicePipeline:
             # the samples were produced on the default stream (e.g. an RCCL scatter)
             cur = torch.cuda.current_stream(device_pcm.device)
             cur.wait_stream(torch.cuda.default_stream(device_pcm.device))
-        reqs = [STTRequest(j.pcm, transcript=j.transcript_hint) for j in jobs]
+        reqs = [STTRequest(j.pcm, transcript=j.transcript_hint, staged=j.staged) for j in jobs]
         self.stt.transcribe(reqs, device_pcm)
         for j, r in zip(jobs, reqs):
             self._stt_post(j, r)
@@ -238,7 +239,7 @@ class VoicePipeline:
         owner = {}
         for j, f in batch:
             j.t["start"] = j.t.get("start", t0)
-            r = STTRequest(j.pcm, transcript=j.transcript_hint)
+            r = STTRequest(j.pcm, transcript=j.transcript_hint, staged=j.staged)
             reqs.append(r)
             owner[id(r)] = (j, f)
         self.stats["stt_batches"] += 1

@@ -38,6 +38,8 @@ class STTRequest:
     pcm: np.ndarray                   # int16 samples @ 16 kHz
     transcript: str | None = None     # teacher-forcing target (synthetic mode)
     max_new_tokens: int = 96
+    staged: object = None             # pinned PCM slot (engine/pcm_staging.py) holding the samples
+    n_samples: int = 0                # samples uploaded (<= 30 s)
     # outputs
     text: str = ""
     sumsq: float = 0.0
@@ -146,41 +148,68 @@ class STTEngine:
     # ------------------------------------------------------------ front end
     def upload(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
                ) -> tuple[torch.Tensor, torch.Tensor]:
-        """PCM16 of all utterances -> one pinned host buffer -> device (side
-        stream) -> fused convert + sum-of-squares kernel -> [B, 480000] f32.
+        """PCM16 of all utterances -> device -> fused convert + pad + sum of
+        squares kernel -> [B, 480000] f32 (the 30 s window).
+
+        GPU: every request's samples sit in a pinned stager slot (the relay's
+        chunks were appended there as they arrived; numpy requests are staged
+        here), each slot goes to HBM with one hipMemcpyAsync on the stager's
+        H2D stream, and this (compute) stream waits on the copies' events.
         ``device_pcm`` (already on the GPU, e.g. scattered by the DP router
-        over RCCL) holds the concatenated samples and skips the H2D copy."""
-        lens = [min(len(r.pcm), N_SAMPLES) for r in reqs]
+        over RCCL) holds the concatenated samples and skips the copies."""
+        lens = [min(self._n_samples(r), N_SAMPLES) for r in reqs]
+        for r, n in zip(reqs, lens):
+            r.n_samples = n
         offs = np.zeros(len(reqs) + 1, np.int64)
         offs[1:] = np.cumsum(lens)
         if device_pcm is not None:
             pcm = device_pcm[: int(offs[-1])]
-            off_d = torch.from_numpy(offs).to(self.device)
-            f32, sumsq = ops.pcm16_to_f32_sumsq(pcm, off_d)
-            return self._pad(f32, offs, lens), sumsq
-        host = torch.empty(int(offs[-1]), dtype=torch.int16, pin_memory=self.is_gpu)
-        hv = host.numpy()
-        for r, o, n in zip(reqs, offs[:-1], lens):
-            hv[o:o + n] = r.pcm[:n]
-        if self.is_gpu:
-            side = torch.cuda.Stream(self.device)
-            with torch.cuda.stream(side):
-                pcm = host.to(self.device, non_blocking=True)
-                off_d = torch.from_numpy(offs).pin_memory().to(self.device, non_blocking=True)
-            torch.cuda.current_stream(self.device).wait_stream(side)
-            pcm.record_stream(torch.cuda.current_stream(self.device))
-            off_d.record_stream(torch.cuda.current_stream(self.device))
+        elif self.is_gpu:
+            pcm = torch.empty(max(1, int(offs[-1])), dtype=torch.int16, device=self.device)
+            cur = torch.cuda.current_stream(self.device).cuda_stream
+            stager = self._stager()
+            for r, o, n in zip(reqs, offs[:-1], lens):
+                slot = r.staged if r.staged is not None else stager.stage(r.pcm)
+                if slot is None:        # every pinned slot busy: a one-off pinned copy
+                    h = torch.from_numpy(np.ascontiguousarray(r.pcm[:n], np.int16)).pin_memory()
+                    pcm[int(o):int(o) + n].copy_(h, non_blocking=True)
+                    continue
+                slot.upload(pcm.data_ptr() + int(o) * 2, n, cur)
+                r.staged = None
         else:
-            pcm, off_d = host, torch.from_numpy(offs)
-        f32, sumsq = ops.pcm16_to_f32_sumsq(pcm, off_d)
-        return self._pad(f32, offs, lens), sumsq
+            pcm = torch.from_numpy(np.concatenate(
+                [np.asarray(self._host_samples(r)[:n], np.int16) for r, n in zip(reqs, lens)]
+                or [np.zeros(0, np.int16)]))
+            for r in reqs:
+                if r.staged is not None:
+                    r.staged.release()
+                    r.staged = None
+        off_t = torch.from_numpy(offs)
+        if self.is_gpu:
+            off_t = off_t.pin_memory().to(self.device, non_blocking=True)
+        return ops.pcm16_to_f32_padded(pcm, off_t, N_SAMPLES, offs)
 
-    def _pad(self, f32: torch.Tensor, offs: np.ndarray, lens: list[int]) -> torch.Tensor:
-        audio = torch.zeros(len(lens), N_SAMPLES, dtype=torch.float32, device=self.device)
-        for i, (o, n) in enumerate(zip(offs[:-1], lens)):
-            if n:
-                audio[i, :n] = f32[int(o):int(o) + n]
-        return audio
+    @staticmethod
+    def _n_samples(r: STTRequest) -> int:
+        return len(r.staged) if r.staged is not None else len(r.pcm)
+
+    @staticmethod
+    def _host_samples(r: STTRequest) -> np.ndarray:
+        return r.staged.numpy() if r.staged is not None else r.pcm
+
+    def _stager(self):
+        """The engine's pinned PCM stager (created on first use)."""
+        if getattr(self, "stager", None) is None:
+            from .pcm_staging import PcmStager
+            self.stager = PcmStager(2 * self.max_batch + 16, N_SAMPLES)
+        return self.stager
+
+    def new_pcm_slot(self):
+        """A pinned slot for one relay's incoming PCM (None: CPU engine or every
+        slot busy - the caller then buffers on the host)."""
+        if not self.is_gpu:
+            return None
+        return self._stager().acquire()
 
     # -------------------------------------------------------------- decode
     def cross_kv(self, enc: torch.Tensor, slots: list[int] | None = None) -> list[torch.Tensor]:
@@ -477,7 +506,7 @@ class STTEngine:
         for r in reqs:
             r.t_enc0, r.t_enc1 = t_enc0, t1
         for i, (r, sl) in enumerate(zip(reqs, slots)):
-            n = max(1, min(len(r.pcm), N_SAMPLES))
+            n = max(1, r.n_samples)
             r.sumsq = float(ss[i])
             r.rms = float(np.sqrt(ss[i] / n))
             r.slot = sl

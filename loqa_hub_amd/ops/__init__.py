@@ -294,6 +294,30 @@ def pcm16_to_f32_sumsq(pcm: torch.Tensor, offsets: torch.Tensor) -> tuple[torch.
     return out, sumsq[:S]
 
 
+def pcm16_to_f32_padded(pcm: torch.Tensor, offsets: torch.Tensor, ld: int,
+                        offsets_host: "np.ndarray | None" = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """pcm int16 [N] (S concatenated segments, offsets int64 [S+1]) -> f32
+    [S, ld] (x / 32767, zero-padded / truncated to ``ld`` samples) and the
+    per-segment sum of squares [S] of the kept samples."""
+    S = offsets.numel() - 1
+    if not _gpu(pcm):
+        out = torch.zeros(S, ld, dtype=torch.float32)
+        seg = offsets.cpu()
+        for i in range(S):
+            n = min(int(seg[i + 1] - seg[i]), ld)
+            out[i, :n] = pcm[int(seg[i]):int(seg[i]) + n].float() / 32767.0
+        return out, out.square().sum(1)
+    assert pcm.dtype == torch.int16 and pcm.is_contiguous()
+    assert offsets.dtype == torch.int64 and offsets.is_contiguous() and offsets.is_cuda
+    out = torch.empty(S, ld, dtype=torch.float32, device=pcm.device)
+    sumsq = torch.empty(max(S, 1), dtype=torch.float32, device=pcm.device)
+    if offsets_host is not None:
+        assert int(offsets_host[-1]) <= pcm.numel()
+    check(kernels().loqa_pcm16_f32_pad(ptr(pcm), ptr(out), ptr(offsets), ptr(sumsq), S, ld,
+                                       stream_ptr(pcm)), "pcm16_f32_pad")
+    return out, sumsq[:S]
+
+
 def log_mel(audio: torch.Tensor, consts: "ref.MelConstants") -> torch.Tensor:
     """audio [B, n_samples] f32 (padded to 30 s) -> whisper log-mel [B, n_mels, frames] bf16."""
     if not _gpu(audio):

@@ -68,6 +68,7 @@ _KERNEL_SIGS = {
     "loqa_rope_kv_append": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_int, c_int, c_int, c_int, c_int, c_void_p],
     "loqa_pcm16_f32_sumsq": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p],
+    "loqa_pcm16_f32_pad": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_void_p],
     "loqa_masked_argmax": [c_void_p, c_int, c_ll, c_int, c_int, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_void_p],  # (..., out_idx, workspace, stream)
     "loqa_attention": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_ll, c_void_p,

@@ -57,24 +57,46 @@ class RelayStream:
     relay_id: str
     stream: object = None                 # object with ``async write(AudioResponse)``
     connected_at: float = field(default_factory=time.monotonic)
-    wake_word_signal: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))
-    speech_audio: list = field(default_factory=list)
     signal_strength: float = 0.0
     status: RelayStatus = RelayStatus.CONNECTED
     cancel: asyncio.Event = field(default_factory=asyncio.Event)
     end_of_speech: asyncio.Event = field(default_factory=asyncio.Event)
     result: asyncio.Future | None = None
     request_id: str = ""
-    # the relay's raw PCM16-LE bytes, wake word + speech, as received (the GPU
-    # path stages these; the float samples exist only for RMS / other backends)
+    # the relay's raw PCM16-LE samples as received (odd trailing bytes
+    # dropped per chunk, as audio_service.go:1048-1101): the wake word for the
+    # RMS arbitration, and wake word + speech for the processor - in a pinned
+    # stager slot on the GPU path (appended as each chunk arrives), otherwise on
+    # the host
+    wake_pcm: bytearray = field(default_factory=bytearray)
     pcm: bytearray = field(default_factory=bytearray)
+    pcm_slot: object = None
+    n_samples: int = 0
+
+    def add_pcm(self, data: bytes) -> None:
+        data = data[: len(data) & ~1]
+        if self.pcm_slot is not None:
+            self.pcm_slot.append(data)
+        else:
+            self.pcm += data
+        self.n_samples += len(data) // 2
+
+    @property
+    def wake_word_signal(self) -> np.ndarray:
+        """Float samples of the wake word (x / 32767)."""
+        return bytes_to_float32_array(bytes(self.wake_pcm))
 
     def full_audio(self) -> np.ndarray:
-        parts = [self.wake_word_signal] + list(self.speech_audio)
-        return np.concatenate(parts) if parts else np.zeros(0, np.float32)
+        """Float samples of wake word + speech (host-buffered relays only)."""
+        return bytes_to_float32_array(bytes(self.pcm))
 
     def full_pcm16(self) -> np.ndarray:
         return np.frombuffer(bytes(self.pcm), dtype="<i2")
+
+    def release_pcm(self) -> None:
+        if self.pcm_slot is not None:
+            self.pcm_slot.release()
+            self.pcm_slot = None
 
 
 @dataclass
@@ -124,6 +146,16 @@ def calculate_signal_strength(samples: np.ndarray) -> float:
         return 0.0
     s = samples.astype(np.float32)
     return float(np.sqrt(np.sum((s * s).astype(np.float64)) / s.size))
+
+
+def pcm16_signal_strength(data: bytes) -> float:
+    """RMS of PCM16-LE bytes in the reference's float scale (x / 32767,
+    ``calculateSignalStrength`` :818-852) straight from the integers."""
+    n = len(data) // 2
+    if n == 0:
+        return 0.0
+    x = np.frombuffer(data[: 2 * n], dtype="<i2").astype(np.int64)
+    return float(np.sqrt(float(np.dot(x, x)) / n)) / 32767.0
 
 
 class AudioService:
@@ -202,10 +234,10 @@ class AudioService:
         for rid, rs in w.relays.items():
             if rs.status != RelayStatus.CONTENDING:
                 continue
-            rs.signal_strength = calculate_signal_strength(rs.wake_word_signal)
+            rs.signal_strength = pcm16_signal_strength(bytes(rs.wake_pcm))
             hublog.log_audio_processing(rid, "arbitration_signal_analysis",
                                         signal_strength=rs.signal_strength,
-                                        samples=int(rs.wake_word_signal.size))
+                                        samples=len(rs.wake_pcm) // 2)
             if rs.signal_strength > best:
                 best, winner = rs.signal_strength, rid
         if winner == "" and w.relays:
@@ -220,6 +252,7 @@ class AudioService:
             else:
                 rs.status = RelayStatus.CANCELLED
                 rs.cancel.set()
+                rs.release_pcm()
                 self.stats["cancelled"] += 1
                 hublog.log_audio_processing(rid, "arbitration_cancelled",
                                             signal_strength=rs.signal_strength, winner=winner)
@@ -249,7 +282,9 @@ class AudioService:
         return rs.status in (RelayStatus.WINNER, RelayStatus.CONNECTED, RelayStatus.CONTENDING)
 
     def cleanup_relay(self, relay_id: str) -> None:
-        self.active_streams.pop(relay_id, None)
+        rs = self.active_streams.pop(relay_id, None)
+        if rs is not None and rs.result is None:
+            rs.release_pcm()          # never processed: give the pinned slot back
 
     # ------------------------------------------------------------ processing
     async def _process_winner(self, rs: RelayStream) -> UtteranceResult:
@@ -259,20 +294,29 @@ class AudioService:
             await asyncio.wait_for(rs.end_of_speech.wait(), self.end_of_speech_wait)
         except asyncio.TimeoutError:
             pass
-        audio = rs.full_audio()
         request_id = rs.request_id or f"req_{time.time_ns()}"
         ev = VoiceEvent.new(rs.relay_id, request_id)
-        ev.set_audio_metadata(int(audio.size), 16000, True)
-        if audio.size == 0:
+        ev.set_audio_metadata(rs.n_samples, 16000, True)
+        if rs.n_samples == 0:
+            rs.release_pcm()
             hublog.log_warn("winner has no audio", relay_id=rs.relay_id)
             res = UtteranceResult(success=False, command="error", response_text=MSG_NO_SPEECH)
         elif self.processor is None:
+            rs.release_pcm()
             res = UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                   error="no voice processor configured")
         else:
             kw = {}
             if getattr(self.processor, "takes_pcm16", False):
-                kw["pcm16"] = rs.full_pcm16()
+                # GPU path: the samples go as PCM16 - the pinned slot itself
+                # (ownership passes to the processor) or the host bytes
+                audio = np.zeros(0, np.float32)
+                if rs.pcm_slot is not None:
+                    kw["pcm_slot"], rs.pcm_slot = rs.pcm_slot, None
+                else:
+                    kw["pcm16"] = rs.full_pcm16()
+            else:
+                audio = rs.full_audio()
             hint = self.transcript_hints(rs.relay_id) if self.transcript_hints else None
             if hint:
                 kw["transcript_hint"] = hint
@@ -328,7 +372,6 @@ class AudioService:
         ``async write(AudioResponse)`` (grpc.aio ServicerContext or a test double)."""
         relay_id = ""
         request_id = f"req_{uuid.uuid4().hex[:12]}"
-        wake: list[np.ndarray] = []
         stream = _ContextWriter(context)
         try:
             async for chunk in request_iterator:
@@ -338,7 +381,6 @@ class AudioService:
                                             wake_word=chunk.is_wake_word)
                 data = chunk.audio_data
                 if chunk.is_wake_word:
-                    wake.append(bytes_to_float32_array(data))
                     key = self.window_key(relay_id)
                     w = self.windows.get(key)
                     if w is None:
@@ -349,14 +391,14 @@ class AudioService:
                         return
                     rs = self.active_streams.get(relay_id)
                     if rs is not None:
-                        rs.wake_word_signal = np.concatenate(wake)
-                        rs.pcm += data[: len(data) & ~1]
+                        self._attach_pcm(rs)
+                        rs.wake_pcm += data[: len(data) & ~1]
+                        rs.add_pcm(data)
                         rs.request_id = request_id
                 else:
                     rs = self.active_streams.get(relay_id)
                     if rs is not None and rs.status != RelayStatus.CANCELLED:
-                        rs.speech_audio.append(bytes_to_float32_array(data))
-                        rs.pcm += data[: len(data) & ~1]
+                        rs.add_pcm(data)
                 if chunk.is_end_of_speech:
                     hublog.log_audio_processing(relay_id, "end_of_speech_detected")
                     if not self.is_relay_active(relay_id):
@@ -371,6 +413,14 @@ class AudioService:
         finally:
             if relay_id:
                 self.cleanup_relay(relay_id)
+
+    def _attach_pcm(self, rs: RelayStream) -> None:
+        """GPU processors hand out a pinned stager slot per relay: its chunks
+        are appended there as they arrive (no host conversion)."""
+        if rs.pcm_slot is None and rs.n_samples == 0:
+            new_slot = getattr(self.processor, "new_pcm_slot", None)
+            if new_slot is not None:
+                rs.pcm_slot = new_slot()
 
     async def _await_result(self, rs: RelayStream, stream: "_ContextWriter") -> None:
         deadline = time.monotonic() + self.end_of_speech_wait

@@ -92,6 +92,10 @@ class GPUVoiceProcessor:
     def attach_publisher(self, publisher) -> None:
         self.publisher = publisher
 
+    def new_pcm_slot(self):
+        """A pinned stager slot for one relay's incoming PCM (AudioService)."""
+        return self.pipeline.stt.new_pcm_slot()
+
     async def close(self) -> None:
         """Stop the engines' scheduler threads (a TP leader also releases its
         followers)."""
@@ -102,14 +106,19 @@ class GPUVoiceProcessor:
 
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
                       sample_rate: int, transcript_hint: str | None = None,
-                      pcm16: np.ndarray | None = None) -> UtteranceResult:
+                      pcm16: np.ndarray | None = None, pcm_slot=None) -> UtteranceResult:
         """``transcript_hint``: synthetic-traffic ground truth that teacher-forces
         the (random-init) Whisper decoder; real relays never pass it. ``pcm16``:
-        the relay's raw samples (skips the float round trip). Concurrent calls
-        are micro-batched by the pipeline (STT batch, continuous LLM batch)."""
+        the relay's raw samples (skips the float round trip); ``pcm_slot``: the
+        pinned stager slot its chunks were appended to as they arrived (the
+        STT upload copies it straight to HBM). Concurrent calls are
+        micro-batched by the pipeline (STT batch, continuous LLM batch)."""
         from ..engine.pipeline import PipelineJob
-        pcm = pcm16 if pcm16 is not None else float_to_pcm16(audio)
-        j = PipelineJob(relay_id, request_id, pcm, transcript_hint)
+        if pcm_slot is not None:
+            pcm = np.zeros(0, np.int16)
+        else:
+            pcm = pcm16 if pcm16 is not None else float_to_pcm16(audio)
+        j = PipelineJob(relay_id, request_id, pcm, transcript_hint, staged=pcm_slot)
         speech = None
         if self.progressive:
             from ..streaming.progressive import ProgressiveSpeech
@@ -120,6 +129,8 @@ class GPUVoiceProcessor:
         try:
             await self.pipeline.submit(j)
         except Exception as e:  # noqa: BLE001
+            if pcm_slot is not None:
+                pcm_slot.release()        # idempotent: a no-op once uploaded
             log.exception("GPU pipeline failed")
             self.stats["errors"] += 1
             if speech is not None:

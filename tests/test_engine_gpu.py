@@ -336,3 +336,30 @@ def test_vits_gpu_matches_fp32_reference():
         assert pg.shape == pc.shape
         assert rel(pg, pc) < 0.1, rel(pg, pc)
         assert pc.abs().mean() > 50
+
+
+def test_pinned_pcm_stager_upload_gpu():
+    """Relay chunks appended into a pinned stager slot (odd trailing bytes
+    dropped per chunk, as the reference) reach HBM byte-identical through the
+    H2D stream, and the padded convert kernel yields x / 32767 with zeros past
+    the utterance; a numpy request in the same batch is staged on the fly."""
+    from loqa_hub_amd.engine.stt_engine import N_SAMPLES, STTRequest
+    eng = STTEngine(whisper_config("whisper-tiny"), "cuda", max_batch=4)
+    rng = np.random.default_rng(7)
+    chunks = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in (3201, 640, 17, 9600)]
+    slot = eng.new_pcm_slot()
+    for c in chunks:
+        slot.append(c)
+    expect = np.frombuffer(b"".join(c[: len(c) & ~1] for c in chunks), "<i2")
+    other = (rng.standard_normal(5000) * 3000).astype(np.int16)
+    reqs = [STTRequest(np.zeros(0, np.int16), staged=slot), STTRequest(other)]
+    audio, sumsq = eng.upload(reqs)
+    torch.cuda.synchronize()
+    a = audio.cpu().numpy()
+    assert a.shape == (2, N_SAMPLES)
+    assert np.array_equal(np.round(a[0, :expect.size] * 32767.0).astype(np.int64), expect.astype(np.int64))
+    assert not a[0, expect.size:].any() and not a[1, other.size:].any()
+    assert np.array_equal(np.round(a[1, :other.size] * 32767.0).astype(np.int64), other.astype(np.int64))
+    ref = (expect.astype(np.float64) / 32767.0) ** 2
+    assert abs(float(sumsq[0]) - ref.sum()) <= 1e-3 * ref.sum()
+    assert reqs[0].staged is None and slot.released
