@@ -436,16 +436,25 @@ class STTEngine:
                 self.stats["gpu_wait_s"] += time.perf_counter() - t1
                 return out
             max_q, host = self._host_meta(live, B_pad, T_pad)
-            return self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
+            out = self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
+            if self.mega is not None and T_pad == ops.WhisperMega.ROWS:
+                self._check_mega()
+            return out
         return self._eager_step(live)
 
     def _check_mega(self) -> None:
-        """Every 32nd one-launch step, read the kernel's sticky error word: an
-        expired (bounded) dependency wait means outputs since then are garbage,
-        so the scheduler fails the batch loudly instead of serving them."""
-        self._mega_steps = getattr(self, "_mega_steps", 0) + 1
-        if self._mega_steps % 32 == 0 and self.mega.error():
-            raise RuntimeError("whisper_mega: a dependency wait expired (kernel error flag set)")
+        """After every one-launch step (opt-in path), read the kernel's sticky
+        error word before the tokens are used: an expired (bounded) dependency
+        wait means this step's outputs are garbage, so the batch fails loudly.
+        The word is then cleared and the engine drops back to the fused
+        8-launches-per-layer path for good."""
+        if self.mega is not None and self.mega.error():
+            self.mega.sync.zero_()
+            self.mega = None
+            self._graphs.clear()           # graphs captured the mega launch
+            self._graphs_frozen = False
+            raise RuntimeError("whisper_mega: a dependency wait expired (kernel error flag set); "
+                               "falling back to the fused decoder step")
 
     def _eager_step(self, live: list[STTRequest]) -> np.ndarray:
         """Reference decode path (hipBLASLt GEMMs, eager launches)."""

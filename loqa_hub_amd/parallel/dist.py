@@ -5,11 +5,24 @@ Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun).
 """
 from __future__ import annotations
 
+import logging
 import os
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
+
+
+log = logging.getLogger("loqa.dist")
+
+
+def _loaded_hip_runtime() -> str:
+    """Path of the libamdhip64 this process (torch) has mapped."""
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64.so" in line:
+                return line.split()[-1]
+    raise RuntimeError("libamdhip64 is not mapped (import torch and touch the GPU first)")
 
 
 @dataclass
@@ -35,8 +48,9 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
         if sched:
             import ctypes
             flag = {"spin": 1, "yield": 2, "block": 4}[sched]
-            rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(flag)
-            print(f"hipSetDeviceFlags({sched}) -> {rc}", flush=True)
+            # the HIP runtime torch already mapped (never a second copy by soname)
+            rc = ctypes.CDLL(_loaded_hip_runtime(), mode=ctypes.RTLD_NOLOAD).hipSetDeviceFlags(flag)
+            log.info("hipSetDeviceFlags(%s) -> %d", sched, rc)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
