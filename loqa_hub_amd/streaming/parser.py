@@ -146,52 +146,51 @@ class OllamaStreamingBackend:
 
 
 class GPUStreamingBackend:
-    """Streams the grammar-constrained decode of the local engine. Concurrent
-    prompts inside ``batch_window`` share one engine call (one batch)."""
+    """Streams the grammar-constrained decode of the local engine. Each prompt
+    joins the engine's RUNNING continuous batch (``LLMEngine.submit_batch``)
+    and its tokens are pushed as every decode step emits them, so streaming
+    sessions share the decode steps (and their weight reads) with every other
+    live sequence instead of running a blocking decode of their own. Engines
+    without a scheduler (CPU tests) fall back to ``generate`` in a worker."""
 
-    def __init__(self, engine, batch_window: float = 0.002):
+    def __init__(self, engine, batch_window: float = 0.0):
         self.engine = engine
         self.batch_window = batch_window
-        self._pending: list[tuple[str, Chan]] = []
-        self._flusher: asyncio.Task | None = None
 
     async def stream(self, prompt: str):
-        ch = Chan(4096)
-        self._pending.append((prompt, ch))
-        loop = asyncio.get_running_loop()
-        if self._flusher is None or self._flusher.done():
-            self._flusher = loop.create_task(self._flush())
-        async for item in ch:
-            if isinstance(item, Exception):
-                raise item
-            yield item
-
-    async def _flush(self) -> None:
-        await asyncio.sleep(self.batch_window)
-        batch, self._pending = self._pending, []
-        if not batch:
-            return
         from ..engine.grammar import single_command_schema
         from ..engine.llm_engine import GenRequest
+        ch = Chan(4096)
         loop = asyncio.get_running_loop()
         tok = self.engine.tok
-        reqs = []
-        for prompt, ch in batch:
-            def push(ids, ch=ch):
-                text = tok.decode(ids)
-                loop.call_soon_threadsafe(ch.try_put, (text, False))
-            reqs.append(GenRequest(tok.encode(prompt, bos=True), single_command_schema(),
-                                   on_tokens=push))
-        try:
-            await loop.run_in_executor(None, self.engine.generate, reqs)
-        except Exception as e:  # noqa: BLE001
-            for _, ch in batch:
+
+        def push(ids):                                  # engine thread
+            loop.call_soon_threadsafe(ch.try_put, (tok.decode(ids), False))
+        req = GenRequest(tok.encode(prompt, bos=True), single_command_schema(), on_tokens=push)
+
+        async def run():
+            try:
+                if self.batch_window:
+                    await asyncio.sleep(self.batch_window)
+                if hasattr(self.engine, "submit_batch") and getattr(self.engine, "is_gpu", False):
+                    await asyncio.wrap_future(self.engine.submit_batch([req]))
+                else:
+                    await loop.run_in_executor(None, self.engine.generate, [req])
+                await asyncio.sleep(0)          # the last call_soon_threadsafe pushes
+                ch.try_put(("", True))
+            except Exception as e:  # noqa: BLE001
                 ch.try_put(e)
+            finally:
                 ch.close()
-            return
-        for _, ch in batch:
-            ch.try_put(("", True))
-            ch.close()
+        task = loop.create_task(run())
+        try:
+            async for item in ch:
+                if isinstance(item, Exception):
+                    raise item
+                yield item
+        finally:
+            if not task.done():
+                await task
 
 
 class StreamingCommandParser:

@@ -156,8 +156,16 @@ class GPUVoiceProcessor:
             if sr:
                 r.audio_duration = max(0, len(audio_b) - 44) / 2 / sr
             m = speech.metrics()
+            done_t = j.t.get("llm_done", 0.0)
+            m["first_phrase_before_decode_done"] = bool(speech.t_first_phrase and done_t
+                                                        and speech.t_first_phrase < done_t)
+            m["first_audio_before_decode_done"] = bool(speech.t_first_audio and done_t
+                                                       and speech.t_first_audio < done_t)
             r.metrics["speech"] = m
             self.stats["progressive"] += 1
+            for k in ("phrase", "audio"):
+                key = f"{k}_before_decode_done"
+                self.stats[key] = self.stats.get(key, 0) + int(m[f"first_{k}_before_decode_done"])
             if m["first_audio_ms"] is not None:
                 self.stats["first_audio_ms_sum"] += m["first_audio_ms"]
                 self.stats["first_audio_n"] += 1

@@ -247,6 +247,7 @@ def test_hub_server_gpu_served(tmp_path, streaming):
     assert ev["intent"] == cmds[0]["intent"]
     if streaming:
         assert stats["progressive"] == 1 and stats["first_audio_n"] == 1
+        assert stats["audio_before_decode_done"] == 1   # phrases before the decode finished
     assert "loqa_audio_processed_total 1.0" in metrics
 
 
@@ -363,3 +364,29 @@ def test_pinned_pcm_stager_upload_gpu():
     ref = (expect.astype(np.float64) / 32767.0) ** 2
     assert abs(float(sumsq[0]) - ref.sum()) <= 1e-3 * ref.sum()
     assert reqs[0].staged is None and slot.released
+
+
+def test_gpu_streaming_backend_joins_continuous_batch():
+    """The streaming parser's GPU backend submits into the running continuous
+    batch (submit_batch) - two concurrent sessions share decode steps."""
+    import asyncio
+
+    from loqa_hub_amd.streaming.parser import GPUStreamingBackend, StreamingCommandParser
+    eng = LLMEngine(llama_config("test-tiny"), "cuda", max_seqs=4, max_seq_len=512)
+    eng.warmup_graphs()
+
+    async def go():
+        p = StreamingCommandParser(GPUStreamingBackend(eng), None)
+        rs = await asyncio.gather(*[p.parse_command_streaming(t) for t in
+                                    ("turn on the kitchen lights", "play some jazz")])
+        out = []
+        for r in rs:
+            toks = [t async for t in r.token_stream]
+            out.append((toks, await asyncio.wait_for(r.final_command.get(), 60)))
+        return out
+    try:
+        out = asyncio.run(go())
+    finally:
+        eng.stop()
+    assert all(len(t) > 3 and c.intent for t, c in out)
+    assert eng.stats["decode_steps"] > 0

@@ -98,6 +98,9 @@ def test_hub_served_cpu(tmp_path, streaming):
     assert all(m["sample_rate"] == 22050 and m["message_type"] == "response" for m in audio)
     if streaming:
         assert stats["progressive"] == 1 and stats["first_audio_n"] == 1
+        # the first phrase went to synthesis while the decode was still running
+        # (the GPU variant also asserts its audio was published by then)
+        assert stats["phrase_before_decode_done"] == 1
     else:
         assert len(audio) == 1
     # the voice event records the decode's parse

@@ -245,3 +245,24 @@ def test_tts_client():
             OpenAITTSClient(cfgmod.load({"TTS_URL": ""}).tts if False else
                             type("C", (), {"url": ""})())
     asyncio.run(go())
+
+
+def test_gpu_streaming_backend_tokens_cpu():
+    """GPUStreamingBackend over the local constrained decode (CPU engine):
+    tokens stream per decode step and the parser's final command parses."""
+    import torch
+
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.streaming.parser import GPUStreamingBackend, StreamingCommandParser
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), max_seqs=4, max_seq_len=512)
+
+    async def go():
+        p = StreamingCommandParser(GPUStreamingBackend(eng), None, max_tokens_per_phrase=4)
+        res = await p.parse_command_streaming("turn on the kitchen lights")
+        toks = [t async for t in res.token_stream]
+        cmd = await asyncio.wait_for(res.final_command.get(), 30)
+        return toks, cmd, res.metrics
+    toks, cmd, m = asyncio.run(go())
+    assert len(toks) > 3 and m.token_count == len(toks) and m.phrase_count >= 1
+    assert cmd.intent
