@@ -30,7 +30,7 @@ import torch
 
 from .. import ops
 from ..models.configs import LlamaConfig
-from .batching import join_futures, plan_step
+from .batching import MPAD_PLAN, join_futures, plan_step, plan_step_mpad
 from ..models.llama import LlamaModel, LlamaWeights, StepMeta, TPGroup
 from .grammar import GrammarState, GrammarTables
 from .kv_cache import PagedKVCache
@@ -531,8 +531,8 @@ class LLMEngine:
         ``step_tokens`` tokens in total and ``max_decode_q`` per sequence; a
         sequence fed only part of its pending tokens carries the rest (its
         logits this step are unused), one left out entirely waits a step."""
-        take = plan_step([len(r.feed) for r in live], self.step_tokens, self.max_decode_q,
-                         self._rr)
+        plan = plan_step_mpad if MPAD_PLAN else plan_step
+        take = plan([len(r.feed) for r in live], self.step_tokens, self.max_decode_q, self._rr)
         self._rr = (self._rr + self.step_tokens) % len(live) if len(live) > self.step_tokens else 0
         step, feeds, carry = [], [], []
         for r, n in zip(live, take):

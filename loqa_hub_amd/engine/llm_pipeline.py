@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from .batching import plan_step
+from .batching import MPAD_PLAN, plan_step, plan_step_mpad
 
 DEV = -1   # feed placeholder: "the token this sequence sampled in its previous step"
 
@@ -136,8 +136,12 @@ class DecodePipeline:
                 cands.append((r, it))
         if not cands:
             return False
-        take = plan_step([len(it[0]) for _, it in cands], eng.step_tokens, eng.max_decode_q,
-                         self.rr)
+        lens = [len(it[0]) for _, it in cands]
+        if MPAD_PLAN:
+            take = plan_step_mpad(lens, eng.step_tokens, eng.max_decode_q, self.rr,
+                                  whole=[it[1] for _, it in cands])
+        else:
+            take = plan_step(lens, eng.step_tokens, eng.max_decode_q, self.rr)
         n_c = len(cands)
         self.rr = (self.rr + eng.step_tokens) % n_c if n_c > eng.step_tokens else 0
         rows, feeds, entries = [], [], []

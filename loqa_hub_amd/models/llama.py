@@ -299,6 +299,13 @@ class LlamaWeights:
 
 PREFILL_DOWN_SPLITS = int(os.environ.get("LOQA_PREFILL_DOWN_SPLITS", "8"))
 PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
+# Prefill projections on the hand-written v2 prefill GEMM (decode copies of the
+# weights, csrc/kernels/gemm_prefill.hip) instead of hipBLASLt: qkv / o / down as
+# f32 split-K slabs summed by their consumer (RoPE + KV append, residual +
+# RMSNorm), gate|up with the SwiGLU epilogue in the GEMM. Split counts per
+# projection (qkv, o, down) for ~300-row prompts.
+PREFILL2 = os.environ.get("LOQA_PREFILL2", "0") != "0"
+PREFILL2_SPLITS = tuple(int(v) for v in os.environ.get("LOQA_PREFILL2_SPLITS", "2,4,8").split(","))
 
 
 def _splitk_slabs(a: torch.Tensor, w: torch.Tensor, S: int) -> torch.Tensor:
@@ -348,6 +355,9 @@ class LlamaModel:
         S_o = PREFILL_O_SPLITS if (S_down and PREFILL_O_SPLITS > 0 and hasattr(w, "decode_layers")
                                    and (H * D) % (PREFILL_O_SPLITS * 128) == 0
                                    and cfg.d_model % ops.PREFILL_GEMM_NT == 0) else 0
+        if (PREFILL2 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 64
+                and not getattr(w, "compact", False) and "wqkv" in w.decode_layers[0]):
+            return self._forward_prefill2(meta, k_cache, v_cache, attn_ws, x, h)
         part = None
         for li, L in enumerate(w.layers):
             if li > 0:
@@ -365,16 +375,18 @@ class LlamaModel:
                                  num_splits=num_splits if meta.decode else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
             if S_o:
-                # o projection on the weight-streaming prefill GEMM (decode copy
+                # o projection on the hand-written prefill GEMM (decode copy
                 # of wo), split-K f32 slabs summed by the norm
-                part_o = ops.prefill_gemm(attn, w.decode_layers[li]["wo"], S_o, slabs=True)
+                part_o = ops.prefill_gemm2(attn, w.decode_layers[li]["wo"], S_o, epi="slabs")
                 h = ops.slab_rmsnorm(part_o, residual, L["mlp_norm"], cfg.norm_eps)
             else:
                 o = tp.all_reduce_(ops.linear(attn, L["wo"]))
                 h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             gu = ops.linear(h, L["w_gate_up"])
             if S_down:
-                part = _splitk_slabs(ops.silu_mul(gu), L["w_down"], S_down)
+                a = ops.silu_mul(gu)
+                part = (ops.prefill_gemm2(a, w.decode_layers[li]["w_down"], S_down, epi="slabs")
+                        if S_o else _splitk_slabs(a, L["w_down"], S_down))
                 continue
             mlp_out = tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["w_down"]))
         if part is not None:
@@ -384,6 +396,43 @@ class LlamaModel:
         sel_mlp = mlp_out.index_select(0, meta.logit_idx)
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
                            residual=sel_res.contiguous())
+
+    def _forward_prefill2(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:
+        """Prefill through the v2 prefill GEMM: per layer qkv slabs -> RoPE + KV
+        append (``slab_rope_append``) -> flash attention -> o slabs -> residual
+        + RMSNorm -> gate|up with the SwiGLU epilogue (norm-folded, pair-
+        permuted decode copy: the norm here is unweighted) -> down slabs ->
+        the next layer's residual + RMSNorm. Four GEMMs and four small kernels
+        per layer, every weight read once from the decode copies."""
+        cfg, w = self.cfg, self.w
+        H, Hkv, D = w.h, w.hkv, cfg.head_dim
+        s_qkv, s_o, s_down = PREFILL2_SPLITS
+        ones = self._ones(x)
+        residual = x
+        part = None
+        for li, L in enumerate(w.layers):
+            P = w.decode_layers[li]
+            if part is not None:
+                h = ops.slab_rmsnorm(part, residual, L["attn_norm"], cfg.norm_eps)
+            pq = ops.prefill_gemm2(h, P["wqkv"], s_qkv, epi="slabs")
+            q = ops.slab_rope_append(pq, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
+                                     H, Hkv, D)
+            attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
+                                 block_tables=meta.block_tables, grouped=False, split_keys=256,
+                                 num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
+            po = ops.prefill_gemm2(attn, P["wo"], s_o, epi="slabs")
+            hn = ops.slab_rmsnorm(po, residual, ones, cfg.norm_eps)
+            a = ops.prefill_gemm2(hn, P["w_gate_up_f"], 1, epi="swiglu")
+            part = ops.prefill_gemm2(a, P["w_down"], s_down, epi="slabs")
+        return ops.slab_rmsnorm(part, residual, w.final_norm, cfg.norm_eps,
+                                row_idx=meta.logit_idx, write_residual=False)
+
+    def _ones(self, x: torch.Tensor) -> torch.Tensor:
+        t = getattr(self, "_ones_d", None)
+        if t is None or t.device != x.device:
+            t = self._ones_d = torch.ones(self.cfg.d_model, dtype=x.dtype, device=x.device)
+        return t
 
     def forward_decode(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
                        attn_ws: ops.AttnWorkspace | None, split_keys: int = 128) -> torch.Tensor:

@@ -1405,3 +1405,47 @@ def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, slabs: bool
         rc = kernels().loqa_gemm_prefill(ptr(x), M, K, ptr(wp), N, 1, ptr(out), None, stream_ptr(x))
     check(rc, "gemm_prefill")
     return out
+
+
+# v2 layouts: (row tiles, feature tiles) per wave and waves along M (the other
+# 4 / WM waves go along N) -> workgroup tile (16 WM rbw) x (16 (4 / WM) ft)
+PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1)}
+# layout 3 (v1's 1 x 4 waves with the one-barrier pipeline) measured fastest on
+# every prefill / encoder shape (profiles/r3_prefill_gemm2_layouts.txt)
+PREFILL2_LAYOUT = int(os.environ.get("LOQA_PREFILL2_LAYOUT", "3"))
+
+
+def prefill_gemm2(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, epi: str = "bf16",
+                  layout: int | None = None) -> torch.Tensor:
+    """x [M, K] bf16 @ W^T for prefill-sized M (64 - a few thousand rows), W
+    pre-shuffled (``shuffle_weight``; ``csrc/kernels/gemm_prefill.hip`` v2).
+    ``epi``: "bf16" -> [M, N]; "slabs" -> f32 split-K partials [S, M, N] (a
+    slab consumer sums them); "swiglu" -> silu(gate) * up [M, N / 2] bf16 from
+    a ``perm_gate_up`` weight (16-row gate|up pair tiles)."""
+    M, K = x.shape
+    N = wp.shape[0] * 16
+    assert wp.shape[1] * 32 == K
+    lay = PREFILL2_LAYOUT if layout is None else layout
+    rbw, ft, wm = PREFILL2_LAYOUTS[lay]
+    e = {"bf16": 0, "slabs": 1, "swiglu": 2}[epi]
+    assert e == 1 or splits == 1
+    if not _gpu(x):
+        part = ref.skinny_gemm(x, wp, splits)
+        if e == 1:
+            return part
+        y = part.sum(0)
+        if e == 2:
+            y = ref.swiglu_pairs(y)
+        return y.to(torch.bfloat16)
+    _bf16_contig(x, "x")
+    assert N % (16 * ft * (4 // wm)) == 0 and K % (splits * 64) == 0, (N, K, splits, lay)
+    if e == 1:
+        out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+        rc = kernels().loqa_gemm_prefill2(ptr(x), M, K, ptr(wp), N, splits, None, ptr(out), 1, lay,
+                                          stream_ptr(x))
+    else:
+        out = torch.empty(M, N // 2 if e == 2 else N, dtype=torch.bfloat16, device=x.device)
+        rc = kernels().loqa_gemm_prefill2(ptr(x), M, K, ptr(wp), N, 1, ptr(out), None, e, lay,
+                                          stream_ptr(x))
+    check(rc, "gemm_prefill2")
+    return out

@@ -457,6 +457,17 @@ def perm_gate_up(F):
     return torch.tensor(rows, dtype=torch.long)
 
 
+def swiglu_pairs(y):
+    """silu(gate) * up of a ``perm_gate_up``-ordered product [M, 2F] (16-column
+    pair tiles: 8 gate, 8 up) -> [M, F] (f32)."""
+    M, F2 = y.shape
+    t = y.float().view(M, F2 // 16, 2, 8)
+    g, u = t[:, :, 0], t[:, :, 1]
+    g = g.to(torch.bfloat16).float()
+    u = u.to(torch.bfloat16).float()
+    return (torch.nn.functional.silu(g) * u).reshape(M, F2 // 2)
+
+
 def fused_ln_stats(rowsq_in, rowsum_in, eps, K):
     """LayerNorm (mean, 1/std) per row from per-tile partial sums [tiles, Mpad]."""
     mean = rowsum_in.float().sum(0) / K

@@ -282,6 +282,11 @@ def _share_gpu_worker(rank, world, port, argv):
     os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       LOQA_NO_TUNE="1")   # ranks sharing one GPU cannot time anything
+    # N processes x HIP's default 4 hardware queues oversubscribe the GPU's
+    # queue slots and the scheduler time-slices the ranks (~28x slower steps,
+    # profiles/r3_tp8_share_hwq.txt): one queue per follower, two for the
+    # leader (decoders, prefill, STT, TTS streams)
+    os.environ["GPU_MAX_HW_QUEUES"] = "2" if rank == 0 else "1"
     sys.argv = [sys.argv[0]] + argv
     main()
 

@@ -267,6 +267,7 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     dev = eng._to_device(host)
     meta = eng._build_meta(dev, max_q, max_ctx, False)
     outs = {}
+    monkeypatch.setattr(llama_mod, "PREFILL2", False)
     for S in (8, 0):   # 8: split-K down + o on the prefill GEMM (4 slabs); 0: hipBLASLt
         monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", S)
         monkeypatch.setattr(llama_mod, "PREFILL_O_SPLITS", 4 if S else 0)
@@ -276,6 +277,32 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     # norm); over 22 random-weight layers that drifts ~2% - a layout or
     # indexing error would be O(1)
     assert torch.isfinite(outs[8]).all() and rel < 4e-2, rel
+
+
+def test_llm_prefill2_matches_hipblaslt_gpu(monkeypatch):
+    """Prefill on the v2 hand-written GEMM (qkv / o / down slabs, SwiGLU
+    epilogue on the norm-folded gate|up copy) vs the hipBLASLt path: final
+    hidden rows of a 300-token prompt agree, and the KV cache rows written by
+    the two paths match."""
+    from loqa_hub_amd.models import llama as llama_mod
+    cfg = llama_config("tinyllama")
+    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(1)
+    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
+    r = GenRequest(toks, multi_command_schema(1))
+    eng.submit(r)
+    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
+    dev = eng._to_device(host)
+    meta = eng._build_meta(dev, max_q, max_ctx, False)
+    outs, kvs = {}, {}
+    for on in (True, False):
+        monkeypatch.setattr(llama_mod, "PREFILL2", on)
+        outs[on] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
+        kvs[on] = (eng.kv.k[-1].float().clone(), eng.kv.v[-1].float().clone())
+    rel = float((outs[True] - outs[False]).norm() / outs[False].norm())
+    assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
+    for a, b in zip(kvs[True], kvs[False]):
+        assert float((a - b).norm() / b.norm()) < 4e-2
 
 
 def _to_cpu(obj, seen=None):

@@ -506,3 +506,34 @@ def test_prefill_gemm(M, N, K, S, slabs):
     y = out.sum(0) if slabs else out.float()
     ref = x.float() @ w.float().t()
     assert float((y - ref).norm() / ref.norm()) < (1e-5 if slabs else 5e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K,S,epi", [(318, 256, 512, 1, "bf16"), (100, 384, 1024, 4, "slabs"),
+                                         (1, 128, 256, 2, "slabs"), (481, 512, 640, 1, "swiglu"),
+                                         (161, 256, 256, 1, "swiglu")])
+def test_prefill_gemm2(layout, M, N, K, S, epi):
+    """Prefill GEMM v2 (2 x 2 waves, csrc/kernels/gemm_prefill.hip) vs fp32:
+    bf16 output, f32 split-K slabs, and the SwiGLU pair-tile epilogue."""
+    from loqa_hub_amd import ops
+    from loqa_hub_amd.ops import reference as R
+    rbw, ft, wm = ops.PREFILL2_LAYOUTS[layout]
+    if N % (16 * ft * (4 // wm)):
+        pytest.skip("N not a multiple of the layout's feature block")
+    g = torch.Generator(device="cuda").manual_seed(M + N + layout)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    if epi == "swiglu":
+        w = w[R.perm_gate_up(N // 2).cuda()].contiguous()
+    out = ops.prefill_gemm2(x, ops.shuffle_weight(w), S, epi=epi, layout=layout)
+    ref = x.float() @ w.float().t()
+    if epi == "slabs":
+        assert out.shape == (S, M, N)
+        assert float((out.sum(0) - ref).norm() / ref.norm()) < 1e-5
+    elif epi == "swiglu":
+        assert out.shape == (M, N // 2)
+        r = R.swiglu_pairs(ref)
+        assert float((out.float() - r).norm() / r.norm()) < 1e-2
+    else:
+        assert float((out.float() - ref).norm() / ref.norm()) < 5e-3
