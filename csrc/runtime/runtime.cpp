@@ -2,7 +2,8 @@
 //
 //  * PcmStager   - pinned (hipHostMalloc) host slots that relay PCM frames are
 //                  appended into as they arrive on the gRPC stream, then moved
-//                  to HBM with hipMemcpyAsync on a dedicated H2D stream; a HIP
+//                  to HBM with hipMemcpyAsync on the consuming stream (or, opt-in,
+//                  a dedicated H2D stream); a HIP
 //                  event per transfer gates slot reuse (SURVEY §2.4 "Host<->device
 //                  data path"). Replaces the reference's per-sample Go
 //                  conversion loop + WAV/HTTP round trip (audio_service.go:1048,
@@ -129,11 +130,17 @@ uint64_t mix_hash(uint64_t h, const int32_t* toks, int n) {
 extern "C" {
 
 // ---------------------------------------------------------------- stager API
-void* loqa_stager_create(int nslots, long long samples_per_slot) {
+// own_stream = 0: each upload is issued on the consuming stream itself. A
+// stream created here, after the serving streams, would take the next of the
+// process's hardware queues (HIP maps streams to queues in creation order) and
+// can land on the LLM decoder's queue: both decoders then run ~2x slower
+// (docs/PERF.md, "the 1.8x cliff"). The PCM copy is ~1 MB, so serialising it
+// on the encoder stream costs nothing measurable.
+void* loqa_stager_create(int nslots, long long samples_per_slot, int own_stream) {
   auto* s = new PcmStager();
   s->cap = samples_per_slot;
   s->slots.resize(nslots);
-  if (hipStreamCreateWithFlags(&s->h2d, hipStreamNonBlocking) != hipSuccess) {
+  if (own_stream && hipStreamCreateWithFlags(&s->h2d, hipStreamNonBlocking) != hipSuccess) {
     delete s;
     return nullptr;
   }
@@ -150,12 +157,15 @@ void* loqa_stager_create(int nslots, long long samples_per_slot) {
 void loqa_stager_destroy(void* h) {
   auto* s = static_cast<PcmStager*>(h);
   if (!s) return;
-  hipStreamSynchronize(s->h2d);
+  for (auto& sl : s->slots) {
+    if (sl.done && sl.in_flight) hipEventSynchronize(sl.done);
+  }
+  if (s->h2d) hipStreamSynchronize(s->h2d);
   for (auto& sl : s->slots) {
     if (sl.host) hipHostFree(sl.host);
     if (sl.done) hipEventDestroy(sl.done);
   }
-  hipStreamDestroy(s->h2d);
+  if (s->h2d) hipStreamDestroy(s->h2d);
   delete s;
 }
 
@@ -196,19 +206,21 @@ const void* loqa_stager_host_ptr(void* h, int slot) {
   return static_cast<PcmStager*>(h)->slots[slot].host;
 }
 
-// Async H2D of the slot's samples into dst (device) on the stager's H2D stream;
-// `wait_stream` (the compute stream) is made to wait for the copy. The slot is
-// recycled once the copy's event has completed.
+// Async H2D of the slot's samples into dst (device): on the stager's own H2D
+// stream (then `wait_stream`, the compute stream, waits for the copy) or, with
+// no own stream, on `wait_stream` itself. The slot is recycled once the copy's
+// event has completed.
 int loqa_stager_upload(void* h, int slot, void* dst, long long max_samples, hipStream_t wait_stream) {
   auto* s = static_cast<PcmStager*>(h);
   Slot& sl = s->slots[slot];
   const long long n = sl.len < max_samples ? sl.len : max_samples;
+  hipStream_t cs = s->h2d ? s->h2d : wait_stream;
   hipError_t e = hipSuccess;
-  if (n > 0) e = hipMemcpyAsync(dst, sl.host, (size_t)n * 2, hipMemcpyHostToDevice, s->h2d);
+  if (n > 0) e = hipMemcpyAsync(dst, sl.host, (size_t)n * 2, hipMemcpyHostToDevice, cs);
   if (e != hipSuccess) return (int)e;
-  e = hipEventRecord(sl.done, s->h2d);
+  e = hipEventRecord(sl.done, cs);
   if (e != hipSuccess) return (int)e;
-  if (wait_stream) e = hipStreamWaitEvent(wait_stream, sl.done, 0);
+  if (wait_stream && s->h2d) e = hipStreamWaitEvent(wait_stream, sl.done, 0);
   std::lock_guard<std::mutex> g(s->mu);
   sl.in_flight = true;
   return (int)e;

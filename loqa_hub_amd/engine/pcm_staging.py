@@ -4,8 +4,10 @@ Relay audio arrives on the gRPC stream as PCM16-LE chunks. On the GPU path
 every chunk is appended, as raw bytes, into a pinned (``hipHostMalloc``) slot
 of the native ``PcmStager`` (``csrc/runtime/runtime.cpp``) the moment it
 arrives; at end of speech the STT engine moves the slot to HBM with one
-``hipMemcpyAsync`` on the stager's dedicated H2D stream, and the compute stream
-waits on that copy's event. Nothing converts the samples on the host: the
+``hipMemcpyAsync`` issued on the encoder's own stream (ordered before the
+log-mel kernel that reads it). A dedicated H2D stream is opt-in
+(``LOQA_STAGER_STREAM=1``): created lazily, after the serving streams, it takes
+the next hardware queue and measured the 2x "cliff" (docs/PERF.md). Nothing converts the samples on the host: the
 reference's per-sample ``bytesToFloat32Array`` (``audio_service.go:1048-1101``)
 and WAV/HTTP round trip (``stt_client.go:365-398``) have no counterpart here -
 the f32 conversion is the fused ``pcm16_f32_pad`` kernel on the device.
@@ -17,6 +19,7 @@ still in flight.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -56,8 +59,8 @@ class PCMSlot:
         return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_int16)), (max(n, 1),))[:n]
 
     def upload(self, dst_ptr: int, max_samples: int, wait_stream: int) -> None:
-        """hipMemcpyAsync of the samples to ``dst_ptr`` on the H2D stream; the
-        stream ``wait_stream`` waits for it. The slot is released (recycled
+        """hipMemcpyAsync of the samples to ``dst_ptr``, ordered before the
+        work that follows on ``wait_stream``. The slot is released (recycled
         once the copy completes)."""
         _lib.check(_lib.runtime().loqa_stager_upload(self.stager._h, self.slot, dst_ptr,
                                                      max_samples, wait_stream), "stager_upload")
@@ -74,7 +77,8 @@ class PcmStager:
 
     def __init__(self, nslots: int = 64, cap_samples: int = 480000):
         self.cap = cap_samples
-        self._h = _lib.runtime().loqa_stager_create(nslots, cap_samples)
+        own = int(os.environ.get("LOQA_STAGER_STREAM", "0") == "1")
+        self._h = _lib.runtime().loqa_stager_create(nslots, cap_samples, own)
         if not self._h:
             raise RuntimeError("PCM stager: pinned allocation failed")
         self._lock = threading.Lock()

@@ -13,6 +13,7 @@ Execution plan per batch of utterances (one GPU):
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -30,6 +31,9 @@ def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> tor
 
 
 DEC_PROJ = ("wqkv", "wo", "xq", "xo", "fc1", "fc2")
+
+# split-K of the encoder o projection on the prefill GEMM (0: hipBLASLt)
+ENC_O_SPLITS = int(os.environ.get("LOQA_ENC_O_SPLITS", "2"))
 
 
 class WhisperWeights:
@@ -79,6 +83,11 @@ class WhisperWeights:
         self.lm_head_p = ops.shuffle_weight(lm)
         del lm
         self.dec_p = [{k: ops.shuffle_weight(L[k]) for k in DEC_PROJ} for L in self.dec]
+        # encoder o projection on the hand-written prefill GEMM (fragment-order
+        # copy; 1500-row windows: 17 vs 21.6 us for hipBLASLt at large-v3,
+        # profiles/r3_prefill_gemm2_layouts.txt)
+        self.enc_wo_p = ([ops.shuffle_weight(L["wo"]) for L in self.enc]
+                         if device.type == "cuda" and d % 128 == 0 and ENC_O_SPLITS else None)
         # fused-epilogue copies: LayerNorm weight folded into qkv / xq / fc1 rows,
         # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
         # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)
@@ -177,8 +186,12 @@ class WhisperModel:
             qkv = ops.linear(h, L["wqkv"], L["bqkv"])
             a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
                               causal=False, max_q=T, cu_k=cu)
-            o = ops.linear(a, L["wo"], L["bo"])
-            h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
+            if getattr(w, "enc_wo_p", None) is not None and (d // 64) % ENC_O_SPLITS == 0:
+                part = ops.prefill_gemm2(a, w.enc_wo_p[i], ENC_O_SPLITS, epi="slabs")
+                h = ops.slab_layernorm(part, residual, L["ln2_w"], L["ln2_b"], 1e-5, bias=L["bo"])
+            else:
+                o = ops.linear(a, L["wo"], L["bo"])
+                h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
             m = ops.linear(h, L["fc1"], L["fc1_b"])
             ops.gelu_bias_(m)
             delta = ops.linear(m, L["fc2"], L["fc2_b"])

@@ -134,7 +134,7 @@ _CAR_SIGS = {
 }
 
 _RUNTIME_SIGS = {
-    "loqa_stager_create": ([c_int, c_ll], c_void_p),
+    "loqa_stager_create": ([c_int, c_ll, c_int], c_void_p),
     "loqa_stager_destroy": ([c_void_p], None),
     "loqa_stager_acquire": ([c_void_p], c_int),
     "loqa_stager_append": ([c_void_p, c_int, c_void_p, c_ll], c_ll),
