@@ -133,8 +133,8 @@ extern "C" {
 // own_stream = 0: each upload is issued on the consuming stream itself. A
 // stream created here, after the serving streams, would take the next of the
 // process's hardware queues (HIP maps streams to queues in creation order) and
-// can land on the LLM decoder's queue: both decoders then run ~2x slower
-// (docs/PERF.md, "the 1.8x cliff"). The PCM copy is ~1 MB, so serialising it
+// can land on a decoder's queue (both decoders ~2x slower when they share one;
+// docs/PERF.md, "the 1.8x cliff"). The PCM copy is ~1 MB, so serialising it
 // on the encoder stream costs nothing measurable.
 void* loqa_stager_create(int nslots, long long samples_per_slot, int own_stream) {
   auto* s = new PcmStager();

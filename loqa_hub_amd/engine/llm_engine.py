@@ -80,7 +80,8 @@ class LLMEngine:
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.tp = tp or TPGroup()
-        from ..utils.streams import decode_cus
+        from ..utils.streams import decode_cus, init_pools
+        init_pools(self.device)       # fixed stream -> hardware-queue placement
         self.max_wgs = decode_cus(self.device, "LOQA_LLM_CUS", "LOQA_LLM_MAX_WGS")
         with ops.decode_cap(self.max_wgs):
             self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp,

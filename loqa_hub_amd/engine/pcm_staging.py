@@ -6,8 +6,9 @@ of the native ``PcmStager`` (``csrc/runtime/runtime.cpp``) the moment it
 arrives; at end of speech the STT engine moves the slot to HBM with one
 ``hipMemcpyAsync`` issued on the encoder's own stream (ordered before the
 log-mel kernel that reads it). A dedicated H2D stream is opt-in
-(``LOQA_STAGER_STREAM=1``): created lazily, after the serving streams, it takes
-the next hardware queue and measured the 2x "cliff" (docs/PERF.md). Nothing converts the samples on the host: the
+(``LOQA_STAGER_STREAM=1``): created lazily, after the serving streams, it would
+take the next hardware queue (stream placement: docs/PERF.md, "the 1.8x
+cliff"). Nothing converts the samples on the host: the
 reference's per-sample ``bytesToFloat32Array`` (``audio_service.go:1048-1101``)
 and WAV/HTTP round trip (``stt_client.go:365-398``) have no counterpart here -
 the f32 conversion is the fused ``pcm16_f32_pad`` kernel on the device.

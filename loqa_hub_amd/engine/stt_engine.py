@@ -31,6 +31,9 @@ from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
 N_SAMPLES = 480000  # 30 s @ 16 kHz
+# numpy PCM of direct submissions staged through the pinned stager (0: a
+# one-off pinned tensor copy per request)
+PCM_STAGER = os.environ.get("LOQA_PCM_STAGER", "1") != "0"
 
 
 @dataclass(eq=False)
@@ -71,7 +74,8 @@ class STTEngine:
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        from ..utils.streams import decode_cus
+        from ..utils.streams import decode_cus, init_pools
+        init_pools(self.device)       # fixed stream -> hardware-queue placement
         self.max_wgs = decode_cus(self.device, "LOQA_STT_CUS", "LOQA_STT_MAX_WGS")
         # optional: tune the decode GEMMs under a background weight stream
         # (ops.contended_tuning; measured noisier and 5 % slower end to end)
@@ -169,7 +173,8 @@ class STTEngine:
             cur = torch.cuda.current_stream(self.device).cuda_stream
             stager = self._stager()
             for r, o, n in zip(reqs, offs[:-1], lens):
-                slot = r.staged if r.staged is not None else stager.stage(r.pcm)
+                slot = r.staged if r.staged is not None else (
+                    stager.stage(r.pcm) if PCM_STAGER else None)
                 if slot is None:        # every pinned slot busy: a one-off pinned copy
                     h = torch.from_numpy(np.ascontiguousarray(r.pcm[:n], np.int16)).pin_memory()
                     pcm[int(o):int(o) + n].copy_(h, non_blocking=True)

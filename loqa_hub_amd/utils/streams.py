@@ -115,11 +115,58 @@ def _log_slot(role: str, st, device, priority: int) -> None:
               flush=True)
 
 
+# Explicit placement: every serving stream is the pool stream of a FIXED index
+# (its hardware queue follows from the index), whatever else drew pool streams
+# before. Defaults = the placement measured best (docs/PERF.md, "Stream
+# placement, round 3"; profiles/r3_stream_placement.txt): the LLM decoder on
+# normal-priority slot 2, the Whisper decoder on high-priority slot 30, the
+# encoder worker on normal-priority slot 28, the prefill worker on slot 3
+# (pools created first thing by init_pools, so slot -> queue is fixed).
+# Round 3 found the old
+# implicit placement had depended on the STT upload drawing one pool stream per
+# batch: removing that draw moved the LLM decoder to slot 0 and halved the
+# throughput (19.1 -> 9.8 utt/s). LOQA_SLOT_<ROLE> overrides (search).
+DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3}
+
+
+def init_pools(device: torch.device) -> None:
+    """Create both PyTorch stream pools (normal and high priority) of ``device``
+    in one go, before the engines create anything else, so pool index ->
+    creation order -> hardware queue is the same in every process that runs
+    this code (the engines call it first thing)."""
+    if torch.device(device).type != "cuda":
+        return
+    _pool_table(device, 0)
+    _pool_table(device, -1)
+
+
+def role_slot(role: str) -> int | None:
+    v = os.environ.get(f"LOQA_SLOT_{role.upper()}")
+    if v is not None:
+        return int(v) if v != "" and int(v) >= 0 else None
+    return DEFAULT_SLOTS.get(role)
+
+
+def placed_stream(device: torch.device, role: str, priority: int = 0):
+    """The serving stream of ``role``: the pool stream at its fixed slot
+    (``LOQA_SLOT_<ROLE>`` = -1: the next pool stream, the old behaviour)."""
+    slot = role_slot(role)
+    if slot is None:
+        st = torch.cuda.Stream(device, priority=priority)
+    else:
+        st = aligned_pool_stream(device, priority, slot)
+    _log_slot(role, st, device, priority)
+    return st
+
+
 def pool_stream(device: torch.device, role: str, priority: int = 0):
-    """A PyTorch pool stream for a worker thread, first drawing
-    ``LOQA_POOL_SKEW_<ROLE>`` extra pool streams (hardware-queue placement
-    search; see decoder_streams)."""
-    for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{role.upper()}", "0") or 0)):
+    """A worker thread's stream: the explicitly placed pool stream of ``role``
+    (``placed_stream``); ``LOQA_POOL_SKEW_<ROLE>`` = n instead draws n extra
+    pool streams and takes the next one (the round-2 placement search)."""
+    skew = int(os.environ.get(f"LOQA_POOL_SKEW_{role.upper()}", "0") or 0)
+    if not skew:
+        return placed_stream(device, role, priority)
+    for _ in range(skew):
         torch.cuda.Stream(device, priority=priority)
     st = torch.cuda.Stream(device, priority=priority)
     _log_slot(role, st, device, priority)
@@ -183,15 +230,10 @@ def stream_for(device: torch.device, env_key: str, priority: int = 0):
         return cu_masked_stream(device, parse_cu_spec(spec, n))
     role = _ROLE.get(env_key)
     if role is None or not os.environ.get("LOQA_QSKEW"):
-        # default: PyTorch pool streams (the placement every number in
-        # docs/PERF.md was measured with; see decoder_streams for the caveat).
+        # default: explicitly placed pool streams (placed_stream);
         # LOQA_POOL_SKEW_STT / _LLM = n draws n pool streams first, moving this
-        # decoder n hardware queues along (placement search).
-        for _ in range(int(os.environ.get(f"LOQA_POOL_SKEW_{(role or '').upper()}", "0") or 0)):
-            torch.cuda.Stream(device, priority=priority)
-        st = torch.cuda.Stream(device, priority=priority)
-        _log_slot(role or env_key, st, device, priority)
-        return st
+        # decoder n hardware queues along (the round-2 placement search).
+        return pool_stream(device, role or env_key, priority)
     _PRIO[role] = priority
     prios = {"stt": _PRIO.get("stt", -1), "llm": _PRIO.get("llm", 0)}
     return decoder_streams(device, prios)[role]
