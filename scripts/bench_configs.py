@@ -195,7 +195,7 @@ def config_3(args, dev, nats) -> dict:
     utts = make_batch(3, 16, [1, 2, 3, 4])
     rows, rollbacks = [], 0
 
-    async def one(i, u):
+    async def one(i, u, faults=True, out=None):
         nonlocal rollbacks
         j = PipelineJob(u.relay_id, f"t{i}", u.pcm, transcript_hint=u.text)
         j.t["start"] = time.perf_counter()
@@ -203,16 +203,20 @@ def config_3(args, dev, nats) -> dict:
                                                   else u.text)
         toks = []
         j.on_tokens = lambda ids: toks.append((time.perf_counter(), len(ids)))
-        fault = i % 4 == 3
-        set_faults("nats_down%0.5" if fault else "")
+        fault = faults and i % 4 == 3
+        if faults:
+            set_faults("nats_down%0.5" if fault else "")
         await pipe._llm_stage([j])
-        set_faults("")
+        if faults:
+            set_faults("")
         if fault and j.queue is not None and j.queue.rollback_occurred:
             rollbacks += 1
         t_first = toks[1][0] if len(toks) > 1 else toks[0][0]
         n_tok = sum(n for _, n in toks)
         dur = toks[-1][0] - toks[0][0]
-        rows.append((j, (t_first - j.t["start"]) * 1e3, n_tok / max(dur, 1e-9)))
+        (rows if out is None else out).append((j, (t_first - j.t["start"]) * 1e3, n_tok / max(dur, 1e-9)))
+
+    loaded: list = []
 
     async def main():
         for i, u in enumerate(utts[:4]):
@@ -220,10 +224,35 @@ def config_3(args, dev, nats) -> dict:
         rows.clear()
         for k in range(args.per_stream * 4):
             await one(k, utts[k % len(utts)])
+        if args.concurrency > 1:
+            # the same streaming path under load: C closed-loop text streams
+            # sharing the continuous batch (no fault injection: it is global)
+            async def client(c):
+                for k in range(args.per_stream):
+                    await one(100 + c * args.per_stream + k, utts[(c + k) % len(utts)], faults=False,
+                              out=loaded)
+            t0 = time.perf_counter()
+            await asyncio.gather(*[client(c) for c in range(args.concurrency)])
+            loaded.append(time.perf_counter() - t0)
     loop.run_until_complete(main())
     jobs = [r[0] for r in rows]
     st = added_command_stats(jobs)
     llm.stop()
+    extra = {}
+    if loaded:
+        wall = loaded.pop()
+        lj = [r[0] for r in loaded]
+        lst = added_command_stats(lj)
+        extra = {
+            "loaded_streams": args.concurrency,
+            "loaded_utterances_per_s": round(len(lj) / wall, 2),
+            "loaded_first_token_ms_p50": round(float(np.median([r[1] for r in loaded])), 2),
+            "loaded_first_token_ms_p90": round(float(np.percentile([r[1] for r in loaded], 90)), 2),
+            "loaded_stream_tokens_per_s_p50": round(float(np.median([r[2] for r in loaded])), 1),
+            "loaded_ms_per_added_command_e2e_marginal":
+                None if lst["e2e_marginal_ms_per_added_command"] is None
+                else round(lst["e2e_marginal_ms_per_added_command"], 2),
+        }
     return {
         "config": 3, "model": "llama3-8b", "n_gpus": 1, "tp": 1, "dtype": "bf16",
         "utterances": len(jobs),
@@ -233,6 +262,7 @@ def config_3(args, dev, nats) -> dict:
         else round(st["e2e_marginal_ms_per_added_command"], 2),
         "ms_per_added_command_ref_equiv": st["ref_equiv_ms_per_added_command"],
         "rollbacks_executed": rollbacks,
+        **extra,
         "data": "synthetic multi-command transcripts + random-init weights (grammar-constrained decode)",
     }
 
@@ -297,6 +327,8 @@ def main() -> int:
     ap.add_argument("--per-stream", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1, help="config 5: tensor-parallel degree")
+    ap.add_argument("--concurrency", type=int, default=8,
+                    help="config 3: closed-loop text streams of the loaded run (1: unloaded only)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="TP ranks share cuda:0 (spawned here when not under torchrun)")
     ap.add_argument("--compact", action="store_true",

@@ -63,7 +63,8 @@ def main(path, layers=32):
         for n, v in by.items():
             per.setdefault(n, []).append(v / 1e3)
     print(f"llm prefill: {len(passes)} passes; median span {st.median(spans):.0f} us, "
-          f"summed own-queue kernel time {st.median(busy):.0f} us, own-queue idle gaps {st.median(gaps):.0f} us")
+          f"summed own-queue kernel time {st.median(busy):.0f} us, "
+          f"own-queue idle gaps {st.median(gaps):.0f} us")
     for n, v in sorted(per.items(), key=lambda kv: -st.median(kv[1]))[:14]:
         print(f"  {st.median(v):9.1f} us/pass  {n}")
 
