@@ -1409,7 +1409,8 @@ def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, slabs: bool
 
 # v2 layouts: (row tiles, feature tiles) per wave and waves along M (the other
 # 4 / WM waves go along N) -> workgroup tile (16 WM rbw) x (16 (4 / WM) ft)
-PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1)}
+PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1),
+                    5: (5, 4, 2), 6: (5, 8, 2), 7: (10, 4, 2)}   # 5-7: v3 (weights via LDS)
 # layout 3 (v1's 1 x 4 waves with the one-barrier pipeline) measured fastest on
 # every prefill / encoder shape (profiles/r3_prefill_gemm2_layouts.txt)
 PREFILL2_LAYOUT = int(os.environ.get("LOQA_PREFILL2_LAYOUT", "3"))

@@ -509,7 +509,7 @@ def test_prefill_gemm(M, N, K, S, slabs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K,S,epi", [(318, 256, 512, 1, "bf16"), (100, 384, 1024, 4, "slabs"),
                                          (1, 128, 256, 2, "slabs"), (481, 512, 640, 1, "swiglu"),
                                          (161, 256, 256, 1, "swiglu")])
