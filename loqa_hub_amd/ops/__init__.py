@@ -1381,36 +1381,12 @@ def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: tor
 
 
 # ------------------------------------------------------------- prefill GEMM
-PREFILL_GEMM_NT = 128     # features per workgroup (kernel constant)
-
-
-def prefill_gemm(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, slabs: bool = False) -> torch.Tensor:
-    """x [M, K] bf16 @ W^T for ~100-512 rows with W given pre-shuffled
-    (``shuffle_weight``), weights streamed once (``csrc/kernels/gemm_prefill.hip``).
-    ``slabs``: f32 split-K partials [S, M, N] (summed by a slab consumer),
-    else bf16 [M, N] (S = 1)."""
-    M, K = x.shape
-    N = wp.shape[0] * 16
-    assert wp.shape[1] * 32 == K
-    if not _gpu(x):
-        part = ref.skinny_gemm(x, wp, splits)
-        return part if slabs else part.sum(0).to(torch.bfloat16)
-    _bf16_contig(x, "x")
-    assert N % PREFILL_GEMM_NT == 0 and K % (splits * 128) == 0 and (slabs or splits == 1)
-    if slabs:
-        out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
-        rc = kernels().loqa_gemm_prefill(ptr(x), M, K, ptr(wp), N, splits, None, ptr(out), stream_ptr(x))
-    else:
-        out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        rc = kernels().loqa_gemm_prefill(ptr(x), M, K, ptr(wp), N, 1, ptr(out), None, stream_ptr(x))
-    check(rc, "gemm_prefill")
-    return out
+PREFILL_GEMM_NT = 128     # features per workgroup of the default layout (3)
 
 
 # v2 layouts: (row tiles, feature tiles) per wave and waves along M (the other
 # 4 / WM waves go along N) -> workgroup tile (16 WM rbw) x (16 (4 / WM) ft)
-PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1),
-                    5: (5, 4, 2), 6: (5, 8, 2), 7: (10, 4, 2)}   # 5-7: v3 (weights via LDS)
+PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1)}
 # layout 3 (v1's 1 x 4 waves with the one-barrier pipeline) measured fastest on
 # every prefill / encoder shape (profiles/r3_prefill_gemm2_layouts.txt)
 PREFILL2_LAYOUT = int(os.environ.get("LOQA_PREFILL2_LAYOUT", "3"))

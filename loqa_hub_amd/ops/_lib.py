@@ -111,7 +111,6 @@ _KERNEL_SIGS = {
     "loqa_step_fetch": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p, c_void_p],
     "loqa_whisper_mega": [c_void_p, c_int, c_void_p],
-    "loqa_gemm_prefill": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "loqa_gemm_prefill2": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                            c_int, c_void_p],
     "loqa_init_uniform4": [c_void_p, c_ll, c_int, c_ll, c_ll, c_ll, ctypes.c_uint, c_float, c_void_p],

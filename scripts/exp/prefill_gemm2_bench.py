@@ -1,5 +1,4 @@
-"""Prefill GEMM v2 (2 x 2 waves, ops.prefill_gemm2) vs hipBLASLt (F.linear) vs
-v1 (ops.prefill_gemm) on the Llama-3-8B prefill projections and the Whisper
+"""Prefill GEMM (ops.prefill_gemm2, every wave layout) vs hipBLASLt (F.linear) on the Llama-3-8B prefill projections and the Whisper
 encoder projections, cold weights (rotated over copies that exceed the
 256 MB Infinity Cache), plus relative error vs fp32.
 
@@ -62,9 +61,6 @@ for name, m, N, K, splits in SHAPES:
             us = timeit(lambda i: ops.prefill_gemm2(x, wps[i], S, epi=epi, layout=lay), nw)
             row[f"v2_l{lay}_s{S}_us"] = us
             row[f"v2_l{lay}_s{S}_err"] = round(err, 5)
-    for S in splits:
-        if N % 128 == 0 and K % (128 * S) == 0:
-            row[f"v1_s{S}_us"] = timeit(lambda i: ops.prefill_gemm(x, wps[i], S, slabs=S > 1), nw)
     best = min((v, k) for k, v in row.items() if k.startswith("v2_") and k.endswith("_us"))
     row["best"] = best[1]
     row["best_tflops"] = round(tflop / best[0], 1)

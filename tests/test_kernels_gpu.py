@@ -494,22 +494,7 @@ def test_attention_prefill2_shapes(D, H, Hkv, lens, causal):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K,S,slabs", [(318, 256, 512, 1, False), (100, 384, 1024, 4, True),
-                                           (161, 128, 256, 2, True)])
-def test_prefill_gemm(M, N, K, S, slabs):
-    """Weight-streaming prefill GEMM (csrc/kernels/gemm_prefill.hip) vs fp32."""
-    from loqa_hub_amd import ops
-    g = torch.Generator(device="cuda").manual_seed(M + N)
-    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
-    out = ops.prefill_gemm(x, ops.shuffle_weight(w), S, slabs=slabs)
-    y = out.sum(0) if slabs else out.float()
-    ref = x.float() @ w.float().t()
-    assert float((y - ref).norm() / ref.norm()) < (1e-5 if slabs else 5e-3)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("layout", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K,S,epi", [(318, 256, 512, 1, "bf16"), (100, 384, 1024, 4, "slabs"),
                                          (1, 128, 256, 2, "slabs"), (481, 512, 640, 1, "swiglu"),
                                          (161, 256, 256, 1, "swiglu")])
