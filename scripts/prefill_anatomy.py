@@ -15,6 +15,11 @@ import statistics as st
 import sys
 
 
+# kernels only the Llama prefill launches (its hipBLASLt GEMMs are shared names)
+LLM_PREFILL = ("attn_prefill2_kernel<128, true>", "rope_kv_append", "rmsnorm", "silu_mul",
+               "gemm_prefill2_kernel", "slab_rope_append")
+
+
 def _open(path):
     return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
 
@@ -58,6 +63,8 @@ def main(path, layers=32):
         gaps.append(g / 1e3)
         by = {}
         for r in mine:
+            if not any(k in r[3] for k in LLM_PREFILL):
+                continue          # hipBLASLt (shared with the encoder) and other engines' kernels
             name = r[3].split("(")[0][:90]
             by[name] = by.get(name, 0) + (r[1] - r[0])
         for n, v in by.items():
