@@ -34,6 +34,11 @@ DEC_PROJ = ("wqkv", "wo", "xq", "xo", "fc1", "fc2")
 
 # split-K of the encoder o projection on the prefill GEMM (0: hipBLASLt)
 ENC_O_SPLITS = int(os.environ.get("LOQA_ENC_O_SPLITS", "2"))
+# conv stem (implicit-im2col conv1d with bias + GELU (+ positions) fused) and
+# the fc2 projection (split-K slabs summed by the next LayerNorm) on the
+# LDS-tiled MFMA GEMM (csrc/kernels/gemm_tile.hip); 0: im2col + hipBLASLt
+ENC_TILE = int(os.environ.get("LOQA_ENC_TILE", "1"))
+ENC_FC2_SPLITS = int(os.environ.get("LOQA_ENC_FC2_SPLITS", "4"))
 
 
 class WhisperWeights:
@@ -88,6 +93,11 @@ class WhisperWeights:
         # profiles/r3_prefill_gemm2_layouts.txt)
         self.enc_wo_p = ([ops.shuffle_weight(L["wo"]) for L in self.enc]
                          if device.type == "cuda" and d % 128 == 0 and ENC_O_SPLITS else None)
+        # conv stem weights in the implicit-im2col order (k = tap * Cin + c)
+        # and f32 biases for the tiled GEMM's epilogue
+        self.conv1_wt = ops.conv_k3_weight(self.conv1_w, cfg.n_mels)
+        self.conv2_wt = ops.conv_k3_weight(self.conv2_w, d)
+        self.conv1_bf, self.conv2_bf = self.conv1_b.float(), self.conv2_b.float()
         # fused-epilogue copies: LayerNorm weight folded into qkv / xq / fc1 rows,
         # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
         # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)
@@ -168,21 +178,37 @@ class WhisperModel:
         d, M = cfg.d_model, cfg.n_mels
         mel = ops.log_mel(audio, self.mel)  # [B, M, 3000] bf16
         frames = mel.shape[-1]
-        cols = ops.im2col_k3(mel, (M * frames, frames, 1), B, M, frames, 1)
-        x1 = ops.linear(cols, w.conv1_w)                      # [B*3000, d]
-        ops.gelu_bias_(x1, w.conv1_b)
-        cols2 = ops.im2col_k3(x1, (frames * d, 1, d), B, d, frames, 2)
-        x = ops.linear(cols2, w.conv2_w)                      # [B*1500, d]
-        ops.gelu_bias_(x, w.conv2_b, w.pos_enc)               # + positional embedding
+        tile = ENC_TILE and audio.is_cuda and d % 128 == 0 and M % 64 == 0
+        if tile:
+            # conv1d stem on the tiled MFMA GEMM: the loader gathers the k = 3
+            # taps from time-major rows (no column matrix), bias + GELU (+ the
+            # sinusoidal positions for conv2) in the epilogue
+            mel_t = mel.transpose(1, 2).contiguous().view(B * frames, M)
+            x1 = ops.gemm_tile(mel_t, w.conv1_wt, bias=w.conv1_bf, act="gelu", conv=(B, 1), layout=0)
+            x = ops.gemm_tile(x1, w.conv2_wt, bias=w.conv2_bf, act="gelu", pos=w.pos_enc,
+                              conv=(B, 2), layout=0)
+        else:
+            cols = ops.im2col_k3(mel, (M * frames, frames, 1), B, M, frames, 1)
+            x1 = ops.linear(cols, w.conv1_w)                      # [B*3000, d]
+            ops.gelu_bias_(x1, w.conv1_b)
+            cols2 = ops.im2col_k3(x1, (frames * d, 1, d), B, d, frames, 2)
+            x = ops.linear(cols2, w.conv2_w)                      # [B*1500, d]
+            ops.gelu_bias_(x, w.conv2_b, w.pos_enc)               # + positional embedding
         T = cfg.n_audio_ctx
         cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device=audio.device)
         H, D = cfg.n_heads, cfg.head_dim
         residual = x
         h = ops.layernorm(x, w.enc[0]["ln1_w"], w.enc[0]["ln1_b"], 1e-5)
         delta = None
+        part2 = None
+        S2 = ENC_FC2_SPLITS if (tile and cfg.ffn_dim % (ENC_FC2_SPLITS * 64) == 0) else 0
         for i, L in enumerate(w.enc):
             if i > 0:
-                h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
+                if part2 is not None:
+                    h = ops.slab_layernorm(part2, residual, L["ln1_w"], L["ln1_b"], 1e-5,
+                                           bias=w.enc[i - 1]["fc2_b"])
+                else:
+                    h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
             qkv = ops.linear(h, L["wqkv"], L["bqkv"])
             a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
                               causal=False, max_q=T, cu_k=cu)
@@ -194,7 +220,15 @@ class WhisperModel:
                 h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
             m = ops.linear(h, L["fc1"], L["fc1_b"])
             ops.gelu_bias_(m)
-            delta = ops.linear(m, L["fc2"], L["fc2_b"])
+            if S2:
+                # fc2 as split-K f32 slabs (hipBLASLt's N = 1280 tiles leave
+                # most CUs idle at 1500 rows), summed by the next LayerNorm
+                part2 = ops.gemm_tile(m, L["fc2"], epi="slabs", splits=S2, layout=4)
+            else:
+                delta = ops.linear(m, L["fc2"], L["fc2_b"])
+        if part2 is not None:
+            return ops.slab_layernorm(part2, residual, w.enc_ln_w, w.enc_ln_b, 1e-5,
+                                      bias=w.enc[-1]["fc2_b"])
         return ops.layernorm(delta, w.enc_ln_w, w.enc_ln_b, 1e-5, residual=residual)
 
     def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:

@@ -22,6 +22,7 @@ import os
 import torch
 
 from . import reference as ref
+from . import _lib
 from ._lib import FusedParams, check, kernels, ptr, stream_ptr
 
 
@@ -1426,3 +1427,140 @@ def prefill_gemm2(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, epi: str =
                                           stream_ptr(x))
     check(rc, "gemm_prefill2")
     return out
+
+
+# ------------------------------------------------------- LDS-tiled MFMA GEMM
+# csrc/kernels/gemm_tile.hip: (waves along N, waves along M, LDS stages); the
+# workgroup tile is (64 * WN features) x (64 * WM rows).
+GEMM_TILE_LAYOUTS = {0: (2, 2, 2), 1: (2, 2, 3), 2: (4, 2, 2), 3: (2, 4, 2), 4: (4, 2, 3),
+                     5: (2, 4, 3), 6: (2, 4, 2), 7: (4, 2, 2), 8: (2, 2, 2), 9: (2, 2, 2)}
+# (FN, FM) 16-wide MFMA fragments per wave along features / rows
+GEMM_TILE_FRAGS = {6: (8, 4), 7: (4, 8), 8: (8, 4), 9: (4, 8)}
+
+
+def gemm_tile_dims(layout: int) -> tuple[int, int]:
+    """(features, rows) of a layout's workgroup tile."""
+    wn, wm, _ = GEMM_TILE_LAYOUTS[layout]
+    fn, fm = GEMM_TILE_FRAGS.get(layout, (4, 4))
+    return 16 * fn * wn, 16 * fm * wm
+_GT_EPI = {"bf16": 0, "slabs": 1, "swiglu": 2}
+_GT_ZEROS: dict = {}
+
+
+def gemm_tile_layout(M: int, N: int, K: int, epi: str = "bf16") -> int:
+    """Layout for a shape: ``LOQA_GT_LAYOUT`` if set, else the measured table
+    (scripts/exp/gemm_tile_bench.py, docs/PERF.md)."""
+    env = os.environ.get("LOQA_GT_LAYOUT")
+    if env:
+        return int(env)
+    return 1
+
+
+def _gt_ref(x2: torch.Tensor, w: torch.Tensor, bias, act: str | None, pos, epi: str, splits: int):
+    xf, wf = x2.float(), w.float()
+    if epi == "slabs":
+        K = xf.shape[1]
+        ks = K // splits
+        return torch.stack([xf[:, s * ks:(s + 1) * ks] @ wf[:, s * ks:(s + 1) * ks].t()
+                            for s in range(splits)])
+    y = xf @ wf.t()
+    if epi == "swiglu":
+        F = w.shape[0] // 2
+        g = y[:, :F].to(torch.bfloat16).float()
+        u = y[:, F:].to(torch.bfloat16).float()
+        return (g * torch.sigmoid(g) * u).to(torch.bfloat16)
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = y.to(torch.bfloat16).float()
+        y = 0.5 * y * (1.0 + torch.erf(y * 0.70710678118654752))
+    if pos is not None:
+        rows = torch.arange(y.shape[0], device=y.device) % pos.shape[0]
+        y = y.to(torch.bfloat16).float() + pos.float()[rows]
+    return y.to(torch.bfloat16)
+
+
+def conv_k3_weight(w: torch.Tensor, cin: int) -> torch.Tensor:
+    """torch conv1d weight flattened [Cout, Cin * 3] (k = c * 3 + tap) -> the
+    tiled GEMM's implicit-im2col order [Cout, 3 * Cin] (k = tap * Cin + c)."""
+    cout = w.shape[0]
+    return w.reshape(cout, cin, 3).permute(0, 2, 1).reshape(cout, 3 * cin).contiguous()
+
+
+def conv_k3_im2col_ref(x: torch.Tensor, B: int, tin: int, stride: int) -> torch.Tensor:
+    """Reference implicit im2col: x [B * tin, cin] time-major -> [B * tout, 3 * cin]
+    (k = tap * cin + c, zero padding 1)."""
+    cin = x.shape[1]
+    xb = x.reshape(B, tin, cin)
+    xp = torch.nn.functional.pad(xb, (0, 0, 1, 1))
+    tout = (tin + 2 - 3) // stride + 1
+    cols = [xp[:, tap: tap + stride * (tout - 1) + 1: stride] for tap in range(3)]
+    return torch.cat(cols, dim=2).reshape(B * tout, 3 * cin)
+
+
+def gemm_tile(x: torch.Tensor, w: torch.Tensor, *, bias: torch.Tensor | None = None,
+              act: str | None = None, pos: torch.Tensor | None = None, epi: str = "bf16",
+              splits: int = 1, layout: int | None = None, out: torch.Tensor | None = None,
+              conv: tuple[int, int] | None = None) -> torch.Tensor:
+    """Y = X W^T on the LDS-tiled MFMA GEMM (``csrc/kernels/gemm_tile.hip``).
+
+    x [M, K] bf16 (row stride may exceed K), w [N, K] bf16 row-major.
+    ``epi``: "bf16" -> [M, N] (+ f32 ``bias``, ``act`` "gelu", + bf16 ``pos``
+    rows m % len(pos)); "slabs" -> f32 split-K partials [S, M, N]; "swiglu" ->
+    silu(gate) * up [M, N / 2] with gate rows [0, N/2) and up rows [N/2, N).
+    ``conv`` = (B, stride): x is a time-major conv input [B * T_in, Cin] and w a
+    ``conv_k3_weight`` [N, 3 * Cin]; the output rows are (b, t_out) of the
+    k = 3, padding 1 conv1d (implicit im2col: the input rows are gathered by the
+    tile loader, no column matrix is built)."""
+    N, K = w.shape
+    if conv is not None:
+        B, stride = conv
+        cin = x.shape[1]
+        assert K == 3 * cin
+        tin = x.shape[0] // B
+        tout = (tin + 2 - 3) // stride + 1
+        M = B * tout
+    else:
+        M = x.shape[0]
+        assert x.shape[1] == K, (x.shape, w.shape)
+    if not _gpu(x):
+        x2 = conv_k3_im2col_ref(x, B, tin, stride) if conv is not None else x
+        y = _gt_ref(x2, w, bias, act, pos, epi, splits)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("gemm_tile needs bf16 operands")
+    if x.stride(1) != 1 or not w.is_contiguous():
+        raise ValueError("gemm_tile needs K-contiguous operands")
+    lay = gemm_tile_layout(M, N, K, epi) if layout is None else layout
+    e = _GT_EPI[epi]
+    p = _lib.GemmTileParams()
+    p.x, p.ldx, p.w = ptr(x), x.stride(0), ptr(w)
+    p.M, p.N, p.K, p.S, p.epi = M, N, K, splits, e
+    p.act = 1 if act == "gelu" else 0
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N
+    p.bias = ptr(bias)
+    if pos is not None:
+        assert pos.dtype == torch.bfloat16 and pos.is_contiguous() and pos.shape[1] == N
+        p.pos, p.pos_rows = ptr(pos), pos.shape[0]
+    if e == 1:
+        y = out if out is not None else torch.empty(splits, M, N, dtype=torch.float32,
+                                                    device=x.device)
+        p.part = ptr(y)
+    else:
+        cols = N // 2 if e == 2 else N
+        y = out if out is not None else torch.empty(M, cols, dtype=torch.bfloat16, device=x.device)
+        assert y.shape == (M, cols) and y.stride(1) == 1
+        p.y, p.ldy = ptr(y), y.stride(0)
+    if conv is not None:
+        z = _GT_ZEROS.get((x.device, cin))
+        if z is None:
+            z = _GT_ZEROS[(x.device, cin)] = torch.zeros(max(cin, 64), dtype=torch.bfloat16,
+                                                         device=x.device)
+        p.conv_cin, p.conv_tin, p.conv_tout, p.conv_stride, p.zeros = cin, tin, tout, stride, ptr(z)
+    p.layout = lay
+    check(kernels().loqa_gemm_tile(ctypes.byref(p), stream_ptr(x)), "gemm_tile")
+    return y

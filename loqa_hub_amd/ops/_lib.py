@@ -43,6 +43,19 @@ class FusedParams(ctypes.Structure):
     ]
 
 
+class GemmTileParams(ctypes.Structure):
+    """Mirror of ``GemmTileParams`` in csrc/kernels/gemm_tile.hip."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_ll), ("w", c_void_p),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("S", c_int),
+        ("epi", c_int), ("act", c_int), ("bias", c_void_p),
+        ("pos", c_void_p), ("pos_rows", c_int),
+        ("y", c_void_p), ("ldy", c_ll), ("part", c_void_p),
+        ("conv_cin", c_int), ("conv_tin", c_int), ("conv_tout", c_int), ("conv_stride", c_int),
+        ("zeros", c_void_p), ("layout", c_int),
+    ]
+
+
 class WhisperMegaParams(ctypes.Structure):
     """Mirror of ``MegaParams`` in csrc/kernels/whisper_mega.hip."""
     _fields_ = [
@@ -83,6 +96,7 @@ _KERNEL_SIGS = {
                          c_void_p],
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "loqa_skinny_fused": [c_void_p, c_void_p],
+    "loqa_gemm_tile": [c_void_p, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
