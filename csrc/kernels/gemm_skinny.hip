@@ -16,6 +16,7 @@
 //     go to f32 slabs part[S][Mpad][N] that the NEXT kernel sums in its prologue
 //     (slab_ops.hip) - deterministic, no atomics, no extra launch.
 #include "common.h"
+#include <stdlib.h>
 
 typedef float float4v_ __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -862,11 +863,34 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   }
 }
 
+// Deep prefetch (LOQA_FUSED_DEEP bit mask, Mpad 16): bit 0 - a wave's whole k
+// range in ONE prefetch group when it is 10 k-steps (Whisper d = 1280, S = 1:
+// every weight load of the wave in flight at once instead of two 2-step
+// groups at a time); bit 1 - 8-step groups when it is a multiple of 8 (Llama
+// K = 4096; measured slower in the pipeline: 3.51 -> 3.68 ms per LLM step). The decode
+// GEMMs are latency-bound beside the concurrent decoder: fewer dependent
+// prefetch rounds per kernel, not bandwidth, is what a shorter kernel needs.
+static int g_fused_deep = -1;
+
 template <int RT, int MT, int WR, int MODE, int NORM>
 static int launch_fused(const FusedArgs& a, hipStream_t st) {
   constexpr int WK = 4 / WR;
   dim3 grid(a.N / (16 * RT * WR), a.S);
   const int kw = a.K / 32 / (a.S * WK);
+  if (g_fused_deep < 0) {
+    const char* e = getenv("LOQA_FUSED_DEEP");
+    g_fused_deep = e ? atoi(e) : 0;
+  }
+  if constexpr (MT == 1) {
+    if ((g_fused_deep & 1) && kw == 10) {
+      hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 10, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    if ((g_fused_deep & 2) && kw % 8 == 0) {
+      hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 8, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+  }
   if (MT <= 2 && kw % 4 == 0)   // Mpad 64: at most 2 k-steps per prefetch group (VGPRs)
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM>), grid, dim3(256), 0, st, a);
   else if (kw % 2 == 0)

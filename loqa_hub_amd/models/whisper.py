@@ -223,7 +223,7 @@ class WhisperModel:
             if S2:
                 # fc2 as split-K f32 slabs (hipBLASLt's N = 1280 tiles leave
                 # most CUs idle at 1500 rows), summed by the next LayerNorm
-                part2 = ops.gemm_tile(m, L["fc2"], epi="slabs", splits=S2, layout=4)
+                part2 = ops.gemm_tile(m, L["fc2"], epi="slabs", splits=S2, layout=0)
             else:
                 delta = ops.linear(m, L["fc2"], L["fc2_b"])
         if part2 is not None:
