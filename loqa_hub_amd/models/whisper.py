@@ -39,6 +39,8 @@ ENC_O_SPLITS = int(os.environ.get("LOQA_ENC_O_SPLITS", "2"))
 # LDS-tiled MFMA GEMM (csrc/kernels/gemm_tile.hip); 0: im2col + hipBLASLt
 ENC_TILE = int(os.environ.get("LOQA_ENC_TILE", "1"))
 ENC_FC2_SPLITS = int(os.environ.get("LOQA_ENC_FC2_SPLITS", "4"))
+# fc1 + bias + GELU as one tiled-GEMM launch (1: instead of hipBLASLt + gelu_bias)
+ENC_FC1_TILE = int(os.environ.get("LOQA_ENC_FC1_TILE", "0"))
 
 
 class WhisperWeights:
@@ -218,8 +220,13 @@ class WhisperModel:
             else:
                 o = ops.linear(a, L["wo"], L["bo"])
                 h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
-            m = ops.linear(h, L["fc1"], L["fc1_b"])
-            ops.gelu_bias_(m)
+            if tile and ENC_FC1_TILE:
+                if "fc1_bf" not in L:
+                    L["fc1_bf"] = L["fc1_b"].float()
+                m = ops.gemm_tile(h, L["fc1"], bias=L["fc1_bf"], act="gelu", layout=0)
+            else:
+                m = ops.linear(h, L["fc1"], L["fc1_b"])
+                ops.gelu_bias_(m)
             if S2:
                 # fc2 as split-K f32 slabs (hipBLASLt's N = 1280 tiles leave
                 # most CUs idle at 1500 rows), summed by the next LayerNorm
