@@ -100,6 +100,7 @@ class WhisperWeights:
         self.conv1_wt = ops.conv_k3_weight(self.conv1_w, cfg.n_mels)
         self.conv2_wt = ops.conv_k3_weight(self.conv2_w, d)
         self.conv1_bf, self.conv2_bf = self.conv1_b.float(), self.conv2_b.float()
+        self.enc_fc1_bf = [L["fc1_b"].float() for L in self.enc]
         # fused-epilogue copies: LayerNorm weight folded into qkv / xq / fc1 rows,
         # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
         # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)
@@ -221,9 +222,7 @@ class WhisperModel:
                 o = ops.linear(a, L["wo"], L["bo"])
                 h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
             if tile and ENC_FC1_TILE:
-                if "fc1_bf" not in L:
-                    L["fc1_bf"] = L["fc1_b"].float()
-                m = ops.gemm_tile(h, L["fc1"], bias=L["fc1_bf"], act="gelu", layout=0)
+                m = ops.gemm_tile(h, L["fc1"], bias=w.enc_fc1_bf[i], act="gelu", layout=0)
             else:
                 m = ops.linear(h, L["fc1"], L["fc1_b"])
                 ops.gelu_bias_(m)
