@@ -114,8 +114,18 @@ class STTEngine:
                                             // self.SPLIT_KEYS))
         # cross-attention K|V of every decoder layer for up to max_batch
         # utterances, written in place each batch (graph-captured steps read it)
-        self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
-                                device=self.device) for _ in range(cfg.dec_layers)]
+        # (with the layer-concatenated weights: one [rows, L * 2d] buffer whose
+        # column blocks are the layers' K|V, written by one tiled GEMM per batch)
+        self.xkv_all = None
+        if (getattr(self.weights, "xkv_all", None) is not None
+                and os.environ.get("LOQA_STT_MEGA", "0") != "1"):
+            self.xkv_all = torch.empty(max_batch * cfg.n_audio_ctx, cfg.dec_layers * 2 * cfg.d_model,
+                                       dtype=torch.bfloat16, device=self.device)
+            d2 = 2 * cfg.d_model
+            self.xkv = [self.xkv_all[:, i * d2:(i + 1) * d2] for i in range(cfg.dec_layers)]
+        else:
+            self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
+                                    device=self.device) for _ in range(cfg.dec_layers)]
         # persistent one-launch decoder step for 16-row steps (ops.WhisperMega)
         self.mega = None
         if (self.fused and self.is_gpu and os.environ.get("LOQA_STT_MEGA", "0") == "1"
@@ -232,6 +242,12 @@ class STTEngine:
                 j += 1
             runs.append((i, slots[i], j - i + 1))
             i = j + 1
+        if self.xkv_all is not None:
+            w = self.weights
+            for i0, s0, m in runs:
+                ops.gemm_tile(enc[i0 * T:(i0 + m) * T], w.xkv_all, bias=w.xkv_all_b,
+                              out=self.xkv_all[s0 * T:(s0 + m) * T], layout=7)
+            return self.xkv
         for L, buf in zip(self.weights.dec, self.xkv):
             for i0, s0, m in runs:
                 torch.addmm(L["xkv_b"], enc[i0 * T:(i0 + m) * T], L["xkv"].t(),

@@ -41,6 +41,9 @@ ENC_TILE = int(os.environ.get("LOQA_ENC_TILE", "1"))
 ENC_FC2_SPLITS = int(os.environ.get("LOQA_ENC_FC2_SPLITS", "4"))
 # fc1 + bias + GELU as one tiled-GEMM launch (1: instead of hipBLASLt + gelu_bias)
 ENC_FC1_TILE = int(os.environ.get("LOQA_ENC_FC1_TILE", "0"))
+# cross-attention K|V of ALL decoder layers as one tiled-GEMM launch over the
+# layer-concatenated weights (0: one hipBLASLt GEMM per layer)
+XKV_TILE = int(os.environ.get("LOQA_XKV_TILE", "1"))
 
 
 class WhisperWeights:
@@ -101,6 +104,15 @@ class WhisperWeights:
         self.conv2_wt = ops.conv_k3_weight(self.conv2_w, d)
         self.conv1_bf, self.conv2_bf = self.conv1_b.float(), self.conv2_b.float()
         self.enc_fc1_bf = [L["fc1_b"].float() for L in self.enc]
+        # the decoder layers' cross K|V weights as ONE [L * 2d, d] matrix (each
+        # layer's "xkv" becomes a row-block view of it, no second copy), so the
+        # cross K|V of an utterance is one tiled GEMM launch
+        self.xkv_all = self.xkv_all_b = None
+        if device.type == "cuda" and XKV_TILE and (len(self.dec) * 2 * d) % 256 == 0 and d % 64 == 0:
+            self.xkv_all = torch.cat([L["xkv"] for L in self.dec]).contiguous()
+            self.xkv_all_b = torch.cat([L["xkv_b"] for L in self.dec]).float()
+            for i, L in enumerate(self.dec):
+                L["xkv"] = self.xkv_all[i * 2 * d:(i + 1) * 2 * d]
         # fused-epilogue copies: LayerNorm weight folded into qkv / xq / fc1 rows,
         # LayerNorm shift + linear bias folded into one f32 bias, qkv rows in
         # (c, c + D/2) pair order (the epilogue writes q and the paged K/V)

@@ -102,3 +102,30 @@ def test_whisper_encoder_tiled_stem_matches_library_path(monkeypatch):
     err = (a.float() - b.float()).abs()
     assert err.max().item() < 0.05 * b.float().abs().max().item(), err.max().item()
     assert err.mean().item() < 0.01 * b.float().abs().mean().item() + 1e-3
+
+
+@pytest.mark.gpu
+def test_cross_kv_one_launch_matches_per_layer(monkeypatch):
+    """Cross-attention K|V of all decoder layers as one tiled GEMM over the
+    layer-concatenated weights against one hipBLASLt GEMM per layer: the
+    K|V buffers agree to bf16 rounding and the greedy transcripts match."""
+    import numpy as np
+
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.models import whisper as wm
+    from loqa_hub_amd.models.configs import whisper_config
+
+    rng = np.random.default_rng(5)
+    pcms = [(rng.standard_normal(n) * 3000).astype(np.int16) for n in (16000, 40000)]
+    outs, kvs = [], []
+    for flag in (1, 0):
+        monkeypatch.setattr(wm, "XKV_TILE", flag)
+        e = STTEngine(whisper_config("whisper-tiny"), "cuda", seed=4, max_batch=4)
+        assert (e.xkv_all is not None) == bool(flag)
+        reqs = [STTRequest(p, max_new_tokens=10) for p in pcms]
+        e.transcribe(reqs)
+        outs.append([r.tokens for r in reqs])
+        kvs.append(torch.stack([x[:2 * 1500].float() for x in e.xkv]).cpu())
+    err = (kvs[0] - kvs[1]).abs().max().item()
+    assert err <= 2e-2 * kvs[1].abs().max().item(), err
+    assert outs[0] == outs[1]
