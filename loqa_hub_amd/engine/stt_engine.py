@@ -134,6 +134,8 @@ class STTEngine:
                                         max_seqs=ops.WhisperMega.ROWS)
         self._graphs: dict[tuple[int, int], dict] = {}
         self._graphs_frozen = False     # see LLMEngine: no capture while serving
+        self._enc_graphs: dict = {}
+        self._enc_pool = None
         # token budget of one decoder step (each new sequence feeds the 4-token
         # SOT prompt; 17+ simultaneous arrivals would exceed ops.MPADS rows)
         self.step_tokens = max(len(self.sot), min(int(os.environ.get("LOQA_STT_STEP_TOKENS", "64")),
@@ -407,12 +409,56 @@ class STTEngine:
         self._step_no = (self._step_no + 1) % (2 * self.RES_SLOTS)   # wraps as the device counter
         return rslot
 
+    # encoder graphs for batches of up to this many utterances (0: eager encoder)
+    ENC_GRAPH_MAX = int(os.environ.get("LOQA_ENC_GRAPH_MAX", "4"))
+
+    def _enc_graph(self, B: int) -> dict:
+        """The Whisper encoder (log-mel -> conv stem -> all layers) for a batch
+        of B padded 30-s windows as ONE graph replay: ~330 kernels per encode
+        launched eagerly from the encoder worker thread leave host-launch gaps
+        between them (and hold the GIL the decoder schedulers need). The graphs
+        share one memory pool; replays run on the encoder's stream one after
+        another, so their intermediates never overlap in time."""
+        g = self._enc_graphs.get(B)
+        if g is not None:
+            return g
+        if self._enc_pool is None:
+            self._enc_pool = torch.cuda.graph_pool_handle()
+        audio = torch.zeros(B, 480000, dtype=torch.float32, device=self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.model.encode(audio)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self._enc_pool, capture_error_mode="thread_local"):
+            out = self.model.encode(audio)
+        g = {"graph": graph, "audio": audio, "out": out}
+        self._enc_graphs[B] = g
+        return g
+
+    def encode(self, audio: torch.Tensor) -> torch.Tensor:
+        """Encoder states [B * 1500, d] of padded audio [B, 480000]: a graph
+        replay for a captured batch size, else the eager encoder."""
+        B = audio.shape[0]
+        g = self._enc_graphs.get(B)
+        if g is None:
+            return self.model.encode(audio)
+        g["audio"].copy_(audio)
+        g["graph"].replay()
+        return g["out"]
+
     def warmup_graphs(self) -> int:
         """Capture every decoder-step graph bucket up front (see
-        ``LLMEngine.warmup_graphs``): sequence x token x context buckets."""
+        ``LLMEngine.warmup_graphs``): sequence x token x context buckets; and
+        the encoder for batches of 1 .. ``ENC_GRAPH_MAX`` utterances."""
         if not self.use_graphs:
             return 0
         n = 0
+        if self.is_gpu:
+            for b in range(1, min(self.ENC_GRAPH_MAX, self.max_batch) + 1):
+                self._enc_graph(b)
+                n += 1
         n_sot = len(self.sot)
         b_max = next((b for b in self.SEQ_BUCKETS if b >= self.max_batch), self.SEQ_BUCKETS[-1])
         for b in self.SEQ_BUCKETS:
@@ -526,7 +572,7 @@ class STTEngine:
             audio, sumsq = self.upload(reqs, device_pcm)
         t0 = time.perf_counter()
         with tr.span("encode", dev, batch=len(reqs)):
-            enc = self.model.encode(audio)
+            enc = self.encode(audio)
             self.cross_kv(enc, slots)
         ss = sumsq.cpu().numpy()
         if self.is_gpu:

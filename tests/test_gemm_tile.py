@@ -129,3 +129,21 @@ def test_cross_kv_one_launch_matches_per_layer(monkeypatch):
     err = (kvs[0] - kvs[1]).abs().max().item()
     assert err <= 2e-2 * kvs[1].abs().max().item(), err
     assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+def test_encoder_graph_replay_matches_eager():
+    """The captured encoder (one graph replay per batch) against the eager
+    encoder on the same inputs, for two different inputs through one graph."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine
+    from loqa_hub_amd.models.configs import whisper_config
+
+    e = STTEngine(whisper_config("whisper-tiny"), "cuda", seed=6, max_batch=4)
+    e._enc_graph(2)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for _ in range(2):
+        audio = (torch.rand(2, 480000, device="cuda", generator=g) - 0.5) * 0.3
+        ref = e.model.encode(audio).float()
+        out = e.encode(audio).float()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
