@@ -135,7 +135,7 @@ class STTEngine:
         self._graphs: dict[tuple[int, int], dict] = {}
         self._graphs_frozen = False     # see LLMEngine: no capture while serving
         self._enc_graphs: dict = {}
-        self._enc_pool = None
+        self._enc_graph_pool = None
         # token budget of one decoder step (each new sequence feeds the 4-token
         # SOT prompt; 17+ simultaneous arrivals would exceed ops.MPADS rows)
         self.step_tokens = max(len(self.sot), min(int(os.environ.get("LOQA_STT_STEP_TOKENS", "64")),
@@ -422,8 +422,8 @@ class STTEngine:
         g = self._enc_graphs.get(B)
         if g is not None:
             return g
-        if self._enc_pool is None:
-            self._enc_pool = torch.cuda.graph_pool_handle()
+        if self._enc_graph_pool is None:
+            self._enc_graph_pool = torch.cuda.graph_pool_handle()
         audio = torch.zeros(B, 480000, dtype=torch.float32, device=self.device)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -431,7 +431,7 @@ class STTEngine:
             self.model.encode(audio)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, pool=self._enc_pool, capture_error_mode="thread_local"):
+        with torch.cuda.graph(graph, pool=self._enc_graph_pool, capture_error_mode="thread_local"):
             out = self.model.encode(audio)
         g = {"graph": graph, "audio": audio, "out": out}
         self._enc_graphs[B] = g
