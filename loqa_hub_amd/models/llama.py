@@ -305,6 +305,9 @@ PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
 # RMSNorm), gate|up with the SwiGLU epilogue in the GEMM. Split counts per
 # projection (qkv, o, down) for ~300-row prompts.
 PREFILL2 = os.environ.get("LOQA_PREFILL2", "0") != "0"
+# prefill gate|up on the v2 prefill GEMM with the SwiGLU epilogue (norm-folded
+# decode copy, unweighted norm in front) instead of hipBLASLt + silu_mul
+PREFILL_GU2 = os.environ.get("LOQA_PREFILL_GU2", "0") != "0"
 PREFILL2_SPLITS = tuple(int(v) for v in os.environ.get("LOQA_PREFILL2_SPLITS", "2,4,8").split(","))
 
 
@@ -374,14 +377,20 @@ class LlamaModel:
                                  grouped=meta.decode, split_keys=split_keys,
                                  num_splits=num_splits if meta.decode else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
+            gu2 = bool(S_o and PREFILL_GU2 and "w_gate_up_f" in w.decode_layers[li])
             if S_o:
                 # o projection on the hand-written prefill GEMM (decode copy
                 # of wo), split-K f32 slabs summed by the norm
                 part_o = ops.prefill_gemm2(attn, w.decode_layers[li]["wo"], S_o, epi="slabs")
-                h = ops.slab_rmsnorm(part_o, residual, L["mlp_norm"], cfg.norm_eps)
+                h = ops.slab_rmsnorm(part_o, residual, self._ones(x) if gu2 else L["mlp_norm"],
+                                     cfg.norm_eps)
             else:
                 o = tp.all_reduce_(ops.linear(attn, L["wo"]))
                 h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
+            if gu2:
+                a = ops.prefill_gemm2(h, w.decode_layers[li]["w_gate_up_f"], 1, epi="swiglu")
+                part = ops.prefill_gemm2(a, w.decode_layers[li]["w_down"], S_down, epi="slabs")
+                continue
             gu = ops.linear(h, L["w_gate_up"])
             if S_down:
                 a = ops.silu_mul(gu)

@@ -44,6 +44,8 @@ ENC_FC1_TILE = int(os.environ.get("LOQA_ENC_FC1_TILE", "0"))
 # cross-attention K|V of ALL decoder layers as one tiled-GEMM launch over the
 # layer-concatenated weights (0: one hipBLASLt GEMM per layer)
 XKV_TILE = int(os.environ.get("LOQA_XKV_TILE", "1"))
+# encoder qkv (+ bias) on the tiled GEMM (0: hipBLASLt)
+ENC_QKV_TILE = int(os.environ.get("LOQA_ENC_QKV_TILE", "0"))
 
 
 class WhisperWeights:
@@ -104,6 +106,7 @@ class WhisperWeights:
         self.conv2_wt = ops.conv_k3_weight(self.conv2_w, d)
         self.conv1_bf, self.conv2_bf = self.conv1_b.float(), self.conv2_b.float()
         self.enc_fc1_bf = [L["fc1_b"].float() for L in self.enc]
+        self.enc_qkv_bf = [L["bqkv"].float() for L in self.enc]
         # the decoder layers' cross K|V weights as ONE [L * 2d, d] matrix (each
         # layer's "xkv" becomes a row-block view of it, no second copy), so the
         # cross K|V of an utterance is one tiled GEMM launch
@@ -224,7 +227,10 @@ class WhisperModel:
                                            bias=w.enc[i - 1]["fc2_b"])
                 else:
                     h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
-            qkv = ops.linear(h, L["wqkv"], L["bqkv"])
+            if tile and ENC_QKV_TILE:
+                qkv = ops.gemm_tile(h, L["wqkv"], bias=w.enc_qkv_bf[i], layout=0)
+            else:
+                qkv = ops.linear(h, L["wqkv"], L["bqkv"])
             a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
                               causal=False, max_q=T, cu_k=cu)
             if getattr(w, "enc_wo_p", None) is not None and (d // 64) % ENC_O_SPLITS == 0:

@@ -309,6 +309,28 @@ def test_llm_prefill2_matches_hipblaslt_gpu(monkeypatch):
         assert float((a - b).norm() / b.norm()) < 4e-2
 
 
+def test_llm_prefill_gu2_matches_hipblaslt_gpu(monkeypatch):
+    """Prefill gate|up on the v2 GEMM's SwiGLU epilogue (norm-folded decode
+    copy behind an unweighted norm; LOQA_PREFILL_GU2) vs hipBLASLt + silu_mul:
+    the final hidden rows of a 300-token prompt agree."""
+    from loqa_hub_amd.models import llama as llama_mod
+    cfg = llama_config("tinyllama")
+    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(2)
+    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
+    r = GenRequest(toks, multi_command_schema(1))
+    eng.submit(r)
+    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
+    dev = eng._to_device(host)
+    meta = eng._build_meta(dev, max_q, max_ctx, False)
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(llama_mod, "PREFILL_GU2", on)
+        outs[on] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
+    rel = float((outs[True] - outs[False]).norm() / outs[False].norm())
+    assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
+
+
 def _to_cpu(obj, seen=None):
     """Deep copy of a weights object with every tensor on the CPU."""
     import copy
