@@ -127,10 +127,12 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_tile_kernel(GemmTileParams 
     for (int i = 0; i < IPW; ++i) {
       const bf16_t* g;
       if (CONV && cb[i] >= 0) {
+        // conv input rows keep only their 16-byte chunk offset (c * 8) in src;
+        // a tap outside [0, T_in) reads the same chunk of the zero row
         const int tt = ct[i] + tap;
-        g = (tt >= 0 && tt < p.conv_tin)
-                ? src[i] + (size_t)(cb[i] + tt) * p.ldx + c0
-                : reinterpret_cast<const bf16_t*>(p.zeros) + ((src[i] - X) & 63);
+        const int c8 = (int)(src[i] - X);
+        g = (tt >= 0 && tt < p.conv_tin) ? X + (size_t)(cb[i] + tt) * p.ldx + c0 + c8
+                                         : reinterpret_cast<const bf16_t*>(p.zeros) + c8;
       } else {
         g = src[i] + kc;
       }
