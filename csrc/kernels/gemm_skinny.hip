@@ -273,13 +273,25 @@ struct XRegs {
   uint4 v[NP];
 };
 
+// Piece -> thread map: the 4 16-B pieces of a k-step fastest, then the chunk's
+// U k-steps, then rows, so 4U consecutive lanes read U x 64 contiguous bytes
+// of one row (whole 128-B lines at U >= 2; guide §5 "x through LDS in full
+// lines": fragment-shaped loads - 16 rows x 64 B per instruction - double the
+// texture-address work at the same bytes).
+template <int MP, int U>
+__device__ __forceinline__ void xc_piece(int idx, int& row, int& u, int& q) {
+  q = idx & 3;
+  const int rest = idx >> 2;
+  u = rest % U;
+  row = rest / U;
+}
+
 template <int MP, int U>
 __device__ __forceinline__ void load_xc(XRegs<MP, U>& r, const bf16_t* x, long long ldx_, int ks) {
 #pragma unroll
   for (int p = 0; p < XRegs<MP, U>::NP; ++p) {
-    const int idx = p * 256 + (int)threadIdx.x;
-    const int q = idx & 3, rest = idx >> 2;
-    const int row = rest % MP, u = rest / MP;
+    int row, u, q;
+    xc_piece<MP, U>(p * 256 + (int)threadIdx.x, row, u, q);
     r.v[p] = *reinterpret_cast<const uint4*>(x + (size_t)row * ldx_ + (size_t)(ks + u) * 32 + q * 8);
   }
 }
@@ -288,9 +300,8 @@ template <int MP, int U>
 __device__ __forceinline__ void store_xc(const XRegs<MP, U>& r, bf16_t* xs) {
 #pragma unroll
   for (int p = 0; p < XRegs<MP, U>::NP; ++p) {
-    const int idx = p * 256 + (int)threadIdx.x;
-    const int q = idx & 3, rest = idx >> 2;
-    const int row = rest % MP, u = rest / MP;
+    int row, u, q;
+    xc_piece<MP, U>(p * 256 + (int)threadIdx.x, row, u, q);
     *reinterpret_cast<uint4*>(xs + (size_t)(u * MP + row) * XROW + q * 8) = r.v[p];
   }
 }
@@ -395,7 +406,7 @@ struct FusedParams {
   int H, Hkv, D, blk;
   int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
   int wr;                 // waves along the rows (1, or 4 with S == 1; any S with xl)
-  int xl;                 // x through LDS (wr == 4; Mpad 64 / 128)
+  int xl;                 // x through LDS (wr == 4; Mpad 32 / 64 / 128)
 };
 
 struct FusedArgs {
@@ -915,7 +926,7 @@ static int dispatch_mt(const FusedArgs& a, int wr, hipStream_t st) {
   }
 }
 
-// XL dispatch: Mpad 64 (MT 4) / 128 (MT 8), 4 waves along rows, any split-K.
+// XL dispatch: Mpad 32 (MT 2) / 64 (MT 4) / 128 (MT 8), 4 waves along rows, any split-K.
 // Prefetch group = one LDS chunk: 4 k-steps, 2 when the VGPR budget is tight.
 template <int RT, int MT, int MODE, int NORM>
 static int launch_xl(const FusedArgs& a, hipStream_t st) {
@@ -926,13 +937,16 @@ static int launch_xl(const FusedArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, UA, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
   else if (kw % 2 == 0)
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
-  else
+  else if constexpr (MT * 16 * 4 >= 256)   // a 1-k-step x chunk must cover the 256 threads' pieces
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, 4, MODE, NORM, 1>), grid, dim3(256), 0, st, a);
+  else
+    return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 
 template <int MODE, int NORM>
 static int dispatch_xl(const FusedArgs& a, int rt, hipStream_t st) {
+  if (a.Mpad == 32) return rt == 2 ? launch_xl<2, 2, MODE, NORM>(a, st) : launch_xl<1, 2, MODE, NORM>(a, st);
   if (a.Mpad == 64) return rt == 2 ? launch_xl<2, 4, MODE, NORM>(a, st) : launch_xl<1, 4, MODE, NORM>(a, st);
   return rt == 2 ? launch_xl<2, 8, MODE, NORM>(a, st) : launch_xl<1, 8, MODE, NORM>(a, st);
 }
@@ -983,7 +997,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
   if (S < 1 || K % (S * 128) || p->ldx % 8 || N % 32 ||
       (Mpad != 16 && Mpad != 32 && Mpad != 64 && !(Mpad == 128 && p->xl)))
     return (int)hipErrorInvalidValue;
-  if (p->xl && (p->wr != 4 || Mpad < 64 || (p->rt != 1 && p->rt != 2) || N % (64 * p->rt)))
+  if (p->xl && (p->wr != 4 || Mpad < 32 || (p->rt != 1 && p->rt != 2) || N % (64 * p->rt)))
     return (int)hipErrorInvalidValue;
   if (S > 1 && (!p->part || !p->counters)) return (int)hipErrorInvalidValue;
   if (p->norm && (!p->rowsq_in || p->rowstat_tiles < 1)) return (int)hipErrorInvalidValue;

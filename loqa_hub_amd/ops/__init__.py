@@ -1145,7 +1145,8 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = 
         # Whisper decoder, took the pipeline from 17.6 to 10.3 utt/s (long-lived
         # 4-wave workgroups: the co-scheduling cliff, docs/PERF.md): opt-in only
         xl = "only" if Mpad == 128 else (
-            "also" if Mpad == 64 and xl_on and os.environ.get("LOQA_TUNE_XL64") == "1" else "no")
+            "also" if Mpad == 64 and xl_on and os.environ.get("LOQA_TUNE_XL64") == "1" else
+            "also" if Mpad == 32 and xl_on and os.environ.get("LOQA_TUNE_XL32") == "1" else "no")
         tune_fused_splits(key, lambda sp, rt, wr, i, xl_=0: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, xl=xl_, **kw), K, rts=rts,
             ncopies=len(copies), wr4=wide, fewest=wide, xl=xl)

@@ -160,11 +160,11 @@ def test_fused_rows_per_wave_layout_gpu(mode, Mpad, rt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["resid", "silu", "act", "rope"])
-@pytest.mark.parametrize("Mpad,rt,S", [(64, 1, 1), (64, 2, 2), (128, 1, 1), (128, 1, 2),
-                                       (128, 2, 1), (128, 2, 4)])
+@pytest.mark.parametrize("Mpad,rt,S", [(32, 1, 1), (32, 2, 2), (32, 2, 4), (64, 1, 1), (64, 2, 2),
+                                       (128, 1, 1), (128, 1, 2), (128, 2, 1), (128, 2, 4)])
 @pytest.mark.parametrize("norm", [None, "rms"])
 def test_fused_xl_layout_gpu(mode, Mpad, rt, S, norm):
-    """The x-through-LDS (XL) layout of the fused GEMM (Mpad 64 / 128, 4 waves
+    """The x-through-LDS (XL) layout of the fused GEMM (Mpad 32 / 64 / 128, 4 waves
     along rows, per-wave split-K tickets) against the fp32 CPU reference of
     the same call, with and without the RMSNorm prologue."""
     from loqa_hub_amd.ops import reference as ref
@@ -261,7 +261,7 @@ def test_fused_layernorm_act_gpu(S, Mpad, rt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,Mpad,rt", [(1, 128, 1), (2, 128, 2), (1, 64, 1)])
+@pytest.mark.parametrize("S,Mpad,rt", [(1, 128, 1), (2, 128, 2), (1, 64, 1), (1, 32, 2)])
 def test_fused_layernorm_act_xl_gpu(S, Mpad, rt):
     _ln_case("cuda", S, Mpad, rt, xl=1)
 
