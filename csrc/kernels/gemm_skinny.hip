@@ -273,17 +273,15 @@ struct XRegs {
   uint4 v[NP];
 };
 
-// Piece -> thread map: the 4 16-B pieces of a k-step fastest, then the chunk's
-// U k-steps, then rows, so 4U consecutive lanes read U x 64 contiguous bytes
-// of one row (whole 128-B lines at U >= 2; guide §5 "x through LDS in full
-// lines": fragment-shaped loads - 16 rows x 64 B per instruction - double the
-// texture-address work at the same bytes).
+// Piece -> thread map: the 4 16-B pieces of a row's k-step fastest, then
+// rows, then the chunk's U k-steps. (A whole-line map - a row's U k-steps
+// across 4U consecutive lanes - measured 1-2% slower end to end.)
 template <int MP, int U>
 __device__ __forceinline__ void xc_piece(int idx, int& row, int& u, int& q) {
   q = idx & 3;
   const int rest = idx >> 2;
-  u = rest % U;
-  row = rest / U;
+  row = rest % MP;
+  u = rest / MP;
 }
 
 template <int MP, int U>
