@@ -37,11 +37,24 @@ class DistInfo:
     def is_main(self) -> bool:
         return self.rank == 0
 
+    @property
+    def comm_device(self) -> torch.device:
+        """Device of the tensors handed to collectives: the GPU under RCCL,
+        the host under gloo (CPU runs and the shared-GPU rehearsal)."""
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
 
 def init_distributed(prefer_gpu: bool = True) -> DistInfo:
+    """LOQA_DIST_SHARE_GPU=1 is a rehearsal mode for a one-GPU box: every rank
+    runs on cuda:0 and the collectives go over gloo on host tensors (RCCL
+    refuses two ranks on one device), so a multi-rank bench exercises the
+    per-rank GPU pipelines, the node's broker and the record gathering."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    share = os.environ.get("LOQA_DIST_SHARE_GPU", "0") == "1"
+    if share:
+        local = 0
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if use_gpu:
         sched = os.environ.get("LOQA_HIP_SCHEDULE")   # experiment: spin | yield | block
@@ -59,7 +72,7 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = "nccl" if use_gpu and not share else "gloo"
         # no device_id: the RCCL communicator (and its streams) is created at
         # the first collective, not here. HIP hands its few hardware queues to
         # streams in first-use order, and which queues the two decoder streams
@@ -89,7 +102,7 @@ def store_exchange(info: DistInfo, key: str, value: str | None = None, timeout_s
 
 def barrier(info: DistInfo) -> None:
     if info.world > 1:
-        if info.device.type == "cuda":
+        if info.comm_device.type == "cuda":
             dist.barrier(device_ids=[info.local_rank])
         else:
             dist.barrier()
@@ -98,7 +111,7 @@ def barrier(info: DistInfo) -> None:
 def max_over_ranks(info: DistInfo, value: float) -> float:
     if info.world == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=info.device)
+    t = torch.tensor([value], dtype=torch.float64, device=info.comm_device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

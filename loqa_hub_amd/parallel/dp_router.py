@@ -41,24 +41,25 @@ def scatter_pcm(info: DistInfo, per_rank: list[list[np.ndarray]] | None, slot_le
     if info.world == 1:
         host = torch.from_numpy(pack_pcm(per_rank[0], slot_len))
         return host.to(info.device)
-    recv = torch.empty(slot_len, dtype=torch.bfloat16, device=info.device)
+    cdev = info.comm_device
+    recv = torch.empty(slot_len, dtype=torch.bfloat16, device=cdev)
     if info.rank == 0:
         packed = np.stack([pack_pcm(p, slot_len) for p in per_rank])
         src = torch.from_numpy(packed)
-        if info.device.type == "cuda":
-            src = src.pin_memory().to(info.device, non_blocking=True)
+        if cdev.type == "cuda":
+            src = src.pin_memory().to(cdev, non_blocking=True)
         chunks = list(src.view(torch.bfloat16).unbind(0))
         dist.scatter(recv, chunks, src=0)
     else:
         dist.scatter(recv, None, src=0)
-    return recv.view(torch.int16)
+    return recv.view(torch.int16).to(info.device)
 
 
 def gather_records(info: DistInfo, rec: torch.Tensor) -> torch.Tensor:
     """all_gather fixed-shape float64 result records [B, F] -> [world*B, F]."""
     if info.world == 1:
         return rec
-    rec = rec.to(info.device)
+    rec = rec.to(info.comm_device)
     out = [torch.empty_like(rec) for _ in range(info.world)]
     dist.all_gather(out, rec)
     return torch.cat(out, 0)

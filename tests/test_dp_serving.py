@@ -83,3 +83,15 @@ def test_fault_spec_parsing(spec):
     assert bool(fi)
     with pytest.raises(ValueError):
         FaultInjector("disk_full")
+
+
+def test_comm_device_follows_backend():
+    """Collective tensors live on the GPU only under RCCL; gloo (CPU runs, the
+    shared-GPU rehearsal) gets host tensors."""
+    import torch
+
+    from loqa_hub_amd.parallel.dist import DistInfo
+    gpu = torch.device("cuda", 0)
+    assert DistInfo(device=gpu, backend="nccl", world=2).comm_device == gpu
+    assert DistInfo(device=gpu, backend="gloo", world=2).comm_device.type == "cpu"
+    assert DistInfo().comm_device.type == "cpu"

@@ -443,3 +443,28 @@ def test_gpu_streaming_backend_joins_continuous_batch():
         eng.stop()
     assert all(len(t) > 3 and c.intent for t, c in out)
     assert eng.stats["decode_steps"] > 0
+
+
+def test_bench_dp2_shared_gpu():
+    """Two bench ranks on the one GPU of a test box (LOQA_DIST_SHARE_GPU=1:
+    gloo control plane, every rank on cuda:0): per-rank GPU pipelines with
+    graphs, the node's one NATS broker, records gathered to rank 0. The RCCL
+    collectives of a real multi-GPU run are the only part not exercised."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", LOQA_DIST_SHARE_GPU="1", LOQA_NO_TUNE="1",
+               OMP_NUM_THREADS="2")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        "29571", "bench.py", "--stt", "test-whisper", "--llm", "test-tiny",
+                        "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch-per-gpu", "2"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 4 and out["queue_success_rate"] == 1.0
+    assert out["command_count_match_rate"] == 1.0
