@@ -16,15 +16,6 @@ import torch.distributed as dist
 log = logging.getLogger("loqa.dist")
 
 
-def _loaded_hip_runtime() -> str:
-    """Path of the libamdhip64 this process (torch) has mapped."""
-    with open("/proc/self/maps") as f:
-        for line in f:
-            if "libamdhip64.so" in line:
-                return line.split()[-1]
-    raise RuntimeError("libamdhip64 is not mapped (import torch and touch the GPU first)")
-
-
 @dataclass
 class DistInfo:
     rank: int = 0
@@ -59,10 +50,10 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
     if use_gpu:
         sched = os.environ.get("LOQA_HIP_SCHEDULE")   # experiment: spin | yield | block
         if sched:
-            import ctypes
+            from ..utils.hip_runtime import hip_runtime
             flag = {"spin": 1, "yield": 2, "block": 4}[sched]
             # the HIP runtime torch already mapped (never a second copy by soname)
-            rc = ctypes.CDLL(_loaded_hip_runtime(), mode=ctypes.RTLD_NOLOAD).hipSetDeviceFlags(flag)
+            rc = hip_runtime().hipSetDeviceFlags(flag)
             log.info("hipSetDeviceFlags(%s) -> %d", sched, rc)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)

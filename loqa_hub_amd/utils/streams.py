@@ -16,6 +16,8 @@ import os
 
 import torch
 
+from .hip_runtime import hip_runtime
+
 N_CUS_DEFAULT = 256
 
 
@@ -55,7 +57,7 @@ _keep: list = []
 
 def cu_masked_stream(device: torch.device, cus: list[int]) -> torch.cuda.ExternalStream:
     """A HIP stream restricted to ``cus`` on ``device`` (wrapped for torch)."""
-    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    hip = hip_runtime()
     n = torch.cuda.get_device_properties(device).multi_processor_count
     words = cu_mask_words(cus, max(n, max(cus) + 1 if cus else n))
     arr = (ctypes.c_uint32 * len(words))(*words)
@@ -178,7 +180,7 @@ _dec_lock = __import__("threading").Lock()
 
 
 def _hip_stream(device: torch.device, priority: int) -> torch.cuda.ExternalStream:
-    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    hip = hip_runtime()
     handle = ctypes.c_void_p()
     with torch.cuda.device(device):
         rc = hip.hipStreamCreateWithPriority(ctypes.byref(handle), ctypes.c_uint(1), ctypes.c_int(priority))

@@ -584,3 +584,18 @@ def test_step_meta_native_matches_python():
     assert pools[1].step_meta([99], [1], B_pad, T_pad, MB, *[np.zeros(T_pad, np.int32)] * 2,
                               np.zeros(B_pad + 1, np.int32), np.zeros(B_pad, np.int32),
                               np.zeros((B_pad, MB), np.int32)) == -1
+
+
+def test_hip_runtime_is_torchs_copy():
+    """Direct HIP calls (CU-masked / prioritised streams, device flags) go to
+    the libamdhip64 torch mapped, never to a second copy loaded by soname."""
+    import torch
+
+    from loqa_hub_amd.utils.hip_runtime import hip_runtime, mapped_hip_path
+    lib = hip_runtime()
+    assert os.path.realpath(mapped_hip_path()).startswith(
+        os.path.realpath(os.path.dirname(os.path.dirname(torch.__file__)))) or "rocm" in mapped_hip_path()
+    assert lib.hipStreamCreateWithPriority is not None
+    with open("/proc/self/maps") as f:
+        copies = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+    assert len(copies) == 1, copies
