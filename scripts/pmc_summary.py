@@ -12,6 +12,7 @@ SIMDS = 256 * 4
 
 def main(paths):
     vals = defaultdict(lambda: defaultdict(list))    # kernel -> counter -> per-dispatch values
+    ncalls: dict = defaultdict(int)                  # kernel -> dispatches (max over passes)
     for p in paths:
         per = defaultdict(lambda: defaultdict(float))  # dispatch -> counter -> sum
         names = {}
@@ -22,12 +23,19 @@ def main(paths):
             per[d]["_dur_s"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
             # GRBM counters repeat per XCD instance: the kernel's cycles are the max
             per[d][c] = max(per[d][c], v) if c.startswith("GRBM_") else per[d][c] + v
+        calls: dict = defaultdict(int)
         for d, cs in per.items():
+            calls[names[d]] += 1
             for c, v in cs.items():
                 vals[names[d]][c].append(v)
+        for k, n in calls.items():
+            ncalls[k] = max(ncalls[k], n)
     print(f"{'kernel':60s} {'MFMA busy %':>11s} {'bf16 TF/s':>9s} {'LDS confl':>9s} "
-          f"{'HBM TB/s':>8s} {'us':>8s}")
-    for k, cs in vals.items():
+          f"{'HBM TB/s':>8s} {'us':>8s} {'calls':>7s}")
+    # heaviest first: calls x median duration
+    order = sorted(vals, key=lambda k: -ncalls[k] * st.median(vals[k]["_dur_s"] or [0.0]))
+    for k in order:
+        cs = vals[k]
         med = {c: st.median(v) for c, v in cs.items()}
         # the dispatch's own timestamps give its duration (GRBM_GUI_ACTIVE is
         # aggregated over hardware instances); cycles at the 2.4 GHz peak clock
@@ -43,6 +51,7 @@ def main(paths):
         fs = med.get("FETCH_SIZE")
         out.append(f"{fs * 1024 / secs / 1e12:8.2f}" if fs is not None and secs else f"{'-':>8s}")
         out.append(f"{secs * 1e6:8.1f}" if secs else f"{'-':>8s}")
+        out.append(f"{ncalls[k]:7d}")
         print(f"{out[0]:60s} " + " ".join(out[1:]))
 
 

@@ -468,3 +468,15 @@ def test_bench_dp2_shared_gpu():
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 4 and out["queue_success_rate"] == 1.0
     assert out["command_count_match_rate"] == 1.0
+
+
+def test_cu_masked_stream_gpu():
+    """A CU-masked stream made through torch's own HIP runtime runs work."""
+    from loqa_hub_amd.utils.streams import cu_masked_stream
+    dev = torch.device("cuda", 0)
+    s = cu_masked_stream(dev, list(range(64)))
+    with torch.cuda.stream(s):
+        x = torch.full((4096,), 2.0, device=dev)
+        y = (x * x).sum()
+    s.synchronize()
+    assert y.item() == 4.0 * 4096
