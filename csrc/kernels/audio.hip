@@ -20,7 +20,12 @@
 #define BIN_TILES 7         // 7 x 32 = 224 >= 201 bins
 #define BASIS_LD 224
 #define FRAMES_PER_WG 32
-#define POW_LD 204          // 202 used (K padded to even), +2 pad
+// LDS row strides are odd (in dwords): the MFMA A operands are read one frame
+// (power row) per lane, 32 lanes per ds_read_b32 group with banks (a/4) % 32,
+// so an even stride put 2 (400) or 8 (204) rows on each bank - 16- / 4-way
+// conflicts (SQ_LDS_BANK_CONFLICT ~9.6 extra cycles per cycle)
+#define FRAME_LD 401        // 400 taps + 1
+#define POW_LD 203          // 202 used (K padded to even) + 1
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
@@ -49,7 +54,7 @@ __global__ __launch_bounds__(512) void logmel_kernel(
     const float* __restrict__ cosb, const float* __restrict__ sinb,
     const float* __restrict__ filt, int n_mels, float* __restrict__ out, int n_frames,
     float* __restrict__ gmax) {
-  __shared__ float frames[FRAMES_PER_WG][NFFT];
+  __shared__ float frames[FRAMES_PER_WG][FRAME_LD];
   __shared__ float power[FRAMES_PER_WG][POW_LD];
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * FRAMES_PER_WG;
