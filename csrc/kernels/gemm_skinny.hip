@@ -883,7 +883,8 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
 // range in ONE prefetch group when it is 10 k-steps (Whisper d = 1280, S = 1:
 // every weight load of the wave in flight at once instead of two 2-step
 // groups at a time); bit 1 - 8-step groups when it is a multiple of 8 (Llama
-// K = 4096; measured slower in the pipeline: 3.51 -> 3.68 ms per LLM step). The decode
+// K = 4096; measured slower in the pipeline: 3.51 -> 3.68 ms per LLM step); bit 2 -
+// the same 8-step groups for the o / qkv shapes only. The decode
 // GEMMs are latency-bound beside the concurrent decoder: fewer dependent
 // prefetch rounds per kernel, not bandwidth, is what a shorter kernel needs.
 static int g_fused_deep = -1;
@@ -903,6 +904,13 @@ static int launch_fused(const FusedArgs& a, hipStream_t st) {
       return (int)hipGetLastError();
     }
     if ((g_fused_deep & 2) && kw % 8 == 0) {
+      hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 8, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    // bit 2 (value 4): only the short Llama GEMMs (o, qkv: N <= 6144, K = 4096),
+    // whose <= 256 workgroups hold one 4-wave group per CU - bytes in flight
+    // per CU, not occupancy, bound them
+    if ((g_fused_deep & 4) && kw % 8 == 0 && a.N <= 6144 && a.K <= 4096) {
       hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 8, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
       return (int)hipGetLastError();
     }
