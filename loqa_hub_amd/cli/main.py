@@ -53,7 +53,8 @@ async def run(cfg, tp_leader=None) -> None:
         n = torch.cuda.device_count()
         want = cfg.gpu.dp or cfg.gpu.num_gpus or 1
         if n > 1 and want > 1:
-            processor = await build_dp_processor(cfg, min(n, want))
+            processor = await build_dp_processor(
+                cfg, min(n, want), server.nats.url if server.nats is not None else "")
         elif n > 0:
             processor = build_gpu_processor(cfg, server.nats, tts="auto", skills=server.skills)
         else:

@@ -45,25 +45,69 @@ log = logging.getLogger("loqa.dp")
 
 
 # --------------------------------------------------------------- worker side
-def _build_worker_processor(spec: dict, device: str):
-    """The per-GPU pipeline (same composition as ``server.build_gpu_processor``)."""
-    from ..engine.llm_engine import LLMEngine
-    from ..engine.pipeline import VoicePipeline
-    from ..engine.stt_engine import STTEngine
-    from ..models.configs import llama_config, whisper_config
-    from ..transport.voice_processor import GPUVoiceProcessor
-    stt = STTEngine(whisper_config(spec["stt_model"]), device, seed=spec.get("seed", 0),
-                    max_batch=spec.get("max_batch", 8), use_graphs=spec.get("use_graphs", True))
-    llm = LLMEngine(llama_config(spec["llm_model"]), device, seed=spec.get("seed", 0),
-                    max_seqs=spec.get("max_batch", 8), max_seq_len=spec.get("max_seq_len", 1024),
-                    use_graphs=spec.get("use_graphs", True))
-    pipe = VoicePipeline(stt, llm, None, min_response_tokens=spec.get("min_response_tokens", 8))
-    pipe.warmup()
-    return GPUVoiceProcessor(pipe, max_batch=spec.get("max_batch", 8),
-                             batch_window=spec.get("batch_window", 0.005))
+async def _build_worker_processor(spec: dict, device: str):
+    """The per-GPU composition - the same one ``server.build_gpu_processor``
+    gives the 1-GPU hub, so every DP worker serves what the 1-GPU hub serves
+    (the reference's winner path, ``audio_service.go:590-761``):
+
+    * STT -> ONE constrained multi-command decode -> command queue publishing
+      every command on ``loqa.voice.commands`` / ``loqa.devices.commands.*``
+      (``audio_service.go:109-156``) over this worker's OWN NATS connection to
+      the hub's broker (``spec["nats_url"]``);
+    * the streaming-predictive bridge on that decode, over this worker's skill
+      manager (the builtin skills + ``skills_dir``);
+    * the reply voice (``HUB_TTS_BACKEND``: on-device VITS on this GPU),
+      progressive phrase by phrase on NATS ``audio.<relay>`` when streaming is
+      enabled (``audio_service.go:693-761``).
+
+    ``spec["cfg"]`` is the hub's ``Config``."""
+    from ..messaging.audio_stream_publisher import AudioStreamPublisher
+    from ..messaging.nats_service import NATSService
+    from ..server import build_gpu_processor, build_tts
+    from ..skills import DefaultSkillLoader, SkillManager, SkillManagerConfig
+    from ..skills.builtin.lights import LightsSkill
+    cfg = spec["cfg"]
+    skills = SkillManager(SkillManagerConfig(skills_dir=spec.get("skills_dir", "./skills"),
+                                             config_store=spec.get("skills_config_store",
+                                                                   "./data/skills")),
+                          DefaultSkillLoader(skills_root=spec.get("skills_dir", "./skills")))
+    await skills.register_plugin(LightsSkill())
+    await skills.start()
+    tts = build_tts(cfg, device)
+    # engines first (minutes of warm-up for the large models), then the bus:
+    # an idle connection is not left unanswered while the loop is blocked
+    proc = build_gpu_processor(cfg, None, device, tts, skills=skills)
+    nats = None
+    if spec.get("nats_url"):
+        nats = NATSService(spec["nats_url"], cfg.nats.reconnect_wait)
+        try:
+            await nats.connect()
+        except Exception as e:  # noqa: BLE001 - as the hub: serve without the bus
+            log.warning("worker cannot connect to NATS at %s: %s", spec["nats_url"], e)
+    proc.pipeline.nats = nats
+    if nats is not None and nats.conn is not None:
+        proc.attach_publisher(AudioStreamPublisher(nats.conn))
+    proc.dp_resources = (nats, skills)
+    return proc
+
+
+async def _close_worker_processor(proc) -> None:
+    close = getattr(proc, "close", None)
+    if close is not None:
+        await close()
+    nats, skills = getattr(proc, "dp_resources", (None, None))
+    if skills is not None:
+        await skills.stop()
+    if nats is not None:
+        await nats.close()
 
 
 def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
+    """One GPU worker. Requests: ``("utt", rid, relay, request_id, pcm16 bytes,
+    sample rate, transcript hint)`` - the relay's raw PCM16-LE bytes, handed
+    to the processor as int16 samples (staged into a pinned slot by the STT
+    engine, converted on the device: no host float round trip) - or
+    ``("int", relay)``: interrupt the reply that relay is still receiving."""
     from ..utils.faults import set_faults
     spec = dict(spec, rank=rank)
     fi = set_faults(spec.get("fault_inject"))
@@ -72,11 +116,16 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
     if device == "cuda":
         import torch
         device = f"cuda:{rank % max(1, torch.cuda.device_count())}"
+    if device.startswith("cuda"):
+        import torch
         torch.cuda.set_device(device)
-    factory = spec.get("factory") or _build_worker_processor
-    proc = factory(spec, device)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
+    factory = spec.get("factory") or _build_worker_processor
+    proc = factory(spec, device)
+    if asyncio.iscoroutine(proc):
+        proc = loop.run_until_complete(proc)
+    takes_pcm16 = getattr(proc, "takes_pcm16", False)
     state = {"inflight": 0, "last_progress": time.monotonic(), "done": 0, "stop": False}
     lock = threading.Lock()
 
@@ -90,9 +139,17 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
             time.sleep(spec.get("heartbeat_s", 0.5))
 
     async def handle(item) -> None:
-        rid, relay_id, request_id, pcm16, sr = item
+        _, rid, relay_id, request_id, data, sr, hint = item
+        pcm16 = np.frombuffer(data, dtype="<i2")
         try:
-            res = await proc.process(relay_id, request_id, pcm16.astype(np.float32) / 32767.0, sr)
+            if takes_pcm16:
+                kw = {"pcm16": pcm16}
+                if hint:
+                    kw["transcript_hint"] = hint
+                res = await proc.process(relay_id, request_id, np.zeros(0, np.float32), sr, **kw)
+            else:
+                res = await proc.process(relay_id, request_id,
+                                         pcm16.astype(np.float32) / 32767.0, sr)
             out = dataclasses.asdict(res)
         except Exception as e:  # noqa: BLE001
             out = dataclasses.asdict(UtteranceResult(success=False, command="error",
@@ -103,6 +160,11 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
             state["last_progress"] = time.monotonic()
         resp_q.put(("res", rank, (rid, out)))
 
+    def interrupt(relay_id: str) -> None:
+        fn = getattr(proc, "interrupt_relay", None)
+        if fn is not None:
+            fn(relay_id)
+
     def reader() -> None:
         received = 0
         while True:
@@ -110,6 +172,9 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
             if item is None:
                 loop.call_soon_threadsafe(loop.stop)
                 return
+            if item[0] == "int":
+                loop.call_soon_threadsafe(interrupt, item[1])
+                continue
             received += 1
             if kill_after is not None and received >= kill_after:
                 os._exit(17)  # injected GPU-worker crash (FAULT_INJECT=gpu_kill)
@@ -124,6 +189,7 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
     resp_q.put(("ready", rank, None))
     try:
         loop.run_forever()
+        loop.run_until_complete(_close_worker_processor(proc))
     finally:
         state["stop"] = True
 
@@ -135,14 +201,37 @@ class _Req:
     fut: asyncio.Future
     worker: int = -1
     attempts: int = 0
+    session: str = ""
+
+
+class _RemoteReply:
+    """The front end's handle on a reply a worker is speaking (a streaming
+    session's cancel target)."""
+
+    def __init__(self, dp: "DPVoiceProcessor", relay_id: str):
+        self.dp, self.relay_id = dp, relay_id
+
+    def cancel(self) -> None:
+        rid = self.dp._relay_req.get(self.relay_id)
+        req = self.dp._reqs.get(rid) if rid is not None else None
+        if req is not None and req.worker >= 0:
+            self.dp._send_interrupt(req.worker, self.relay_id)
 
 
 class DPVoiceProcessor:
     """``VoiceProcessor`` over one worker process per GPU."""
 
+    takes_pcm16 = True      # AudioService hands over the relay's raw PCM16 samples
+    tts = None              # the reply voice lives in the workers
+
     def __init__(self, spec: dict, n_workers: int, *, watchdog_s: float = 60.0,
                  ready_timeout: float = 900.0, max_attempts: int = 3):
         self.spec = dict(spec)
+        cfg = self.spec.get("cfg")
+        self.progressive = bool(cfg is not None and cfg.streaming.enabled
+                                and cfg.gpu.tts_backend != "none")
+        self.streaming = None
+        self._relay_req: dict[str, int] = {}
         self.n = n_workers
         self.watchdog_s = watchdog_s
         self.ready_timeout = ready_timeout
@@ -156,6 +245,7 @@ class DPVoiceProcessor:
         self._ready = [False] * n_workers
         self.failures: list[dict] = []
         self._running = False
+        self._served = 0
 
     # lifecycle
     async def start(self) -> None:
@@ -198,14 +288,56 @@ class DPVoiceProcessor:
 
     # routing
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
-                      sample_rate: int) -> UtteranceResult:
-        pcm16 = np.clip(np.round(np.asarray(audio, np.float32) * 32767.0), -32768,
-                        32767).astype(np.int16)
+                      sample_rate: int, transcript_hint: str | None = None,
+                      pcm16: np.ndarray | None = None, pcm_slot=None) -> UtteranceResult:
+        """``pcm16``: the relay's raw samples as received (``AudioService``
+        passes them: ``takes_pcm16``); they travel to the worker as PCM16-LE
+        bytes. Float ``audio`` (other callers) is quantised once here."""
+        if pcm16 is not None:
+            data = np.ascontiguousarray(pcm16, dtype="<i2").tobytes()
+        else:
+            data = np.clip(np.round(np.asarray(audio, np.float32) * 32767.0), -32768,
+                           32767).astype("<i2").tobytes()
+        if pcm_slot is not None:          # never handed out (no new_pcm_slot here)
+            pcm_slot.release()
         rid = next(self._ids)
-        req = _Req((relay_id, request_id, pcm16, sample_rate), self._loop.create_future())
+        req = _Req(("utt", relay_id, request_id, data, sample_rate, transcript_hint),
+                   self._loop.create_future())
         self._reqs[rid] = req
+        self._relay_req[relay_id] = rid
+        if self.streaming is not None and self.progressive:
+            req.session = f"dp_{rid}_{request_id}"
+            self.streaming.begin_speech_session(req.session, _RemoteReply(self, relay_id))
         self._dispatch(rid)
-        return await req.fut
+        try:
+            return await req.fut
+        finally:
+            if self._relay_req.get(relay_id) == rid:
+                del self._relay_req[relay_id]
+
+    def attach_publisher(self, publisher) -> None:
+        """Workers publish over their own NATS connections; the hub's
+        publisher only delivers replies that were not already published."""
+
+    def attach_streaming(self, components) -> None:
+        self.streaming = components
+
+    def interrupt_relay(self, relay_id: str, reason: str = "new_command") -> bool:
+        """Forward a new-winner interrupt to the worker speaking to ``relay_id``."""
+        rid = self._relay_req.get(relay_id)
+        req = self._reqs.get(rid) if rid is not None else None
+        if req is None or req.worker < 0:
+            return False
+        ih = self.streaming.interrupt_handler if self.streaming is not None else None
+        if ih is not None and req.session in ih.active:
+            ih.interrupt_session(req.session, reason)
+        else:
+            self._send_interrupt(req.worker, relay_id)
+        return True
+
+    def _send_interrupt(self, w: int, relay_id: str) -> None:
+        if self.router.healthy[w]:
+            self._req_qs[w].put(("int", relay_id))
 
     def _dispatch(self, rid: int) -> None:
         req = self._reqs[rid]
@@ -219,10 +351,13 @@ class DPVoiceProcessor:
             return
         req.worker = w
         self._pending[w].add(rid)
-        self._req_qs[w].put((rid,) + req.args)
+        self._req_qs[w].put(("utt", rid) + req.args[1:])
 
     def _finish(self, rid: int, res: UtteranceResult) -> None:
         req = self._reqs.pop(rid, None)
+        if req is not None and req.session and self.streaming is not None:
+            sm = (res.metrics or {}).get("speech", {}).get("streaming")
+            self.streaming.end_speech_session(req.session, sm)
         if req is not None and not req.fut.done():
             req.fut.set_result(res)
 
@@ -251,6 +386,7 @@ class DPVoiceProcessor:
                 self._pending[w].discard(rid)
                 self.router.done(w)
             self._finish(rid, UtteranceResult(**d))
+            self._served += 1
 
     # health
     async def _watch(self) -> None:
@@ -293,6 +429,17 @@ class DPVoiceProcessor:
                                                   error=f"worker failures: {why}"))
             else:
                 self._dispatch(rid)
+
+    @property
+    def stats(self) -> dict:
+        """The workers' processor counters summed (as of their last heartbeat)."""
+        out: dict = {}
+        for hb in self._hb:
+            for k, v in (hb.get("stats") or {}).items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    out[k] = out.get(k, 0) + v
+        out["served"] = self._served
+        return out
 
     def metrics(self) -> dict:
         """Per-worker counters aggregated on the front-end (D3)."""

@@ -121,13 +121,18 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
                              max_tokens_per_phrase=sc.max_tokens_per_phrase)
 
 
-async def build_dp_processor(cfg: Config, n_gpus: int):
-    """One worker process per GPU behind the least-loaded router (D1)."""
+async def build_dp_processor(cfg: Config, n_gpus: int, nats_url: str = "", *,
+                             device: str = "cuda", skills_dir: str = "./skills",
+                             skills_config_store: str = "./data/skills", **spec_kw):
+    """One worker process per GPU behind the least-loaded router (D1). Each
+    worker builds the full per-GPU composition (``build_gpu_processor``: STT,
+    constrained decode, command queue over its own connection to the hub's
+    NATS broker at ``nats_url``, bridge, reply voice, progressive speech).
+    ``device``: "cuda" (worker r on cuda:r), "cuda:0" (every worker on one
+    GPU: the shared-GPU rehearsal) or "cpu"."""
     from .parallel.dp_serving import DPVoiceProcessor
-    g = cfg.gpu
-    spec = {"device": "cuda", "stt_model": g.stt_model, "llm_model": g.llm_model,
-            "max_batch": min(g.max_batch, 64), "max_seq_len": g.max_seq_len,
-            "use_graphs": g.use_graphs, "seed": g.seed}
+    spec = {"device": device, "cfg": cfg, "nats_url": nats_url, "seed": cfg.gpu.seed,
+            "skills_dir": skills_dir, "skills_config_store": skills_config_store, **spec_kw}
     dp = DPVoiceProcessor(spec, n_gpus)
     await dp.start()
     return dp
@@ -222,6 +227,14 @@ class HubServer:
         if hasattr(self.processor, "attach_publisher"):
             self.processor.attach_publisher(publisher)   # progressive per-phrase speech
         await self._check_tts()
+        if (self.streaming is None and self.cfg.streaming.enabled
+                and hasattr(self.processor, "attach_streaming")):
+            # streaming_constructor.go:38-126, composed into the served hub: the
+            # processor's progressive replies are the streaming sessions
+            from .streaming.components import StreamingComponents
+            self.streaming = StreamingComponents.for_processor(self.cfg, self.processor)
+        if self.streaming is not None and hasattr(self.processor, "attach_streaming"):
+            self.processor.attach_streaming(self.streaming)
         a = self.cfg.arbitration
         self.audio_service = AudioService(
             self.processor, window_duration=a.window, scope=a.scope, relay_groups=a.relay_groups,

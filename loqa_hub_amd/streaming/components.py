@@ -21,7 +21,8 @@ from ..llm.tts import TextToSpeech, TTSOptions
 from .audio_pipeline import StreamingAudioPipeline
 from .interrupt import StreamingInterruptHandler
 from .metrics import StreamingMetricsCollector
-from .parser import OllamaStreamingBackend, StreamingCommandParser, StreamingResult
+from .parser import (GPUStreamingBackend, OllamaStreamingBackend, StreamingCommandParser,
+                     StreamingMetrics, StreamingResult)
 
 log = logging.getLogger("loqa.streaming")
 
@@ -84,6 +85,47 @@ class StreamingComponents:
                     raise RuntimeError(f"streaming test failed and fallback disabled: {e}") from e
                 log.warning("streaming self-test failed, fallback enabled: %s", e)
         return comps
+
+    @classmethod
+    def for_processor(cls, cfg, processor) -> "StreamingComponents":
+        """The hub's components when the replies stream from the on-GPU decode
+        (``streaming_constructor.go:38-126``, composed - the reference never
+        constructs them). The parser streams the local engine's constrained
+        decode (``GPUStreamingBackend``: it joins the running batch); the audio
+        pipeline is the processor's own progressive pipeline, so
+        ``active_pipelines`` counts replies being spoken. A data-parallel
+        front end has no local engine: its replies stream inside the GPU
+        workers, which report each session's metrics with the result. No
+        self-test decode is run at start-up (the reference's self-test probes
+        an external Ollama; the engine here is already warmed up)."""
+        sc = cfg.streaming
+        pipe = getattr(processor, "pipeline", None)
+        llm = getattr(pipe, "llm", None)
+        backend = GPUStreamingBackend(llm) if llm is not None else None
+        parser = StreamingCommandParser(backend, None, sc.enabled,
+                                        max_buffer_time=sc.max_buffer_time,
+                                        max_tokens_per_phrase=sc.max_tokens_per_phrase)
+        audio = getattr(processor, "speech_pipeline", None) or StreamingAudioPipeline(
+            getattr(processor, "tts", None), tts_options_from(cfg),
+            sc.audio_concurrency if sc.audio_concurrency > 0 else 3)
+        return cls(parser, audio, StreamingInterruptHandler(sc.interrupt_timeout,
+                                                            2 * sc.interrupt_timeout),
+                   StreamingMetricsCollector(sc.metrics_enabled))
+
+    # -- progressive replies of the voice processors as streaming sessions
+    def begin_speech_session(self, session_id: str, speech) -> None:
+        """``speech``: anything with ``cancel()`` (a ``ProgressiveSpeech``, or
+        the DP front end's handle on a worker's reply)."""
+        self.metrics.record_session_start(session_id)
+        self.interrupt_handler.register_session(session_id, cancel=speech.cancel,
+                                                audio_pipeline=speech)
+
+    def end_speech_session(self, session_id: str, m: dict | None) -> None:
+        if m:
+            self.metrics.record_session_metrics(session_id, StreamingMetrics(**m))
+        s = self.interrupt_handler.active.get(session_id)
+        if s is not None and s.interrupted_at is None:
+            self.interrupt_handler.active.pop(session_id, None)
 
     def update_configuration(self, cfg) -> None:
         if cfg is None:

@@ -23,7 +23,7 @@ import struct
 import time
 
 from .audio_pipeline import StreamingAudioPipeline
-from .chan import Chan
+from .chan import Chan, ChannelClosed
 from .parser import PhraseBuffer
 
 log = logging.getLogger("loqa.streaming.progressive")
@@ -138,10 +138,16 @@ class ProgressiveSpeech:
         self.chunks: list = []
         self.published = 0
         self.t_start = time.perf_counter()
+        self.mono_start = time.monotonic()   # the streaming metrics' clock
+        self.t_first_piece = 0.0       # first character of the reply field
         self.t_first_phrase = 0.0      # first phrase handed to TTS
         self.t_first_audio = 0.0       # first phrase's audio published
         self.t_field_closed = 0.0      # the reply field was complete
+        self.t_done = 0.0              # every phrase delivered (or interrupted)
         self.text: list[str] = []
+        self.n_pieces = 0
+        self.n_phrases = 0
+        self.interrupted = False
         self._closed = False
         self._consumer = self.loop.create_task(self._consume())
 
@@ -154,6 +160,9 @@ class ProgressiveSpeech:
             return
         piece, closed = self.tap.feed(self.tok.decode(ids))
         if piece:
+            if not self.t_first_piece:
+                self.t_first_piece = time.perf_counter()
+            self.n_pieces += 1
             self.text.append(piece)
             phrase = self.pb.add_token(piece)
             if phrase:
@@ -170,6 +179,7 @@ class ProgressiveSpeech:
             return
         if not self.t_first_phrase:
             self.t_first_phrase = time.perf_counter()
+        self.n_phrases += 1
         if not self.phrases.try_put(phrase.strip()):
             log.warning("phrase queue full for %s, phrase dropped", self.relay_id)
 
@@ -178,10 +188,22 @@ class ProgressiveSpeech:
             self._closed = True
             self.phrases.close()
 
+    def cancel(self) -> None:
+        """Interrupt the reply (a new wake word from the same relay,
+        ``streaming_interrupt_handler.go:69-119``): no further phrase is
+        synthesised or published; ``finish`` returns what was already spoken.
+        The decode and its command queue are not affected."""
+        if self.interrupted or self.t_done:
+            return
+        self.interrupted = True
+        self._close()
+        # cancels the synthesis tasks and closes the chunk stream _consume reads
+        self.loop.create_task(self.pipeline.stop_pipeline(self.session_id))
+
     async def _consume(self) -> None:
         try:
             async for chunk in self.pc.audio_chunks:
-                if chunk.is_last:
+                if chunk.is_last or self.interrupted:
                     break
                 self.chunks.append(chunk)
                 if self.publisher is not None:
@@ -196,7 +218,10 @@ class ProgressiveSpeech:
                         log.warning("phrase publish to %s failed: %s", self.relay_id, e)
                 if not self.t_first_audio:
                     self.t_first_audio = time.perf_counter()
+        except ChannelClosed:
+            pass
         finally:
+            self.t_done = time.perf_counter()
             await self.pipeline.stop_pipeline(self.session_id)
 
     async def finish(self, fallback_text: str = "") -> tuple[bytes, int]:
@@ -229,4 +254,17 @@ class ProgressiveSpeech:
             return round((t - self.t_start) * 1e3, 2) if t else None
         return {"first_phrase_ms": ms(self.t_first_phrase), "first_audio_ms": ms(self.t_first_audio),
                 "field_closed_ms": ms(self.t_field_closed), "phrases": len(self.chunks),
-                "published": self.published}
+                "published": self.published, "interrupted": self.interrupted,
+                "streaming": self.streaming_metrics()}
+
+    def streaming_metrics(self) -> dict:
+        """The session as ``streaming.parser.StreamingMetrics`` fields (monotonic
+        clock, ``streaming_metrics.go:121-153``): first token = first character
+        of the reply field, completion = every phrase delivered."""
+        def mono(t):
+            return self.mono_start + (t - self.t_start) if t else 0.0
+        return {"start_time": self.mono_start, "first_token_time": mono(self.t_first_piece),
+                "first_phrase_time": mono(self.t_first_phrase),
+                "completion_time": 0.0 if self.interrupted else mono(self.t_done),
+                "token_count": self.n_pieces, "phrase_count": self.n_phrases,
+                "buffer_overflows": 0, "interrupt_count": int(self.interrupted)}

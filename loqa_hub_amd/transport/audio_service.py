@@ -288,6 +288,15 @@ class AudioService:
 
     # ------------------------------------------------------------ processing
     async def _process_winner(self, rs: RelayStream) -> UtteranceResult:
+        # a new command from this relay interrupts the reply it may still be
+        # receiving (progressive speech; streaming_interrupt_handler.go:69-119)
+        interrupt = getattr(self.processor, "interrupt_relay", None)
+        if interrupt is not None:
+            try:
+                if interrupt(rs.relay_id):
+                    self.stats["interrupted"] = self.stats.get("interrupted", 0) + 1
+            except Exception as e:  # noqa: BLE001
+                hublog.log_warn("reply interrupt failed", relay_id=rs.relay_id, error=str(e))
         # collect speech until end-of-speech (bounded), instead of the reference's
         # snapshot at window close
         try:

@@ -84,13 +84,34 @@ class GPUVoiceProcessor:
         self.speech_pipeline = speech_pipeline
         self.max_buffer_time, self.max_tokens_per_phrase = max_buffer_time, max_tokens_per_phrase
         self.publisher = None           # NATS audio publisher (HubServer.start attaches it)
+        self.streaming = None           # StreamingComponents (HubServer.start attaches them)
+        self._speaking: dict[str, object] = {}   # relay id -> its reply still being spoken
         pipeline.batch_window, pipeline.max_batch = batch_window, max_batch
         self.stats = {"utterances": 0, "errors": 0, "bridge_sessions": 0, "bridge_ack": 0,
-                      "bridge_fallback": 0,
+                      "bridge_fallback": 0, "interrupted": 0,
                       "progressive": 0, "first_audio_ms_sum": 0.0, "first_audio_n": 0}
 
     def attach_publisher(self, publisher) -> None:
         self.publisher = publisher
+
+    def attach_streaming(self, components) -> None:
+        """Progressive replies become streaming sessions: registered with the
+        interrupt handler, recorded in the streaming metrics."""
+        self.streaming = components
+
+    def interrupt_relay(self, relay_id: str, reason: str = "new_command") -> bool:
+        """A new wake-word winner on ``relay_id``: stop speaking the reply that
+        relay is still receiving (``streaming_interrupt_handler.go:69-119``)."""
+        speech = self._speaking.get(relay_id)
+        if speech is None or speech.interrupted or speech.t_done:
+            return False
+        self.stats["interrupted"] += 1
+        ih = self.streaming.interrupt_handler if self.streaming is not None else None
+        if ih is not None and speech.session_id in ih.active:
+            ih.interrupt_session(speech.session_id, reason)
+        else:
+            speech.cancel()
+        return True
 
     def new_pcm_slot(self):
         """A pinned stager slot for one relay's incoming PCM (AudioService)."""
@@ -126,6 +147,9 @@ class GPUVoiceProcessor:
                                        self.publisher, max_buffer_time=self.max_buffer_time,
                                        max_tokens_per_phrase=self.max_tokens_per_phrase)
             j.on_tokens = speech.on_tokens
+            self._speaking[relay_id] = speech
+            if self.streaming is not None:
+                self.streaming.begin_speech_session(speech.session_id, speech)
         try:
             await self.pipeline.submit(j)
         except Exception as e:  # noqa: BLE001
@@ -134,13 +158,13 @@ class GPUVoiceProcessor:
             log.exception("GPU pipeline failed")
             self.stats["errors"] += 1
             if speech is not None:
-                await speech.finish()
+                await self._end_speech(relay_id, speech)
             return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                    error=str(e))
         self.stats["utterances"] += 1
         if j.stt_failed:
             if speech is not None:
-                await speech.finish()
+                await self._end_speech(relay_id, speech)
             return UtteranceResult(success=False, command="error", response_text=MSG_STT_FAILED,
                                    error=j.error)
         text = j.transcription.text if j.transcription else ""
@@ -150,7 +174,7 @@ class GPUVoiceProcessor:
         if self.bridge is not None and r.success and j.multi is not None and j.multi.commands:
             await self._bridge(r, j, ack=speech is None)
         if speech is not None:
-            audio_b, sr = await speech.finish(r.response_text)
+            audio_b, sr = await self._end_speech(relay_id, speech, r.response_text)
             r.audio, r.audio_format, r.audio_sample_rate = audio_b, "wav", sr
             r.audio_published = self.publisher is not None and speech.published > 0
             if sr:
@@ -172,6 +196,15 @@ class GPUVoiceProcessor:
         elif self.tts is not None:
             await self._speak([r])
         return r
+
+    async def _end_speech(self, relay_id: str, speech, fallback_text: str = ""):
+        try:
+            return await speech.finish(fallback_text)
+        finally:
+            if self._speaking.get(relay_id) is speech:
+                del self._speaking[relay_id]
+            if self.streaming is not None:
+                self.streaming.end_speech_session(speech.session_id, speech.streaming_metrics())
 
     async def _bridge(self, r: UtteranceResult, j, ack: bool) -> None:
         """The streaming-predictive bridge on the shared decode: classification

@@ -229,30 +229,28 @@ def test_hub_server_gpu_served(tmp_path, streaming):
     tiny encoder + decoder graphs, constrained Llama decode, command queue on
     NATS), the bridge runs on that decode, the reply is spoken by on-GPU VITS -
     progressively, phrase by phrase, when streaming is enabled - and published
-    on NATS audio.<relay>; the voice event lands in SQLite and /api."""
-    import base64
+    on NATS audio.<relay>; the voice event lands in SQLite and /api; the
+    streaming routes answer from the composed streaming subsystem. (With this
+    test's small models the whole decode is shorter than one VITS synthesis,
+    so audio-before-decode-end is measured on config 5:
+    scripts/bench_configs.py first_audio_before_decode_done.)"""
+    from tests.test_hub_served import _check_served, _served
+    res = _served(tmp_path, "cuda:0", streaming=streaming, llm="test-tiny", stt="whisper-tiny",
+                  tts_model="test-vits")
+    _check_served(*res, streaming=streaming, relays=("kitchen-relay",))
 
-    from loqa_hub_amd.engine.grammar import INTENTS
-    from tests.test_hub_served import _served
-    got, audio, cmds, events, stats, metrics = _served(
-        tmp_path, "cuda:0", streaming=streaming, llm="test-tiny", stt="whisper-tiny",
-        tts_model="test-vits")
-    last = got[-1]
-    assert last.command == "voice_command_success" and last.success
-    assert last.transcription == "turn on the kitchen lights and then play some jazz"
-    assert len(cmds) == 2
-    assert audio and all(base64.b64decode(m["audio_data"])[:4] == b"RIFF" for m in audio)
-    ev = events[0]
-    assert ev["transcription"] == last.transcription and ev["intent"] in INTENTS
-    assert ev["intent"] == cmds[0]["intent"]
-    if streaming:
-        assert stats["progressive"] == 1 and stats["first_audio_n"] == 1
-        # the first phrase went to synthesis while the decode was still running
-        # (with this test's small models the whole decode is shorter than one
-        # VITS synthesis, so audio-before-decode-end is measured on config 5:
-        # scripts/bench_configs.py first_audio_before_decode_done)
-        assert stats["phrase_before_decode_done"] == 1
-    assert "loqa_audio_processed_total 1.0" in metrics
+
+def test_hub_server_gpu_served_dp_shared(tmp_path):
+    """The served DP hub on the GPU: two worker processes (sharing cuda:0
+    here; one per GPU on a node), each with the full composition - its own
+    NATS connection, VITS, bridge, progressive speech, pinned PCM staging of
+    the raw PCM16 the front end ships."""
+    from tests.test_hub_served import _check_served, _served
+    relays = ("kitchen-relay", "bedroom-relay")
+    res = _served(tmp_path, "cuda:0", streaming=True, llm="test-tiny", stt="whisper-tiny",
+                  tts_model="test-vits", dp=2, relays=relays)
+    _check_served(*res, streaming=True, relays=relays)
+    assert sorted(res[4]["dp_workers"]) == [0, 1]
 
 
 def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
