@@ -112,6 +112,193 @@ async def _start_hub(args, pipe, nats_port: int, info):
     return srv, hints
 
 
+class CommandCounter:
+    """--mode hub: the commands each served utterance actually published on
+    ``loqa.voice.commands`` (counted per request id), matched to the relay's
+    utterances through the voice events (one per processed utterance, in
+    order per relay) - the parsed command count, not the expected one."""
+
+    def __init__(self, client):
+        self.client = client
+        self.per_request: dict[str, int] = {}
+
+    @classmethod
+    async def start(cls, url: str) -> "CommandCounter":
+        from loqa_hub_amd.messaging.nats_client import NATSClient
+        c = NATSClient(name="bench-command-counter")
+        await c.connect(url)
+        self = cls(c)
+
+        def on_msg(m):
+            rid = json.loads(m.data).get("request_id", "")
+            self.per_request[rid] = self.per_request.get(rid, 0) + 1
+        await c.subscribe("loqa.voice.commands", on_msg)
+        await c.flush()
+        return self
+
+    async def records(self, srv, hub_recs: dict) -> list[list[float]]:
+        """[parsed commands, expected, ok, latency ms] per timed utterance."""
+        from loqa_hub_amd.storage.voice_events_store import ListOptions
+        await asyncio.sleep(0.2)
+        await self.client.flush()
+        evs = srv.events.list(ListOptions(sort_by="timestamp", sort_order="ASC"))
+        by_relay: dict[str, list[str]] = {}
+        for ev in evs:
+            by_relay.setdefault(ev.relay_id, []).append(ev.request_id)
+        out = []
+        for relay, recs in hub_recs.items():
+            rids = by_relay.get(relay, [])[-len(recs):]
+            rids = [""] * (len(recs) - len(rids)) + rids
+            for (expected, ok, lat), rid in zip(recs, rids):
+                out.append([float(self.per_request.get(rid, 0)), float(expected), ok, lat])
+        return out
+
+    async def close(self) -> None:
+        await self.client.close()
+
+
+def hub_summary(srv, recs: list, args) -> tuple[float | None, dict]:
+    """Served-path statistics: the end-to-end marginal cost of an added command
+    (slope of the relay-side latency over the parsed command count) and the
+    hub's own counters."""
+    from loqa_hub_amd.storage.voice_events_store import ListOptions
+    r = np.array(recs, dtype=np.float64).reshape(-1, 4)
+    slope = (float(np.polyfit(r[:, 0], r[:, 3], 1)[0])
+             if len(r) and len(set(r[:, 0])) >= 2 else None)
+    return slope, {"voice_events": srv.events.count(ListOptions()),
+                   "audio_service": dict(srv.audio_service.stats),
+                   "processor": dict(srv.processor.stats),
+                   "latency_ms_p50": round(float(np.median(r[:, 3])), 1) if len(r) else None,
+                   "latency_ms_p90": round(float(np.percentile(r[:, 3], 90)), 1) if len(r) else None,
+                   "window_ms": args.window_ms}
+
+
+def run_hub_dp(args) -> int:
+    """``--mode hub`` over ``--gpus N`` (or with ``--tts``): the served hub as
+    deployed for BASELINE config 4 - one front-end process (gRPC relays,
+    per-group arbitration, voice events in SQLite) and one worker process per
+    GPU, each with the full composition (``server.build_dp_processor``). B
+    relays per GPU, each a closed loop of StreamAudio calls. The front end
+    never touches a GPU. ``LOQA_DIST_SHARE_GPU=1``: every worker on cuda:0
+    (the rehearsal on a one-GPU box)."""
+    import tempfile
+
+    import grpc
+
+    from loqa_hub_amd import config as cfgmod
+    from loqa_hub_amd.server import HubServer, build_dp_processor
+    from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
+    N, B = args.gpus, args.batch_per_gpu
+    mix = [int(x) for x in args.mix.split(",")]
+    if args.cpu_smoke:
+        args.stt, args.llm, args.tts_model = "test-whisper", "test-tiny", "test-vits"
+    port, broker = spawn_broker()
+    tmp = tempfile.mkdtemp(prefix="loqa-bench-hub-")
+    cfg = cfgmod.load({"LOQA_DB_PATH": os.path.join(tmp, "hub.db"),
+                       "NATS_URL": f"nats://127.0.0.1:{port}",
+                       "ARBITRATION_SCOPE": "per_relay_group",
+                       "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms",
+                       "HUB_STT_MODEL": args.stt, "HUB_LLM_MODEL": args.llm,
+                       "HUB_TTS_MODEL": args.tts_model, "HUB_MAX_BATCH": str(max(B, 8)),
+                       "HUB_TTS_BACKEND": "gpu" if args.tts else "none",
+                       "STREAMING_ENABLED": "true" if args.tts else "false",
+                       "HUB_USE_GRAPHS": "false" if args.no_graphs else "true",
+                       "HUB_SEED": str(args.seed)})
+    device = ("cpu" if args.cpu_smoke else
+              "cuda:0" if os.environ.get("LOQA_DIST_SHARE_GPU", "0") == "1" else "cuda")
+    n_per_stream = args.warmup + args.steps
+    from loqa_hub_amd.engine.synthetic import make_unique
+    counts = [mix[(ci + k) % len(mix)] for ci in range(N * B) for k in range(n_per_stream)]
+    uniq = make_unique(args.seed, counts)
+    hints: dict[str, str] = {}
+    hub_recs: dict[str, list] = {}
+
+    async def main() -> dict:
+        srv = HubServer(cfg, skills_dir=os.path.join(tmp, "skills"),
+                        skills_config_store=os.path.join(tmp, "skillcfg"),
+                        transcript_hints=hints.get)
+        await srv._connect_nats()
+        t_init = time.perf_counter()
+        srv.processor = await build_dp_processor(cfg, N, srv.nats.url, device=device,
+                                                 skills_dir=os.path.join(tmp, "skills"),
+                                                 skills_config_store=os.path.join(tmp, "skillcfg"))
+        t_init = time.perf_counter() - t_init
+        await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
+        counter = await CommandCounter.start(srv.nats.url)
+
+        async def client(ci: int, ch, n: int, record: bool) -> None:
+            call = stream_audio_stub(ch)
+            relay = f"relay-{ci}"
+            for k in range(n):
+                u = uniq[ci * n_per_stream + k + (args.warmup if record else 0)]
+                hints[relay] = u.text
+                data = np.ascontiguousarray(u.pcm, dtype="<i2").tobytes()
+                wake, rest = data[:9600], data[9600:]
+
+                async def chunks():
+                    yield AudioChunk(relay_id=relay, audio_data=wake, sample_rate=16000,
+                                     is_wake_word=True)
+                    for o in range(0, max(len(rest), 1), 3200):
+                        yield AudioChunk(relay_id=relay, audio_data=rest[o:o + 3200],
+                                         sample_rate=16000, is_end_of_speech=o + 3200 >= len(rest))
+                t_s = time.perf_counter()
+                got = [r async for r in call(chunks())]
+                lat = (time.perf_counter() - t_s) * 1e3
+                if record:
+                    hub_recs.setdefault(relay, []).append(
+                        [u.n_commands, float(bool(got) and got[-1].success), lat])
+
+        async def run(n: int, record: bool) -> None:
+            async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
+                await asyncio.gather(*[client(ci, ch, n, record) for ci in range(N * B)])
+        try:
+            await run(args.warmup, False)
+            t0 = time.perf_counter()
+            await run(args.steps, True)
+            elapsed = time.perf_counter() - t0
+            recs = await counter.records(srv, hub_recs)
+            slope, hub_stats = hub_summary(srv, recs, args)
+            hub_stats["dp"] = srv.processor.metrics()
+            if srv.streaming is not None:
+                hub_stats["streaming"] = srv.streaming.metrics.get_aggregate_metrics().to_json()
+        finally:
+            await counter.close()
+            await srv.stop()
+        r = np.array(recs, dtype=np.float64).reshape(-1, 4)
+        return {"elapsed": elapsed, "slope": slope, "hub": hub_stats, "init_s": t_init,
+                "ok": float(r[:, 2].mean()) if len(r) else 0.0,
+                "match": float((r[:, 0] == r[:, 1]).mean()) if len(r) else 0.0}
+    try:
+        res = asyncio.run(main())
+    finally:
+        broker.stdin.close()
+        broker.wait(timeout=10)
+    value = N * B * args.steps / res["elapsed"]
+    e2e = res["slope"]
+    print(json.dumps({
+        "metric": ("utterances_per_sec (multi-command utterances; ms per added command "
+                   "reported alongside)"),
+        "value": round(value, 3), "unit": "utterances/s", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(res["elapsed"] / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": ("synthetic speech-like PCM16 over gRPC relays, every utterance a distinct "
+                 "transcript + random-init weights (teacher-forced STT, grammar-constrained LLM)"),
+        "config": {"model": f"{args.stt} + {args.llm}" + (f" + {args.tts_model}" if args.tts else ""),
+                   "global_batch": N * B, "seq_len": 1500, "parallelism": f"dp{N}",
+                   "commands_mix": mix, "baseline_config": 4, "mode": "hub",
+                   "served": "front end + one worker process per GPU",
+                   "shared_gpu": device == "cuda:0", "concurrent_streams_per_gpu": B,
+                   "tts": args.tts},
+        "ms_per_added_command_e2e_marginal": None if e2e is None else round(e2e, 3),
+        "baseline_ms_per_added_command": BASELINE_MS_PER_ADDED_COMMAND,
+        "added_command_speedup_vs_baseline": (None if not e2e or e2e <= 0 else
+                                              round(BASELINE_MS_PER_ADDED_COMMAND / e2e, 3)),
+        "queue_success_rate": round(res["ok"], 4),
+        "command_count_match_rate": round(res["match"], 4),
+        "hub": res["hub"], "init_s": round(res["init_s"], 2)}), flush=True)
+    return 0
+
+
 def relaunch(n: int, argv: list[str]) -> int:
     """``--gpus N`` without torchrun: run this bench under torch.distributed.run
     with N ranks (a child process; nothing here has touched the GPU)."""
@@ -128,7 +315,8 @@ def relaunch(n: int, argv: list[str]) -> int:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (default: WORLD_SIZE under torchrun, else 1)")
     # 8 utterances per stream: a whole number of passes over the 4-way command
     # mix for every stream (5 ends on an unbalanced tail: measured 17.4-17.5
     # vs 18.7-18.9 utt/s at 4, 8 and 12)
@@ -151,9 +339,18 @@ def main(argv=None) -> int:
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
     ap.add_argument("--stt-priority", type=int, default=-1,
                     help="HIP stream priority of the STT worker (-1 high, 0 normal)")
+    ap.add_argument("--tts", action="store_true",
+                    help="--mode hub: every reply spoken by on-GPU VITS (progressive)")
+    ap.add_argument("--tts-model", default="vits-ljs")
     args = ap.parse_args(argv)
 
     world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(world_env or "1")
+    if args.mode == "hub" and world_env is None and (args.gpus > 1 or args.tts):
+        # the served multi-GPU hub: ONE front-end process (gRPC, arbitration,
+        # events) over one worker process per GPU (parallel/dp_serving.py)
+        return run_hub_dp(args)
     if world_env is None and args.gpus > 1:
         return relaunch(args.gpus, sys.argv[1:] if argv is None else list(argv))
     if int(world_env or "1") != args.gpus:
@@ -265,10 +462,12 @@ def main(argv=None) -> int:
         await asyncio.gather(*[client(ci) for ci in range(B)])
 
     recs_local: list[list[float]] = []
+    hub_recs: dict[str, list] = {}
 
     hub = None
     if args.mode == "hub":
         hub = loop.run_until_complete(_start_hub(args, pipe, port, info))
+        cmd_counter = loop.run_until_complete(CommandCounter.start(f"nats://127.0.0.1:{port}"))
 
     async def run_hub(n: int, record: bool) -> None:
         """--mode hub: B relays per GPU, each a closed loop of gRPC StreamAudio
@@ -301,7 +500,7 @@ def main(argv=None) -> int:
                 lat = (time.perf_counter() - t_s) * 1e3
                 ok = bool(got) and got[-1].success
                 if record:
-                    recs_local.append([u.n_commands, u.n_commands, float(ok), lat])
+                    hub_recs.setdefault(relay, []).append([u.n_commands, float(ok), lat])
         async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
             await asyncio.gather(*[client(ci, ch) for ci in range(B)])
 
@@ -322,22 +521,15 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
 
+    if hub is not None:
+        recs_local = loop.run_until_complete(cmd_counter.records(hub[0], hub_recs))
     if args.mode in ("closed", "hub") and recs_local:
         step.records.append(gather_records(info, torch.tensor(recs_local, dtype=torch.float64)).cpu())
     stats = added_command_stats(all_jobs)
     hub_stats = None
     if hub is not None:
-        # served path: per-utterance latency at the relay vs its command count
-        r = np.array(recs_local, dtype=np.float64)
-        slope = float(np.polyfit(r[:, 0], r[:, 3], 1)[0]) if len(set(r[:, 0])) >= 2 else None
-        stats["e2e_marginal_ms_per_added_command"] = slope
-        srv = hub[0]
-        from loqa_hub_amd.storage.voice_events_store import ListOptions
-        hub_stats = {"voice_events": srv.events.count(ListOptions()),
-                     "audio_service": dict(srv.audio_service.stats),
-                     "processor": dict(srv.processor.stats),
-                     "latency_ms_p50": round(float(np.median(r[:, 3])), 1),
-                     "window_ms": args.window_ms}
+        stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub[0], recs_local,
+                                                                            args)
     def _mean_ms(a, b):
         v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
         return round(float(np.mean(v)) * 1e3, 2) if v else None
@@ -400,6 +592,7 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     if hub is not None:
+        loop.run_until_complete(cmd_counter.close())
         loop.run_until_complete(hub[0].stop())
     loop.run_until_complete(nats.close())
     pdist.shutdown(info)
