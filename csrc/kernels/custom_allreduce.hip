@@ -207,6 +207,8 @@ __global__ __launch_bounds__(256) void car_twoshot_kernel(CarPeers peers, const 
 // from the owner's memory, never a stale L2 line); the buffers live in the
 // uncached region, so the GEMM's stores are in memory when its kernel ends.
 #define CAR_KEY_ROWS 256      // rows of the argmax exchange
+#define CAR_ERR_TOKEN (-2)    // argmax output of a step whose collectives failed
+#define CAR_MAX_TOKEN_ID 0x1ffff  // 17-bit token ids in the argmax records
 #define CAR_SYS 17            // buffer-op cache policy: sc0 | sc1 (system coherent)
 
 typedef unsigned car_u32x4 __attribute__((ext_vector_type(4)));
@@ -387,8 +389,15 @@ __global__ __launch_bounds__(256) void car_argmax_kernel(CarPeers peers, long lo
       const unsigned long long k = v & ((1ull << 49) - 1);
       best = k > best ? k : best;
     }
-    out[b] = (!ok || best == 0) ? -1 : (int)(0x1ffffu - (unsigned)(best & 0x1ffffu));
+    out[b] = !ok ? CAR_ERR_TOKEN : best == 0 ? -1 : (int)(0x1ffffu - (unsigned)(best & 0x1ffffu));
   }
+  // the sticky error word rides on every step's sampled tokens: any collective
+  // of this step (or an earlier one) that timed out turns every row into
+  // CAR_ERR_TOKEN, so the host sees it in the result it reads anyway - no
+  // separate read of the word per step
+  __syncthreads();
+  if (ld_sys(&me->error))
+    for (int b = threadIdx.x; b < B; b += blockDim.x) out[b] = CAR_ERR_TOKEN;
   car_epoch_done(me, e, 1);
 }
 
@@ -509,11 +518,15 @@ extern "C" int loqa_car_resid(void* hp, int which, void* residual, float* rowsq_
 }
 
 // out[b] = global argmax over ranks of (logits[b, idx[b]], idx[b] + lo); -1 if
-// no rank allowed any token. idx: this rank's masked argmax (-1 = none).
+// no rank allowed any token, CAR_ERR_TOKEN if a collective timed out.
+// idx: this rank's masked argmax (-1 = none).
+// shard: this rank's vocab width; every global id (lo .. lo + shard - 1) must
+// fit the record's 17-bit id field.
 extern "C" int loqa_car_argmax(void* hp, const float* logits, long long ld, const int* idx, int B,
-                               int lo, int* out, hipStream_t s) {
+                               int lo, int shard, int* out, hipStream_t s) {
   CarHandle* h = static_cast<CarHandle*>(hp);
-  if (B < 1 || B > CAR_KEY_ROWS || lo < 0) return (int)hipErrorInvalidValue;
+  if (B < 1 || B > CAR_KEY_ROWS || lo < 0 || lo + shard - 1 > CAR_MAX_TOKEN_ID || shard < 1)
+    return (int)hipErrorInvalidValue;
   for (int q = 0; q < h->world; ++q)
     if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(car_argmax_kernel, dim3(1), dim3(256), 0, s, h->peers, (long long)car_key_off(h),
@@ -528,6 +541,21 @@ extern "C" int loqa_car_error(void* hp) {
   hipMemcpy(&v, &reinterpret_cast<CarSignals*>(h->local)->error, sizeof(unsigned),
             hipMemcpyDeviceToHost);
   return (int)v;
+}
+
+// copy `bytes` of device memory into input buffer `which` (start-up self-test)
+extern "C" int loqa_car_fill_inbuf(void* hp, int which, const void* src, long long bytes,
+                                   hipStream_t s) {
+  CarHandle* h = static_cast<CarHandle*>(hp);
+  if (which < 0 || which > 1 || bytes < 0 || (size_t)bytes > h->in_bytes) return (int)hipErrorInvalidValue;
+  return (int)hipMemcpyAsync(h->local + car_in_off(h, which), src, (size_t)bytes,
+                             hipMemcpyDeviceToDevice, s);
+}
+
+// clear this rank's sticky error word (start-up self-test only)
+extern "C" int loqa_car_clear_error(void* hp) {
+  CarHandle* h = static_cast<CarHandle*>(hp);
+  return (int)hipMemset(&reinterpret_cast<CarSignals*>(h->local)->error, 0, sizeof(unsigned));
 }
 
 extern "C" void loqa_car_destroy(void* hp) {

@@ -14,6 +14,10 @@
 // larger than a slot is split into continuation chunks. Publishing is a
 // memcpy and a release store (~1 us); a follower that is waiting spins
 // briefly, then sleeps in growing steps, so an idle hub costs no CPU.
+//
+// Liveness: every rank stamps its own heartbeat word (steady-clock us, from a
+// thread of its own); the leader reads the followers' ages to detect a lost
+// follower even while the hub is idle (no collective would notice it then).
 #include <atomic>
 #include <cerrno>
 #include <chrono>
@@ -39,7 +43,13 @@ struct Header {
   uint64_t slot_bytes;
   alignas(64) std::atomic<uint64_t> published;
   alignas(64) std::atomic<uint64_t> consumed[kMaxWorld];
+  alignas(64) std::atomic<int64_t> beat[kMaxWorld];   // steady-clock us; 0 = never
 };
+
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct SlotHead {
   uint64_t seq;
@@ -201,6 +211,20 @@ long long loqa_tpctl_recv(void* h, void* buf, long long cap, int* stop, long lon
     if (!(sh.flags & kFlagMore)) break;
   }
   return overflow ? -3 : total;
+}
+
+// this rank's heartbeat
+void loqa_tpctl_beat(void* h) {
+  Ctl* c = static_cast<Ctl*>(h);
+  if (c) c->hdr->beat[c->rank].store(now_us(), std::memory_order_release);
+}
+
+// microseconds since rank r last beat; -1 if it never did
+long long loqa_tpctl_beat_age(void* h, int r) {
+  Ctl* c = static_cast<Ctl*>(h);
+  if (!c || r < 0 || r >= (int)c->hdr->world) return -2;
+  const int64_t b = c->hdr->beat[r].load(std::memory_order_acquire);
+  return b == 0 ? -1 : (long long)(now_us() - b);
 }
 
 void loqa_tpctl_close(void* h) {

@@ -203,6 +203,7 @@ class GPUConfig:
     tts_backend: str = "gpu"          # gpu | http | none
     use_graphs: bool = True
     seed: int = 0
+    tp_fallback_model: str = "llama3-8b"   # a failed TP group degrades to this ("none": off)
     stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
     llm_checkpoint: str = ""
 
@@ -348,6 +349,7 @@ def load(env=None) -> Config:
             tts_backend=env_str(e, "gpu", "HUB_TTS_BACKEND"),
             use_graphs=env_bool(e, True, "HUB_USE_GRAPHS"),
             seed=env_int(e, 0, "HUB_SEED"),
+            tp_fallback_model=env_str(e, "llama3-8b", "HUB_TP_FALLBACK_MODEL"),
             stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
             llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
         ),

@@ -18,6 +18,7 @@ sequence) plus one small pinned H2D copy of the step metadata.
 """
 from __future__ import annotations
 
+import logging
 import os
 import queue
 import threading
@@ -35,6 +36,9 @@ from ..models.llama import LlamaModel, LlamaWeights, StepMeta, TPGroup
 from .grammar import GrammarState, GrammarTables
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
+from ..parallel.custom_allreduce import ERR_TOKEN, CollectiveError
+
+log = logging.getLogger("loqa.llm")
 
 
 @dataclass
@@ -179,6 +183,14 @@ class LLMEngine:
         # 19.1 utt/s; docs/PERF.md)
         self.mixed_prefill = (os.environ.get("LOQA_MIXED_PREFILL", "0") == "1"
                               and not getattr(self.weights, "compact", False))
+        # prefill coalescing (serialised prefill): while a decode batch of at
+        # least ``hold_min_live`` sequences keeps the GPU busy, new prompts wait
+        # up to ``hold_ms`` (or until ``hold_tokens`` prompt tokens are waiting)
+        # so that several arrivals share ONE prefill pass - a pass streams every
+        # weight once (~16 GB for the 8B model) whatever its token count
+        self.hold_ms = float(os.environ.get("LOQA_PREFILL_HOLD_MS", "0"))
+        self.hold_tokens = int(os.environ.get("LOQA_PREFILL_HOLD_TOKENS", "1200"))
+        self.hold_min_live = int(os.environ.get("LOQA_PREFILL_HOLD_MIN_LIVE", "3"))
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
@@ -260,7 +272,7 @@ class LLMEngine:
             w0 = lo // 32
             self._local_mask = self.masks[:, w0:w0 + (V + 31) // 32].contiguous()
         idx = ops.masked_argmax(logits, self._local_mask, mask_rows)
-        if self.tp.car is not None and logits.is_cuda:
+        if self.tp.car is not None and logits.is_cuda and self.tp.car.argmax_fits(lo, V):
             if logits.dtype != torch.float32:
                 logits = logits.float()
             return self.tp.car.argmax(logits, idx, lo)
@@ -434,13 +446,21 @@ class LLMEngine:
             if getattr(r, "inline", False):   # prompt fed through decode steps
                 self.stats["prefill_tokens"] += r.inline   # type: ignore[attr-defined]
                 self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
+        if t < 0:
+            if self.tp.world > 1 and t == ERR_TOKEN:
+                raise CollectiveError(f"TP rank {self.tp.rank}: a collective timed out "
+                                      "(a peer rank is gone or hung)")
+            raise RuntimeError(f"no token allowed for sequence {r.seq_id} (sampled {t})")
         r.token_times.append(now)
         r.steps += 1
         forced = r.grammar.advance(int(t))
         self.stats["sampled_tokens"] += 1
         self.stats["forced_tokens"] += len(forced)
         if r.on_tokens is not None:
-            r.on_tokens([int(t)] + forced)
+            try:
+                r.on_tokens([int(t)] + forced)
+            except Exception:  # noqa: BLE001 - a consumer's hook never reaches the scheduler
+                log.exception("on_tokens hook of sequence %d failed", r.seq_id)
         if r.grammar.done:
             r.done = True
             r.t_done = now
@@ -630,7 +650,18 @@ class LLMEngine:
             return join_futures([self.submit_batch(reqs[i:i + cap], on_done)
                                  for i in range(0, len(reqs), cap)], reqs)
         self._inbox.put((reqs, on_done, fut))
+        if getattr(self, "_fatal", None) is not None:
+            self._fail_inbox()         # raced a TP failure: the scheduler is gone
         return fut
+
+    def _fail_inbox(self) -> None:
+        while True:
+            try:
+                it = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            if it is not None and not it[2].done():
+                it[2].set_exception(self._fatal)
 
     def _schedule(self, stream_priority: int) -> None:
         try:
@@ -660,6 +691,8 @@ class LLMEngine:
         # sized for that many)
         waiting: list[tuple] = []
         cap = max(1, self.max_seqs)
+        held: list[GenRequest] = []     # admitted, waiting for a coalesced prefill pass
+        held_t0 = 0.0
         pf_pool = self._prefill_executor() if self.overlap_prefill else None
         if self.pipelined:
             from .llm_pipeline import DecodePipeline
@@ -667,14 +700,14 @@ class LLMEngine:
         pl = self._pl
         t_end = 0.0
         while self._running:
-            idle = not live and not pending and not waiting
+            idle = not live and not pending and not waiting and not held
             items = self._next_items(idle)
             if items is None:          # TP follower: the leader stopped
                 break
             waiting += [it for it in items if it is not None]
             try:
                 new: list[GenRequest] = []
-                active = len(live) + sum(len(r) for r, _ in pending)
+                active = len(live) + len(held) + sum(len(r) for r, _ in pending)
                 while waiting and active + len(new) + len(waiting[0][0]) <= cap:
                     reqs, cb, fut = waiting.pop(0)
                     if not reqs:
@@ -695,6 +728,17 @@ class LLMEngine:
                             pl.admit(r)
                     live += inl
                     new = [r for r in new if len(r.feed) > self.inline_prefill]
+                if self.hold_ms > 0 and pf_pool is None and self.tp_ctl is None:
+                    if new and not held:
+                        held_t0 = time.perf_counter()
+                    held += new
+                    new = []
+                    if held and (len(live) < self.hold_min_live
+                                 or sum(len(r.feed) for r in held) >= self.hold_tokens
+                                 or (time.perf_counter() - held_t0) * 1e3 >= self.hold_ms):
+                        new, held = held, []
+                        self.stats["prefill_passes_coalesced"] = (
+                            self.stats.get("prefill_passes_coalesced", 0) + (len(new) > 1))
                 if new:
                     if pf_pool is not None:
                         pending.append((new, pf_pool.submit(self._prefill_timed, new)))
@@ -753,6 +797,10 @@ class LLMEngine:
                 else:
                     t_end = 0.0
             except Exception as e:  # noqa: BLE001 - fail every waiting batch loudly
+                if isinstance(e, CollectiveError):
+                    log.error("%s", e)
+                else:
+                    log.exception("LLM scheduler iteration failed")
                 # in-flight prefills / pipelined steps still write KV into their
                 # sequences' blocks: let them finish before the blocks go back
                 wait([f for _, f in pending])
@@ -774,25 +822,74 @@ class LLMEngine:
                 for _, _, fut in waiting:
                     if not fut.done():
                         fut.set_exception(e)
-                live, pending, waiting = [], [], []
+                live, pending, waiting, held = [], [], [], []
+                if self.tp_ctl is not None:
+                    # lock-step TP: the ranks' scheduler states may now differ
+                    # (this rank reset, the others did not), so the group
+                    # cannot continue - stop it and report
+                    self._tp_fail(e)
+                    break
 
         if self.tp_ctl is not None and self.tp_ctl.leader:
-            self.tp_ctl.publish([], stop=True)
+            try:
+                self.tp_ctl.publish([], stop=True, timeout_s=2.0)
+            except Exception as e:  # noqa: BLE001 - a follower is gone: nothing to stop
+                log.warning("TP stop record not delivered: %s", e)
+
+    def _tp_fail(self, e: Exception) -> None:
+        """The TP group failed: later submissions fail at once, followers get
+        the stop record, and the owner's ``on_tp_failure`` hook (the hub's
+        degradation to a single-GPU engine) runs."""
+        self._fatal = e if isinstance(e, CollectiveError) else CollectiveError(
+            f"TP group stopped after a scheduler failure on rank {self.tp.rank}: {e}")
+        self._running = False
+        self.stats["tp_failed"] = 1
+        self._fail_inbox()         # submissions that raced the failure
+        hook = getattr(self, "on_tp_failure", None)
+        if hook is not None:
+            try:
+                hook(self._fatal)
+            except Exception:  # noqa: BLE001
+                log.exception("on_tp_failure hook failed")
 
     def _next_items(self, idle: bool) -> list | None:
         """This scheduler iteration's new inbox items (blocking when idle).
         TP leader: also publishes them; TP follower: replays the leader's
         record instead of reading an inbox (None once the leader stopped)."""
         ctl = self.tp_ctl
-        if ctl is None or ctl.leader:
+        if ctl is None:
             items = [self._inbox.get()] if idle else []   # idle: block for work
             while True:
                 try:
                     items.append(self._inbox.get_nowait())
                 except queue.Empty:
                     break
-            if ctl is not None:
-                ctl.publish([[(r.prompt, r.schema) for r in it[0]] for it in items if it is not None])
+            return items
+        if ctl.leader:
+            items = []
+            while True:
+                # idle: block for work, waking up to check the followers' heartbeats
+                self._check_followers()
+                if not idle:
+                    break
+                try:
+                    items.append(self._inbox.get(timeout=0.25))
+                    break
+                except queue.Empty:
+                    continue
+            while True:
+                try:
+                    items.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            try:
+                ctl.publish([[(r.prompt, r.schema) for r in it[0]] for it in items if it is not None],
+                            timeout_s=self.tp_follower_timeout)
+            except RuntimeError as e:
+                for it in items:
+                    if it is not None and not it[2].done():
+                        it[2].set_exception(CollectiveError(str(e)))
+                raise CollectiveError(str(e)) from e
             return items
         while True:
             rec, stop = ctl.recv(timeout_s=0.5)
@@ -803,6 +900,15 @@ class LLMEngine:
                 break
         self.stats["tp_records"] = self.stats.get("tp_records", 0) + 1
         return [([GenRequest(list(p), sch) for p, sch in batch], None, Future()) for batch in rec]
+
+    # a follower whose heartbeat is this old is gone (its process died)
+    tp_follower_timeout = float(os.environ.get("LOQA_TP_FOLLOWER_TIMEOUT", "10"))
+
+    def _check_followers(self) -> None:
+        lost = self.tp_ctl.lost_followers(self.tp_follower_timeout)
+        if lost:
+            raise CollectiveError(f"TP followers {lost} stopped heart-beating "
+                                  f"for {self.tp_follower_timeout:.0f} s")
 
     def follow(self, stream_priority: int = 0) -> None:
         """TP follower rank: run the scheduler on the calling thread, replaying
@@ -818,6 +924,7 @@ class LLMEngine:
         t0 = time.perf_counter()
         self.prefill(reqs, riders)
         self.stats["prefill_s"] += time.perf_counter() - t0
+        self.stats["prefill_passes"] = self.stats.get("prefill_passes", 0) + 1
 
     def _prefill_executor(self) -> ThreadPoolExecutor:
         if getattr(self, "_pf_pool", None) is None:
@@ -840,7 +947,10 @@ class LLMEngine:
         def done(r: GenRequest) -> None:   # scheduler or prefill thread
             self.kv.pool.free_seq(r.seq_id)
             if cb is not None:
-                cb(r)
+                try:
+                    cb(r)
+                except Exception:  # noqa: BLE001 - the caller's callback, not the scheduler's
+                    log.exception("completion callback of sequence %d failed", r.seq_id)
             with self._cells_lock:
                 cell[0] -= 1
                 last = cell[0] == 0

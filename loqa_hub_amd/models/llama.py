@@ -64,6 +64,9 @@ class TPGroup:
                 torch.device(device).type == "cuda":
             from ..parallel.custom_allreduce import CustomAllReduce
             ar = CustomAllReduce(group)
+            # every collective checked against the host reduction before the
+            # group serves (raises on every rank on a mismatch)
+            ar.self_test()
         return cls(rank, world, group, ar)
 
     @property

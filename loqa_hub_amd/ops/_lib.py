@@ -137,12 +137,15 @@ _CAR_SIGS = {
     "loqa_car_create": ([c_int, c_int, c_ll, c_ll], c_void_p),
     "loqa_car_inbuf": ([c_void_p, c_int], c_void_p),
     "loqa_car_resid": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
-    "loqa_car_argmax": ([c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
+    "loqa_car_argmax": ([c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
+                        c_int),
     "loqa_car_handle": ([c_void_p, c_void_p], c_int),
     "loqa_car_handle_size": ([], c_int),
     "loqa_car_open": ([c_void_p, c_void_p], c_int),
     "loqa_car_allreduce": ([c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p], c_int),
     "loqa_car_error": ([c_void_p], c_int),
+    "loqa_car_clear_error": ([c_void_p], c_int),
+    "loqa_car_fill_inbuf": ([c_void_p, c_int, c_void_p, c_ll, c_void_p], c_int),
     "loqa_car_destroy": ([c_void_p], None),
 }
 
@@ -173,6 +176,8 @@ _RUNTIME_SIGS = {
     "loqa_tpctl_publish": ([c_void_p, c_void_p, c_ll, c_int, c_ll], c_int),
     "loqa_tpctl_recv": ([c_void_p, c_void_p, c_ll, ctypes.POINTER(c_int), c_ll], c_ll),
     "loqa_tpctl_close": ([c_void_p], None),
+    "loqa_tpctl_beat": ([c_void_p], None),
+    "loqa_tpctl_beat_age": ([c_void_p, c_int], c_ll),
 }
 
 

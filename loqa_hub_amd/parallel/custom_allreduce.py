@@ -52,6 +52,15 @@ class DeviceView:
         return self.shape[1] if dim == 0 else 1
 
 
+class CollectiveError(RuntimeError):
+    """A tensor-parallel collective timed out (a peer never arrived): the
+    group can no longer agree and must stop."""
+
+
+ERR_TOKEN = -2            # argmax output of a step whose collectives failed
+MAX_TOKEN_ID = (1 << 17) - 1   # token ids carried by the argmax records
+
+
 class CustomAllReduce:
     # TP decode-step input buffers: up to 128 token rows x 8192 features f32
     DEFAULT_IN_BYTES = 128 * 8192 * 4
@@ -140,20 +149,124 @@ class CustomAllReduce:
                out: torch.Tensor | None = None) -> torch.Tensor:
         """Global masked argmax over the vocab shards: ``logits`` [B, V/tp] f32
         (this rank's shard, global ids lo..lo+V/tp), ``idx`` [B] int32 this
-        rank's masked argmax (-1: nothing allowed). Returns int32 [B]."""
+        rank's masked argmax (-1: nothing allowed). Returns int32 [B]; every
+        row is ``ERR_TOKEN`` when a collective of the group timed out."""
         B = idx.numel()
         assert logits.dtype == torch.float32 and logits.stride(-1) == 1 and logits.shape[0] >= B
         assert idx.dtype == torch.int32 and idx.is_contiguous()
+        if not self.argmax_fits(lo, logits.shape[1]):
+            raise ValueError(f"vocab shard {lo}+{logits.shape[1]} exceeds the argmax records' "
+                             f"{MAX_TOKEN_ID + 1} token ids")
         if out is None:
             out = torch.empty(B, dtype=torch.int32, device=idx.device)
         _lib.check(_lib.kernels().loqa_car_argmax(self._h, logits.data_ptr(), logits.stride(0),
-                                                  idx.data_ptr(), B, lo, out.data_ptr(),
-                                                  _lib.stream_ptr(idx)), "car_argmax")
+                                                  idx.data_ptr(), B, lo, logits.shape[1],
+                                                  out.data_ptr(), _lib.stream_ptr(idx)), "car_argmax")
         self.calls += 1
         return out
 
+    @staticmethod
+    def argmax_fits(lo: int, shard: int) -> bool:
+        return lo >= 0 and shard >= 1 and lo + shard - 1 <= MAX_TOKEN_ID
+
     def error(self) -> bool:
         return bool(_lib.kernels().loqa_car_error(self._h))
+
+    def clear_error(self) -> None:
+        _lib.check(_lib.kernels().loqa_car_clear_error(self._h), "car_clear_error")
+
+    # ------------------------------------------------------ start-up check
+    def self_test(self, d: int | None = None) -> dict:
+        """Run every collective of this group once on seeded random data and
+        check it against the host (gloo) reduction of the same data; raise on
+        any mismatch, on every rank together (a TP group that
+        cannot reduce correctly - a broken IPC mapping, a link, a protocol
+        bug - must never start serving).
+
+        * ``__call__``: f32 one-shot and two-shot sizes, bitwise against the
+          rank-ordered f32 sum;
+        * ``resid``: residual + rank-ordered f32 partial sums, one bf16
+          rounding - bitwise; the row statistics within f32 rounding;
+        * ``argmax``: the global (max logit, lowest id) over the shards - exact.
+        """
+        W, r = self.world, self.rank
+        dev = self.device
+        d = d or 512 * W
+        fails: list[str] = []
+
+        def gen(tag: int) -> torch.Generator:
+            return torch.Generator().manual_seed(9000 + 131 * tag + r)
+
+        def gather(t: torch.Tensor) -> list[torch.Tensor]:
+            parts = [torch.empty_like(t) for _ in range(W)]
+            dist.all_gather(parts, t, group=self.group)
+            return parts
+
+        calls0 = self.calls
+        # 1. in-place all-reduce, one-shot and two-shot
+        for n in (4096, 1 << 18):
+            x = torch.randn(n, generator=gen(n))
+            ref = torch.zeros(n)
+            for p in gather(x):
+                ref += p
+            y = x.to(dev)
+            self(y)
+            torch.cuda.synchronize(dev)
+            if not torch.equal(y.cpu(), ref):
+                fails.append(f"all-reduce n={n}: max err {(y.cpu() - ref).abs().max().item():.3g}")
+        # 2. the residual epilogue (reduce-scatter + all-gather + statistics)
+        Mpad = 16
+        nblk = self.resid_blocks(d)
+        res0 = torch.randn(Mpad, d, generator=torch.Generator().manual_seed(77)).to(torch.bfloat16)
+        part = torch.randn(Mpad, d, generator=gen(1)) * 0.5
+        ref = res0.float()
+        for p in gather(part):
+            ref = ref + p
+        ref = ref.to(torch.bfloat16)
+        for which in (0, 1):
+            pd = part.to(dev)
+            _lib.check(_lib.kernels().loqa_car_fill_inbuf(self._h, which, pd.data_ptr(),
+                                                          pd.numel() * 4, _lib.stream_ptr(pd)),
+                       "car_fill_inbuf")
+            resid = res0.to(dev)
+            rowsq = torch.zeros(W * nblk * Mpad, dtype=torch.float32, device=dev)
+            self.resid(which, resid, rowsq, nblk)
+            torch.cuda.synchronize(dev)
+            if not torch.equal(resid.cpu(), ref):
+                bad = (resid.cpu().float() != ref.float()).sum().item()
+                fails.append(f"resid[{which}]: {bad} of {ref.numel()} elements differ")
+            sq = rowsq.view(W * nblk, Mpad).sum(0).cpu()
+            want = ref.float().square().sum(1)
+            if not torch.allclose(sq, want, rtol=1e-5, atol=1e-3):
+                fails.append(f"resid[{which}] row statistics: max err {(sq - want).abs().max().item():.3g}")
+        # 3. vocab-parallel argmax (self-tagged records)
+        B, shard = 8, 1024
+        lg = torch.randn(B, shard, generator=gen(2))
+        idx = lg.argmax(1).to(torch.int32)
+        idx[B - 1] = -1                        # a row with nothing allowed on this shard
+        if r == 0:
+            idx[B - 2] = -1
+        got = self.argmax(lg.to(dev), idx.to(dev), r * shard)
+        torch.cuda.synchronize(dev)
+        best = [(-float("inf"), -1)] * B
+        for q, (l, i) in enumerate(zip(gather(lg), gather(idx))):
+            for b in range(B):
+                if i[b] >= 0:
+                    v, tok = float(l[b, i[b]]), int(i[b]) + q * shard
+                    if v > best[b][0] or (v == best[b][0] and tok < best[b][1]):
+                        best[b] = (v, tok)
+        want = [t for _, t in best]
+        if got.cpu().tolist() != want:
+            fails.append(f"argmax: {got.cpu().tolist()} != {want}")
+        if self.error():
+            fails.append("a collective timed out")
+        self.calls = calls0
+        verdicts = [None] * W
+        dist.all_gather_object(verdicts, fails, group=self.group)
+        bad = {q: v for q, v in enumerate(verdicts) if v}
+        if bad:
+            raise CollectiveError(f"custom all-reduce self-test failed: {bad}")
+        return {"ranks": W, "checks": 6}
 
     def close(self) -> None:
         if self._h:

@@ -54,6 +54,41 @@ class TPControl:
                                f"{[i for i, v in enumerate(ok) if not v]}")
         self._cap = 16 << 20
         self._buf = ctypes.create_string_buffer(self._cap)
+        self._beating = False
+
+    # ------------------------------------------------------------ liveness
+    def start_heartbeat(self, period_s: float = 0.25) -> None:
+        """Stamp this rank's heartbeat word every ``period_s`` from a daemon
+        thread (a follower that dies stops beating; one whose GPU hangs keeps
+        beating but trips the collectives' bounded waits instead)."""
+        import threading
+        if self._beating:
+            return
+        self._beating = True
+        lib = _lib.runtime()
+
+        def run():
+            import time
+            while self._beating and getattr(self, "_h", None):
+                lib.loqa_tpctl_beat(self._h)
+                time.sleep(period_s)
+        lib.loqa_tpctl_beat(self._h)
+        self._beat_thread = threading.Thread(target=run, name=f"tpctl-beat-{self.rank}", daemon=True)
+        self._beat_thread.start()
+
+    def beat_ages(self) -> list[float]:
+        """Seconds since each rank's last heartbeat (-1: never beat)."""
+        lib = _lib.runtime()
+        out = []
+        for r in range(self.world):
+            a = lib.loqa_tpctl_beat_age(self._h, r)
+            out.append(-1.0 if a < 0 else a / 1e6)
+        return out
+
+    def lost_followers(self, max_age_s: float) -> list[int]:
+        """Followers that beat once and then stopped for ``max_age_s``."""
+        ages = self.beat_ages()
+        return [r for r in range(1, self.world) if ages[r] > max_age_s]
 
     @property
     def leader(self) -> bool:
@@ -83,6 +118,10 @@ class TPControl:
             return pickle.loads(ctypes.string_at(self._buf, n)), bool(stop.value)
 
     def close(self) -> None:
+        self._beating = False
+        t = getattr(self, "_beat_thread", None)
+        if t is not None:
+            t.join(timeout=2.0)
         if getattr(self, "_h", None):
             _lib.runtime().loqa_tpctl_close(self._h)
             self._h = None

@@ -28,6 +28,8 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -72,6 +74,7 @@ def build_tp_llm(lcfg, info: DistInfo, *, seed: int = 0, max_seqs: int = 64,
                     block_size=block_size, tp=tp, use_graphs=use_graphs, weights=weights,
                     compact=compact)
     eng.tp_ctl = TPControl(info.rank, info.world, control_tag(), dist.group.WORLD)
+    eng.tp_ctl.start_heartbeat()
     return eng
 
 
@@ -87,3 +90,71 @@ def run_follower(eng) -> dict:
         raise RuntimeError(f"TP rank {eng.tp.rank}: a collective timed out")
     eng.tp_ctl.close()
     return stats
+
+
+class TPFailover:
+    """Degradation of a failed tensor-parallel group ("TP=8 ...
+    fall back to the 8B DP path and flag it in metrics"; the reference's own
+    discipline is to fall back to a working path and tell the user -
+    ``audio_service.go:641-664`` bridge -> parser, ``:261-287`` service retry).
+
+    The leader engine calls ``on_failure`` from its scheduler thread when a
+    collective times out, a follower stops heart-beating, or an iteration
+    fails (``LLMEngine._tp_fail``): its in-flight and queued requests have
+    already failed (the hub answers them with the STT-failed reply), the
+    followers got the stop record. This builds the fallback engine
+    (``HUB_TP_FALLBACK_MODEL``, default Llama-3-8B, on the leader's GPU: it
+    fits beside the 70B shard in 288 GB) on a thread of its own and swaps it
+    into the voice pipeline; until then every utterance fails fast. The
+    fallback decodes eagerly (no graph capture while the STT engine serves).
+    ``stats``: ``tp_degraded`` (1 once failed), ``tp_fallback_ready``."""
+
+    def __init__(self, processor, lcfg, device, *, seed: int = 0, max_seqs: int = 64,
+                 max_seq_len: int = 1024, block_size: int = 16, build=None):
+        self.processor, self.lcfg, self.device = processor, lcfg, device
+        self.kw = dict(seed=seed, max_seqs=max_seqs, max_seq_len=max_seq_len,
+                       block_size=block_size, use_graphs=False)
+        self._build = build
+        self.error = ""
+        self.t_failed = 0.0
+        self.ready = threading.Event()
+        self._lock = threading.Lock()
+
+    def attach(self, leader) -> "TPFailover":
+        leader.on_tp_failure = self.on_failure
+        return self
+
+    def on_failure(self, err: Exception) -> None:
+        with self._lock:
+            if self.t_failed:
+                return
+            self.t_failed = time.monotonic()
+            self.error = str(err)
+        st = self.processor.stats
+        st["tp_degraded"] = 1
+        st["tp_fallback_ready"] = 0
+        log.error("tensor-parallel group failed (%s): serving falls back to %s on %s",
+                  err, self.lcfg.name, self.device)
+        threading.Thread(target=self._swap, name="tp-failover", daemon=True).start()
+
+    def _swap(self) -> None:
+        try:
+            if self._build is not None:
+                eng = self._build()
+            else:
+                from ..engine.llm_engine import LLMEngine
+                eng = LLMEngine(self.lcfg, self.device, **self.kw)
+            old = self.processor.pipeline.llm
+            self.processor.pipeline.llm = eng
+            self.processor.stats["tp_fallback_ready"] = 1
+            self.processor.stats["tp_failover_s"] = round(time.monotonic() - self.t_failed, 3)
+            self.ready.set()
+            log.warning("fallback LLM engine %s serving (%.1f s after the TP failure)",
+                        self.lcfg.name, time.monotonic() - self.t_failed)
+            try:
+                if old.tp_ctl is not None:
+                    old.tp_ctl.close()
+            except Exception:  # noqa: BLE001
+                pass
+        except Exception:  # noqa: BLE001
+            log.exception("building the fallback LLM engine failed: the hub cannot parse commands")

@@ -112,13 +112,20 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
     pipe = VoicePipeline(stt, llm, nats)
     pipe.warmup()
     sc = cfg.streaming
-    return GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64),
+    proc = GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64),
                              bridge=build_bridge(skills, tts) if bridge else None,
                              bridge_timeout=cfg.arbitration.bridge_timeout,
                              progressive=sc.enabled, tts_options=tts_options_from(cfg),
                              tts_format=cfg.tts.response_format,
                              max_buffer_time=sc.max_buffer_time,
                              max_tokens_per_phrase=sc.max_tokens_per_phrase)
+    if llm.tp.world > 1 and g.tp_fallback_model != "none":
+        # a failed TP group degrades to a single-GPU engine
+        from .parallel.tp_serving import TPFailover
+        proc.tp_failover = TPFailover(proc, llama_config(g.tp_fallback_model), device, seed=g.seed,
+                                      max_seqs=g.max_batch, max_seq_len=g.max_seq_len,
+                                      block_size=g.kv_block).attach(llm)
+    return proc
 
 
 async def build_dp_processor(cfg: Config, n_gpus: int, nats_url: str = "", *,

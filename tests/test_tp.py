@@ -162,3 +162,98 @@ def test_tp_lockstep_scheduler_matches_single(tmp_path):
     fol = json.load(open(tmp_path / "follower1.json"))
     assert lead["decode_steps"] == fol["decode_steps"] > 0 and fol["records"] > 0
     assert lead["outs"] == ref
+
+
+def _failover_worker(rank, world, port, out_dir):
+    """Rank 1 dies mid-decode (os._exit after a few replayed iterations); the
+    leader's collectives fail, its requests fail, the group stops and the
+    TPFailover swaps a single-rank engine into the 'processor'."""
+    import datetime
+    import threading
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=30))
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import TPGroup
+    from loqa_hub_amd.parallel.tp_control import TPControl
+    from loqa_hub_amd.parallel.tp_serving import TPFailover
+    cfg = llama_config("test-tiny")
+    tp = TPGroup(rank, world, dist.group.WORLD)
+    eng = LLMEngine(cfg, "cpu", max_seqs=4, max_seq_len=256, tp=tp, seed=5)
+    eng.tp_ctl = TPControl(rank, world, f"fo{port}", dist.group.WORLD)
+    eng.tp_ctl.start_heartbeat(0.05)
+    if rank != 0:
+        def killer():
+            while eng.stats.get("tp_records", 0) < 6:
+                time.sleep(0.001)
+            os._exit(9)              # the follower process dies mid-decode
+        threading.Thread(target=killer, daemon=True).start()
+        eng.follow()
+        os._exit(0)
+
+    class Pipe:
+        llm = eng
+
+    class Proc:
+        pipeline = Pipe()
+        stats = {}
+    proc = Proc()
+    fo = TPFailover(proc, cfg, "cpu", seed=5, max_seqs=4, max_seq_len=256).attach(eng)
+    res = {}
+    t0 = time.monotonic()
+    try:
+        futs = [eng.submit_batch(_prompt_reqs(eng)[i:i + 1]) for i in range(2)]
+        res["wave1"] = [r.output for f in futs for r in f.result(timeout=120)]
+        res["wave1_ok"] = True
+    except Exception as e:  # noqa: BLE001
+        res["wave1_error"] = f"{type(e).__name__}: {e}"
+    res["detect_s"] = time.monotonic() - t0
+    # a submission after the failure fails fast on the dead group
+    try:
+        eng.submit_batch(_prompt_reqs(eng)[:1]).result(timeout=5)
+        res["late_ok"] = True
+    except Exception as e:  # noqa: BLE001
+        res["late_error"] = type(e).__name__
+    res["ready"] = fo.ready.wait(120)
+    new = proc.pipeline.llm
+    res["swapped"] = new is not eng and new.tp.world == 1
+    res["outs"] = [r.output for r in new.submit_batch(_prompt_reqs(new)).result(timeout=120)] \
+        if res["swapped"] else []
+    res["stats"] = dict(proc.stats)
+    new.stop()
+    with open(os.path.join(out_dir, "failover.json"), "w") as f:
+        json.dump(res, f)
+    sys.stdout.flush()
+    os._exit(0)
+
+
+def test_tp_follower_death_fails_over(tmp_path):
+    """a follower that dies mid-decode stops the
+    TP group - the leader's in-flight requests fail loudly instead of hanging
+    or decoding garbage - and serving continues on the single-rank fallback
+    engine, flagged ``tp_degraded``."""
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    single = LLMEngine(llama_config("test-tiny"), "cpu", max_seqs=4, max_seq_len=256, seed=5)
+    ref = [r.output for r in single.generate(_prompt_reqs(single))]
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_failover_worker, args=(r, 2, port, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert procs[1].exitcode == 9
+    res = json.load(open(tmp_path / "failover.json"))
+    assert "wave1_error" in res, res          # the in-flight requests failed
+    assert res["late_error"] == "CollectiveError"
+    assert res["ready"] and res["swapped"]
+    assert res["stats"]["tp_degraded"] == 1 and res["stats"]["tp_fallback_ready"] == 1
+    assert res["outs"] == ref                 # the fallback serves correct parses
+    print(res["wave1_error"], round(res["detect_s"], 2), res["stats"])

@@ -20,6 +20,7 @@ degree the same model):
   collective error, and the constrained outputs are valid with the same
   command counts as TP=1."""
 import json
+import sys
 import os
 import socket
 
@@ -179,3 +180,97 @@ def test_tp_decode_matches_tp1(tmp_path):
         same = sum(a == b for a, b in zip(lead["outs"], ref["outs"]))
         print(f"TP={world}: logits max err {err:.3g} (scale {scale:.3g}), greedy agreement "
               f"{agree.float().mean().item():.3f}, identical outputs {same}/{len(ref['outs'])}")
+
+
+def _failover_worker(rank, world, port, out_dir):
+    """TP=2 on the shared GPU; rank 1 freezes mid-decode (SIGSTOP: a hung
+    follower - its IPC memory stays mapped, so nothing reads freed memory).
+    The leader's collectives time out, the error word rides on the step's
+    sampled tokens (ERR_TOKEN), the group stops, and TPFailover swaps in a
+    single-GPU engine."""
+    import signal
+    import threading
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import TPGroup
+    from loqa_hub_amd.parallel.tp_control import TPControl
+    from loqa_hub_amd.parallel.tp_serving import TPFailover
+    cfg = llama_config("llama3-8b", n_layers=2)
+    tp = TPGroup.create(rank, world, dist.group.WORLD, device=dev)   # runs the self-test
+    eng = LLMEngine(cfg, dev, max_seqs=8, max_seq_len=512, tp=tp, seed=11)
+    eng.tp_ctl = TPControl(rank, world, f"gpufo{port}", dist.group.WORLD)
+    eng.tp_ctl.start_heartbeat(0.1)
+    eng.warmup_graphs()
+    if rank != 0:
+        def freezer():
+            while eng.stats.get("tp_records", 0) < 8:
+                time.sleep(0.001)
+            with open(os.path.join(out_dir, "frozen"), "w") as f:
+                f.write(str(os.getpid()))
+            os.kill(os.getpid(), signal.SIGSTOP)
+        threading.Thread(target=freezer, daemon=True).start()
+        eng.follow()
+        os._exit(0)
+
+    class Pipe:
+        llm = eng
+
+    class Proc:
+        pipeline = Pipe()
+        stats = {}
+    proc = Proc()
+    fo = TPFailover(proc, cfg, dev, seed=11, max_seqs=8, max_seq_len=512).attach(eng)
+    res = {}
+    t0 = time.monotonic()
+    try:
+        futs = [eng.submit_batch([r]) for r in _reqs(eng, 0)]
+        res["outs"] = [r.output for f in futs for r in f.result(timeout=180)]
+    except Exception as e:  # noqa: BLE001
+        res["error"] = f"{type(e).__name__}: {e}"
+    res["detect_s"] = time.monotonic() - t0
+    res["car_error"] = tp.car.error()
+    res["ready"] = fo.ready.wait(180)
+    new = proc.pipeline.llm
+    res["swapped"] = new is not eng and new.tp.world == 1
+    if res["swapped"]:
+        futs = [new.submit_batch([r]) for r in _reqs(new, 1)]
+        res["fallback_outs"] = [r.output for f in futs for r in f.result(timeout=180)]
+        new.stop()
+    res["stats"] = dict(proc.stats)
+    with open(os.path.join(out_dir, "failover.json"), "w") as f:
+        json.dump(res, f)
+    sys.stdout.flush()
+    os._exit(0)
+
+
+def test_tp_follower_hang_fails_over(tmp_path):
+    """A TP follower that stops mid-decode: the leader fails its in-flight
+    requests (no garbage tokens, no endless spin), stops the group and serves
+    on the fallback engine with ``tp_degraded`` set."""
+    import signal
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_failover_worker, args=(r, 2, port, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    procs[0].join(timeout=420)
+    for p in procs:                     # the frozen follower, and anything left
+        if p.is_alive():
+            os.kill(p.pid, signal.SIGKILL)
+            p.join(timeout=10)
+    res = json.load(open(tmp_path / "failover.json"))
+    print(res.get("error"), res["detect_s"], res["stats"])
+    assert os.path.exists(tmp_path / "frozen")
+    assert "error" in res and "CollectiveError" in res["error"], res
+    assert res["car_error"]
+    assert res["ready"] and res["swapped"]
+    assert res["stats"]["tp_degraded"] == 1 and res["stats"]["tp_fallback_ready"] == 1
+    assert len(res["fallback_outs"]) == 3
+    for out, n in zip(res["fallback_outs"], (1, 3, 2)):
+        assert len(json.loads(out)["commands"]) == n
