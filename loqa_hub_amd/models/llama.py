@@ -308,6 +308,12 @@ PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
 # RMSNorm), gate|up with the SwiGLU epilogue in the GEMM. Split counts per
 # projection (qkv, o, down) for ~300-row prompts.
 PREFILL2 = os.environ.get("LOQA_PREFILL2", "0") != "0"
+# prompt passes on the split-K tiled GEMM (no hipBLASLt, no f32 slabs)
+PREFILL3 = os.environ.get("LOQA_PREFILL3", "0") != "0"
+
+
+def L0_KEYS(w) -> set:
+    return set(w.layers[0]) if w.layers else set()
 # prefill gate|up on the v2 prefill GEMM with the SwiGLU epilogue (norm-folded
 # decode copy, unweighted norm in front) instead of hipBLASLt + silu_mul
 PREFILL_GU2 = os.environ.get("LOQA_PREFILL_GU2", "0") != "0"
@@ -361,6 +367,9 @@ class LlamaModel:
         S_o = PREFILL_O_SPLITS if (S_down and PREFILL_O_SPLITS > 0 and hasattr(w, "decode_layers")
                                    and (H * D) % (PREFILL_O_SPLITS * 128) == 0
                                    and cfg.d_model % ops.PREFILL_GEMM_NT == 0) else 0
+        if (PREFILL3 and x.is_cuda and tp.world == 1 and not meta.decode
+                and not getattr(w, "compact", False) and "wqkv" in L0_KEYS(w)):
+            return self._forward_prefill3(meta, k_cache, v_cache, attn_ws, x, h)
         if (PREFILL2 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 64
                 and not getattr(w, "compact", False) and "wqkv" in w.decode_layers[0]):
             return self._forward_prefill2(meta, k_cache, v_cache, attn_ws, x, h)
@@ -408,6 +417,33 @@ class LlamaModel:
         sel_mlp = mlp_out.index_select(0, meta.logit_idx)
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
                            residual=sel_res.contiguous())
+
+    def _forward_prefill3(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:
+        """Prompt pass on the split-K tiled GEMM (``ops.gemm_sk``: the K chunks
+        of a tile are summed in-launch, so no f32 slabs are written or
+        re-read): per layer qkv (bf16) -> RoPE + KV append -> flash attention
+        -> o added straight into the residual stream (one rounding) -> RMSNorm
+        -> gate|up with the SwiGLU epilogue -> down added into the residual ->
+        the next layer's RMSNorm. Every projection streams its row-major
+        weights once; no hipBLASLt call."""
+        cfg, w = self.cfg, self.w
+        H, Hkv, D = w.h, w.hkv, cfg.head_dim
+        residual = x.contiguous()
+        for li, L in enumerate(w.layers):
+            if li > 0:
+                h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
+            qkv = ops.gemm_sk(h, L["wqkv"])
+            ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
+                               H, Hkv, D)
+            attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
+                                 block_tables=meta.block_tables, grouped=False, split_keys=256,
+                                 num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
+            ops.gemm_sk(attn, L["wo"], epi="resid", residual=residual)
+            hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
+            a = ops.gemm_sk(hn, L["w_gate_up"], epi="swiglu")
+            ops.gemm_sk(a, L["w_down"], epi="resid", residual=residual)
+        return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 
     def _forward_prefill2(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:
         """Prefill through the v2 prefill GEMM: per layer qkv slabs -> RoPE + KV

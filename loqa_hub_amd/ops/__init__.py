@@ -1565,3 +1565,133 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, *, bias: torch.Tensor | None = N
     p.layout = lay
     check(kernels().loqa_gemm_tile(ctypes.byref(p), stream_ptr(x)), "gemm_tile")
     return y
+
+
+# ---------------------------------------------------------------------------
+# Split-K tiled GEMM with an in-launch reduction (csrc/kernels/gemm_sk.hip)
+_SK_EPI = {"bf16": 0, "swiglu": 1, "resid": 2}
+# layout -> (features, rows, resident workgroups per CU (LDS), per-CU efficiency)
+# efficiency: relative MFMA rate of the wave tile (LDS bytes per MFMA: 64 x 64
+# = 1.0; 64 x 32 tiles read 1.5x the LDS per MFMA; 128 x 64 0.75x)
+SK_LAYOUTS = {0: (128, 128, 2, 1.0), 1: (128, 64, 3, 0.85), 2: (256, 64, 2, 1.0),
+              3: (256, 128, 1, 1.0), 4: (128, 64, 2, 0.9), 5: (128, 128, 1, 1.05),
+              6: (256, 256, 1, 1.15), 7: (64, 64, 4, 0.6), 8: (256, 64, 1, 1.05)}
+SK_CUS = 256
+_SK_WS: dict = {}
+
+
+def gemm_sk_plan(M: int, N: int, K: int, epi: str = "bf16",
+                 layouts=(0, 1, 2, 3, 6)) -> tuple[int, int]:
+    """(layout, K chunks) for a shape: ``LOQA_SK=layout,S`` if set, else the
+    analytic plan - the fewest MFMA-cycle rounds over the resident workgroup
+    slots, counting padded rows, wave-tile efficiency and a per-chunk cost of
+    the split-K reduction."""
+    env = os.environ.get("LOQA_SK")
+    if env:
+        lay, s = (int(v) for v in env.split(","))
+        return lay, s
+    KT = K // 64
+    best, best_t = (1, 1), float("inf")
+    for lay in layouts:
+        bn, bm, occ, eff = SK_LAYOUTS[lay]
+        if N % bn or (epi == "swiglu" and (bn // 2) % 32):
+            continue
+        tiles = -(-M // bm) * (N // bn)
+        for s in (1, 2, 3, 4, 6, 8, 12, 16):
+            if s > KT or (s > 1 and KT // s < 4):
+                continue
+            if epi == "swiglu" and s > 2:
+                continue          # the partials of a wide SwiGLU tile cost more than they balance
+            grid = tiles * s
+            slots = SK_CUS * occ
+            rounds = -(-grid // slots)
+            # per-workgroup time ~ tile MFMA work of its chunk; a round runs
+            # `occ` workgroups per CU sharing its MFMA pipes
+            t_wg = bm * bn * (KT / s) / eff
+            t = rounds * t_wg * occ + (s > 1) * bm * bn * 24.0 + 2000.0 * bm * bn / 16384
+            if t < best_t:
+                best, best_t = (lay, s), t
+    return best
+
+
+def _sk_workspace(dev: torch.device, stream: int, floats: int, tiles: int):
+    key = (dev, stream)
+    ws = _SK_WS.get(key)
+    if ws is None or ws[0].numel() < floats or ws[1].numel() < tiles:
+        f = max(floats, 0 if ws is None else ws[0].numel())
+        t = max(tiles, 0 if ws is None else ws[1].numel())
+        ws = (torch.empty(f, dtype=torch.float32, device=dev),
+              torch.zeros(t, dtype=torch.int32, device=dev))
+        _SK_WS[key] = ws
+    return ws
+
+
+def _sk_ref(x: torch.Tensor, w: torch.Tensor, epi: str, bias, residual):
+    y = x.float() @ w.float().t()
+    if epi == "swiglu":
+        F = w.shape[0] // 2
+        g = y[:, :F].to(torch.bfloat16).float()
+        u = y[:, F:].to(torch.bfloat16).float()
+        return (g * torch.sigmoid(g) * u).to(torch.bfloat16)
+    if epi == "resid":
+        return (residual.float() + y).to(torch.bfloat16)
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(torch.bfloat16)
+
+
+def gemm_sk(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
+            residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+            layout: int | None = None, splits: int | None = None) -> torch.Tensor:
+    """Y = X W^T on the split-K tiled GEMM (``csrc/kernels/gemm_sk.hip``); the
+    S K-chunks of a tile are summed in-launch by the tile's last workgroup.
+
+    x [M, K] bf16 (row stride may exceed K), w [N, K] bf16 row-major.
+    ``epi``: "bf16" -> [M, N] (+ f32 ``bias``); "swiglu" -> silu(gate) * up
+    [M, N / 2] (gate rows [0, N/2), up rows [N/2, N)); "resid" -> ``residual``
+    [M, N] += X W^T in place (one bf16 rounding), returned."""
+    N, K = w.shape
+    M = x.shape[0]
+    assert x.shape[1] == K, (x.shape, w.shape)
+    if epi == "resid":
+        assert residual is not None and residual.shape == (M, N)
+    if not _gpu(x):
+        y = _sk_ref(x, w, epi, bias, residual)
+        dst = residual if epi == "resid" else out
+        if dst is not None:
+            dst.copy_(y)
+            return dst
+        return y
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("gemm_sk needs bf16 operands")
+    if x.stride(1) != 1 or not w.is_contiguous():
+        raise ValueError("gemm_sk needs K-contiguous operands")
+    if layout is None or splits is None:
+        pl, ps = gemm_sk_plan(M, N, K, epi)
+        layout = pl if layout is None else layout
+        splits = ps if splits is None else splits
+    bn, bm = SK_LAYOUTS[layout][:2]
+    if N % bn or K % 64:
+        raise ValueError(f"gemm_sk layout {layout}: N {N} / K {K} not tileable")
+    p = _lib.GemmSkParams()
+    p.x, p.ldx, p.w = ptr(x), x.stride(0), ptr(w)
+    p.M, p.N, p.K, p.S, p.epi = M, N, K, splits, _SK_EPI[epi]
+    if bias is not None:
+        assert epi == "bf16" and bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N
+    p.bias = ptr(bias)
+    if epi == "resid":
+        y = residual
+        assert y.dtype == torch.bfloat16 and y.stride(1) == 1
+    else:
+        cols = N // 2 if epi == "swiglu" else N
+        y = out if out is not None else torch.empty(M, cols, dtype=torch.bfloat16, device=x.device)
+        assert y.shape == (M, cols) and y.stride(1) == 1
+    p.y, p.ldy = ptr(y), y.stride(0)
+    st = stream_ptr(x)
+    if splits > 1:
+        tiles = -(-M // bm) * (N // bn)
+        ws, cnt = _sk_workspace(x.device, st, tiles * splits * bm * bn, tiles)
+        p.ws, p.counters = ptr(ws), ptr(cnt)
+    p.layout = layout
+    check(kernels().loqa_gemm_sk(ctypes.byref(p), st), "gemm_sk")
+    return y

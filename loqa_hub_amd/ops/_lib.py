@@ -56,6 +56,17 @@ class GemmTileParams(ctypes.Structure):
     ]
 
 
+class GemmSkParams(ctypes.Structure):
+    """Mirror of ``GemmSkParams`` in csrc/kernels/gemm_sk.hip."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_ll), ("w", c_void_p),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("S", c_int),
+        ("epi", c_int), ("bias", c_void_p),
+        ("y", c_void_p), ("ldy", c_ll),
+        ("ws", c_void_p), ("counters", c_void_p), ("layout", c_int),
+    ]
+
+
 class WhisperMegaParams(ctypes.Structure):
     """Mirror of ``MegaParams`` in csrc/kernels/whisper_mega.hip."""
     _fields_ = [
@@ -97,6 +108,8 @@ _KERNEL_SIGS = {
     "loqa_shuffle_weight": [c_void_p, c_void_p, c_int, c_int, c_void_p],
     "loqa_skinny_fused": [c_void_p, c_void_p],
     "loqa_gemm_tile": [c_void_p, c_void_p],
+    "loqa_gemm_sk": [c_void_p, c_void_p],
+    "loqa_gemm_sk_dims": [c_int, c_void_p, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,

@@ -307,6 +307,35 @@ def test_llm_prefill2_matches_hipblaslt_gpu(monkeypatch):
         assert float((a - b).norm() / b.norm()) < 4e-2
 
 
+@pytest.mark.parametrize("model", ["tinyllama", "llama3-8b"])
+def test_llm_prefill3_matches_hipblaslt_gpu(monkeypatch, model):
+    """Prefill on the split-K tiled GEMM (qkv, o + residual, gate|up + SwiGLU,
+    down + residual; in-launch K reduction) vs plain hipBLASLt GEMMs +
+    rmsnorm: final hidden rows of a 300-token prompt and the KV rows agree."""
+    from loqa_hub_amd.models import llama as llama_mod
+    cfg = llama_config(model, n_layers=4) if model == "llama3-8b" else llama_config(model)
+    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(4)
+    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
+    r = GenRequest(toks, multi_command_schema(1))
+    eng.submit(r)
+    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
+    dev = eng._to_device(host)
+    meta = eng._build_meta(dev, max_q, max_ctx, False)
+    outs, kvs = {}, {}
+    monkeypatch.setattr(llama_mod, "PREFILL2", False)
+    for on in (True, False):
+        monkeypatch.setattr(llama_mod, "PREFILL3", on)
+        monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", 0)
+        monkeypatch.setattr(llama_mod, "PREFILL_O_SPLITS", 0)
+        outs[on] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
+        kvs[on] = (eng.kv.k[-1].float().clone(), eng.kv.v[-1].float().clone())
+    rel = float((outs[True] - outs[False]).norm() / outs[False].norm())
+    assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
+    for a, b in zip(kvs[True], kvs[False]):
+        assert float((a - b).norm() / b.norm()) < 4e-2
+
+
 def test_llm_prefill_gu2_matches_hipblaslt_gpu(monkeypatch):
     """Prefill gate|up on the v2 GEMM's SwiGLU epilogue (norm-folded decode
     copy behind an unweighted norm; LOQA_PREFILL_GU2) vs hipBLASLt + silu_mul:

@@ -1,0 +1,73 @@
+"""Split-K tiled MFMA GEMM with the in-launch reduction (csrc/kernels/gemm_sk.hip)
+against the fp32 torch reference of the same op: every layout, K-chunk count
+and epilogue (bf16 + bias, SwiGLU, residual add), ragged M, and the bitwise
+determinism of the last-arriver reduction."""
+import pytest
+import torch
+
+from loqa_hub_amd import ops
+
+
+def _rel(a, b):
+    return (a.float().cpu() - b.float().cpu()).abs().max().item() / max(b.float().abs().max().item(), 1e-6)
+
+
+def test_gemm_sk_cpu_reference_and_plan():
+    torch.manual_seed(0)
+    x = torch.randn(33, 128).bfloat16()
+    w = torch.randn(256, 128).bfloat16()
+    y = ops.gemm_sk(x, w)
+    assert _rel(y, x.float() @ w.float().t()) < 1e-2
+    res = torch.randn(33, 256).bfloat16()
+    r0 = res.clone()
+    out = ops.gemm_sk(x, w, epi="resid", residual=res)
+    assert out is res and _rel(res, r0.float() + x.float() @ w.float().t()) < 1e-2
+    sw = ops.gemm_sk(x, w, epi="swiglu")
+    assert sw.shape == (33, 128)
+    # the planner always returns a tileable layout
+    for M, N, K in ((295, 6144, 4096), (295, 4096, 14336), (420, 28672, 4096), (1500, 3840, 1280),
+                    (3000, 5120, 1280), (64, 4096, 4096)):
+        for epi in ("bf16", "swiglu", "resid"):
+            lay, s = ops.gemm_sk_plan(M, N, K, epi)
+            bn = ops.SK_LAYOUTS[lay][0]
+            assert N % bn == 0 and 1 <= s <= K // 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", sorted(ops.SK_LAYOUTS))
+def test_gemm_sk_gpu_matches_fp32(layout):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(layout)
+    bn, bm = ops.SK_LAYOUTS[layout][:2]
+    for M, K in ((bm * 2 + 37, 512), (17, 256), (300, 1024)):
+        N = bn * 3
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+        b = torch.randn(N, device=dev) * 0.1
+        for S in (1, 2, 3, 5):
+            if S > K // 64:
+                continue
+            y = ops.gemm_sk(x, w, bias=b, layout=layout, splits=S)
+            r = ops._sk_ref(x.cpu(), w.cpu(), "bf16", b.cpu(), None)
+            assert _rel(y, r) < 1e-2, (layout, M, K, S)
+            res = torch.randn(M, N, device=dev).bfloat16()
+            rr = ops._sk_ref(x.cpu(), w.cpu(), "resid", None, res.cpu())
+            ops.gemm_sk(x, w, epi="resid", residual=res, layout=layout, splits=S)
+            assert _rel(res, rr) < 1e-2, (layout, M, K, S, "resid")
+            sw = ops.gemm_sk(x, w, epi="swiglu", layout=layout, splits=S)
+            rs = ops._sk_ref(x.cpu(), w.cpu(), "swiglu", None, None)
+            assert _rel(sw, rs) < 2e-2, (layout, M, K, S, "swiglu")
+
+
+@pytest.mark.gpu
+def test_gemm_sk_split_reduction_is_deterministic():
+    """The last arriver sums the K chunks in fixed order: repeated launches give
+    bitwise-identical outputs although the arrival order varies."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    x = torch.randn(301, 4096, device=dev).bfloat16()
+    w = (torch.randn(4096, 4096, device=dev) * 0.02).bfloat16()
+    ref = ops.gemm_sk(x, w, layout=1, splits=6)
+    for _ in range(5):
+        assert torch.equal(ops.gemm_sk(x, w, layout=1, splits=6), ref)
+    assert _rel(ref, ops._sk_ref(x.cpu(), w.cpu(), "bf16", None, None)) < 1e-2
