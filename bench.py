@@ -259,6 +259,14 @@ def run_hub_dp(args) -> int:
             recs = await counter.records(srv, hub_recs)
             slope, hub_stats = hub_summary(srv, recs, args)
             hub_stats["dp"] = srv.processor.metrics()
+            ps = srv.processor.stats
+            if args.tts and ps.get("tts_phrases"):
+                sr = 22050.0
+                hub_stats["tts"] = {
+                    "phrases_per_s": round(ps["tts_phrases"] / max(elapsed, 1e-9), 2),
+                    "audio_s_per_wall_s": round(ps["tts_samples"] / sr / max(elapsed, 1e-9), 2),
+                    "gpu_s_per_audio_s": round(ps["tts_gpu_s"] / max(ps["tts_samples"] / sr, 1e-9), 4),
+                    "note": "counters since start (warm-up included)"}
             if srv.streaming is not None:
                 hub_stats["streaming"] = srv.streaming.metrics.get_aggregate_metrics().to_json()
         finally:
@@ -342,12 +350,14 @@ def main(argv=None) -> int:
     ap.add_argument("--tts", action="store_true",
                     help="--mode hub: every reply spoken by on-GPU VITS (progressive)")
     ap.add_argument("--tts-model", default="vits-ljs")
+    ap.add_argument("--served-dp", action="store_true",
+                    help="--mode hub: serve through the DP front end + worker processes at any N")
     args = ap.parse_args(argv)
 
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus is None:
         args.gpus = int(world_env or "1")
-    if args.mode == "hub" and world_env is None and (args.gpus > 1 or args.tts):
+    if args.mode == "hub" and world_env is None and (args.gpus > 1 or args.tts or args.served_dp):
         # the served multi-GPU hub: ONE front-end process (gRPC, arbitration,
         # events) over one worker process per GPU (parallel/dp_serving.py)
         return run_hub_dp(args)

@@ -534,13 +534,15 @@ extern "C" int loqa_car_argmax(void* hp, const float* logits, long long ld, cons
   return (int)hipGetLastError();
 }
 
-// nonzero when a barrier timed out (a peer never arrived)
+// 1 when a barrier timed out (a peer never arrived), 0 if not, a negative
+// hipError_t when the word cannot be read (the device is in a failed state)
 extern "C" int loqa_car_error(void* hp) {
   CarHandle* h = static_cast<CarHandle*>(hp);
   unsigned v = 0;
-  hipMemcpy(&v, &reinterpret_cast<CarSignals*>(h->local)->error, sizeof(unsigned),
-            hipMemcpyDeviceToHost);
-  return (int)v;
+  const hipError_t e = hipMemcpy(&v, &reinterpret_cast<CarSignals*>(h->local)->error,
+                                 sizeof(unsigned), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return -(int)e;
+  return v ? 1 : 0;
 }
 
 // copy `bytes` of device memory into input buffer `which` (start-up self-test)

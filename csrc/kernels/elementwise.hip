@@ -354,7 +354,10 @@ __global__ __launch_bounds__(256) void step_fetch_kernel(int* __restrict__ d32,
     int v = src[i];
     if (i < T) {   // tokens: a staged src slot >= 0 takes that sequence's last sampled token
       const int sl = src[src_off + i];
-      if (sl >= 0) v = last_tok[sl];
+      // a failed step's sentinel (-1 nothing allowed, -2 collective error)
+      // must never become an embedding row index: the host fails those
+      // sequences when it reads the step, this one only has to stay in bounds
+      if (sl >= 0) v = max(last_tok[sl], 0);
     }
     d32[i] = v;
   }

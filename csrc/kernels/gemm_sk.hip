@@ -19,11 +19,12 @@
 // order with a tile's K chunks adjacent on one XCD.
 //
 // Epilogues (applied once per output element, by the tile's reducer):
-//   SK_BF16   y = bf16(acc (+ bias))
+//   SK_BF16   y = bf16(acc (+ bias)), optionally GELU (Whisper encoder fc1)
 //   SK_SWIGLU y[:, f] = silu(gate_f) * up_f (a wave tile holds TN/2 gate and the
 //             matching TN/2 up features, row-permuted at staging)
-//   SK_RESID  y = bf16(y + acc): the row-parallel projections (o, down) add
-//             straight into the residual stream, one rounding.
+//   SK_RESID  y = bf16(y + (acc + bias)): the row-parallel projections (o,
+//             down, encoder o / fc2) add straight into the residual stream, one
+//             rounding.
 #include "common.h"
 
 #define SK_BK 64
@@ -34,8 +35,8 @@ struct GemmSkParams {
   const void* x; long long ldx;   // [M, K] bf16 rows
   const void* w;                  // [N, K] bf16 row-major (SwiGLU: gate rows [0, N/2), up [N/2, N))
   int M, N, K, S;                 // S: K chunks per output tile
-  int epi;
-  const float* bias;              // [N] f32 or null (SK_BF16 only)
+  int epi, act;                   // act (SK_BF16): 0 none, 1 GELU (erf) after the bias
+  const float* bias;              // [N] f32 or null (SK_BF16, SK_RESID)
   void* y; long long ldy;         // bf16 output (SK_RESID: the residual, updated in place)
   float* ws;                      // S > 1: [tiles][S][BM * BN] f32 partials
   int* counters;                  // S > 1: [tiles] ints, zero on entry (left zero)
@@ -230,6 +231,12 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_sk_kernel(GemmSkParams p) {
       }
     }
   } else if constexpr (EPI == SK_RESID) {
+    float4 bv[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int n = n0 + wn * TN + 16 * i + 4 * fq;
+      bv[i] = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int m = m0 + wm * TM + 16 * j + fr;
@@ -239,8 +246,10 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_sk_kernel(GemmSkParams p) {
         const int n = n0 + wn * TN + 16 * i + 4 * fq;
         uint2* yp = reinterpret_cast<uint2*>(Y + (size_t)m * p.ldy + n);
         const uint2 rv = *yp;
-        const float o0 = bf2f(rv.x & 0xffff) + acc[i][j][0], o1 = bf2f(rv.x >> 16) + acc[i][j][1];
-        const float o2 = bf2f(rv.y & 0xffff) + acc[i][j][2], o3 = bf2f(rv.y >> 16) + acc[i][j][3];
+        const float o0 = bf2f(rv.x & 0xffff) + (acc[i][j][0] + bv[i].x);
+        const float o1 = bf2f(rv.x >> 16) + (acc[i][j][1] + bv[i].y);
+        const float o2 = bf2f(rv.y & 0xffff) + (acc[i][j][2] + bv[i].z);
+        const float o3 = bf2f(rv.y >> 16) + (acc[i][j][3] + bv[i].w);
         *yp = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
       }
     }
@@ -258,9 +267,17 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_sk_kernel(GemmSkParams p) {
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
         const int n = n0 + wn * TN + 16 * i + 4 * fq;
+        float o[4] = {acc[i][j][0] + bv[i].x, acc[i][j][1] + bv[i].y, acc[i][j][2] + bv[i].z,
+                      acc[i][j][3] + bv[i].w};
+        if (p.act == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = bf2f(f2bf(o[r]));
+            o[r] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+          }
+        }
         *reinterpret_cast<uint2*>(Y + (size_t)m * p.ldy + n) =
-            make_uint2(pack_bf16x2(acc[i][j][0] + bv[i].x, acc[i][j][1] + bv[i].y),
-                       pack_bf16x2(acc[i][j][2] + bv[i].z, acc[i][j][3] + bv[i].w));
+            make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
       }
     }
   }
@@ -306,7 +323,7 @@ extern "C" int loqa_gemm_sk(const GemmSkParams* p, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if (p->S > 1 && (!p->ws || !p->counters)) return (int)hipErrorInvalidValue;
   if (p->ldx % 8 || p->ldy % 4) return (int)hipErrorInvalidValue;
-  if (p->epi != SK_BF16 && p->bias) return (int)hipErrorInvalidValue;
+  if ((p->epi == SK_SWIGLU && p->bias) || (p->epi != SK_BF16 && p->act)) return (int)hipErrorInvalidValue;
   switch (p->layout) {
     case 0: return sk_launch<2, 2, 4, 4, 2>(*p, st);
     case 1: return sk_launch<2, 2, 4, 2, 2>(*p, st);

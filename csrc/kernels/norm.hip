@@ -153,7 +153,7 @@ __global__ void embed_pos_kernel(const int* __restrict__ tokens, const int* __re
                                  const bf16_t* __restrict__ te, const bf16_t* __restrict__ pe,
                                  bf16_t* __restrict__ out, int d) {
   const int row = blockIdx.x;
-  const uint4* a = reinterpret_cast<const uint4*>(te + (size_t)tokens[row] * d);
+  const uint4* a = reinterpret_cast<const uint4*>(te + (size_t)max(tokens[row], 0) * d);
   const uint4* b = reinterpret_cast<const uint4*>(pe + (size_t)positions[row] * d);
   uint4* o = reinterpret_cast<uint4*>(out + (size_t)row * d);
   for (int c = threadIdx.x; c < (d >> 3); c += blockDim.x) {
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NORM_THREADS) void embed_stats_kernel(
   __shared__ float scratch[NORM_THREADS / 64];
   const int row = blockIdx.x;
   const int nvec = d >> 3;
-  const uint4* a = reinterpret_cast<const uint4*>(te + (size_t)tokens[row] * d);
+  const uint4* a = reinterpret_cast<const uint4*>(te + (size_t)max(tokens[row], 0) * d);
   const uint4* b = pe ? reinterpret_cast<const uint4*>(pe + (size_t)positions[row] * d) : nullptr;
   uint4* o = reinterpret_cast<uint4*>(out + (size_t)row * d);
   float ss = 0.f, s1 = 0.f;

@@ -380,7 +380,9 @@ class LLMEngine:
         if device_io:
             return self._forward_sample(meta, dev["mask_rows"])
         src = dev["src"]
-        tok = torch.where(src >= 0, self.last_tok[src.clamp(min=0).long()], dev["tokens"])
+        # (a failed step's negative sentinel never becomes an embedding index)
+        tok = torch.where(src >= 0, self.last_tok[src.clamp(min=0).long()].clamp(min=0),
+                          dev["tokens"])
         meta = StepMeta(tokens=tok, positions=meta.positions, slots=meta.slots, cu_q=meta.cu_q,
                         ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
                         logit_idx=meta.logit_idx, max_q=meta.max_q, max_ctx=meta.max_ctx,

@@ -23,8 +23,7 @@ import torch
 
 from .. import ops
 from ..models.configs import WhisperConfig
-from ..models.whisper import (WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused,
-                              decode_step_mega)
+from ..models.whisper import WhisperModel, WhisperWeights, decode_step_fast, decode_step_fused
 from ..utils.tracing import tracer
 from .batching import join_futures, plan_step
 from .kv_cache import PagedKVCache
@@ -117,8 +116,7 @@ class STTEngine:
         # (with the layer-concatenated weights: one [rows, L * 2d] buffer whose
         # column blocks are the layers' K|V, written by one tiled GEMM per batch)
         self.xkv_all = None
-        if (getattr(self.weights, "xkv_all", None) is not None
-                and os.environ.get("LOQA_STT_MEGA", "0") != "1"):
+        if getattr(self.weights, "xkv_all", None) is not None:
             self.xkv_all = torch.empty(max_batch * cfg.n_audio_ctx, cfg.dec_layers * 2 * cfg.d_model,
                                        dtype=torch.bfloat16, device=self.device)
             d2 = 2 * cfg.d_model
@@ -126,12 +124,6 @@ class STTEngine:
         else:
             self.xkv = [torch.empty(max_batch * cfg.n_audio_ctx, 2 * cfg.d_model, dtype=torch.bfloat16,
                                     device=self.device) for _ in range(cfg.dec_layers)]
-        # persistent one-launch decoder step for 16-row steps (ops.WhisperMega)
-        self.mega = None
-        if (self.fused and self.is_gpu and os.environ.get("LOQA_STT_MEGA", "0") == "1"
-                and cfg.head_dim == 64 and cfg.d_model % 128 == 0 and cfg.d_model <= 1280):
-            self.mega = ops.WhisperMega(self.model.w, self.kv.k, self.kv.v, self.xkv,
-                                        max_seqs=ops.WhisperMega.ROWS)
         self._graphs: dict[tuple[int, int], dict] = {}
         self._graphs_frozen = False     # see LLMEngine: no capture while serving
         self._enc_graphs: dict = {}
@@ -158,8 +150,7 @@ class STTEngine:
             self.last_tok = torch.zeros(max_batch + 1, dtype=torch.int32, device=self.device)
         # two decoder steps in flight (the host prepares step j+1 while step j
         # runs); LOQA_STT_PIPELINE=0: one synchronous step at a time
-        self.pipelined = self.use_graphs and os.environ.get("LOQA_STT_PIPELINE", "1") != "0" \
-            and self.mega is None
+        self.pipelined = self.use_graphs and os.environ.get("LOQA_STT_PIPELINE", "1") != "0"
 
     # ------------------------------------------------------------ front end
     def upload(self, reqs: list[STTRequest], device_pcm: torch.Tensor | None = None
@@ -315,12 +306,6 @@ class STTEngine:
 
     def _fast_forward(self, dev: dict, max_q: int, B_pad: int, ctx: int | None = None) -> torch.Tensor:
         ns = self._self_splits(ctx)
-        if (self.mega is not None and dev["tokens"].numel() == ops.WhisperMega.ROWS
-                and B_pad <= self.mega.max_seqs):
-            logits = decode_step_mega(self.model, dev["tokens"], dev["positions"], dev["slots"],
-                                      dev["cu_q"], dev["ctx_lens"], dev["block_tables"],
-                                      dev["enc_starts"], dev["enc_lens"], dev["logit_idx"], self.mega)
-            return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
         if self.fused and dev["tokens"].numel() <= 64:
             logits = decode_step_fused(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                        dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
@@ -497,31 +482,12 @@ class STTEngine:
                 rslot = self._replay(g)
                 torch.cuda.current_stream(self.device).synchronize()
                 out = self._res_ring[rslot, :B].numpy().copy()
-                if self.mega is not None and T_pad == ops.WhisperMega.ROWS:
-                    self._check_mega()
                 self.stats["host_pre_s"] += t1 - t0
                 self.stats["gpu_wait_s"] += time.perf_counter() - t1
                 return out
             max_q, host = self._host_meta(live, B_pad, T_pad)
-            out = self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
-            if self.mega is not None and T_pad == ops.WhisperMega.ROWS:
-                self._check_mega()
-            return out
+            return self._fast_forward(self._dev(host), max_q, B_pad)[:B].cpu().numpy()
         return self._eager_step(live)
-
-    def _check_mega(self) -> None:
-        """After every one-launch step (opt-in path), read the kernel's sticky
-        error word before the tokens are used: an expired (bounded) dependency
-        wait means this step's outputs are garbage, so the batch fails loudly.
-        The word is then cleared and the engine drops back to the fused
-        8-launches-per-layer path for good."""
-        if self.mega is not None and self.mega.error():
-            self.mega.sync.zero_()
-            self.mega = None
-            self._graphs.clear()           # graphs captured the mega launch
-            self._graphs_frozen = False
-            raise RuntimeError("whisper_mega: a dependency wait expired (kernel error flag set); "
-                               "falling back to the fused decoder step")
 
     def _eager_step(self, live: list[STTRequest]) -> np.ndarray:
         """Reference decode path (hipBLASLt GEMMs, eager launches)."""

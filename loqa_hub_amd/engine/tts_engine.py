@@ -41,6 +41,7 @@ class VitsTTSEngine:
         self._pending: list[tuple[str, float, asyncio.Future]] = []
         self._flusher: asyncio.Task | None = None
         self._gpu_lock = threading.Lock()
+        self._stream = None            # the placed TTS stream (utils/streams.py), created lazily
         self._seed = seed
         self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0}
 
@@ -57,7 +58,7 @@ class VitsTTSEngine:
         lens = torch.tensor([len(i) for i in ids], dtype=torch.int32, device=self.device)
         # one length scale per batch (the engine groups by speed upstream)
         ls = 1.0 / max(1e-3, float(np.mean(speeds)))
-        with self._gpu_lock, torch.inference_mode():
+        with self._gpu_lock, torch.inference_mode(), self._stream_ctx():
             t0 = time.perf_counter()
             self._seed += 1
             pcm, n = self.model.synthesize(torch.from_numpy(arr).to(self.device), lens,
@@ -68,6 +69,19 @@ class VitsTTSEngine:
         self.stats["phrases"] += len(texts)
         self.stats["samples"] += int(n.sum())
         return [pcm[b, : int(n[b])].copy() for b in range(len(texts))]
+
+    def _stream_ctx(self):
+        """VITS runs on its own explicitly placed pool stream (a fixed hardware
+        queue beside the decoders, docs/PERF.md "Stream placement"), never on
+        whatever stream the executor thread happens to default to."""
+        import contextlib
+        if self.device.type != "cuda":
+            return contextlib.nullcontext()
+        if self._stream is None:
+            from ..utils.streams import init_pools, placed_stream
+            init_pools(self.device)
+            self._stream = placed_stream(self.device, "tts")
+        return torch.cuda.stream(self._stream)
 
     # ------------------------------------------------------ TextToSpeech API
     async def synthesize(self, text: str, options: TTSOptions | None = None) -> TTSResult:

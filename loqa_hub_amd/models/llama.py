@@ -308,8 +308,9 @@ PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
 # RMSNorm), gate|up with the SwiGLU epilogue in the GEMM. Split counts per
 # projection (qkv, o, down) for ~300-row prompts.
 PREFILL2 = os.environ.get("LOQA_PREFILL2", "0") != "0"
-# prompt passes on the split-K tiled GEMM (no hipBLASLt, no f32 slabs)
-PREFILL3 = os.environ.get("LOQA_PREFILL3", "0") != "0"
+# prompt passes on the split-K tiled GEMM (no f32 slabs): 1 every projection,
+# 2 only the residual projections o / down (qkv, gate|up on hipBLASLt)
+PREFILL3 = int(os.environ.get("LOQA_PREFILL3", "0"))
 
 
 def L0_KEYS(w) -> set:
@@ -432,7 +433,7 @@ class LlamaModel:
         for li, L in enumerate(w.layers):
             if li > 0:
                 h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
-            qkv = ops.gemm_sk(h, L["wqkv"])
+            qkv = ops.linear(h, L["wqkv"]) if PREFILL3 == 2 else ops.gemm_sk(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
             attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
@@ -441,7 +442,8 @@ class LlamaModel:
                                  num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
             ops.gemm_sk(attn, L["wo"], epi="resid", residual=residual)
             hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
-            a = ops.gemm_sk(hn, L["w_gate_up"], epi="swiglu")
+            a = (ops.silu_mul(ops.linear(hn, L["w_gate_up"])) if PREFILL3 == 2
+                 else ops.gemm_sk(hn, L["w_gate_up"], epi="swiglu"))
             ops.gemm_sk(a, L["w_down"], epi="resid", residual=residual)
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 

@@ -46,6 +46,8 @@ ENC_FC1_TILE = int(os.environ.get("LOQA_ENC_FC1_TILE", "0"))
 XKV_TILE = int(os.environ.get("LOQA_XKV_TILE", "1"))
 # encoder qkv (+ bias) on the tiled GEMM (0: hipBLASLt)
 ENC_QKV_TILE = int(os.environ.get("LOQA_ENC_QKV_TILE", "0"))
+# every encoder projection on the split-K tiled GEMM (ops.gemm_sk)
+ENC_SK = int(os.environ.get("LOQA_ENC_SK", "0"))
 
 
 class WhisperWeights:
@@ -107,6 +109,8 @@ class WhisperWeights:
         self.conv1_bf, self.conv2_bf = self.conv1_b.float(), self.conv2_b.float()
         self.enc_fc1_bf = [L["fc1_b"].float() for L in self.enc]
         self.enc_qkv_bf = [L["bqkv"].float() for L in self.enc]
+        self.enc_o_bf = [L["bo"].float() for L in self.enc]
+        self.enc_fc2_bf = [L["fc2_b"].float() for L in self.enc]
         # the decoder layers' cross K|V weights as ONE [L * 2d, d] matrix (each
         # layer's "xkv" becomes a row-block view of it, no second copy), so the
         # cross K|V of an utterance is one tiled GEMM launch
@@ -215,6 +219,8 @@ class WhisperModel:
         T = cfg.n_audio_ctx
         cu = torch.arange(0, (B + 1) * T, T, dtype=torch.int32, device=audio.device)
         H, D = cfg.n_heads, cfg.head_dim
+        if tile and ENC_SK:
+            return self._encode_sk(x, cu, T)
         residual = x
         h = ops.layernorm(x, w.enc[0]["ln1_w"], w.enc[0]["ln1_b"], 1e-5)
         delta = None
@@ -254,6 +260,24 @@ class WhisperModel:
             return ops.slab_layernorm(part2, residual, w.enc_ln_w, w.enc_ln_b, 1e-5,
                                       bias=w.enc[-1]["fc2_b"])
         return ops.layernorm(delta, w.enc_ln_w, w.enc_ln_b, 1e-5, residual=residual)
+
+    def _encode_sk(self, x: torch.Tensor, cu: torch.Tensor, T: int) -> torch.Tensor:
+        """Encoder layers on the split-K tiled GEMM (no hipBLASLt): qkv (+ f32
+        bias), flash attention, o (+ bias) added straight into the residual,
+        LayerNorm, fc1 (+ bias, GELU), fc2 (+ bias) added into the residual."""
+        cfg, w = self.cfg, self.w
+        d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
+        residual = x.contiguous()
+        for i, L in enumerate(w.enc):
+            h = ops.layernorm(residual, L["ln1_w"], L["ln1_b"], 1e-5)
+            qkv = ops.gemm_sk(h, L["wqkv"], bias=w.enc_qkv_bf[i])
+            a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
+                              causal=False, max_q=T, cu_k=cu)
+            ops.gemm_sk(a, L["wo"], epi="resid", residual=residual, bias=w.enc_o_bf[i])
+            h = ops.layernorm(residual, L["ln2_w"], L["ln2_b"], 1e-5)
+            m = ops.gemm_sk(h, L["fc1"], bias=w.enc_fc1_bf[i], act="gelu")
+            ops.gemm_sk(m, L["fc2"], epi="resid", residual=residual, bias=w.enc_fc2_bf[i])
+        return ops.layernorm(residual, w.enc_ln_w, w.enc_ln_b, 1e-5)
 
     def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:
         """Per decoder layer [B*1500, 2d] cross-attention K|V (computed once)."""
@@ -404,22 +428,6 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
         hf = ops.layernorm(residual, w.dec_ln_w, w.dec_ln_b, 1e-5, row_idx=logit_idx)
     else:
         hf = ops.layernorm(residual.index_select(0, logit_idx), w.dec_ln_w, w.dec_ln_b, 1e-5)
-    return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
-
-
-def decode_step_mega(model: "WhisperModel", tokens: torch.Tensor, positions: torch.Tensor,
-                     slots: torch.Tensor, cu_q: torch.Tensor, ctx_lens: torch.Tensor,
-                     block_tables: torch.Tensor, enc_starts: torch.Tensor, enc_lens: torch.Tensor,
-                     logit_idx: torch.Tensor, mega) -> torch.Tensor:
-    """Decoder step with every layer in ONE persistent launch
-    (``ops.whisper_mega``): embedding -> 32 x (qkv, self-attention, o, xq,
-    cross-attention, xo, fc1, fc2) as a dependency-ordered work list -> final
-    LayerNorm of the logit rows -> vocab GEMM. 16 token rows (Mpad 16); same
-    metadata contract as ``decode_step_fused``."""
-    w = model.w
-    residual = ops.embed_pos(tokens, positions, w.tok_embed, w.dec_pos)
-    ops.whisper_mega(mega, residual, slots, cu_q, ctx_lens, block_tables, enc_starts, enc_lens)
-    hf = ops.layernorm(residual, w.dec_ln_w, w.dec_ln_b, 1e-5, row_idx=logit_idx)
     return ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0]
 
 

@@ -1304,84 +1304,6 @@ def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, pos
     return q_out
 
 
-# ------------------------------------------- Whisper decoder: one persistent launch
-class WhisperMega:
-    """State of the persistent Whisper decoder-step kernel
-    (``csrc/kernels/whisper_mega.hip``): the per-layer pointer table, the
-    inter-phase activation buffers, the split partials and the per-step sync
-    words. Built once per engine; every buffer is fixed so a captured graph
-    replays against it. Token rows per step: ``ROWS`` (Mpad 16)."""
-    ROWS = 16
-    XSK = 256          # cross-attention keys per split (kernel constant)
-
-    def __init__(self, w, k_cache: torch.Tensor, v_cache: torch.Tensor, xkv: list[torch.Tensor],
-                 max_seqs: int, grid: int | None = None):
-        cfg = w.cfg
-        d, H, D, F = cfg.d_model, cfg.n_heads, cfg.head_dim, w.dec[0]["fc1"].shape[0]
-        assert D == 64 and H * D == d and d % 128 == 0 and d <= 1280 and F % 128 == 0
-        dev = k_cache.device
-        self.d, self.H, self.F, self.L = d, H, F, cfg.dec_layers
-        self.nsplit = (cfg.n_audio_ctx + self.XSK - 1) // self.XSK
-        self.max_seqs = max_seqs
-        self.blk = k_cache.shape[3]
-        self.kv_bytes = k_cache[0].numel() * 2
-        assert self.kv_bytes < 2 ** 31
-        rows = []
-        for i, (L, P) in enumerate(zip(w.dec, w.dec_p)):
-            rows.append([P[k].data_ptr() for k in ("wqkv", "wo", "xq", "xo", "fc1", "fc2")]
-                        + [L[k].data_ptr() for k in ("bqkv", "bo", "xq_b", "xo_b", "fc1_b", "fc2_b")]
-                        + [L[k].data_ptr() for k in ("ln1_w", "ln1_b", "lnx_w", "lnx_b", "ln2_w", "ln2_b")]
-                        + [k_cache[i].data_ptr(), v_cache[i].data_ptr(), xkv[i].data_ptr()])
-        self._keep = (w, k_cache, v_cache, xkv)       # the table points into these
-        self.table = torch.tensor(rows, dtype=torch.int64).to(dev)
-        R = self.ROWS
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        self.qb = torch.zeros(R, d, **bf)
-        self.ab = torch.zeros(R, d, **bf)
-        self.xqb = torch.zeros(R, d, **bf)
-        self.mb = torch.zeros(R, F, **bf)
-        self.part = torch.zeros(max_seqs * H * self.nsplit * R * 66, dtype=torch.float32, device=dev)
-        self.sync = torch.zeros(self.L * 8 + max_seqs * H + 1, dtype=torch.int32, device=dev)
-        self.grid = grid or int(os.environ.get("LOQA_STT_MEGA_WGS", "256"))
-        self.eps = 1e-5
-        self.scale_log2 = (1.0 / math.sqrt(D)) * 1.4426950408889634
-        # optional int64 [items * 5] buffer: per-item s_memrealtime stamps
-        # (scripts/exp/whisper_mega_bench.py)
-        self.dbg: torch.Tensor | None = None
-
-    def error(self) -> int:
-        """Non-zero once any step's bounded dependency wait expired (sticky:
-        the per-step reset leaves word 0 alone; host read)."""
-        return int(self.sync[0].item())
-
-
-def whisper_mega(m: WhisperMega, x: torch.Tensor, slots: torch.Tensor, cu_q: torch.Tensor,
-                 ctx_lens: torch.Tensor, block_tables: torch.Tensor, enc_starts: torch.Tensor,
-                 enc_lens: torch.Tensor) -> torch.Tensor:
-    """All decoder layers of one Whisper step on the residual rows ``x``
-    [16, d] bf16 (embedded tokens in, pre-final-LayerNorm residual out), in one
-    launch. Metadata as for the fused path (``STTEngine._host_meta``)."""
-    from ._lib import WhisperMegaParams
-    B = cu_q.numel() - 1
-    R = m.ROWS
-    assert x.is_cuda and x.shape == (R, m.d) and x.dtype == torch.bfloat16 and x.is_contiguous()
-    assert slots.numel() == R and 0 < B <= m.max_seqs
-    for t in (slots, cu_q, ctx_lens, block_tables, enc_starts, enc_lens):
-        assert t.dtype == torch.int32 and t.is_contiguous() and t.is_cuda
-    p = WhisperMegaParams()
-    p.layers, p.L = ptr(m.table), m.L
-    p.x, p.qb, p.ab, p.xqb, p.mb = ptr(x), ptr(m.qb), ptr(m.ab), ptr(m.xqb), ptr(m.mb)
-    p.part, p.sync = ptr(m.part), ptr(m.sync)
-    p.slots, p.cu_q, p.ctx_lens, p.block_tables = ptr(slots), ptr(cu_q), ptr(ctx_lens), ptr(block_tables)
-    p.max_blocks, p.blk = block_tables.shape[1], m.blk
-    p.enc_starts, p.enc_lens = ptr(enc_starts), ptr(enc_lens)
-    p.B, p.d, p.H, p.ffn, p.nsplit = B, m.d, m.H, m.F, m.nsplit
-    p.kv_bytes, p.eps, p.scale_log2 = m.kv_bytes, m.eps, m.scale_log2
-    p.dbg = ptr(m.dbg)
-    check(kernels().loqa_whisper_mega(ctypes.byref(p), m.grid, stream_ptr(x)), "whisper_mega")
-    return x
-
-
 # ------------------------------------------------------------- prefill GEMM
 PREFILL_GEMM_NT = 128     # features per workgroup of the default layout (3)
 
@@ -1580,35 +1502,48 @@ SK_CUS = 256
 _SK_WS: dict = {}
 
 
+# measured picks (scripts/exp/gemm_sk_bench.py --grid, cold weights, one
+# MI355X; profiles/r4_gemm_sk_grid.txt): (N, K) -> [(max M, layout, chunks)]
+SK_TABLE = {
+    (6144, 4096): [(400, 4, 1), (900, 5, 1), (1 << 30, 0, 1)],        # Llama-3-8B qkv
+    (4096, 4096): [(900, 4, 1), (1 << 30, 1, 1)],                     # o
+    (28672, 4096): [(400, 4, 1), (1 << 30, 0, 1)],                    # gate|up
+    (4096, 14336): [(400, 8, 3), (900, 0, 3), (1 << 30, 0, 1)],       # down
+    (3840, 1280): [(1 << 30, 0, 1)],                                  # Whisper-large-v3 enc qkv
+    (1280, 1280): [(2000, 4, 1), (4000, 5, 1), (1 << 30, 3, 1)],      # enc o
+    (5120, 1280): [(1 << 30, 0, 1)],                                  # enc fc1
+    (1280, 5120): [(2000, 4, 1), (4000, 5, 1), (1 << 30, 0, 1)],      # enc fc2
+}
+
+
 def gemm_sk_plan(M: int, N: int, K: int, epi: str = "bf16",
-                 layouts=(0, 1, 2, 3, 6)) -> tuple[int, int]:
-    """(layout, K chunks) for a shape: ``LOQA_SK=layout,S`` if set, else the
-    analytic plan - the fewest MFMA-cycle rounds over the resident workgroup
-    slots, counting padded rows, wave-tile efficiency and a per-chunk cost of
-    the split-K reduction."""
+                 layouts=(0, 1, 2, 3, 4, 5)) -> tuple[int, int]:
+    """(layout, K chunks) for a shape: ``LOQA_SK=layout,S`` if set, the
+    measured table for the served shapes, else an analytic plan - the fewest
+    MFMA-cycle rounds over the resident workgroup slots, counting padded rows
+    and wave-tile efficiency, with at most 3 K chunks (each chunk's partial
+    costs a write and a serial read in the reduction: 16 chunks measured up
+    to 7x slower than 1)."""
     env = os.environ.get("LOQA_SK")
     if env:
         lay, s = (int(v) for v in env.split(","))
         return lay, s
+    for m_max, lay, s in SK_TABLE.get((N, K), ()):
+        if M <= m_max and N % SK_LAYOUTS[lay][0] == 0:
+            return lay, s
     KT = K // 64
-    best, best_t = (1, 1), float("inf")
+    best, best_t = (7, 1), float("inf")
     for lay in layouts:
         bn, bm, occ, eff = SK_LAYOUTS[lay]
-        if N % bn or (epi == "swiglu" and (bn // 2) % 32):
+        if N % bn:
             continue
         tiles = -(-M // bm) * (N // bn)
-        for s in (1, 2, 3, 4, 6, 8, 12, 16):
-            if s > KT or (s > 1 and KT // s < 4):
+        for s in (1, 2, 3):
+            if s > KT or (s > 1 and KT // s < 8) or (epi == "swiglu" and s > 1):
                 continue
-            if epi == "swiglu" and s > 2:
-                continue          # the partials of a wide SwiGLU tile cost more than they balance
             grid = tiles * s
-            slots = SK_CUS * occ
-            rounds = -(-grid // slots)
-            # per-workgroup time ~ tile MFMA work of its chunk; a round runs
-            # `occ` workgroups per CU sharing its MFMA pipes
-            t_wg = bm * bn * (KT / s) / eff
-            t = rounds * t_wg * occ + (s > 1) * bm * bn * 24.0 + 2000.0 * bm * bn / 16384
+            rounds = -(-grid // (SK_CUS * occ))
+            t = rounds * occ * bm * bn * (KT / s) / eff + (s - 1) * bm * bn * 64.0
             if t < best_t:
                 best, best_t = (lay, s), t
     return best
@@ -1626,37 +1561,41 @@ def _sk_workspace(dev: torch.device, stream: int, floats: int, tiles: int):
     return ws
 
 
-def _sk_ref(x: torch.Tensor, w: torch.Tensor, epi: str, bias, residual):
+def _sk_ref(x: torch.Tensor, w: torch.Tensor, epi: str, bias, residual, act: str | None = None):
     y = x.float() @ w.float().t()
     if epi == "swiglu":
         F = w.shape[0] // 2
         g = y[:, :F].to(torch.bfloat16).float()
         u = y[:, F:].to(torch.bfloat16).float()
         return (g * torch.sigmoid(g) * u).to(torch.bfloat16)
-    if epi == "resid":
-        return (residual.float() + y).to(torch.bfloat16)
     if bias is not None:
         y = y + bias.float()
+    if epi == "resid":
+        return (residual.float() + y).to(torch.bfloat16)
+    if act == "gelu":
+        y = y.to(torch.bfloat16).float()
+        y = 0.5 * y * (1.0 + torch.erf(y * 0.70710678118654752))
     return y.to(torch.bfloat16)
 
 
 def gemm_sk(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
-            residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
-            layout: int | None = None, splits: int | None = None) -> torch.Tensor:
+            act: str | None = None, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None, layout: int | None = None,
+            splits: int | None = None) -> torch.Tensor:
     """Y = X W^T on the split-K tiled GEMM (``csrc/kernels/gemm_sk.hip``); the
     S K-chunks of a tile are summed in-launch by the tile's last workgroup.
 
     x [M, K] bf16 (row stride may exceed K), w [N, K] bf16 row-major.
-    ``epi``: "bf16" -> [M, N] (+ f32 ``bias``); "swiglu" -> silu(gate) * up
+    ``epi``: "bf16" -> [M, N] (+ f32 ``bias``, ``act`` "gelu"); "swiglu" -> silu(gate) * up
     [M, N / 2] (gate rows [0, N/2), up rows [N/2, N)); "resid" -> ``residual``
-    [M, N] += X W^T in place (one bf16 rounding), returned."""
+    [M, N] += X W^T (+ ``bias``) in place (one bf16 rounding), returned."""
     N, K = w.shape
     M = x.shape[0]
     assert x.shape[1] == K, (x.shape, w.shape)
     if epi == "resid":
         assert residual is not None and residual.shape == (M, N)
     if not _gpu(x):
-        y = _sk_ref(x, w, epi, bias, residual)
+        y = _sk_ref(x, w, epi, bias, residual, act)
         dst = residual if epi == "resid" else out
         if dst is not None:
             dst.copy_(y)
@@ -1676,8 +1615,10 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
     p = _lib.GemmSkParams()
     p.x, p.ldx, p.w = ptr(x), x.stride(0), ptr(w)
     p.M, p.N, p.K, p.S, p.epi = M, N, K, splits, _SK_EPI[epi]
+    p.act = 1 if act == "gelu" else 0
+    assert not act or epi == "bf16"
     if bias is not None:
-        assert epi == "bf16" and bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N
+        assert epi != "swiglu" and bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N
     p.bias = ptr(bias)
     if epi == "resid":
         y = residual

@@ -61,24 +61,9 @@ class GemmSkParams(ctypes.Structure):
     _fields_ = [
         ("x", c_void_p), ("ldx", c_ll), ("w", c_void_p),
         ("M", c_int), ("N", c_int), ("K", c_int), ("S", c_int),
-        ("epi", c_int), ("bias", c_void_p),
+        ("epi", c_int), ("act", c_int), ("bias", c_void_p),
         ("y", c_void_p), ("ldy", c_ll),
         ("ws", c_void_p), ("counters", c_void_p), ("layout", c_int),
-    ]
-
-
-class WhisperMegaParams(ctypes.Structure):
-    """Mirror of ``MegaParams`` in csrc/kernels/whisper_mega.hip."""
-    _fields_ = [
-        ("layers", c_void_p), ("L", c_int),
-        ("x", c_void_p), ("qb", c_void_p), ("ab", c_void_p), ("xqb", c_void_p), ("mb", c_void_p),
-        ("part", c_void_p), ("sync", c_void_p),
-        ("slots", c_void_p), ("cu_q", c_void_p), ("ctx_lens", c_void_p), ("block_tables", c_void_p),
-        ("max_blocks", c_int), ("blk", c_int),
-        ("enc_starts", c_void_p), ("enc_lens", c_void_p),
-        ("B", c_int), ("d", c_int), ("H", c_int), ("ffn", c_int), ("nsplit", c_int),
-        ("kv_bytes", c_int), ("eps", c_float), ("scale_log2", c_float),
-        ("dbg", c_void_p),
     ]
 
 
@@ -137,7 +122,6 @@ _KERNEL_SIGS = {
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_step_fetch": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
                         c_int, c_int, c_void_p, c_void_p],
-    "loqa_whisper_mega": [c_void_p, c_int, c_void_p],
     "loqa_gemm_prefill2": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                            c_int, c_void_p],
     "loqa_init_uniform4": [c_void_p, c_ll, c_int, c_ll, c_ll, c_ll, ctypes.c_uint, c_float, c_void_p],

@@ -170,7 +170,10 @@ class CustomAllReduce:
         return lo >= 0 and shard >= 1 and lo + shard - 1 <= MAX_TOKEN_ID
 
     def error(self) -> bool:
-        return bool(_lib.kernels().loqa_car_error(self._h))
+        v = _lib.kernels().loqa_car_error(self._h)
+        if v < 0:
+            raise RuntimeError(f"custom all-reduce: error word unreadable (hipError {-v})")
+        return bool(v)
 
     def clear_error(self) -> None:
         _lib.check(_lib.kernels().loqa_car_clear_error(self._h), "car_clear_error")

@@ -133,8 +133,12 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
         while not state["stop"]:
             with lock:
                 age = time.monotonic() - state["last_progress"]
+                st = dict(getattr(proc, "stats", {}))
+                tts = getattr(proc, "tts", None)
+                for k, v in (getattr(tts, "stats", None) or {}).items():
+                    st["tts_" + k] = v
                 hb = {"inflight": state["inflight"], "since_progress": age,
-                      "done": state["done"], "stats": dict(getattr(proc, "stats", {}))}
+                      "done": state["done"], "stats": st}
             resp_q.put(("hb", rank, hb))
             time.sleep(spec.get("heartbeat_s", 0.5))
 

@@ -123,12 +123,13 @@ def _log_slot(role: str, st, device, priority: int) -> None:
 # placement, round 3"; profiles/r3_stream_placement.txt): the LLM decoder on
 # normal-priority slot 2, the Whisper decoder on high-priority slot 30, the
 # encoder worker on normal-priority slot 28, the prefill worker on slot 3
-# (pools created first thing by init_pools, so slot -> queue is fixed).
+# (pools created first thing by init_pools, so slot -> queue is fixed); VITS
+# (progressive reply speech) on normal-priority slot 29.
 # Round 3 found the old
 # implicit placement had depended on the STT upload drawing one pool stream per
 # batch: removing that draw moved the LLM decoder to slot 0 and halved the
 # throughput (19.1 -> 9.8 utt/s). LOQA_SLOT_<ROLE> overrides (search).
-DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3}
+DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3, "tts": 29}
 
 
 def init_pools(device: torch.device) -> None:

@@ -71,3 +71,29 @@ def test_gemm_sk_split_reduction_is_deterministic():
     for _ in range(5):
         assert torch.equal(ops.gemm_sk(x, w, layout=1, splits=6), ref)
     assert _rel(ref, ops._sk_ref(x.cpu(), w.cpu(), "bf16", None, None)) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["test-whisper", "whisper-large-v3"])
+def test_whisper_encoder_sk_matches_library_path(monkeypatch, name):
+    """Every encoder projection on the split-K tiled GEMM (qkv + bias, o +
+    bias into the residual, fc1 + bias + GELU, fc2 + bias into the residual)
+    against the hipBLASLt / slab path on the same weights."""
+    from loqa_hub_amd.models import whisper as wm
+    from loqa_hub_amd.models.configs import whisper_config
+
+    dev = torch.device("cuda", 0)
+    cfg = whisper_config(name, n_mels=128, enc_layers=3)
+    w = wm.WhisperWeights(cfg, dev, seed=3)
+    model = wm.WhisperModel(w)
+    g = torch.Generator(device=dev).manual_seed(5)
+    audio = (torch.rand(2, 480000, device=dev, generator=g) - 0.5) * 0.2
+    monkeypatch.setattr(wm, "ENC_SK", 1)
+    a = model.encode(audio)
+    monkeypatch.setattr(wm, "ENC_SK", 0)
+    b = model.encode(audio)
+    assert a.shape == b.shape == (2 * 1500, cfg.d_model)
+    assert torch.isfinite(a.float()).all()
+    err = (a.float() - b.float()).abs()
+    assert err.max().item() < 0.05 * b.float().abs().max().item(), err.max().item()
+    assert err.mean().item() < 0.01 * b.float().abs().mean().item() + 1e-3
