@@ -1636,3 +1636,62 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
     p.layout = layout
     check(kernels().loqa_gemm_sk(ctypes.byref(p), st), "gemm_sk")
     return y
+
+
+# ---------------------------------------------------------------------------
+# Row-resident weight-streaming GEMM (csrc/kernels/gemm_ws.hip)
+_WS_EPI = {"bf16": 0, "swiglu": 1, "resid": 2}
+WS_MAX_BM = 384
+
+
+def gemm_ws_rows(M: int, depth: int = 0) -> int:
+    """Rows per workgroup: M split into the fewest blocks of <= 384 rows
+    (<= 256 at depth 1), each rounded up to 64."""
+    cap = WS_MAX_BM if depth == 0 else 256
+    nb = -(-M // cap)
+    return -(-(-(-M // nb)) // 64) * 64
+
+
+def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
+            act: str | None = None, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None, depth: int | None = None,
+            bm: int | None = None) -> torch.Tensor:
+    """Y = X W^T on the row-resident weight-streaming GEMM: a workgroup owns
+    128 output features x all the rows of its row block (up to 384), so every
+    weight byte is read once. Epilogues as :func:`gemm_sk`."""
+    N, K = w.shape
+    M = x.shape[0]
+    assert x.shape[1] == K, (x.shape, w.shape)
+    if epi == "resid":
+        assert residual is not None and residual.shape == (M, N)
+    if not _gpu(x):
+        y = _sk_ref(x, w, epi, bias, residual, act)
+        dst = residual if epi == "resid" else out
+        if dst is not None:
+            dst.copy_(y)
+            return dst
+        return y
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("gemm_ws needs bf16 operands")
+    if x.stride(1) != 1 or not w.is_contiguous() or N % 128 or K % 64:
+        raise ValueError("gemm_ws needs K-contiguous operands, N % 128 == 0, K % 64 == 0")
+    depth = int(os.environ.get("LOQA_WS_DEPTH", "0")) if depth is None else depth
+    p = _lib.GemmWsParams()
+    p.x, p.ldx, p.w = ptr(x), x.stride(0), ptr(w)
+    p.M, p.N, p.K, p.epi = M, N, K, _WS_EPI[epi]
+    p.act = 1 if act == "gelu" else 0
+    assert not act or epi == "bf16"
+    if bias is not None:
+        assert epi != "swiglu" and bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N
+    p.bias = ptr(bias)
+    if epi == "resid":
+        y = residual
+        assert y.dtype == torch.bfloat16 and y.stride(1) == 1
+    else:
+        cols = N // 2 if epi == "swiglu" else N
+        y = out if out is not None else torch.empty(M, cols, dtype=torch.bfloat16, device=x.device)
+        assert y.shape == (M, cols) and y.stride(1) == 1
+    p.y, p.ldy = ptr(y), y.stride(0)
+    p.bm = gemm_ws_rows(M, depth) if bm is None else bm
+    check(kernels().loqa_gemm_ws(ctypes.byref(p), depth, stream_ptr(x)), "gemm_ws")
+    return y

@@ -67,6 +67,16 @@ class GemmSkParams(ctypes.Structure):
     ]
 
 
+class GemmWsParams(ctypes.Structure):
+    """Mirror of ``GemmWsParams`` in csrc/kernels/gemm_ws.hip."""
+    _fields_ = [
+        ("x", c_void_p), ("ldx", c_ll), ("w", c_void_p),
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("epi", c_int), ("act", c_int), ("bias", c_void_p),
+        ("y", c_void_p), ("ldy", c_ll), ("bm", c_int),
+    ]
+
+
 _KERNEL_SIGS = {
     "loqa_rmsnorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p,
                      c_void_p],
@@ -95,6 +105,7 @@ _KERNEL_SIGS = {
     "loqa_gemm_tile": [c_void_p, c_void_p],
     "loqa_gemm_sk": [c_void_p, c_void_p],
     "loqa_gemm_sk_dims": [c_int, c_void_p, c_void_p],
+    "loqa_gemm_ws": [c_void_p, c_int, c_void_p],
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,

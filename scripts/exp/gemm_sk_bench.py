@@ -39,10 +39,13 @@ def main():
     ap.add_argument("--ms", default="300,600,1200")
     ap.add_argument("--wms", default="1500,3000,6000")
     ap.add_argument("--grid", action="store_true", help="time every (layout, S)")
+    ap.add_argument("--only", default="", help="comma list of shape names")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cases = [(m, k, v) for m in map(int, a.ms.split(",")) for k, v in LLAMA.items()]
     cases += [(m, k, v) for m in map(int, a.wms.split(",")) for k, v in WHISPER.items()]
+    if a.only:
+        cases = [c for c in cases if c[1] in a.only.split(",")]
     for M, name, (N, K, epi) in cases:
         wbytes = N * K * 2
         n_w = max(2, (768 << 20) // wbytes)
@@ -59,7 +62,16 @@ def main():
             else:
                 ops.gemm_sk(x, ws[i], epi=epi, layout=lay, splits=s)
         t_plan = timeit(run, n_w)
+        ws_t = {}
+        for depth in (0, 1):
+            def run_ws(i, depth=depth):
+                if epi == "resid":
+                    ops.gemm_ws(x, ws[i], epi="resid", residual=res, depth=depth)
+                else:
+                    ops.gemm_ws(x, ws[i], epi=epi, depth=depth)
+            ws_t[depth] = round(timeit(run_ws, n_w), 1)
         out = {"shape": name, "M": M, "N": N, "K": K, "epi": epi, "hipblaslt_us": round(t_blas, 1),
+               "ws_us": ws_t,
                "hipblaslt_pf": round(flops / t_blas / 1e9, 3), "plan": [lay, s],
                "plan_us": round(t_plan, 1), "plan_pf": round(flops / t_plan / 1e9, 3)}
         if a.grid:

@@ -97,3 +97,30 @@ def test_whisper_encoder_sk_matches_library_path(monkeypatch, name):
     err = (a.float() - b.float()).abs()
     assert err.max().item() < 0.05 * b.float().abs().max().item(), err.max().item()
     assert err.mean().item() < 0.01 * b.float().abs().mean().item() + 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [0, 1])
+def test_gemm_ws_gpu_matches_fp32(depth):
+    """Row-resident weight-streaming GEMM: every row-block size, ragged M,
+    every epilogue, against the fp32 reference."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(10 + depth)
+    for M, N, K in ((300, 384, 512), (17, 256, 128), (385, 128, 256), (1000, 256, 192), (64, 512, 64)):
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+        b = torch.randn(N, device=dev) * 0.1
+        y = ops.gemm_ws(x, w, bias=b, act="gelu", depth=depth)
+        assert _rel(y, ops._sk_ref(x.cpu(), w.cpu(), "bf16", b.cpu(), None, "gelu")) < 1e-2, (M, N, K)
+        res = torch.randn(M, N, device=dev).bfloat16()
+        rr = ops._sk_ref(x.cpu(), w.cpu(), "resid", b.cpu(), res.cpu())
+        ops.gemm_ws(x, w, epi="resid", residual=res, bias=b, depth=depth)
+        assert _rel(res, rr) < 1e-2, (M, N, K, "resid")
+        sw = ops.gemm_ws(x, w, epi="swiglu", depth=depth)
+        assert _rel(sw, ops._sk_ref(x.cpu(), w.cpu(), "swiglu", None, None)) < 2e-2, (M, N, K, "swiglu")
+    # explicit row blocks, every size the kernel takes
+    x = torch.randn(700, 256, device=dev).bfloat16()
+    w = (torch.randn(256, 256, device=dev) * 0.05).bfloat16()
+    ref = ops._sk_ref(x.cpu(), w.cpu(), "bf16", None, None)
+    for bm in (64, 128, 192, 256) + ((320, 384) if depth == 0 else ()):
+        assert _rel(ops.gemm_ws(x, w, depth=depth, bm=bm), ref) < 1e-2, bm
