@@ -120,24 +120,48 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_sk_kernel(GemmSkParams p) {
     return *reinterpret_cast<const bf16x8*>(lds + buf * STAGE + row * 128 + 16 * (c ^ ((row >> 1) & 7)));
   };
   auto compute = [&](int buf) {
+    // Half 0's fragments (activations first), then its MFMAs row by row with
+    // half 1's fragment reads issued between them (sched barriers pin the
+    // order), then half 1's MFMAs: only half 0's reads are exposed, and at most
+    // FN + FM + 2 LDS reads are ever outstanding (the 4-bit lgkmcnt: with more
+    // pending, the waitcnt pass can only wait for all of them).
+    static_assert(FN + FM + 2 <= 15, "outstanding LDS reads exceed lgkmcnt");
     bf16x8 af[2][FN], bfr[2][FM];
+    {
+      constexpr int sub = 0;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
+      for (int j = 0; j < FM; ++j) bfr[0][j] = frag(buf, BN + wm * TM + 16 * j + fr, 4 * sub + fq);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) af[sub][i] = frag(buf, wn * TN + 16 * i + fr, 4 * sub + fq);
+      for (int i = 0; i < FN; ++i) af[0][i] = frag(buf, wn * TN + 16 * i + fr, 4 * sub + fq);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < FM; ++j) bfr[sub][j] = frag(buf, BN + wm * TM + 16 * j + fr, 4 * sub + fq);
+    for (int i = 0; i < FN; ++i) {
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+      {
+        constexpr int sub = 1;
+        af[1][i] = frag(buf, wn * TN + 16 * i + fr, 4 * sub + fq);
+        if (i < FM) {
+          const int j = i;
+          bfr[1][j] = frag(buf, BN + wm * TM + 16 * j + fr, 4 * sub + fq);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[sub][i], bfr[sub][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+    for (int j = FN; j < FM; ++j) {
+      constexpr int sub = 1;
+      bfr[1][j] = frag(buf, BN + wm * TM + 16 * j + fr, 4 * sub + fq);
     }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   int issued = 0;

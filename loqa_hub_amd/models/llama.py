@@ -433,18 +433,18 @@ class LlamaModel:
         for li, L in enumerate(w.layers):
             if li > 0:
                 h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
-            qkv = ops.linear(h, L["wqkv"]) if PREFILL3 == 2 else ops.gemm_sk(h, L["wqkv"])
+            qkv = ops.linear(h, L["wqkv"]) if PREFILL3 == 2 else ops.proj(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
             attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
                                  head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
                                  block_tables=meta.block_tables, grouped=False, split_keys=256,
                                  num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
-            ops.gemm_sk(attn, L["wo"], epi="resid", residual=residual)
+            ops.proj(attn, L["wo"], epi="resid", residual=residual)
             hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
             a = (ops.silu_mul(ops.linear(hn, L["w_gate_up"])) if PREFILL3 == 2
-                 else ops.gemm_sk(hn, L["w_gate_up"], epi="swiglu"))
-            ops.gemm_sk(a, L["w_down"], epi="resid", residual=residual)
+                 else ops.proj(hn, L["w_gate_up"], epi="swiglu"))
+            ops.proj(a, L["w_down"], epi="resid", residual=residual)
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 
     def _forward_prefill2(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:

@@ -270,13 +270,13 @@ class WhisperModel:
         residual = x.contiguous()
         for i, L in enumerate(w.enc):
             h = ops.layernorm(residual, L["ln1_w"], L["ln1_b"], 1e-5)
-            qkv = ops.gemm_sk(h, L["wqkv"], bias=w.enc_qkv_bf[i])
+            qkv = ops.proj(h, L["wqkv"], bias=w.enc_qkv_bf[i])
             a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
                               causal=False, max_q=T, cu_k=cu)
-            ops.gemm_sk(a, L["wo"], epi="resid", residual=residual, bias=w.enc_o_bf[i])
+            ops.proj(a, L["wo"], epi="resid", residual=residual, bias=w.enc_o_bf[i])
             h = ops.layernorm(residual, L["ln2_w"], L["ln2_b"], 1e-5)
-            m = ops.gemm_sk(h, L["fc1"], bias=w.enc_fc1_bf[i], act="gelu")
-            ops.gemm_sk(m, L["fc2"], epi="resid", residual=residual, bias=w.enc_fc2_bf[i])
+            m = ops.proj(h, L["fc1"], bias=w.enc_fc1_bf[i], act="gelu")
+            ops.proj(m, L["fc2"], epi="resid", residual=residual, bias=w.enc_fc2_bf[i])
         return ops.layernorm(residual, w.enc_ln_w, w.enc_ln_b, 1e-5)
 
     def cross_kv(self, enc: torch.Tensor) -> list[torch.Tensor]:

@@ -1695,3 +1695,40 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
     p.bm = gemm_ws_rows(M, depth) if bm is None else bm
     check(kernels().loqa_gemm_ws(ctypes.byref(p), depth, stream_ptr(x)), "gemm_ws")
     return y
+
+
+# ---------------------------------------------------------------------------
+# Projection dispatch for prompt passes (prefill, Whisper encoder): the
+# hand-written GEMM measured fastest per (N, K) and row count
+# (scripts/exp/gemm_sk_bench.py --grid, cold weights; profiles/r4_gemm_proj_grid.txt):
+# ("sk", layout, K chunks) = gemm_sk, ("ws", depth) = gemm_ws.
+PROJ_TABLE = {
+    (6144, 4096): [(400, ("sk", 4, 1)), (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],     # Llama qkv
+    (4096, 4096): [(900, ("sk", 4, 1)), (1 << 30, ("sk", 0, 1))],                         # o
+    (28672, 4096): [(384, ("ws", 0)), (900, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],      # gate|up
+    (4096, 14336): [(400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],   # down
+    (3840, 1280): [(2000, ("ws", 1)), (1 << 30, ("sk", 6, 1))],                           # enc qkv
+    (1280, 1280): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc o
+    (5120, 1280): [(2000, ("ws", 1)), (1 << 30, ("sk", 6, 1))],                           # enc fc1
+    (1280, 5120): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc fc2
+}
+
+
+def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
+         act: str | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
+    """A prompt-pass projection on the fastest hand-written GEMM for its shape
+    (``PROJ_TABLE``; shapes outside it: the gemm_sk planner). Epilogues as
+    :func:`gemm_sk`."""
+    M = x.shape[0]
+    N, K = w.shape
+    choice = None
+    for m_max, c in PROJ_TABLE.get((N, K), ()):
+        if M <= m_max:
+            choice = c
+            break
+    if choice is not None and choice[0] == "ws" and N % 128 == 0:
+        return gemm_ws(x, w, epi=epi, bias=bias, act=act, residual=residual, depth=choice[1])
+    if choice is not None and choice[0] == "sk" and N % SK_LAYOUTS[choice[1]][0] == 0:
+        return gemm_sk(x, w, epi=epi, bias=bias, act=act, residual=residual, layout=choice[1],
+                       splits=choice[2])
+    return gemm_sk(x, w, epi=epi, bias=bias, act=act, residual=residual)
