@@ -264,6 +264,30 @@ __device__ __forceinline__ void car_epoch_done(CarSignals* me, unsigned e, int n
 // vs W * Mpad * d * 2 for a one-shot bf16 sum - and f32 partials keep the
 // numerics of the single-GPU residual epilogue (one rounding).
 // rowsq_out gets W * nblk tiles: tile q * nblk + b = rank q's sub-slice b.
+// One row chunk of a residual all-reduce block: residual slice + the world
+// f32 partials in rank order (one bf16 rounding) and the sub-slice's row sum of
+// squares (fixed fma order, then a butterfly over the row's lanes). Shared by
+// the IPC kernel and its single-process emulation (tp_emul_resid_kernel), so
+// the emulation is bitwise the same arithmetic.
+__device__ __forceinline__ float car_resid_math(uint2 rv, const car_u32x4* v, int world, uint2& o) {
+  float acc[4] = {bf2f(rv.x & 0xffff), bf2f(rv.x >> 16), bf2f(rv.y & 0xffff), bf2f(rv.y >> 16)};
+#pragma unroll
+  for (int q = 0; q < CAR_MAX_WORLD; ++q) {
+    if (q >= world) break;
+    acc[0] += __uint_as_float(v[q].x); acc[1] += __uint_as_float(v[q].y);
+    acc[2] += __uint_as_float(v[q].z); acc[3] += __uint_as_float(v[q].w);
+  }
+  o.x = pack_bf16x2(acc[0], acc[1]);
+  o.y = pack_bf16x2(acc[2], acc[3]);
+  const float h0 = bf2f(o.x & 0xffff), h1 = bf2f(o.x >> 16), h2 = bf2f(o.y & 0xffff), h3 = bf2f(o.y >> 16);
+  return __builtin_fmaf(h3, h3, __builtin_fmaf(h2, h2, __builtin_fmaf(h1, h1, h0 * h0)));
+}
+
+__device__ __forceinline__ float car_row_butterfly(float sq, int vpr) {
+  for (int o = 1; o < vpr; o <<= 1) sq += __shfl_xor(sq, o, 64);
+  return sq;
+}
+
 __global__ __launch_bounds__(256) void car_resid_kernel(CarPeers peers, long long in_off, long long res_off,
                                                         long long st_off, bf16_t* __restrict__ residual,
                                                         float* __restrict__ rowsq_out, int Mpad, int d,
@@ -288,28 +312,18 @@ __global__ __launch_bounds__(256) void car_resid_kernel(CarPeers peers, long lon
       if (act) {
         const size_t el = (size_t)m * d + c0 + cv * 4;
         const uint2 rv = *reinterpret_cast<const uint2*>(residual + el);
-        float acc[4] = {bf2f(rv.x & 0xffff), bf2f(rv.x >> 16), bf2f(rv.y & 0xffff), bf2f(rv.y >> 16)};
         car_u32x4 v[CAR_MAX_WORLD];
 #pragma unroll
         for (int q = 0; q < CAR_MAX_WORLD; ++q)
           if (q < world)
             v[q] = __builtin_amdgcn_raw_buffer_load_b128(car_rsrc(peers.base[q] + in_off, in_bytes),
                                                          (unsigned)(el * 4), 0, CAR_SYS);
-#pragma unroll
-        for (int q = 0; q < CAR_MAX_WORLD; ++q) {
-          if (q >= world) break;
-          acc[0] += __uint_as_float(v[q].x); acc[1] += __uint_as_float(v[q].y);
-          acc[2] += __uint_as_float(v[q].z); acc[3] += __uint_as_float(v[q].w);
-        }
         uint2 o;
-        o.x = pack_bf16x2(acc[0], acc[1]);
-        o.y = pack_bf16x2(acc[2], acc[3]);
+        sq = car_resid_math(rv, v, world, o);
         *reinterpret_cast<uint2*>(residual + el) = o;
         *reinterpret_cast<uint2*>(rmine + el) = o;
-        const float h0 = bf2f(o.x & 0xffff), h1 = bf2f(o.x >> 16), h2 = bf2f(o.y & 0xffff), h3 = bf2f(o.y >> 16);
-        sq = h0 * h0 + h1 * h1 + h2 * h2 + h3 * h3;
       }
-      for (int o = 1; o < vpr; o <<= 1) sq += __shfl_xor(sq, o, 64);
+      sq = car_row_butterfly(sq, vpr);
       if (cv == 0 && act) {
         smine[(size_t)blk * Mpad + m] = sq;
         rowsq_out[((size_t)rank * nblk + blk) * Mpad + m] = sq;
@@ -399,6 +413,54 @@ __global__ __launch_bounds__(256) void car_argmax_kernel(CarPeers peers, long lo
   if (ld_sys(&me->error))
     for (int b = threadIdx.x; b < B; b += blockDim.x) out[b] = CAR_ERR_TOKEN;
   car_epoch_done(me, e, 1);
+}
+
+// Single-process emulation of a TP=world residual all-reduce (TP=1 runs the
+// W shard partials itself): block (q, b) does exactly what block b of rank q
+// does in phase 1 of car_resid_kernel, over plain loads of the W partials
+// [world][Mpad][d] f32, and writes the combined residual slice and the
+// statistics tile q * nblk + b. Phase 2 (the all-gather) has nothing to do in
+// one process.
+__global__ __launch_bounds__(256) void tp_emul_resid_kernel(const float* __restrict__ partials,
+                                                            bf16_t* __restrict__ residual,
+                                                            float* __restrict__ rowsq_out, int Mpad, int d,
+                                                            int world, int nblk) {
+  const int q = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+  const int owned = d / world, cw = owned / nblk;
+  const int c0 = q * owned + blk * cw;
+  const int vpr = cw >> 2;
+  const int rpp = 256 / vpr, r0 = threadIdx.x / vpr, cv = threadIdx.x % vpr;
+  const size_t plane = (size_t)Mpad * d;
+  for (int m0 = 0; m0 < Mpad; m0 += rpp) {
+    const int m = m0 + r0;
+    const bool act = r0 < rpp && m < Mpad;
+    float sq = 0.f;
+    if (act) {
+      const size_t el = (size_t)m * d + c0 + cv * 4;
+      const uint2 rv = *reinterpret_cast<const uint2*>(residual + el);
+      car_u32x4 v[CAR_MAX_WORLD];
+#pragma unroll
+      for (int r = 0; r < CAR_MAX_WORLD; ++r)
+        if (r < world) v[r] = *reinterpret_cast<const car_u32x4*>(partials + r * plane + el);
+      uint2 o;
+      sq = car_resid_math(rv, v, world, o);
+      *reinterpret_cast<uint2*>(residual + el) = o;
+    }
+    sq = car_row_butterfly(sq, vpr);
+    if (cv == 0 && act) rowsq_out[((size_t)q * nblk + blk) * Mpad + m] = sq;
+  }
+}
+
+extern "C" int loqa_tp_emul_resid(const float* partials, void* residual, float* rowsq_out, int Mpad, int d,
+                                  int world, int nblk, hipStream_t s) {
+  if (world < 1 || world > CAR_MAX_WORLD || nblk < 1 || nblk > CAR_MAX_BLOCKS || d % (world * nblk) ||
+      Mpad < 1)
+    return (int)hipErrorInvalidValue;
+  const int cw = d / world / nblk, vpr = cw / 4;
+  if (cw % 8 || vpr > 64 || (vpr & (vpr - 1))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tp_emul_resid_kernel, dim3(world * nblk), dim3(256), 0, s, partials, (bf16_t*)residual,
+                     rowsq_out, Mpad, d, world, nblk);
+  return (int)hipGetLastError();
 }
 
 struct CarHandle {

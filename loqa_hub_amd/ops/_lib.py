@@ -154,6 +154,7 @@ _CAR_SIGS = {
     "loqa_car_error": ([c_void_p], c_int),
     "loqa_car_clear_error": ([c_void_p], c_int),
     "loqa_car_fill_inbuf": ([c_void_p, c_int, c_void_p, c_ll, c_void_p], c_int),
+    "loqa_tp_emul_resid": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p], c_int),
     "loqa_car_destroy": ([c_void_p], None),
 }
 

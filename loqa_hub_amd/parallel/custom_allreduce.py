@@ -61,27 +61,43 @@ ERR_TOKEN = -2            # argmax output of a step whose collectives failed
 MAX_TOKEN_ID = (1 << 17) - 1   # token ids carried by the argmax records
 
 
+def resid_blocks_for(d: int, world: int) -> int:
+    """Residual all-reduce workgroups per rank for width ``d`` at TP ``world``
+    (also the layout the TP emulation reproduces)."""
+    owned = d // world
+    for cw in (64, 32, 128, 16, 256, 8):
+        nb = owned // cw
+        if d % world == 0 and owned % cw == 0 and 1 <= nb <= 64:
+            return nb
+    raise ValueError(f"no residual all-reduce layout for d = {d}, world = {world}")
+
+
 class CustomAllReduce:
     # TP decode-step input buffers: up to 128 token rows x 8192 features f32
     DEFAULT_IN_BYTES = 128 * 8192 * 4
 
-    def __init__(self, group=None, slot_bytes: int = 16 << 20, in_bytes: int | None = None):
+    def __init__(self, group=None, slot_bytes: int = 16 << 20, in_bytes: int | None = None,
+                 solo: bool = False):
+        """``solo``: a one-rank handle with no process group (the single-GPU
+        timing of one TP rank's step, ``scripts/config5_projection.py``): every
+        collective runs the same kernel over this rank's buffers only."""
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        self.rank = 0 if solo else dist.get_rank(group)
+        self.world = 1 if solo else dist.get_world_size(group)
         self.slot_bytes = slot_bytes
         self.in_bytes = self.DEFAULT_IN_BYTES if in_bytes is None else in_bytes
         lib = _lib.kernels()
         self._h = lib.loqa_car_create(self.rank, self.world, slot_bytes, self.in_bytes)
         if not self._h:
             raise RuntimeError("custom all-reduce: staging allocation failed")
-        hs = lib.loqa_car_handle_size()
-        buf = ctypes.create_string_buffer(hs)
-        _lib.check(lib.loqa_car_handle(self._h, buf), "hipIpcGetMemHandle")
-        handles = [None] * self.world
-        dist.all_gather_object(handles, bytes(buf.raw), group=group)
-        blob = ctypes.create_string_buffer(b"".join(handles), hs * self.world)
-        _lib.check(lib.loqa_car_open(self._h, blob), "hipIpcOpenMemHandle")
+        if not solo:
+            hs = lib.loqa_car_handle_size()
+            buf = ctypes.create_string_buffer(hs)
+            _lib.check(lib.loqa_car_handle(self._h, buf), "hipIpcGetMemHandle")
+            handles = [None] * self.world
+            dist.all_gather_object(handles, bytes(buf.raw), group=group)
+            blob = ctypes.create_string_buffer(b"".join(handles), hs * self.world)
+            _lib.check(lib.loqa_car_open(self._h, blob), "hipIpcOpenMemHandle")
         self.device = torch.device("cuda", torch.cuda.current_device())
         self.calls = 0
         self.fallbacks = 0
@@ -127,12 +143,7 @@ class CustomAllReduce:
         """Workgroups per rank of ``resid``: each owns a sub-slice of 64
         features (16 f32x4 lanes per row) of this rank's d / world columns, at
         most 64 workgroups; the next norm reads world x blocks statistic tiles."""
-        owned = d // self.world
-        for cw in (64, 32, 128, 16, 256, 8):
-            nb = owned // cw
-            if d % self.world == 0 and owned % cw == 0 and 1 <= nb <= 64:
-                return nb
-        raise ValueError(f"no residual all-reduce layout for d = {d}, world = {self.world}")
+        return resid_blocks_for(d, self.world)
 
     def resid(self, which: int, residual: torch.Tensor, rowsq: torch.Tensor, nblk: int) -> None:
         """residual += sum over ranks of inbuf(which); row sums of squares ->

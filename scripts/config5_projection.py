@@ -1,0 +1,110 @@
+"""BASELINE config 5 (Llama-3-70B intent decoder at TP=8) projected from ONE
+MI355X: time one TP rank's decode step at its real shard shapes.
+
+The rank-0 shard of Llama-3-70B (qkv 8192 -> 1280, o 1024 -> 8192, gate|up
+8192 -> 7168, down 3584 -> 8192, lm_head 8192 -> 16032; the d = 8192 decode
+GEMMs tuned by the same contended tuner as serving) runs the fused TP decode
+step - 80 layers x (qkv, attention, o -> residual all-reduce, gate|up, down ->
+residual all-reduce), final norm, vocab-shard lm_head, argmax combine -
+graph-captured and replayed. The collectives run the real custom all-reduce
+kernels on a one-rank handle (``CustomAllReduce(solo=True)``): the same
+reduce / statistics / argmax work over local buffers, without the cross-GPU
+flag exchanges and xGMI reads. The projection adds those from a stated
+per-collective model (``--xgmi-us``), so the result is a range, not a claim.
+
+    python scripts/config5_projection.py [--batch 8] [--ctx 384] [--tokens 16]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-70b")
+    ap.add_argument("--tp", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=8, help="live sequences per step")
+    ap.add_argument("--tokens", type=int, default=16, help="padded token rows per step (Mpad)")
+    ap.add_argument("--ctx", type=int, default=384, help="context length of every sequence")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--layers", type=int, default=0, help="override layer count (0: the model's)")
+    ap.add_argument("--xgmi-us", default="3,6",
+                    help="extra latency per cross-GPU collective (low,high): flag exchange + xGMI reads")
+    a = ap.parse_args()
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import TPGroup
+    from loqa_hub_amd.parallel.custom_allreduce import CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = llama_config(a.model, **({"n_layers": a.layers} if a.layers else {}))
+    tp = TPGroup(0, a.tp, None, CustomAllReduce(solo=True))
+    t0 = time.perf_counter()
+    eng = LLMEngine(cfg, dev, max_seqs=max(8, a.batch), max_seq_len=max(512, a.ctx + 64), tp=tp,
+                    use_graphs=False)
+    t_init = time.perf_counter() - t0
+    # B sequences with `ctx` tokens of context, each feeding T / B tokens
+    per = max(1, a.tokens // a.batch)
+    reqs = [GenRequest(list(range(5, 5 + a.ctx - per)), []) for _ in range(a.batch)]
+    for r in reqs:
+        r.seq_id = eng._next_id
+        eng._next_id += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+        # claim the context's KV slots (contents do not matter for timing)
+        eng._meta([r], [r.prompt], decode=False)
+    feeds = [[7] * per for _ in reqs]
+    max_q, max_ctx, host = eng._meta(reqs, feeds, True, a.batch, a.tokens)
+    host["mask_rows"] = np.zeros(a.batch, np.int32)
+    d = eng._to_device(host)
+    meta = eng._build_meta(d, max_q, max_ctx, True)
+
+    def step():
+        logits = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+        return eng._tp_argmax(logits[: a.batch], d["mask_rows"])
+
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(a.iters):
+        g.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    step_ms = ev0.elapsed_time(ev1) / a.iters
+    L = cfg.n_layers
+    n_coll = 2 * L + 1
+    lo, hi = (float(v) for v in a.xgmi_us.split(","))
+    w = eng.weights
+    shard_bytes = sum(t.numel() * t.element_size() for P in w.decode_layers for t in P.values()
+                      if isinstance(t, torch.Tensor)) + w.lm_head_p.numel() * 2
+    out = {"model": cfg.name, "tp": a.tp, "rank_shard_weight_GB": round(shard_bytes / 1e9, 2),
+           "batch": a.batch, "token_rows": a.tokens, "ctx": a.ctx, "layers": L,
+           "rank_step_ms_local_collectives": round(step_ms, 3),
+           "rank_step_weight_TBps": round(shard_bytes / (step_ms * 1e-3) / 1e12, 2),
+           "collectives_per_step": n_coll, "xgmi_us_per_collective": [lo, hi],
+           "projected_step_ms": [round(step_ms + n_coll * lo / 1e3, 3), round(step_ms + n_coll * hi / 1e3, 3)],
+           "init_s": round(t_init, 1)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

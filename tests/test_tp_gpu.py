@@ -274,3 +274,101 @@ def test_tp_follower_hang_fails_over(tmp_path):
     assert len(res["fallback_outs"]) == 3
     for out, n in zip(res["fallback_outs"], (1, 3, 2)):
         assert len(json.loads(out)["commands"]) == n
+
+
+def _decode_teacher(meta_fn, fwd_fn, add_seq, steps: int = 10):
+    """Three sequences whose 24-token prompts go in through decode steps (8
+    tokens per sequence per step, the jump-forward row limit of Llama-3-8B's
+    GQA groups), then ``steps`` one-token steps of fixed tokens: the logits
+    of every step (per shard) - no prefill kernel involved."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest
+    reqs = [GenRequest(list(range(100 + 7 * i, 124 + 7 * i)), []) for i in range(3)]
+    for sid, r in enumerate(reqs, start=1):
+        r.seq_id = sid
+        add_seq(sid)
+    feeds_seq = [[r.prompt[c:c + 8] for r in reqs] for c in range(0, 24, 8)]
+    feeds_seq += [[[(1000 + 37 * t + 11 * i) % 120000] for i in range(3)] for t in range(steps)]
+    out = []
+    for feeds in feeds_seq:
+        T = sum(len(f) for f in feeds)
+        meta = meta_fn(reqs, feeds, 3, 16 if T <= 16 else 32)
+        out.append(fwd_fn(meta))
+    torch.cuda.synchronize()
+    return out
+
+
+def _bitwise_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOQA_NO_TUNE="1")
+    if world >= 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        from loqa_hub_amd.engine.llm_engine import LLMEngine
+        from loqa_hub_amd.models.configs import llama_config
+        from loqa_hub_amd.models.llama import TPGroup
+        cfg = llama_config("llama3-8b", n_layers=4)
+        tp = TPGroup.create(rank, world, dist.group.WORLD, device=dev)
+        eng = LLMEngine(cfg, dev, max_seqs=8, max_seq_len=512, tp=tp, seed=11, use_graphs=False)
+
+        def meta_fn(reqs, feeds, B, T):
+            max_q, max_ctx, host = eng._meta(reqs, feeds, True, B, T)
+            return eng._build_meta(eng._to_device(host), max_q, max_ctx, True)
+
+        def fwd(meta):
+            lg = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)[:3]
+            lgf = lg.float().contiguous()
+            tok = tp.car.argmax(lgf, lgf.argmax(1).to(torch.int32), rank * lgf.shape[1])
+            return lgf.cpu(), tok.cpu()
+        real = _decode_teacher(meta_fn, fwd, lambda sid: eng.kv.pool.add_seq(sid, []))
+        torch.save({"logits": [l for l, _ in real], "tokens": [t for _, t in real]},
+                   os.path.join(out_dir, f"real{world}_r{rank}.pt"))
+        dist.barrier()
+        if rank == 0:
+            from loqa_hub_amd.parallel.tp_emulation import TPEmulation
+            emu = TPEmulation(cfg, dev, world, seed=11, max_seqs=8, max_seq_len=512)
+
+            def emeta(reqs, feeds, B, T):
+                return emu.meta(reqs, feeds, B, T)[0]
+
+            def efwd(meta):
+                shards = [s[:3].float().contiguous() for s in emu.forward_decode_fused(meta)]
+                tok = TPEmulation.argmax_combine([s.cpu() for s in shards],
+                                                 [s.argmax(1).to(torch.int32).cpu() for s in shards])
+                return [s.cpu() for s in shards], tok
+            em = _decode_teacher(emeta, efwd, emu.add_seq)
+            torch.save({"logits": [l for l, _ in em], "tokens": [t for _, t in em]},
+                       os.path.join(out_dir, f"emu{world}.pt"))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+    sys.stdout.flush()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_decode_bitwise_equals_emulation(tmp_path, world):
+    """TP=W over the real IPC collectives (W processes sharing cuda:0) vs the
+    single-process TP emulation of the same W shards (parallel/tp_emulation.py):
+    every logit shard of every decode step and every combined greedy token is
+    BITWISE equal (replaces round 3's 2% / 90% tolerances)."""
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_bitwise_worker, args=(r, world, port, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    emu = torch.load(tmp_path / f"emu{world}.pt", weights_only=True)
+    for r in range(world):
+        real = torch.load(tmp_path / f"real{world}_r{r}.pt", weights_only=True)
+        for step, (a, b) in enumerate(zip(real["logits"], emu["logits"])):
+            assert torch.equal(a, b[r]), (world, r, step, (a - b[r]).abs().max().item())
+        for step, (a, b) in enumerate(zip(real["tokens"], emu["tokens"])):
+            assert torch.equal(a.to(torch.int32), b.to(torch.int32)), (world, r, step, a, b)
