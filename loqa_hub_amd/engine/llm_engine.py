@@ -23,7 +23,7 @@ import os
 import queue
 import threading
 import time
-from concurrent.futures import FIRST_COMPLETED, Future, ThreadPoolExecutor, wait
+from concurrent.futures import Future
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -84,9 +84,9 @@ class LLMEngine:
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.tp = tp or TPGroup()
-        from ..utils.streams import decode_cus, init_pools
+        from ..utils.streams import decode_cap, init_pools
         init_pools(self.device)       # fixed stream -> hardware-queue placement
-        self.max_wgs = decode_cus(self.device, "LOQA_LLM_CUS", "LOQA_LLM_MAX_WGS")
+        self.max_wgs = decode_cap("LOQA_LLM_MAX_WGS")
         with ops.decode_cap(self.max_wgs):
             self.weights = weights or LlamaWeights(cfg, self.device, seed=seed, tp=self.tp,
                                                    compact=compact)
@@ -159,42 +159,18 @@ class LLMEngine:
         # rank 0 publishes each scheduler iteration's arrivals, followers replay
         self.tp_ctl = None
         self._cells_lock = threading.Lock()
-        # prefill placement (continuous-batching scheduler). Serialised (default):
-        # the scheduler runs a step's new prompts on the decode stream between
-        # two decode steps, all arrivals of that boundary in ONE pass. Overlapped
-        # (LOQA_OVERLAP_PREFILL=1): a worker thread + stream runs them beside the
-        # decode steps. With distinct ~320-token prompts the overlapped prefill's
-        # hipBLASLt GEMMs slowed every concurrent decode step (4.1 -> 4.6 ms) and
-        # the Whisper decoder: 18.3-18.5 vs 17.9-18.0 utt/s serialised.
-        # Tensor parallel: every collective must be issued in the same order on
-        # every rank, so prefill stays on the decode stream (no overlap).
-        self.overlap_prefill = (self.is_gpu and self.tp.world == 1
-                                and os.environ.get("LOQA_OVERLAP_PREFILL", "0") == "1")
-        if self.overlap_prefill and self.pipelined:
-            # a pipelined step still in flight writes KV blocks that completion /
-            # misprediction already returned to the pool; only the decode stream's
-            # own order makes that safe, and an overlapped prefill on another
-            # stream could be handed those blocks - the two are exclusive
-            self.pipelined = False
-        # mixed steps (LOQA_MIXED_PREFILL=1): a serialised prefill also feeds
-        # every live sequence's next token. Opt-in: in the 8-stream bench it
-        # saves the prefill's wait behind in-flight steps but the pipeline
-        # drain costs as much (LLM thread time 10.51 vs 10.50 s, 19.0 vs
-        # 19.1 utt/s; docs/PERF.md)
-        self.mixed_prefill = (os.environ.get("LOQA_MIXED_PREFILL", "0") == "1"
-                              and not getattr(self.weights, "compact", False))
-        # prefill coalescing (serialised prefill): while a decode batch of at
-        # least ``hold_min_live`` sequences keeps the GPU busy, new prompts wait
-        # up to ``hold_ms`` (or until ``hold_tokens`` prompt tokens are waiting)
-        # so that several arrivals share ONE prefill pass - a pass streams every
-        # weight once (~16 GB for the 8B model) whatever its token count
-        self.hold_ms = float(os.environ.get("LOQA_PREFILL_HOLD_MS", "0"))
-        self.hold_tokens = int(os.environ.get("LOQA_PREFILL_HOLD_TOKENS", "1200"))
-        self.hold_min_live = int(os.environ.get("LOQA_PREFILL_HOLD_MIN_LIVE", "3"))
+        # prefill placement (continuous-batching scheduler): the scheduler runs
+        # a step boundary's new prompts on the decode stream between two decode
+        # steps, all arrivals of that boundary in ONE pass (serialised). Two
+        # measured alternatives lost and were removed in round 4 (docs/PERF.md):
+        # a prefill worker stream overlapped with the decode steps (its GEMMs
+        # slowed every concurrent step, 17.9-18.0 vs 18.3-18.5 utt/s) and mixed
+        # steps whose prefill pass also carried the live sequences' next tokens
+        # (the pipeline drain cost what the rider tokens saved).
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
-                      "host_post_s": 0.0, "replay_call_s": 0.0, "sched_s": 0.0, "mixed_riders": 0}
+                      "host_post_s": 0.0, "replay_call_s": 0.0, "sched_s": 0.0}
 
     # ------------------------------------------------------------- metadata
     def _meta(self, seqs: list[GenRequest], feeds: list[list[int]], decode: bool,
@@ -488,18 +464,10 @@ class LLMEngine:
                 continue  # long forced run split across steps: logits of this step unused
             self._commit(r, int(t), now)
 
-    def prefill(self, reqs: list[GenRequest], riders: list[GenRequest] | None = None) -> None:
-        """Run the prompts (chunked) and sample each sequence's first token.
-
-        ``riders``: live decoding sequences whose next feed (``feed``: the
-        sampled token plus any forced literal) joins the FIRST chunk - a mixed
-        step. The prefill's GEMMs are compute-bound at ~300 rows, so the extra
-        rows cost little, and each rider advances by one sampled token without
-        a decode step of its own (one whole weight pass saved per prefill)."""
+    def prefill(self, reqs: list[GenRequest]) -> None:
+        """Run the prompts (chunked) and sample each sequence's first token."""
         if getattr(self.weights, "compact", False):
-            assert not riders, "mixed steps need the hipBLASLt prefill path"
             return self._prefill_fused(reqs)
-        riders = [r for r in (riders or []) if r.feed and not r.done]
         i = 0
         while i < len(reqs):
             batch, T = [], 0
@@ -507,12 +475,6 @@ class LLMEngine:
                 batch.append(reqs[i])
                 T += len(reqs[i].feed)
                 i += 1
-            n_new = len(batch)
-            if riders:
-                batch += riders
-                self.stats["mixed_riders"] += len(riders)
-                self.stats["decode_tokens"] += sum(len(r.feed) for r in riders)
-                riders = []
             feeds = [r.feed for r in batch]
             max_q, max_ctx, host = self._meta(batch, feeds, decode=False)
             rows = np.array([r.grammar.mask_row() for r in batch], np.int32)
@@ -521,7 +483,7 @@ class LLMEngine:
             meta = self._build_meta(dev, max_q, max_ctx, False)
             nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
             self.stats["prefill_tokens"] += T
-            for r in batch[:n_new]:
+            for r in batch:
                 self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
             self._sample_and_advance(batch, nxt, time.perf_counter())
 
@@ -622,7 +584,6 @@ class LLMEngine:
         tune_switch_interval()
         self._inbox: queue.Queue = queue.Queue()
         self._running = True
-        stream_priority = int(os.environ.get("LOQA_LLM_PRIORITY", stream_priority))
         self._sched = threading.Thread(target=self._schedule, args=(stream_priority,),
                                        name="llm-scheduler", daemon=True)
         self._sched.start()
@@ -668,9 +629,9 @@ class LLMEngine:
     def _schedule(self, stream_priority: int) -> None:
         try:
             if self.is_gpu:
-                from ..utils.streams import stream_for
+                from ..utils.streams import placed_stream
                 torch.cuda.set_device(self.device)
-                torch.cuda.set_stream(stream_for(self.device, "LOQA_LLM_CUS", stream_priority))
+                torch.cuda.set_stream(placed_stream(self.device, "llm", stream_priority))
         except Exception as e:  # noqa: BLE001 - never leave submitters waiting
             self._fatal = e
             while True:
@@ -682,34 +643,25 @@ class LLMEngine:
                     it[2].set_exception(e)
         live: list[GenRequest] = []
         cells: dict[int, list] = {}   # id(cell) -> [remaining, future, reqs]
-        # prefills run on their own worker thread + stream, OVERLAPPED with the
-        # running decode batch (a new arrival no longer stalls every live
-        # sequence for a whole prefill pass); a request joins the decode batch
-        # at the first step boundary after its prefill completed (the worker
-        # synchronises on its first sampled token, so its KV writes are done)
-        pending: list[tuple[list[GenRequest], Future]] = []
         # inbox items not yet admitted: at most max_seqs sequences are live or
         # prefilling at once (the KV pool and the captured graph buckets are
         # sized for that many)
         waiting: list[tuple] = []
         cap = max(1, self.max_seqs)
-        held: list[GenRequest] = []     # admitted, waiting for a coalesced prefill pass
-        held_t0 = 0.0
-        pf_pool = self._prefill_executor() if self.overlap_prefill else None
         if self.pipelined:
             from .llm_pipeline import DecodePipeline
             self._pl = DecodePipeline(self)
         pl = self._pl
         t_end = 0.0
         while self._running:
-            idle = not live and not pending and not waiting and not held
+            idle = not live and not waiting
             items = self._next_items(idle)
             if items is None:          # TP follower: the leader stopped
                 break
             waiting += [it for it in items if it is not None]
             try:
                 new: list[GenRequest] = []
-                active = len(live) + len(held) + sum(len(r) for r, _ in pending)
+                active = len(live)
                 while waiting and active + len(new) + len(waiting[0][0]) <= cap:
                     reqs, cb, fut = waiting.pop(0)
                     if not reqs:
@@ -730,59 +682,14 @@ class LLMEngine:
                             pl.admit(r)
                     live += inl
                     new = [r for r in new if len(r.feed) > self.inline_prefill]
-                if self.hold_ms > 0 and pf_pool is None and self.tp_ctl is None:
-                    if new and not held:
-                        held_t0 = time.perf_counter()
-                    held += new
-                    new = []
-                    if held and (len(live) < self.hold_min_live
-                                 or sum(len(r.feed) for r in held) >= self.hold_tokens
-                                 or (time.perf_counter() - held_t0) * 1e3 >= self.hold_ms):
-                        new, held = held, []
-                        self.stats["prefill_passes_coalesced"] = (
-                            self.stats.get("prefill_passes_coalesced", 0) + (len(new) > 1))
                 if new:
-                    if pf_pool is not None:
-                        pending.append((new, pf_pool.submit(self._prefill_timed, new)))
-                    else:
-                        riders: list[GenRequest] = []
-                        if self.mixed_prefill and live:
-                            # mixed step: the live sequences' next feeds ride
-                            # along on the prefill pass (their in-flight
-                            # pipelined steps are retired first)
-                            if pl is not None:
-                                pl.drain()
-                                riders = [r for r in live if not r.done and r.pl_host]
-                                for r in riders:
-                                    r.feed, r.pl_host = list(r.pl_host), []
-                            else:
-                                riders = [r for r in live if not r.done and r.feed]
-                        self._prefill_timed(new, riders)
-                        if pl is not None:
-                            for r in riders:
-                                if not r.done:
-                                    r.pl_host = list(r.feed)
-                        live = [r for r in live if not r.done]
-                        joined = [r for r in new if not r.done]
-                        if pl is not None:
-                            for r in joined:
-                                pl.admit(r)
-                        live += joined
-                if pending:
-                    if not live:   # nothing to decode: wait for a prefill (or new work)
-                        wait([f for _, f in pending], timeout=0.002, return_when=FIRST_COMPLETED)
-                    still = []
-                    for reqs, f in pending:
-                        if f.done():
-                            f.result()                     # re-raise a prefill failure
-                            joined = [r for r in reqs if not r.done]
-                            if pl is not None:
-                                for r in joined:
-                                    pl.admit(r)
-                            live += joined
-                        else:
-                            still.append((reqs, f))
-                    pending = still
+                    self._prefill_timed(new)
+                    live = [r for r in live if not r.done]
+                    joined = [r for r in new if not r.done]
+                    if pl is not None:
+                        for r in joined:
+                            pl.admit(r)
+                    live += joined
                 if live:
                     t0 = time.perf_counter()
                     if t_end:
@@ -803,9 +710,8 @@ class LLMEngine:
                     log.error("%s", e)
                 else:
                     log.exception("LLM scheduler iteration failed")
-                # in-flight prefills / pipelined steps still write KV into their
-                # sequences' blocks: let them finish before the blocks go back
-                wait([f for _, f in pending])
+                # in-flight pipelined steps still write KV into their sequences'
+                # blocks: let them finish before the blocks go back
                 if pl is not None:
                     pl.abort()
                     self._free_seq_slots = list(range(self.max_seqs))
@@ -824,7 +730,7 @@ class LLMEngine:
                 for _, _, fut in waiting:
                     if not fut.done():
                         fut.set_exception(e)
-                live, pending, waiting, held = [], [], [], []
+                live, waiting = [], []
                 if self.tp_ctl is not None:
                     # lock-step TP: the ranks' scheduler states may now differ
                     # (this rank reset, the others did not), so the group
@@ -920,30 +826,13 @@ class LLMEngine:
         tune_switch_interval()
         self._inbox = queue.Queue()
         self._running = True
-        self._schedule(int(os.environ.get("LOQA_LLM_PRIORITY", stream_priority)))
+        self._schedule(stream_priority)
 
-    def _prefill_timed(self, reqs: list[GenRequest], riders: list[GenRequest] | None = None) -> None:
+    def _prefill_timed(self, reqs: list[GenRequest]) -> None:
         t0 = time.perf_counter()
-        self.prefill(reqs, riders)
+        self.prefill(reqs)
         self.stats["prefill_s"] += time.perf_counter() - t0
         self.stats["prefill_passes"] = self.stats.get("prefill_passes", 0) + 1
-
-    def _prefill_executor(self) -> ThreadPoolExecutor:
-        if getattr(self, "_pf_pool", None) is None:
-            dev = self.device
-
-            def init():
-                if dev.type == "cuda":
-                    from ..utils.streams import cu_masked_stream, parse_cu_spec, pool_stream
-                    torch.cuda.set_device(dev)
-                    spec = os.environ.get("LOQA_PREFILL_CUS", "")
-                    if spec:   # experiment: confine the overlapped prefill to a CU subset
-                        n = torch.cuda.get_device_properties(dev).multi_processor_count
-                        torch.cuda.set_stream(cu_masked_stream(dev, parse_cu_spec(spec, n)))
-                    else:
-                        torch.cuda.set_stream(pool_stream(dev, "prefill"))
-            self._pf_pool = ThreadPoolExecutor(1, thread_name_prefix="llm-prefill", initializer=init)
-        return self._pf_pool
 
     def _completion(self, cb, cell, cells):
         def done(r: GenRequest) -> None:   # scheduler or prefill thread

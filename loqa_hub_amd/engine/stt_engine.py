@@ -73,9 +73,9 @@ class STTEngine:
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        from ..utils.streams import decode_cus, init_pools
+        from ..utils.streams import decode_cap, init_pools
         init_pools(self.device)       # fixed stream -> hardware-queue placement
-        self.max_wgs = decode_cus(self.device, "LOQA_STT_CUS", "LOQA_STT_MAX_WGS")
+        self.max_wgs = decode_cap("LOQA_STT_MAX_WGS")
         # optional: tune the decode GEMMs under a background weight stream
         # (ops.contended_tuning; measured noisier and 5 % slower end to end)
         with ops.decode_cap(self.max_wgs), ops.contended_tuning(self.device, contended_tuning):
@@ -664,9 +664,9 @@ class STTEngine:
     def _schedule(self, stream_priority: int) -> None:
         try:
             if self.is_gpu:
-                from ..utils.streams import stream_for
+                from ..utils.streams import placed_stream
                 torch.cuda.set_device(self.device)
-                torch.cuda.set_stream(stream_for(self.device, "LOQA_STT_CUS", stream_priority))
+                torch.cuda.set_stream(placed_stream(self.device, "stt", stream_priority))
         except Exception as e:  # noqa: BLE001 - never leave submitters waiting
             self._fatal = e
             while True:
@@ -773,11 +773,8 @@ class STTEngine:
             dev = self.device
 
             def init():
-                from ..utils.streams import pool_stream
+                from ..utils.streams import placed_stream
                 torch.cuda.set_device(dev)
-                # LOQA_ENCODER_PRIORITY=-1: the encoder's workgroups are
-                # dispatched ahead of the decoders' (placement experiment)
-                prio = int(os.environ.get("LOQA_ENCODER_PRIORITY", "0"))
-                torch.cuda.set_stream(pool_stream(dev, "encoder", prio))
+                torch.cuda.set_stream(placed_stream(dev, "encoder"))
             self._enc_pool = ThreadPoolExecutor(1, thread_name_prefix="stt-encoder", initializer=init)
         return self._enc_pool

@@ -302,12 +302,6 @@ class LlamaWeights:
 
 PREFILL_DOWN_SPLITS = int(os.environ.get("LOQA_PREFILL_DOWN_SPLITS", "8"))
 PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
-# Prefill projections on the hand-written v2 prefill GEMM (decode copies of the
-# weights, csrc/kernels/gemm_prefill.hip) instead of hipBLASLt: qkv / o / down as
-# f32 split-K slabs summed by their consumer (RoPE + KV append, residual +
-# RMSNorm), gate|up with the SwiGLU epilogue in the GEMM. Split counts per
-# projection (qkv, o, down) for ~300-row prompts.
-PREFILL2 = os.environ.get("LOQA_PREFILL2", "0") != "0"
 # prompt passes on the split-K tiled GEMM (no f32 slabs): 1 every projection,
 # 2 only the residual projections o / down (qkv, gate|up on hipBLASLt)
 PREFILL3 = int(os.environ.get("LOQA_PREFILL3", "0"))
@@ -315,10 +309,6 @@ PREFILL3 = int(os.environ.get("LOQA_PREFILL3", "0"))
 
 def L0_KEYS(w) -> set:
     return set(w.layers[0]) if w.layers else set()
-# prefill gate|up on the v2 prefill GEMM with the SwiGLU epilogue (norm-folded
-# decode copy, unweighted norm in front) instead of hipBLASLt + silu_mul
-PREFILL_GU2 = os.environ.get("LOQA_PREFILL_GU2", "0") != "0"
-PREFILL2_SPLITS = tuple(int(v) for v in os.environ.get("LOQA_PREFILL2_SPLITS", "2,4,8").split(","))
 
 
 def _splitk_slabs(a: torch.Tensor, w: torch.Tensor, S: int) -> torch.Tensor:
@@ -371,9 +361,6 @@ class LlamaModel:
         if (PREFILL3 and x.is_cuda and tp.world == 1 and not meta.decode
                 and not getattr(w, "compact", False) and "wqkv" in L0_KEYS(w)):
             return self._forward_prefill3(meta, k_cache, v_cache, attn_ws, x, h)
-        if (PREFILL2 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 64
-                and not getattr(w, "compact", False) and "wqkv" in w.decode_layers[0]):
-            return self._forward_prefill2(meta, k_cache, v_cache, attn_ws, x, h)
         part = None
         for li, L in enumerate(w.layers):
             if li > 0:
@@ -390,20 +377,14 @@ class LlamaModel:
                                  grouped=meta.decode, split_keys=split_keys,
                                  num_splits=num_splits if meta.decode else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
-            gu2 = bool(S_o and PREFILL_GU2 and "w_gate_up_f" in w.decode_layers[li])
             if S_o:
                 # o projection on the hand-written prefill GEMM (decode copy
                 # of wo), split-K f32 slabs summed by the norm
                 part_o = ops.prefill_gemm2(attn, w.decode_layers[li]["wo"], S_o, epi="slabs")
-                h = ops.slab_rmsnorm(part_o, residual, self._ones(x) if gu2 else L["mlp_norm"],
-                                     cfg.norm_eps)
+                h = ops.slab_rmsnorm(part_o, residual, L["mlp_norm"], cfg.norm_eps)
             else:
                 o = tp.all_reduce_(ops.linear(attn, L["wo"]))
                 h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
-            if gu2:
-                a = ops.prefill_gemm2(h, w.decode_layers[li]["w_gate_up_f"], 1, epi="swiglu")
-                part = ops.prefill_gemm2(a, w.decode_layers[li]["w_down"], S_down, epi="slabs")
-                continue
             gu = ops.linear(h, L["w_gate_up"])
             if S_down:
                 a = ops.silu_mul(gu)
@@ -446,37 +427,6 @@ class LlamaModel:
                  else ops.proj(hn, L["w_gate_up"], epi="swiglu"))
             ops.proj(a, L["w_down"], epi="resid", residual=residual)
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
-
-    def _forward_prefill2(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:
-        """Prefill through the v2 prefill GEMM: per layer qkv slabs -> RoPE + KV
-        append (``slab_rope_append``) -> flash attention -> o slabs -> residual
-        + RMSNorm -> gate|up with the SwiGLU epilogue (norm-folded, pair-
-        permuted decode copy: the norm here is unweighted) -> down slabs ->
-        the next layer's residual + RMSNorm. Four GEMMs and four small kernels
-        per layer, every weight read once from the decode copies."""
-        cfg, w = self.cfg, self.w
-        H, Hkv, D = w.h, w.hkv, cfg.head_dim
-        s_qkv, s_o, s_down = PREFILL2_SPLITS
-        ones = self._ones(x)
-        residual = x
-        part = None
-        for li, L in enumerate(w.layers):
-            P = w.decode_layers[li]
-            if part is not None:
-                h = ops.slab_rmsnorm(part, residual, L["attn_norm"], cfg.norm_eps)
-            pq = ops.prefill_gemm2(h, P["wqkv"], s_qkv, epi="slabs")
-            q = ops.slab_rope_append(pq, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
-                                     H, Hkv, D)
-            attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
-                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
-                                 block_tables=meta.block_tables, grouped=False, split_keys=256,
-                                 num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
-            po = ops.prefill_gemm2(attn, P["wo"], s_o, epi="slabs")
-            hn = ops.slab_rmsnorm(po, residual, ones, cfg.norm_eps)
-            a = ops.prefill_gemm2(hn, P["w_gate_up_f"], 1, epi="swiglu")
-            part = ops.prefill_gemm2(a, P["w_down"], s_down, epi="slabs")
-        return ops.slab_rmsnorm(part, residual, w.final_norm, cfg.norm_eps,
-                                row_idx=meta.logit_idx, write_residual=False)
 
     def _ones(self, x: torch.Tensor) -> torch.Tensor:
         t = getattr(self, "_ones_d", None)

@@ -39,13 +39,9 @@ ENC_O_SPLITS = int(os.environ.get("LOQA_ENC_O_SPLITS", "2"))
 # LDS-tiled MFMA GEMM (csrc/kernels/gemm_tile.hip); 0: im2col + hipBLASLt
 ENC_TILE = int(os.environ.get("LOQA_ENC_TILE", "1"))
 ENC_FC2_SPLITS = int(os.environ.get("LOQA_ENC_FC2_SPLITS", "4"))
-# fc1 + bias + GELU as one tiled-GEMM launch (1: instead of hipBLASLt + gelu_bias)
-ENC_FC1_TILE = int(os.environ.get("LOQA_ENC_FC1_TILE", "0"))
 # cross-attention K|V of ALL decoder layers as one tiled-GEMM launch over the
 # layer-concatenated weights (0: one hipBLASLt GEMM per layer)
 XKV_TILE = int(os.environ.get("LOQA_XKV_TILE", "1"))
-# encoder qkv (+ bias) on the tiled GEMM (0: hipBLASLt)
-ENC_QKV_TILE = int(os.environ.get("LOQA_ENC_QKV_TILE", "0"))
 # every encoder projection on the split-K tiled GEMM (ops.gemm_sk)
 ENC_SK = int(os.environ.get("LOQA_ENC_SK", "0"))
 
@@ -233,10 +229,7 @@ class WhisperModel:
                                            bias=w.enc[i - 1]["fc2_b"])
                 else:
                     h = ops.layernorm(delta, L["ln1_w"], L["ln1_b"], 1e-5, residual=residual)
-            if tile and ENC_QKV_TILE:
-                qkv = ops.gemm_tile(h, L["wqkv"], bias=w.enc_qkv_bf[i], layout=0)
-            else:
-                qkv = ops.linear(h, L["wqkv"], L["bqkv"])
+            qkv = ops.linear(h, L["wqkv"], L["bqkv"])
             a = ops.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], cu, n_heads=H, n_kv=H, head_dim=D,
                               causal=False, max_q=T, cu_k=cu)
             if getattr(w, "enc_wo_p", None) is not None and (d // 64) % ENC_O_SPLITS == 0:
@@ -245,11 +238,8 @@ class WhisperModel:
             else:
                 o = ops.linear(a, L["wo"], L["bo"])
                 h = ops.layernorm(o, L["ln2_w"], L["ln2_b"], 1e-5, residual=residual)
-            if tile and ENC_FC1_TILE:
-                m = ops.gemm_tile(h, L["fc1"], bias=w.enc_fc1_bf[i], act="gelu", layout=0)
-            else:
-                m = ops.linear(h, L["fc1"], L["fc1_b"])
-                ops.gelu_bias_(m)
+            m = ops.linear(h, L["fc1"], L["fc1_b"])
+            ops.gelu_bias_(m)
             if S2:
                 # fc2 as split-K f32 slabs (hipBLASLt's N = 1280 tiles leave
                 # most CUs idle at 1500 rows), summed by the next LayerNorm

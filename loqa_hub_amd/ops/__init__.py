@@ -1141,12 +1141,11 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = 
                       head_dim=D)
         wide = Mpad <= 32 or prefill
         rts = (1, 2, 4) if (prefill and Mpad == 64) else (1, 2)
-        # XL layouts at Mpad 64 win in isolation but, as decode steps beside the
-        # Whisper decoder, took the pipeline from 17.6 to 10.3 utt/s (long-lived
-        # 4-wave workgroups: the co-scheduling cliff, docs/PERF.md): opt-in only
-        xl = "only" if Mpad == 128 else (
-            "also" if Mpad == 64 and xl_on and os.environ.get("LOQA_TUNE_XL64") == "1" else
-            "also" if Mpad == 32 and xl_on and os.environ.get("LOQA_TUNE_XL32") == "1" else "no")
+        # XL layouts only at Mpad 128: at Mpad 64 / 32 they win in isolation but,
+        # as decode steps beside the Whisper decoder, took the pipeline from 17.6
+        # to 10.3 utt/s (long-lived 4-wave workgroups: the co-scheduling cliff,
+        # docs/PERF.md)
+        xl = "only" if Mpad == 128 else "no"
         tune_fused_splits(key, lambda sp, rt, wr, i, xl_=0: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, xl=xl_, **kw), K, rts=rts,
             ncopies=len(copies), wr4=wide, fewest=wide, xl=xl)

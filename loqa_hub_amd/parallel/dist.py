@@ -48,13 +48,6 @@ def init_distributed(prefer_gpu: bool = True) -> DistInfo:
         local = 0
     use_gpu = prefer_gpu and torch.cuda.is_available()
     if use_gpu:
-        sched = os.environ.get("LOQA_HIP_SCHEDULE")   # experiment: spin | yield | block
-        if sched:
-            from ..utils.hip_runtime import hip_runtime
-            flag = {"spin": 1, "yield": 2, "block": 4}[sched]
-            # the HIP runtime torch already mapped (never a second copy by soname)
-            rc = hip_runtime().hipSetDeviceFlags(flag)
-            log.info("hipSetDeviceFlags(%s) -> %d", sched, rc)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

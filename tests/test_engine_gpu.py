@@ -75,40 +75,6 @@ def test_llm_pipelined_decode_gpu():
         assert len(json.loads(o)["commands"]) == n
 
 
-def test_llm_mixed_prefill_gpu(monkeypatch):
-    """Mixed steps on the GPU (the live sequences' feeds ride on a prefill pass
-    through hipBLASLt GEMMs and the split-KV prefill attention, after a drain
-    of the pipelined steps): every request completes with valid output and the
-    expected command count, the KV pool and sequence slots are all returned."""
-    import time as _t
-    monkeypatch.setenv("LOQA_MIXED_PREFILL", "1")
-    monkeypatch.setenv("LOQA_INLINE_PREFILL", "0")
-    cfg = llama_config("test-tiny")
-    eng = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
-    assert eng.mixed_prefill and eng.pipelined
-    n_list = [2, 3, 1, 4, 2, 1]
-    tok = eng.tok
-    reqs = [GenRequest(tok.encode(f"Voice command: turn on the lights {i}", bos=True),
-                       multi_command_schema(n, min_response_tokens=3)) for i, n in enumerate(n_list)]
-    eng.warmup_graphs()
-    eng.start()
-    try:
-        fa = eng.submit_batch(reqs[:3])
-        t0 = _t.time()
-        while not all(r.t_first for r in reqs[:3]) and _t.time() - t0 < 60:
-            _t.sleep(0.001)
-        fb = eng.submit_batch(reqs[3:])
-        fa.result(timeout=120)
-        fb.result(timeout=120)
-    finally:
-        eng.stop()
-    assert eng.stats["mixed_riders"] > 0
-    for r, n in zip(reqs, n_list):
-        assert len(json.loads(r.output)["commands"]) == n
-    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
-    assert sorted(eng._free_seq_slots) == list(range(8))
-
-
 def test_llm_gpu_matches_cpu_reference_first_tokens():
     cfg = llama_config("test-tiny")
     g = LLMEngine(cfg, "cuda", max_seqs=4, use_graphs=False)
@@ -281,33 +247,6 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     assert torch.isfinite(outs[8]).all() and rel < 4e-2, rel
 
 
-def test_llm_prefill2_matches_hipblaslt_gpu(monkeypatch):
-    """Prefill on the v2 hand-written GEMM (qkv / o / down slabs, SwiGLU
-    epilogue on the norm-folded gate|up copy) vs the hipBLASLt path: final
-    hidden rows of a 300-token prompt agree, and the KV cache rows written by
-    the two paths match."""
-    from loqa_hub_amd.models import llama as llama_mod
-    cfg = llama_config("tinyllama")
-    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
-    g = torch.Generator().manual_seed(1)
-    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
-    r = GenRequest(toks, multi_command_schema(1))
-    eng.submit(r)
-    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
-    dev = eng._to_device(host)
-    meta = eng._build_meta(dev, max_q, max_ctx, False)
-    outs, kvs = {}, {}
-    for on in (True, False):
-        monkeypatch.setattr(llama_mod, "PREFILL2", on)
-        outs[on] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
-        kvs[on] = (eng.kv.k[-1].float().clone(), eng.kv.v[-1].float().clone())
-    rel = float((outs[True] - outs[False]).norm() / outs[False].norm())
-    assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
-    for a, b in zip(kvs[True], kvs[False]):
-        assert float((a - b).norm() / b.norm()) < 4e-2
-
-
-@pytest.mark.parametrize("model", ["tinyllama", "llama3-8b"])
 def test_llm_prefill3_matches_hipblaslt_gpu(monkeypatch, model):
     """Prefill on the split-K tiled GEMM (qkv, o + residual, gate|up + SwiGLU,
     down + residual; in-launch K reduction) vs plain hipBLASLt GEMMs +
@@ -334,28 +273,6 @@ def test_llm_prefill3_matches_hipblaslt_gpu(monkeypatch, model):
     assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
     for a, b in zip(kvs[True], kvs[False]):
         assert float((a - b).norm() / b.norm()) < 4e-2
-
-
-def test_llm_prefill_gu2_matches_hipblaslt_gpu(monkeypatch):
-    """Prefill gate|up on the v2 GEMM's SwiGLU epilogue (norm-folded decode
-    copy behind an unweighted norm; LOQA_PREFILL_GU2) vs hipBLASLt + silu_mul:
-    the final hidden rows of a 300-token prompt agree."""
-    from loqa_hub_amd.models import llama as llama_mod
-    cfg = llama_config("tinyllama")
-    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=512, use_graphs=False)
-    g = torch.Generator().manual_seed(2)
-    toks = torch.randint(3, 30000, (300,), generator=g).tolist()
-    r = GenRequest(toks, multi_command_schema(1))
-    eng.submit(r)
-    max_q, max_ctx, host = eng._meta([r], [r.feed], decode=False)
-    dev = eng._to_device(host)
-    meta = eng._build_meta(dev, max_q, max_ctx, False)
-    outs = {}
-    for on in (True, False):
-        monkeypatch.setattr(llama_mod, "PREFILL_GU2", on)
-        outs[on] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
-    rel = float((outs[True] - outs[False]).norm() / outs[False].norm())
-    assert torch.isfinite(outs[True]).all() and rel < 4e-2, rel
 
 
 def _to_cpu(obj, seen=None):
@@ -497,11 +414,18 @@ def test_bench_dp2_shared_gpu():
     assert out["command_count_match_rate"] == 1.0
 
 
-def test_cu_masked_stream_gpu():
-    """A CU-masked stream made through torch's own HIP runtime runs work."""
-    from loqa_hub_amd.utils.streams import cu_masked_stream
+def test_placed_stream_slot_gpu():
+    """Every serving stream is the pool stream at its fixed slot, whatever
+    drew pool streams before it, and runs work."""
+    from loqa_hub_amd.utils.streams import DEFAULT_SLOTS, init_pools, placed_stream, pool_slot
     dev = torch.device("cuda", 0)
-    s = cu_masked_stream(dev, list(range(64)))
+    init_pools(dev)
+    for _ in range(5):
+        torch.cuda.Stream(dev)            # move the pool cursor
+    s = placed_stream(dev, "llm")
+    assert pool_slot(s, dev, 0) == DEFAULT_SLOTS["llm"]
+    h = placed_stream(dev, "stt", -1)
+    assert pool_slot(h, dev, -1) == DEFAULT_SLOTS["stt"]
     with torch.cuda.stream(s):
         x = torch.full((4096,), 2.0, device=dev)
         y = (x * x).sum()
