@@ -266,6 +266,9 @@ def run_hub_dp(args) -> int:
                     "phrases_per_s": round(ps["tts_phrases"] / max(elapsed, 1e-9), 2),
                     "audio_s_per_wall_s": round(ps["tts_samples"] / sr / max(elapsed, 1e-9), 2),
                     "gpu_s_per_audio_s": round(ps["tts_gpu_s"] / max(ps["tts_samples"] / sr, 1e-9), 4),
+                    "host_launch_ms_per_batch": round(1e3 * ps.get("tts_launch_s", 0.0)
+                                                      / max(ps.get("tts_batches", 1), 1), 3),
+                    "phrases_per_batch": round(ps["tts_phrases"] / max(ps.get("tts_batches", 1), 1), 2),
                     "note": "counters since start (warm-up included)"}
             if srv.streaming is not None:
                 hub_stats["streaming"] = srv.streaming.metrics.get_aggregate_metrics().to_json()

@@ -96,12 +96,17 @@ __device__ __forceinline__ float gauss(unsigned seed, unsigned long long idx) {
 }
 
 // stats [B][T][2C] (m_p | logs_p); cum [B][T] inclusive cumulative frame counts;
-// z [B][F][C]; frames past flen[b] are zero.
+// z [B][F][C]; frames past flen[b] are zero. The noise of (row, frame, channel)
+// does not depend on F, so a frame-padded (graph-bucketed) launch draws the
+// same latent as an exact one. seed_dev (optional): the seed read on the
+// device, so a captured graph draws fresh noise per replay.
 __global__ void expand_sample_kernel(const bf16_t* __restrict__ stats, int ld_stats,
                                      const int* __restrict__ cum, int T,
                                      const int* __restrict__ flen, bf16_t* __restrict__ z, int F,
-                                     int C, float noise_scale, unsigned seed) {
+                                     int C, float noise_scale, unsigned seed,
+                                     const unsigned* __restrict__ seed_dev) {
   const int f = blockIdx.x, b = blockIdx.y;
+  if (seed_dev) seed = *seed_dev;
   bf16_t* zr = z + ((size_t)b * F + f) * C;
   if (f >= flen[b]) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) zr[c] = f2bf(0.f);
@@ -116,16 +121,17 @@ __global__ void expand_sample_kernel(const bf16_t* __restrict__ stats, int ld_st
   const bf16_t* sr = stats + ((size_t)b * T + lo) * ld_stats;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float m = bf2f(sr[c]), lg = bf2f(sr[C + c]);
-    const unsigned long long idx = ((unsigned long long)b * F + f) * C + c;
+    const unsigned long long idx = (((unsigned long long)b << 24) + f) * C + c;
     zr[c] = f2bf(m + gauss(seed, idx) * __expf(lg) * noise_scale);
   }
 }
 
 extern "C" int loqa_expand_sample(const void* stats, int ld_stats, const int* cum, int B, int T,
                                   const int* flen, void* z, int F, int C, float noise_scale,
-                                  unsigned seed, hipStream_t s) {
+                                  unsigned seed, const unsigned* seed_dev, hipStream_t s) {
   if (B <= 0 || F <= 0) return 0;
+  if (F >= (1 << 24)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(expand_sample_kernel, dim3(F, B), dim3(128), 0, s, (const bf16_t*)stats,
-                     ld_stats, cum, T, flen, (bf16_t*)z, F, C, noise_scale, seed);
+                     ld_stats, cum, T, flen, (bf16_t*)z, F, C, noise_scale, seed, seed_dev);
   return (int)hipGetLastError();
 }

@@ -19,7 +19,7 @@ import torch
 
 from ..llm.tts import TTSOptions, TTSResult
 from ..models.configs import VitsConfig
-from ..models.vits import VitsModel, VitsWeights, text_to_ids
+from ..models.vits import VitsGraphRunner, VitsModel, VitsWeights, text_to_ids
 from ..utils.faults import faults
 
 
@@ -32,10 +32,14 @@ def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
 
 class VitsTTSEngine:
     def __init__(self, cfg: VitsConfig, device, *, seed: int = 0, batch_window: float = 0.003,
-                 max_batch: int = 32):
+                 max_batch: int = 32, use_graphs: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.model = VitsModel(VitsWeights(cfg, self.device, seed=seed))
+        # bucketed HIP-graph replay (models/vits.py VitsGraphRunner), built
+        # lazily on the placed TTS stream
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._runner: VitsGraphRunner | None = None
         self.batch_window = batch_window
         self.max_batch = max_batch
         self._pending: list[tuple[str, float, asyncio.Future]] = []
@@ -43,7 +47,7 @@ class VitsTTSEngine:
         self._gpu_lock = threading.Lock()
         self._stream = None            # the placed TTS stream (utils/streams.py), created lazily
         self._seed = seed
-        self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0}
+        self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0, "launch_s": 0.0}
 
     # ---------------------------------------------------------------- batch
     def synthesize_batch(self, texts: list[str], speeds: list[float] | None = None
@@ -61,11 +65,19 @@ class VitsTTSEngine:
         with self._gpu_lock, torch.inference_mode(), self._stream_ctx():
             t0 = time.perf_counter()
             self._seed += 1
-            pcm, n = self.model.synthesize(torch.from_numpy(arr).to(self.device), lens,
-                                           seed=self._seed, length_scale=ls)
+            if self.use_graphs and self._runner is None:
+                self._runner = VitsGraphRunner(self.model, self.device)
+            synth = self._runner.synthesize if self._runner is not None else self.model.synthesize
+            pcm, n = synth(torch.from_numpy(arr).to(self.device), lens, seed=self._seed,
+                           length_scale=ls)
+            t1 = time.perf_counter()
             pcm, n = pcm.cpu().numpy(), n.cpu().numpy()
-            self.stats["gpu_s"] += time.perf_counter() - t0   # launch to result on the host
+            t2 = time.perf_counter()
+            self.stats["gpu_s"] += t2 - t0       # launch to result on the host
+            self.stats["launch_s"] += t1 - t0    # host side: launches + the frame-count sync
         self.stats["batches"] += 1
+        if self._runner is not None:
+            self.stats.update({f"graph_{k}": v for k, v in self._runner.stats.items()})
         self.stats["phrases"] += len(texts)
         self.stats["samples"] += int(n.sum())
         return [pcm[b, : int(n[b])].copy() for b in range(len(texts))]

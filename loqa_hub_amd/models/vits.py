@@ -138,6 +138,7 @@ class VitsModel:
                                      cfg.window)
             y = ops.conv1d(a, L["o"], res=x, lens=lens)                       # x + attn
             x = ops.layernorm(y.view(-1, H), L["ln1_w"], L["ln1_b"], 1e-5).view_as(y)
+            x = x * mask          # the FFN conv reads its neighbours: padded rows zero
             f = ops.conv1d(x, L["ffn1"], act="relu", lens=lens)
             y = ops.conv1d(f, L["ffn2"], res=x, lens=lens)
             x = ops.layernorm(y.view(-1, H), L["ln2_w"], L["ln2_b"], 1e-5).view_as(y)
@@ -148,8 +149,10 @@ class VitsModel:
                   ) -> torch.Tensor:
         d = self.w.dp
         Fd = d["c1"].Cout
+        T = x.shape[1]
+        mask = (torch.arange(T, device=x.device)[None, :] < lens[:, None].long())[..., None]
         h = ops.conv1d(x, d["c1"], act="relu", lens=lens)
-        h = ops.layernorm(h.view(-1, Fd), d["ln1_w"], d["ln1_b"], 1e-5).view_as(h)
+        h = ops.layernorm(h.view(-1, Fd), d["ln1_w"], d["ln1_b"], 1e-5).view_as(h) * mask
         h = ops.conv1d(h, d["c2"], act="relu", lens=lens)
         h = ops.layernorm(h.view(-1, Fd), d["ln2_w"], d["ln2_b"], 1e-5).view_as(h)
         logw = ops.conv1d(h, d["proj"], lens=lens)[..., 0].float()
@@ -200,16 +203,133 @@ class VitsModel:
         return pcm[..., 0]
 
     # ---------------------------------------------------------------- full
-    def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
-                   length_scale: float = 1.0) -> tuple[torch.Tensor, torch.Tensor]:
-        """ids [B, T] -> (PCM16 [B, S], samples per utterance [B])."""
+    def text_phase(self, ids: torch.Tensor, lens: torch.Tensor, length_scale
+                   ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Text encoder + durations -> (stats, cum, flen); ``length_scale`` a
+        float or a device scalar (graph replay)."""
         stats, x = self.encode_text(ids, lens)
         dur = self.durations(x, lens, length_scale)
-        cum = torch.cumsum(dur, dim=1, dtype=torch.int32)
-        flen = cum[:, -1].contiguous()
-        F = int(flen.max().item())
-        z = ops.expand_sample(stats, cum.contiguous(), flen, F, self.NOISE_SCALE, seed)
+        cum = torch.cumsum(dur, dim=1, dtype=torch.int32).contiguous()
+        return stats, cum, cum[:, -1].contiguous()
+
+    def audio_phase(self, stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F: int,
+                    seed: int = 0, seed_dev: torch.Tensor | None = None) -> torch.Tensor:
+        """Prior sample over F frames + reverse flow + vocoder -> PCM16 [B, F * hop]."""
+        z = ops.expand_sample(stats, cum, flen, F, self.NOISE_SCALE, seed, seed_dev=seed_dev)
         z = self.flow_reverse(z, flen)
-        hop = int(math.prod(self.cfg.upsample_rates))
-        pcm = self.decode(z, (flen * hop).to(torch.int32))
-        return pcm, flen * hop
+        return self.decode(z, (flen * self.hop).to(torch.int32))
+
+    @property
+    def hop(self) -> int:
+        return int(math.prod(self.cfg.upsample_rates))
+
+    def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
+                   length_scale: float = 1.0, frame_step: int = 1
+                   ) -> tuple[torch.Tensor, torch.Tensor]:
+        """ids [B, T] -> (PCM16 [B, S], samples per utterance [B]). The frame
+        count is rounded up to ``frame_step`` (the graph runner's buckets)."""
+        stats, cum, flen = self.text_phase(ids, lens, length_scale)
+        F = int(flen.max().item())
+        F = -(-F // frame_step) * frame_step
+        return self.audio_phase(stats, cum, flen, F, seed), flen * self.hop
+
+
+class VitsGraphRunner:
+    """``VitsModel.synthesize`` as two HIP-graph replays per shape bucket.
+
+    The frame count is data-dependent (predicted durations), so a synthesis is
+    cut where the host must learn it: graph 1 (text encoder + durations) per
+    (batch, symbols) bucket, one host read of the longest frame count, then
+    graph 2 (prior sample + reverse flow + HiFi-GAN vocoder) per (batch,
+    symbols, frames) bucket. ~190 eager launches become 2 replays, so a phrase
+    batch holds the GIL for microseconds instead of milliseconds beside the
+    decoder schedulers. Padding is inert: every stage masks by ``lens`` /
+    ``flen``, rows are independent, and the prior noise of a frame does not
+    depend on the padded frame count, so a bucketed replay gives the rows of
+    the eager ``synthesize(..., frame_step=F_STEP)``. The seed and the length
+    scale are device scalars written before each replay. Buckets are captured
+    lazily into ONE memory pool; replays are serialised by the caller (the TTS
+    engine's GPU lock), every call runs graph 1 then graph 2 of the same
+    (batch, symbols) bucket, and graph 1's outputs stay alive, so no later
+    capture can hand out their memory."""
+    B_BUCKETS = (1, 2, 4, 8, 16, 32)
+    T_STEP = 64
+    F_STEP = 128
+
+    def __init__(self, model: VitsModel, device, *, max_symbols: int = 512, max_frames: int = 4096):
+        self.model = model
+        self.device = torch.device(device)
+        self.max_symbols = max_symbols
+        self.max_frames = max_frames
+        self.pool = torch.cuda.graph_pool_handle()
+        self._text: dict = {}
+        self._audio: dict = {}
+        self.stats = {"replays": 0, "captures": 0, "eager": 0}
+
+    def _bucket_b(self, B: int) -> int | None:
+        for b in self.B_BUCKETS:
+            if B <= b:
+                return b
+        return None
+
+    def _capture(self, fn):
+        st = torch.cuda.current_stream(self.device)
+        fn()                       # warm-up outside the graph (kernels, allocator)
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        # the placed TTS stream (never a new pool stream: utils/streams.py);
+        # thread-local capture: the decoder threads keep launching meanwhile
+        with torch.cuda.graph(g, pool=self.pool, stream=st, capture_error_mode="thread_local"):
+            out = fn()
+        self.stats["captures"] += 1
+        return g, out
+
+    def _text_graph(self, Bb: int, Tb: int):
+        ent = self._text.get((Bb, Tb))
+        if ent is None:
+            ids = torch.zeros(Bb, Tb, dtype=torch.int64, device=self.device)
+            lens = torch.ones(Bb, dtype=torch.int32, device=self.device)
+            ls = torch.ones(1, dtype=torch.float32, device=self.device)
+            g, out = self._capture(lambda: self.model.text_phase(ids, lens, ls))
+            ent = self._text[(Bb, Tb)] = (g, ids, lens, ls, out)
+        return ent
+
+    def _audio_graph(self, Bb: int, Tb: int, Fb: int, text_out):
+        ent = self._audio.get((Bb, Tb, Fb))
+        if ent is None:
+            seed = torch.zeros(1, dtype=torch.int32, device=self.device)
+            stats, cum, flen = text_out
+            g, pcm = self._capture(lambda: self.model.audio_phase(stats, cum, flen, Fb,
+                                                                  seed_dev=seed))
+            ent = self._audio[(Bb, Tb, Fb)] = (g, seed, pcm)
+        return ent
+
+    def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
+                   length_scale: float = 1.0) -> tuple[torch.Tensor, torch.Tensor]:
+        """As ``VitsModel.synthesize``; shapes outside the buckets run eagerly."""
+        B, T = ids.shape
+        Bb = self._bucket_b(B)
+        Tb = -(-T // self.T_STEP) * self.T_STEP
+        if Bb is None or Tb > self.max_symbols:
+            self.stats["eager"] += 1
+            return self.model.synthesize(ids, lens, seed=seed, length_scale=length_scale,
+                                         frame_step=self.F_STEP)
+        g1, s_ids, s_lens, s_ls, text_out = self._text_graph(Bb, Tb)
+        s_ids.zero_()
+        s_ids[:B, :T].copy_(ids)
+        s_lens.fill_(1)
+        s_lens[:B].copy_(lens)
+        s_ls.fill_(float(length_scale))
+        g1.replay()
+        stats, cum, flen = text_out
+        F = int(flen[:B].max().item())
+        Fb = -(-F // self.F_STEP) * self.F_STEP
+        if Fb > self.max_frames:
+            self.stats["eager"] += 1
+            pcm = self.model.audio_phase(stats[:B], cum[:B], flen[:B].contiguous(), Fb, seed)
+            return pcm, flen[:B] * self.model.hop
+        g2, s_seed, pcm = self._audio_graph(Bb, Tb, Fb, text_out)
+        s_seed.fill_(seed & 0x7FFFFFFF)
+        g2.replay()
+        self.stats["replays"] += 1
+        return pcm[:B], flen[:B] * self.model.hop

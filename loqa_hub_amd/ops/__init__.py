@@ -1008,8 +1008,10 @@ def relpos_attention(qkv: torch.Tensor, emb_k: torch.Tensor, emb_v: torch.Tensor
 
 
 def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F: int,
-                  noise_scale: float, seed: int = 0) -> torch.Tensor:
-    """Length regulation + prior sampling: [B, T, 2C] stats -> z_p [B, F, C] bf16."""
+                  noise_scale: float, seed: int = 0,
+                  seed_dev: torch.Tensor | None = None) -> torch.Tensor:
+    """Length regulation + prior sampling: [B, T, 2C] stats -> z_p [B, F, C] bf16.
+    ``seed_dev`` (GPU, int32 [1]): the seed read on the device (graph replay)."""
     B, T, C2 = stats.shape
     if not _gpu(stats):
         g = torch.Generator().manual_seed(seed)
@@ -1019,7 +1021,7 @@ def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F:
     z = torch.empty(B, F, C2 // 2, dtype=torch.bfloat16, device=stats.device)
     check(kernels().loqa_expand_sample(ptr(stats), stats.stride(1), ptr(cum), B, T, ptr(flen),
                                        ptr(z), F, C2 // 2, float(noise_scale), seed & 0xFFFFFFFF,
-                                       stream_ptr(stats)), "expand_sample")
+                                       ptr(seed_dev), stream_ptr(stats)), "expand_sample")
     return z
 
 

@@ -128,7 +128,7 @@ _KERNEL_SIGS = {
     "loqa_relpos_attention": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                               c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
     "loqa_expand_sample": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
-                           c_int, c_float, ctypes.c_uint, c_void_p],
+                           c_int, c_float, ctypes.c_uint, c_void_p, c_void_p],
     "loqa_slab_silu_mul": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_slab_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "loqa_step_fetch": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_engine_gpu.py tests/test_gemm_sk.py -k "prefill3 or encoder_sk" > gpurun_out/r4_g6_tests.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/r4_g6_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_engine_gpu.py tests/test_gemm_sk.py tests/test_kernels_gpu.py -k "prefill3 or encoder_sk or vits or expand" > gpurun_out/r4_g6_tests.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/r4_g6_tests.log; exit 1; }
 grep -E "passed|failed" gpurun_out/r4_g6_tests.log | tail -2
 ab() {  # name env...
   local name=$1; shift

