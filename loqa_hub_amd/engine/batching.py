@@ -20,13 +20,12 @@ than ``max_q``.
 """
 from __future__ import annotations
 
-import os
 import threading
 from concurrent.futures import Future
 
 # LLM decode steps: cap a step's tokens at a smaller padded-row bucket when
 # that samples more sequences per unit of step cost (plan_step_mpad)
-MPAD_PLAN = os.environ.get("LOQA_MPAD_PLAN", "1") != "0"
+MPAD_PLAN = True
 
 
 def join_futures(parts: list[Future], result) -> Future:

@@ -30,9 +30,9 @@ from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
 N_SAMPLES = 480000  # 30 s @ 16 kHz
-# numpy PCM of direct submissions staged through the pinned stager (0: a
+# numpy PCM of direct submissions staged through the pinned stager (False: a
 # one-off pinned tensor copy per request)
-PCM_STAGER = os.environ.get("LOQA_PCM_STAGER", "1") != "0"
+PCM_STAGER = True
 
 
 @dataclass(eq=False)
@@ -395,7 +395,7 @@ class STTEngine:
         return rslot
 
     # encoder graphs for batches of up to this many utterances (0: eager encoder)
-    ENC_GRAPH_MAX = int(os.environ.get("LOQA_ENC_GRAPH_MAX", "4"))
+    ENC_GRAPH_MAX = 4
 
     def _enc_graph(self, B: int) -> dict:
         """The Whisper encoder (log-mel -> conv stem -> all layers) for a batch
@@ -683,8 +683,9 @@ class STTEngine:
         # the encoder runs on its own worker thread + stream, overlapped with
         # the running decoder batch (an arrival's encode no longer stalls every
         # live transcription); requests join at the next step boundary after
-        # their encoder output and cross-attention K|V are complete
-        overlap = self.is_gpu and os.environ.get("LOQA_OVERLAP_ENCODER", "1") != "0"
+        # their encoder output and cross-attention K|V are complete (inline
+        # encodes measured 1.8x slower, docs/PERF.md)
+        overlap = self.is_gpu
         enc_pool = self._encoder_executor() if overlap else None
         pl = None
         if self.pipelined:

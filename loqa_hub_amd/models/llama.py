@@ -300,25 +300,14 @@ class LlamaWeights:
         return n * 2
 
 
-PREFILL_DOWN_SPLITS = int(os.environ.get("LOQA_PREFILL_DOWN_SPLITS", "8"))
-PREFILL_O_SPLITS = int(os.environ.get("LOQA_PREFILL_O_SPLITS", "4"))
-# prompt passes on the split-K tiled GEMM (no f32 slabs): 1 every projection,
-# 2 only the residual projections o / down (qkv, gate|up on hipBLASLt)
-PREFILL3 = int(os.environ.get("LOQA_PREFILL3", "0"))
+# prompt passes on the hand-written GEMMs (ops.proj: split-K tiled / weight-
+# streaming MFMA kernels with fused SwiGLU / residual epilogues); 0: hipBLASLt
+# (measured: 19.23 / 19.30 vs 19.15 / 18.99 utt/s, docs/PERF.md "Round 4")
+PREFILL_HW = os.environ.get("LOQA_PREFILL_HW", "1") != "0"
 
 
 def L0_KEYS(w) -> set:
     return set(w.layers[0]) if w.layers else set()
-
-
-def _splitk_slabs(a: torch.Tensor, w: torch.Tensor, S: int) -> torch.Tensor:
-    """a [T, K] @ w[N, K]^T as S split-K f32 slabs [S, T, N] (strided views, one
-    batched GEMM); the consumer (``ops.slab_rmsnorm``) sums them."""
-    T, K = a.shape
-    N = w.shape[0]
-    xs = a.view(T, S, K // S).transpose(0, 1)           # [S, T, K/S]
-    ws = w.view(N, S, K // S).permute(1, 2, 0)          # [S, K/S, N]
-    return torch.bmm(xs, ws, out_dtype=torch.float32)
 
 
 class LlamaModel:
@@ -348,26 +337,12 @@ class LlamaModel:
         h = ops.rmsnorm(x, w.layers[0]["attn_norm"], cfg.norm_eps)
         split_keys = 256
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
-        # down projection as split-K f32 slabs summed by the next norm (one
-        # strided-batched GEMM: hipBLASLt's best down tile count at ~300 rows
-        # leaves most CUs idle, PERF.md)
-        S_down = PREFILL_DOWN_SPLITS
-        if not (S_down > 0 and x.is_cuda and tp.world == 1 and not meta.decode and x.shape[0] >= 128
-                and w.f % S_down == 0):
-            S_down = 0
-        S_o = PREFILL_O_SPLITS if (S_down and PREFILL_O_SPLITS > 0 and hasattr(w, "decode_layers")
-                                   and (H * D) % (PREFILL_O_SPLITS * 128) == 0
-                                   and cfg.d_model % ops.PREFILL_GEMM_NT == 0) else 0
-        if (PREFILL3 and x.is_cuda and tp.world == 1 and not meta.decode
+        if (PREFILL_HW and x.is_cuda and tp.world == 1 and not meta.decode
                 and not getattr(w, "compact", False) and "wqkv" in L0_KEYS(w)):
-            return self._forward_prefill3(meta, k_cache, v_cache, attn_ws, x, h)
-        part = None
+            return self._forward_prefill_hw(meta, k_cache, v_cache, attn_ws, x, h)
         for li, L in enumerate(w.layers):
             if li > 0:
-                if part is not None:
-                    h = ops.slab_rmsnorm(part, residual, L["attn_norm"], cfg.norm_eps)
-                else:
-                    h = ops.rmsnorm(mlp_out, L["attn_norm"], cfg.norm_eps, residual=residual)
+                h = ops.rmsnorm(mlp_out, L["attn_norm"], cfg.norm_eps, residual=residual)
             qkv = ops.linear(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
@@ -377,44 +352,31 @@ class LlamaModel:
                                  grouped=meta.decode, split_keys=split_keys,
                                  num_splits=num_splits if meta.decode else 1,
                                  workspace=attn_ws, max_k=meta.max_ctx)
-            if S_o:
-                # o projection on the hand-written prefill GEMM (decode copy
-                # of wo), split-K f32 slabs summed by the norm
-                part_o = ops.prefill_gemm2(attn, w.decode_layers[li]["wo"], S_o, epi="slabs")
-                h = ops.slab_rmsnorm(part_o, residual, L["mlp_norm"], cfg.norm_eps)
-            else:
-                o = tp.all_reduce_(ops.linear(attn, L["wo"]))
-                h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
+            o = tp.all_reduce_(ops.linear(attn, L["wo"]))
+            h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             gu = ops.linear(h, L["w_gate_up"])
-            if S_down:
-                a = ops.silu_mul(gu)
-                part = (ops.prefill_gemm2(a, w.decode_layers[li]["w_down"], S_down, epi="slabs")
-                        if S_o else _splitk_slabs(a, L["w_down"], S_down))
-                continue
             mlp_out = tp.all_reduce_(ops.linear(ops.silu_mul(gu), L["w_down"]))
-        if part is not None:
-            return ops.slab_rmsnorm(part, residual, w.final_norm, cfg.norm_eps,
-                                    row_idx=meta.logit_idx, write_residual=False)
         sel_res = residual.index_select(0, meta.logit_idx)
         sel_mlp = mlp_out.index_select(0, meta.logit_idx)
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
                            residual=sel_res.contiguous())
 
-    def _forward_prefill3(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h) -> torch.Tensor:
-        """Prompt pass on the split-K tiled GEMM (``ops.gemm_sk``: the K chunks
-        of a tile are summed in-launch, so no f32 slabs are written or
-        re-read): per layer qkv (bf16) -> RoPE + KV append -> flash attention
-        -> o added straight into the residual stream (one rounding) -> RMSNorm
-        -> gate|up with the SwiGLU epilogue -> down added into the residual ->
-        the next layer's RMSNorm. Every projection streams its row-major
-        weights once; no hipBLASLt call."""
+    def _forward_prefill_hw(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h
+                            ) -> torch.Tensor:
+        """Prompt pass on the hand-written GEMMs (``ops.proj``: per shape the
+        measured faster of the split-K tiled GEMM, whose K chunks are summed
+        in-launch, and the row-resident weight-streaming GEMM): per layer qkv
+        (bf16) -> RoPE + KV append -> flash attention -> o added straight into
+        the residual stream (one rounding) -> RMSNorm -> gate|up with the
+        SwiGLU epilogue -> down added into the residual -> the next layer's
+        RMSNorm. No hipBLASLt call, no f32 slab written or re-read."""
         cfg, w = self.cfg, self.w
         H, Hkv, D = w.h, w.hkv, cfg.head_dim
         residual = x.contiguous()
         for li, L in enumerate(w.layers):
             if li > 0:
                 h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
-            qkv = ops.linear(h, L["wqkv"]) if PREFILL3 == 2 else ops.proj(h, L["wqkv"])
+            qkv = ops.proj(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
             attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
@@ -423,8 +385,7 @@ class LlamaModel:
                                  num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
             ops.proj(attn, L["wo"], epi="resid", residual=residual)
             hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
-            a = (ops.silu_mul(ops.linear(hn, L["w_gate_up"])) if PREFILL3 == 2
-                 else ops.proj(hn, L["w_gate_up"], epi="swiglu"))
+            a = ops.proj(hn, L["w_gate_up"], epi="swiglu")
             ops.proj(a, L["w_down"], epi="resid", residual=residual)
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 

@@ -32,16 +32,17 @@ def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> tor
 
 DEC_PROJ = ("wqkv", "wo", "xq", "xo", "fc1", "fc2")
 
+# Measured choices (docs/PERF.md), module constants so tests can flip them:
 # split-K of the encoder o projection on the prefill GEMM (0: hipBLASLt)
-ENC_O_SPLITS = int(os.environ.get("LOQA_ENC_O_SPLITS", "2"))
+ENC_O_SPLITS = 2
 # conv stem (implicit-im2col conv1d with bias + GELU (+ positions) fused) and
 # the fc2 projection (split-K slabs summed by the next LayerNorm) on the
-# LDS-tiled MFMA GEMM (csrc/kernels/gemm_tile.hip); 0: im2col + hipBLASLt
-ENC_TILE = int(os.environ.get("LOQA_ENC_TILE", "1"))
-ENC_FC2_SPLITS = int(os.environ.get("LOQA_ENC_FC2_SPLITS", "4"))
+# LDS-tiled MFMA GEMM (csrc/kernels/gemm_tile.hip); False: im2col + hipBLASLt
+ENC_TILE = True
+ENC_FC2_SPLITS = 4
 # cross-attention K|V of ALL decoder layers as one tiled-GEMM launch over the
-# layer-concatenated weights (0: one hipBLASLt GEMM per layer)
-XKV_TILE = int(os.environ.get("LOQA_XKV_TILE", "1"))
+# layer-concatenated weights (False: one hipBLASLt GEMM per layer)
+XKV_TILE = True
 # every encoder projection on the split-K tiled GEMM (ops.gemm_sk)
 ENC_SK = int(os.environ.get("LOQA_ENC_SK", "0"))
 

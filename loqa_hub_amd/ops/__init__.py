@@ -435,8 +435,8 @@ MAX_DECODE_WGS = int(os.environ.get("LOQA_MAX_DECODE_WGS", "256"))
 # 1-GPU box - cannot time anything meaningful, and the timing dominates start-up)
 NO_TUNE = os.environ.get("LOQA_NO_TUNE", "0") == "1"
 # fused-GEMM decode steps: embedding + layer-0 row statistics in one launch and
-# the final norm gathering its logit rows itself (0: the unfused torch ops)
-FUSED_EMBED = os.environ.get("LOQA_FUSED_EMBED", "1") != "0"
+# the final norm gathering its logit rows itself (False: the unfused torch ops)
+FUSED_EMBED = True
 _CAP = [MAX_DECODE_WGS]   # active co-scheduling cap while tuning (see decode_cap)
 
 
@@ -1314,7 +1314,7 @@ PREFILL_GEMM_NT = 128     # features per workgroup of the default layout (3)
 PREFILL2_LAYOUTS = {0: (5, 4, 2), 1: (10, 4, 2), 2: (5, 2, 2), 3: (10, 2, 1), 4: (10, 4, 1)}
 # layout 3 (v1's 1 x 4 waves with the one-barrier pipeline) measured fastest on
 # every prefill / encoder shape (profiles/r3_prefill_gemm2_layouts.txt)
-PREFILL2_LAYOUT = int(os.environ.get("LOQA_PREFILL2_LAYOUT", "3"))
+PREFILL2_LAYOUT = 3
 
 
 def prefill_gemm2(x: torch.Tensor, wp: torch.Tensor, splits: int = 1, epi: str = "bf16",
@@ -1372,11 +1372,9 @@ _GT_ZEROS: dict = {}
 
 
 def gemm_tile_layout(M: int, N: int, K: int, epi: str = "bf16") -> int:
-    """Layout for a shape: ``LOQA_GT_LAYOUT`` if set, else the measured table
-    (scripts/exp/gemm_tile_bench.py, docs/PERF.md)."""
-    env = os.environ.get("LOQA_GT_LAYOUT")
-    if env:
-        return int(env)
+    """Layout for a shape: the measured best (layout 1 on every served shape,
+    scripts/exp/gemm_tile_bench.py, docs/PERF.md); callers pass ``layout=``
+    to force another."""
     return 1
 
 
@@ -1519,16 +1517,12 @@ SK_TABLE = {
 
 def gemm_sk_plan(M: int, N: int, K: int, epi: str = "bf16",
                  layouts=(0, 1, 2, 3, 4, 5)) -> tuple[int, int]:
-    """(layout, K chunks) for a shape: ``LOQA_SK=layout,S`` if set, the
-    measured table for the served shapes, else an analytic plan - the fewest
+    """(layout, K chunks) for a shape: the measured table for the served
+    shapes, else an analytic plan - the fewest
     MFMA-cycle rounds over the resident workgroup slots, counting padded rows
     and wave-tile efficiency, with at most 3 K chunks (each chunk's partial
     costs a write and a serial read in the reduction: 16 chunks measured up
     to 7x slower than 1)."""
-    env = os.environ.get("LOQA_SK")
-    if env:
-        lay, s = (int(v) for v in env.split(","))
-        return lay, s
     for m_max, lay, s in SK_TABLE.get((N, K), ()):
         if M <= m_max and N % SK_LAYOUTS[lay][0] == 0:
             return lay, s
@@ -1676,7 +1670,7 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
         raise TypeError("gemm_ws needs bf16 operands")
     if x.stride(1) != 1 or not w.is_contiguous() or N % 128 or K % 64:
         raise ValueError("gemm_ws needs K-contiguous operands, N % 128 == 0, K % 64 == 0")
-    depth = int(os.environ.get("LOQA_WS_DEPTH", "0")) if depth is None else depth
+    depth = 0 if depth is None else depth
     p = _lib.GemmWsParams()
     p.x, p.ldx, p.w = ptr(x), x.stride(0), ptr(w)
     p.M, p.N, p.K, p.epi = M, N, K, _WS_EPI[epi]
@@ -1708,9 +1702,12 @@ PROJ_TABLE = {
     (4096, 4096): [(900, ("sk", 4, 1)), (1 << 30, ("sk", 0, 1))],                         # o
     (28672, 4096): [(384, ("ws", 0)), (900, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],      # gate|up
     (4096, 14336): [(400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],   # down
-    (3840, 1280): [(2000, ("ws", 1)), (1 << 30, ("sk", 6, 1))],                           # enc qkv
+    # encoder qkv / fc1: gemm_ws is ~8% faster alone (24.2 / 25.8 vs 26.2 / 28.2
+    # us) but its long-lived 512-thread workgroups cost the concurrent decoders
+    # more than that (encoder on ws: 18.82 / 19.02 vs 19.15 / 18.99 utt/s)
+    (3840, 1280): [(2000, ("sk", 1, 1)), (1 << 30, ("sk", 6, 1))],                        # enc qkv
     (1280, 1280): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc o
-    (5120, 1280): [(2000, ("ws", 1)), (1 << 30, ("sk", 6, 1))],                           # enc fc1
+    (5120, 1280): [(2000, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],                        # enc fc1
     (1280, 5120): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc fc2
 }
 

@@ -56,12 +56,6 @@ def aligned_pool_stream(device: torch.device, priority: int, slot: int):
     raise RuntimeError("pool stream slot not found")
 
 
-def _log_slot(role: str, st, device, priority: int) -> None:
-    if os.environ.get("LOQA_LOG_STREAMS"):
-        print(f"[streams] {role}: priority {priority} pool slot {pool_slot(st, device, priority)}",
-              flush=True)
-
-
 # Explicit placement: every serving stream is the pool stream of a FIXED index
 # (its hardware queue follows from the index), whatever else drew pool streams
 # before. Defaults = the placement measured best (docs/PERF.md, "Stream
@@ -103,7 +97,6 @@ def placed_stream(device: torch.device, role: str, priority: int = 0):
         st = torch.cuda.Stream(device, priority=priority)
     else:
         st = aligned_pool_stream(device, priority, slot)
-    _log_slot(role, st, device, priority)
     return st
 
 
