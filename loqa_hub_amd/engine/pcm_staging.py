@@ -5,10 +5,11 @@ every chunk is appended, as raw bytes, into a pinned (``hipHostMalloc``) slot
 of the native ``PcmStager`` (``csrc/runtime/runtime.cpp``) the moment it
 arrives; at end of speech the STT engine moves the slot to HBM with one
 ``hipMemcpyAsync`` issued on the encoder's own stream (ordered before the
-log-mel kernel that reads it). A dedicated H2D stream is opt-in
-(``LOQA_STAGER_STREAM=1``): created lazily, after the serving streams, it would
-take the next hardware queue (stream placement: docs/PERF.md, "the 1.8x
-cliff"). Nothing converts the samples on the host: the
+log-mel kernel that reads it). A dedicated H2D stream (the native stager's
+``own_stream`` mode) measured 2-4% slower end to end (18.75 / 18.35 vs 19.11 /
+19.11 utt/s, docs/PERF.md "Round 4"): created after the serving streams it
+lands on an arbitrary hardware queue, and the copy needs the encoder's order
+anyway. Nothing converts the samples on the host: the
 reference's per-sample ``bytesToFloat32Array`` (``audio_service.go:1048-1101``)
 and WAV/HTTP round trip (``stt_client.go:365-398``) have no counterpart here -
 the f32 conversion is the fused ``pcm16_f32_pad`` kernel on the device.
@@ -20,7 +21,6 @@ still in flight.
 from __future__ import annotations
 
 import ctypes
-import os
 import threading
 
 import numpy as np
@@ -76,10 +76,9 @@ class PCMSlot:
 class PcmStager:
     """Pool of pinned PCM slots with an H2D stream (native ``PcmStager``)."""
 
-    def __init__(self, nslots: int = 64, cap_samples: int = 480000):
+    def __init__(self, nslots: int = 64, cap_samples: int = 480000, own_stream: bool = False):
         self.cap = cap_samples
-        own = int(os.environ.get("LOQA_STAGER_STREAM", "0") == "1")
-        self._h = _lib.runtime().loqa_stager_create(nslots, cap_samples, own)
+        self._h = _lib.runtime().loqa_stager_create(nslots, cap_samples, int(own_stream))
         if not self._h:
             raise RuntimeError("PCM stager: pinned allocation failed")
         self._lock = threading.Lock()

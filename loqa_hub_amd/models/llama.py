@@ -496,5 +496,18 @@ class LlamaModel:
                                max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        """Local vocab shard logits [B, V/tp] (bf16)."""
-        return ops.linear(hidden, self.w.lm_head)
+        """Local vocab shard logits [B, V/tp]. On the GPU the prompt pass's few
+        sampling rows go through the decode steps' weight-streaming lm_head
+        (pre-shuffled copy, rows padded to 16; f32 logits), not hipBLASLt."""
+        w = self.w
+        B = hidden.shape[0]
+        if (hidden.is_cuda and getattr(w, "lm_head_p", None) is not None
+                and B <= ops.MPADS[-1]):
+            Mpad = ops.mpad_for(B)
+            x = hidden
+            if Mpad != B:
+                x = torch.zeros(Mpad, hidden.shape[1], dtype=hidden.dtype, device=hidden.device)
+                x[:B] = hidden
+            return ops.skinny_gemm(x.contiguous(), w.lm_head_p, 1,
+                                   max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:B, :w.v]
+        return ops.linear(hidden, w.lm_head)

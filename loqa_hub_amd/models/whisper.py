@@ -43,8 +43,10 @@ ENC_FC2_SPLITS = 4
 # cross-attention K|V of ALL decoder layers as one tiled-GEMM launch over the
 # layer-concatenated weights (False: one hipBLASLt GEMM per layer)
 XKV_TILE = True
-# every encoder projection on the split-K tiled GEMM (ops.gemm_sk)
-ENC_SK = int(os.environ.get("LOQA_ENC_SK", "0"))
+# every encoder projection on the hand-written GEMMs (ops.proj: split-K tiled;
+# 19.26 / 19.10 vs 19.11 / 19.11 utt/s with qkv / fc1 on hipBLASLt,
+# docs/PERF.md "Round 4"); 0: hipBLASLt qkv / fc1, prefill GEMM v2 o
+ENC_SK = int(os.environ.get("LOQA_ENC_SK", "1"))
 
 
 class WhisperWeights:

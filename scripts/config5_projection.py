@@ -93,8 +93,12 @@ def main() -> int:
     n_coll = 2 * L + 1
     lo, hi = (float(v) for v in a.xgmi_us.split(","))
     w = eng.weights
-    shard_bytes = sum(t.numel() * t.element_size() for P in w.decode_layers for t in P.values()
-                      if isinstance(t, torch.Tensor)) + w.lm_head_p.numel() * 2
+    # the bytes one fused decode step streams: the norm-folded / row-permuted
+    # qkv and gate|up copies, o, down, the vocab-shard lm_head (decode_layers
+    # also holds the unfused qkv / gate|up copies, which the step never reads)
+    fused_keys = ("wqkv_f", "wo", "w_gate_up_f", "w_down")
+    shard_bytes = sum(P[k].numel() * P[k].element_size() for P in w.decode_layers
+                      for k in fused_keys) + w.lm_head_p.numel() * 2
     out = {"model": cfg.name, "tp": a.tp, "rank_shard_weight_GB": round(shard_bytes / 1e9, 2),
            "batch": a.batch, "token_rows": a.tokens, "ctx": a.ctx, "layers": L,
            "rank_step_ms_local_collectives": round(step_ms, 3),

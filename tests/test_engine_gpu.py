@@ -282,6 +282,25 @@ def test_llm_prefill_hw_matches_hipblaslt_gpu(monkeypatch, model):
         assert float((a - b).norm() / b.norm()) < 4e-2
 
 
+def test_prefill_logits_on_skinny_lm_head_gpu():
+    """The prompt pass's sampling rows go through the decode steps'
+    weight-streaming lm_head (no hipBLASLt): f32 logits agree with the bf16
+    hipBLASLt GEMM and give the same argmax."""
+    cfg = llama_config("tinyllama")
+    eng = LLMEngine(cfg, "cuda", max_seqs=2, max_seq_len=256, use_graphs=False)
+    w = eng.weights
+    for B in (1, 3, 16, 20):
+        h = torch.randn(B, cfg.d_model, device="cuda").bfloat16()
+        got = eng.model.logits(h).float()
+        ref = torch.nn.functional.linear(h, w.lm_head).float()
+        assert got.shape == ref.shape == (B, w.v)
+        rel = float((got - ref).norm() / ref.norm())
+        assert rel < 1e-2, (B, rel)
+        top2 = ref.topk(2, dim=-1).values
+        tie = (top2[:, 0] - top2[:, 1]) < 0.05 * ref.abs().max()
+        assert bool(((got.argmax(-1) == ref.argmax(-1)) | tie).all())
+
+
 def _to_cpu(obj, seen=None):
     """Deep copy of a weights object with every tensor on the CPU."""
     import copy

