@@ -38,6 +38,8 @@ struct ConvArgs {
   int cout_real;                                 // channels actually stored (gated: of the output)
 };
 
+#define CONV_U 8   // K slices per load group
+
 __device__ __forceinline__ float16v mfma32(const bf16x8& a, const bf16x8& b, const float16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -53,56 +55,106 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvArgs p) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
   if (t0 < p.Tq) {
+    // K slices s = tap * nC + c (16 input channels each), taken CONV_U at a
+    // time: every slice's x and w fragments of a group are requested before
+    // the group's first MFMA, so CONV_U x 2 16-byte loads per lane are in
+    // flight instead of one dependent pair per MFMA (the loop was load-latency
+    // bound: 2.4% MFMA busy, profiles/r4_pmc_vits.txt). Same slice order as a
+    // plain tap-major loop, so the sums are unchanged. Loads past the end are
+    // clamped to the last slice and their MFMAs skipped (wave-uniform).
     const int to = t0 + r;
+    const bool tv = to < p.Tq;
+    const int tbase = to * p.stride - p.pad;
+    const int nC = p.Cin >> 4, KC = p.K * nC;
     const bf16_t* wrow = p.w + (size_t)(co0 + r) * p.K * p.Cin + 8 * kh;
-    for (int tap = 0; tap < p.K; ++tap) {
-      const int ti = to * p.stride + tap * p.dil - p.pad;
-      const bool ok = to < p.Tq && ti >= 0 && ti < p.Tin;
-      const bf16_t* xr = xb + (size_t)(ok ? ti : 0) * p.ldx + 8 * kh;
-      const bf16_t* wr = wrow + (size_t)tap * p.Cin;
-      for (int c = 0; c < p.Cin; c += 16) {
-        uint4 av = ok ? *reinterpret_cast<const uint4*>(xr + c) : make_uint4(0, 0, 0, 0);
-        const uint4 bv = *reinterpret_cast<const uint4*>(wr + c);
+    const bf16_t* xcol = xb + 8 * kh;
+    for (int s0 = 0; s0 < KC; s0 += CONV_U) {
+      uint4 av[CONV_U], bv[CONV_U];
+#pragma unroll
+      for (int u = 0; u < CONV_U; ++u) {
+        const int sl = min(s0 + u, KC - 1);
+        const int tap = sl / nC, c = sl - tap * nC;
+        const int ti = tbase + tap * p.dil;
+        const bool ok = tv && ti >= 0 && ti < p.Tin;
+        const uint4 xv = *reinterpret_cast<const uint4*>(xcol + (size_t)(ok ? ti : 0) * p.ldx + 16 * c);
+        av[u] = ok ? xv : make_uint4(0, 0, 0, 0);
+        bv[u] = *reinterpret_cast<const uint4*>(wrow + (size_t)tap * p.Cin + 16 * c);
+      }
+#pragma unroll
+      for (int u = 0; u < CONV_U; ++u) {
+        if (s0 + u >= KC) break;          // wave-uniform
+        uint4 a = av[u];
         if (p.pre_act == 1) {
           float f[8];
-          unpack8(av, f);
+          unpack8(a, f);
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : f[j] * p.pre_slope;
-          av = pack8(f);
+          a = pack8(f);
         }
-        acc = mfma32(*reinterpret_cast<const bf16x8*>(&av), *reinterpret_cast<const bf16x8*>(&bv), acc);
+        acc = mfma32(*reinterpret_cast<const bf16x8*>(&a), *reinterpret_cast<const bf16x8*>(&bv[u]), acc);
       }
     }
   }
-  // epilogue: C[t][co], lane column co = co0 + (lane & 31), rows t over registers
+  // epilogue: C[t][co], lane column co = co0 + (lane & 31), rows t over registers.
+  // Two phases: every row's residual / accumulator element is requested first
+  // (clamped addresses, one wait), then the values are finished and stored -
+  // a load-use pair per row serialised 16 memory round trips per wave.
   const int co = co0 + r;
   const float bias = p.bias ? bf2f(p.bias[co]) : 0.f;
   const int vlen = p.lens ? p.lens[b] : p.Tout;
+  int oc = co;
+  bool lane_ok = true;
+  if (p.post_act == 3) {            // sigmoid half hands its value to the partner lane
+    lane_ok = !(r & 16);
+    oc = (co0 >> 1) + (r & 15);
+  }
+  lane_ok = lane_ok && oc < p.cout_real;
+  const int occ = lane_ok ? oc : 0;
+  float rv[16], cv[16];
+  int oix[16];
+  unsigned okm = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int trow = t0 + (j & 3) + 8 * (j >> 2) + 4 * kh;
+    const int oi = trow * p.ostride + p.ophase;
+    const bool ok = lane_ok && trow < p.Tq && oi >= 0 && oi < p.Tout;
+    okm |= (unsigned)ok << j;
+    oix[j] = ok ? oi : 0;
+    rv[j] = 0.f;
+    cv[j] = 0.f;
+  }
+  // one wave-uniform branch per operand around all 16 loads: no join point
+  // between a load and the next (a join makes the compiler drain vmcnt)
+  if (p.res) {
+    const bf16_t* rbase = p.res + (size_t)b * p.rb + occ;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rv[j] = bf2f(rbase[(size_t)oix[j] * p.ldr]);
+  }
+  if (p.acc) {
+    const bf16_t* abase = p.acc + (size_t)b * p.ab + occ;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) cv[j] = bf2f(abase[(size_t)oix[j] * p.lda]);
+  }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int trow = t0 + (j & 3) + 8 * (j >> 2) + 4 * kh;
     float v = acc[j] + bias;
     float partner = 0.f;
     if (p.post_act == 3) partner = __shfl_xor(v, 16, 64);
-    if (trow >= p.Tq) continue;
+    if (!((okm >> j) & 1)) continue;
     const int oi = trow * p.ostride + p.ophase;
-    if (oi < 0 || oi >= p.Tout) continue;
-    int oc = co;
     if (p.post_act == 1) {
       v = fmaxf(v, 0.f);
     } else if (p.post_act == 2) {
       v = tanhf(v);
     } else if (p.post_act == 3) {
-      if (r & 16) continue;  // sigmoid half: its value was handed to the partner lane
       // bf16-rounded operands, as the unfused model computes them
       const float a = bf2f(f2bf(v)), g = bf2f(f2bf(partner));
       v = tanhf(a) * (1.f / (1.f + __expf(-g)));
-      oc = (co0 >> 1) + (r & 15);
     }
-    if (oc >= p.cout_real) continue;
-    if (p.res) v += bf2f(p.res[(size_t)b * p.rb + (size_t)oi * p.ldr + oc]);
+    v += rv[j];
     v *= p.alpha;
-    if (p.acc) v += bf2f(p.acc[(size_t)b * p.ab + (size_t)oi * p.lda + oc]);
+    v += cv[j];
     if (oi >= vlen) v = 0.f;
     if (p.out_pcm16) {
       const float c = fminf(fmaxf(v, -1.f), 1.f);
