@@ -304,11 +304,7 @@ class LlamaWeights:
 # streaming MFMA kernels with fused SwiGLU / residual epilogues); 0: hipBLASLt
 # (measured: 19.23 / 19.30 vs 19.15 / 18.99 utt/s, docs/PERF.md "Round 4")
 PREFILL_HW = os.environ.get("LOQA_PREFILL_HW", "1") != "0"
-# o / down of the hand-written prompt pass as split-K f32 slabs of the
-# weight-streaming prefill GEMM (gemm_prefill.hip v2: weights read once, 4 / 8
-# K chunks fill the CUs at N = 4096), summed by the next norm (slab_rmsnorm);
-# 0: the split-K tiled GEMM adding into the residual in-launch
-PREFILL_SLABS = (4, 8) if os.environ.get("LOQA_PREFILL_SLABS", "1") != "0" else None
+
 
 
 def L0_KEYS(w) -> set:
@@ -374,23 +370,16 @@ class LlamaModel:
         (bf16) -> RoPE + KV append -> flash attention -> o added straight into
         the residual stream (one rounding) -> RMSNorm -> gate|up with the
         SwiGLU epilogue -> down added into the residual -> the next layer's
-        RMSNorm. No hipBLASLt call. With ``PREFILL_SLABS`` o and down run on
-        the weight-streaming prefill GEMM as f32 split-K slabs that the next
-        norm sums into the residual (``slab_rmsnorm``)."""
+        RMSNorm. No hipBLASLt call, no f32 slab written or re-read. (o / down
+        as prefill-GEMM f32 slabs summed by the next norm is 9% faster alone,
+        7.73 vs 8.46 ms per 318-token pass, but ~1% slower beside the
+        decoders: docs/PERF.md "Round 4".)"""
         cfg, w = self.cfg, self.w
         H, Hkv, D = w.h, w.hkv, cfg.head_dim
         residual = x.contiguous()
-        slabs = PREFILL_SLABS
-        if slabs is not None and not (getattr(w, "decode_layers", None)
-                                      and (H * D) % (slabs[0] * 64) == 0
-                                      and w.f % (slabs[1] * 64) == 0
-                                      and cfg.d_model % ops.PREFILL_GEMM_NT == 0):
-            slabs = None
-        part = None
         for li, L in enumerate(w.layers):
             if li > 0:
-                h = (ops.slab_rmsnorm(part, residual, L["attn_norm"], cfg.norm_eps)
-                     if part is not None else ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps))
+                h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
             qkv = ops.proj(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
@@ -398,20 +387,10 @@ class LlamaModel:
                                  head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
                                  block_tables=meta.block_tables, grouped=False, split_keys=256,
                                  num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
-            if slabs is not None:
-                part = ops.prefill_gemm2(attn, w.decode_layers[li]["wo"], slabs[0], epi="slabs")
-                hn = ops.slab_rmsnorm(part, residual, L["mlp_norm"], cfg.norm_eps)
-            else:
-                ops.proj(attn, L["wo"], epi="resid", residual=residual)
-                hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
+            ops.proj(attn, L["wo"], epi="resid", residual=residual)
+            hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
             a = ops.proj(hn, L["w_gate_up"], epi="swiglu")
-            if slabs is not None:
-                part = ops.prefill_gemm2(a, w.decode_layers[li]["w_down"], slabs[1], epi="slabs")
-            else:
-                ops.proj(a, L["w_down"], epi="resid", residual=residual)
-        if part is not None:
-            return ops.slab_rmsnorm(part, residual, w.final_norm, cfg.norm_eps,
-                                    row_idx=meta.logit_idx, write_residual=False)
+            ops.proj(a, L["w_down"], epi="resid", residual=residual)
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 
     def _ones(self, x: torch.Tensor) -> torch.Tensor:

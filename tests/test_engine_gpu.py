@@ -272,14 +272,11 @@ def test_llm_prefill_hw_matches_hipblaslt_gpu(monkeypatch, model):
     dev = eng._to_device(host)
     meta = eng._build_meta(dev, max_q, max_ctx, False)
     outs, kvs = {}, {}
-    # hand-written with o / down as prefill-GEMM f32 slabs (default), with o /
-    # down on the split-K tiled GEMM adding in-launch, and hipBLASLt
-    for key, on, slabs in (("slabs", True, (4, 8)), ("sk", True, None), ("blas", False, None)):
+    for key, on in (("hw", True), ("blas", False)):
         monkeypatch.setattr(llama_mod, "PREFILL_HW", on)
-        monkeypatch.setattr(llama_mod, "PREFILL_SLABS", slabs)
         outs[key] = eng.model.forward(meta, eng.kv.k, eng.kv.v, eng.attn_ws).float()
         kvs[key] = (eng.kv.k[-1].float().clone(), eng.kv.v[-1].float().clone())
-    for key in ("slabs", "sk"):
+    for key in ("hw",):
         rel = float((outs[key] - outs["blas"]).norm() / outs["blas"].norm())
         assert torch.isfinite(outs[key]).all() and rel < 4e-2, (key, rel)
         for a, b in zip(kvs[key], kvs["blas"]):
