@@ -122,6 +122,13 @@ class LLMEngine:
         # batch directly, its tail fed max_decode_q tokens per step (it shares
         # the decode steps' weight reads instead of a whole pass of its own)
         self.inline_prefill = int(os.environ.get("LOQA_INLINE_PREFILL", "64"))
+        # chunked prompt passes (0: off): while sequences are decoding, a new
+        # prompt goes in chunks of this many tokens, each chunk in ONE pass
+        # together with every live sequence's next feed (a mixed step: the
+        # chunk rides on the decode step's weight reads instead of stalling
+        # the live sequences for a whole prompt pass); with nothing decoding
+        # the whole prompt is one pass (_mixed_step)
+        self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "0"))
         # token budget of one decode step: every live sequence feeds its sampled
         # token plus a jump-forward literal, so without a cap 17+ sequences in a
         # forced run would exceed the fused GEMMs' row limit (ops.MPADS);
@@ -642,6 +649,7 @@ class LLMEngine:
                 if it is not None and not it[2].done():
                     it[2].set_exception(e)
         live: list[GenRequest] = []
+        prefilling: list[GenRequest] = []   # chunked prompts not yet through (chunk_prefill)
         cells: dict[int, list] = {}   # id(cell) -> [remaining, future, reqs]
         # inbox items not yet admitted: at most max_seqs sequences are live or
         # prefilling at once (the KV pool and the captured graph buckets are
@@ -654,14 +662,14 @@ class LLMEngine:
         pl = self._pl
         t_end = 0.0
         while self._running:
-            idle = not live and not waiting
+            idle = not live and not waiting and not prefilling
             items = self._next_items(idle)
             if items is None:          # TP follower: the leader stopped
                 break
             waiting += [it for it in items if it is not None]
             try:
                 new: list[GenRequest] = []
-                active = len(live)
+                active = len(live) + len(prefilling)
                 while waiting and active + len(new) + len(waiting[0][0]) <= cap:
                     reqs, cb, fut = waiting.pop(0)
                     if not reqs:
@@ -682,6 +690,11 @@ class LLMEngine:
                             pl.admit(r)
                     live += inl
                     new = [r for r in new if len(r.feed) > self.inline_prefill]
+                if new and self.chunk_prefill > 0:
+                    for r in new:
+                        r.chunk_total = len(r.feed)   # type: ignore[attr-defined]
+                    prefilling += new
+                    new = []
                 if new:
                     self._prefill_timed(new)
                     live = [r for r in live if not r.done]
@@ -690,7 +703,15 @@ class LLMEngine:
                         for r in joined:
                             pl.admit(r)
                     live += joined
-                if live:
+                if prefilling:
+                    t0 = time.perf_counter()
+                    live += self._mixed_step([r for r in live if not r.done], prefilling)
+                    prefilling = [r for r in prefilling
+                                  if not getattr(r, "chunk_done", False) and not r.done]
+                    live = [r for r in live if not r.done]
+                    t_end = time.perf_counter()
+                    self.stats["mixed_s"] = self.stats.get("mixed_s", 0.0) + t_end - t0
+                elif live:
                     t0 = time.perf_counter()
                     if t_end:
                         self.stats["sched_s"] += t0 - t_end   # loop work between steps
@@ -730,7 +751,7 @@ class LLMEngine:
                 for _, _, fut in waiting:
                     if not fut.done():
                         fut.set_exception(e)
-                live, waiting = [], []
+                live, waiting, prefilling = [], [], []
                 if self.tp_ctl is not None:
                     # lock-step TP: the ranks' scheduler states may now differ
                     # (this rank reset, the others did not), so the group
@@ -827,6 +848,69 @@ class LLMEngine:
         self._inbox = queue.Queue()
         self._running = True
         self._schedule(stream_priority)
+
+    def _mixed_step(self, live: list[GenRequest], prefilling: list[GenRequest]
+                    ) -> list[GenRequest]:
+        """One pass over every live sequence's whole next feed plus the next
+        chunk (``chunk_prefill`` tokens) of the waiting prompts, on the prompt
+        pass's hand-written GEMMs: the chunk shares the decode step's weight
+        reads. The live sequences sample as in a decode step; a prompt whose
+        last chunk went in samples its first token and joins. With no live
+        sequence the prompts go in whole (one pass). The pipelined decode is
+        drained first (its in-flight steps retired), so every feed is
+        host-known. Returns the requests that finished their prompt."""
+        pl = self._pl
+        if pl is not None:
+            pl.drain()
+            live = [r for r in live if not r.done]
+        rows: list[GenRequest] = []
+        feeds: list[list[int]] = []
+        kinds: list[int] = []          # 0 live sequence, 1 last prompt chunk, 2 prompt chunk
+        for r in live:
+            f = r.pl_host if pl is not None else r.feed   # type: ignore[attr-defined]
+            if f:
+                rows.append(r)
+                feeds.append(list(f))
+                kinds.append(0)
+        budget = self.chunk_prefill if rows else self.prefill_chunk
+        for r in prefilling:
+            if budget <= 0:
+                break
+            n = min(len(r.feed), budget)
+            rows.append(r)
+            feeds.append(r.feed[:n])
+            kinds.append(1 if n == len(r.feed) else 2)
+            budget -= n
+        max_q, max_ctx, host = self._meta(rows, feeds, decode=False)
+        host["mask_rows"] = np.array([r.grammar.mask_row() for r in rows], np.int32)
+        dev = self._to_device(host)
+        meta = self._build_meta(dev, max_q, max_ctx, False)
+        nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
+        now = time.perf_counter()
+        joined: list[GenRequest] = []
+        n_dec = 0
+        for r, f, k, t in zip(rows, feeds, kinds, nxt.tolist()):
+            if k == 2:                 # a prompt's inner chunk: logits unused
+                r.feed = r.feed[len(f):]
+                continue
+            if k == 1:                 # the prompt is in: first sampled token
+                r.feed = []
+                r.chunk_done = True    # type: ignore[attr-defined]
+                self.stats["prefill_tokens"] += r.chunk_total   # type: ignore[attr-defined]
+                self.kv.pool.cache_prefix(r.seq_id, r._prompt_full)  # type: ignore[attr-defined]
+                self._commit(r, int(t), now)
+                if not r.done:
+                    if pl is not None:
+                        pl.admit(r)
+                    joined.append(r)
+                continue
+            n_dec += len(f)
+            forced = self._commit(r, int(t), now)
+            if pl is not None and not r.done:
+                r.pl_host = [int(t)] + forced   # type: ignore[attr-defined]
+        self.stats["mixed_steps"] = self.stats.get("mixed_steps", 0) + 1
+        self.stats["decode_tokens"] += n_dec
+        return joined
 
     def _prefill_timed(self, reqs: list[GenRequest]) -> None:
         t0 = time.perf_counter()

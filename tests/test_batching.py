@@ -2,6 +2,7 @@
 schedulers (17+ sequences in a forced-literal run, or 33+ STT
 arrivals feeding their SOT prompt, used to exceed the fused GEMMs' row limit
 and fail every in-flight request)."""
+import json
 import numpy as np
 import pytest
 import torch
@@ -174,3 +175,45 @@ def test_llm_pipelined_decode_matches_cpu():
     assert got2 == ref
     assert eng2._pl.stats["pl_discard"] > 0
     assert sorted(eng2._free_seq_slots) == list(range(6))
+
+
+def _run_chunked(chunk: str, pipelined: bool, monkeypatch):
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    monkeypatch.setenv("LOQA_CHUNK_PREFILL", chunk)
+    monkeypatch.setenv("LOQA_INLINE_PREFILL", "0")     # every arrival takes a prompt pass
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=6,
+                    max_seq_len=512, use_graphs=False)
+    eng.pipelined = pipelined
+    texts = ["turn on the lights and play music", "dim the kitchen lights", "hello there",
+             "turn off the tv then lock the door", "what time is it", "play music"]
+    reqs = [GenRequest(eng.tok.encode(t, bos=True), multi_command_schema(n))
+            for t, n in zip(texts, (2, 1, 1, 3, 1, 4))]
+    import time as _t
+    try:
+        eng.start()
+        fa = eng.submit_batch(reqs[:3])
+        t0 = _t.time()
+        while not all(r.t_first for r in reqs[:3]) and _t.time() - t0 < 120:
+            _t.sleep(0.002)           # the first batch is decoding: the second is chunked in
+        fb = eng.submit_batch(reqs[3:])
+        fa.result(timeout=300)
+        fb.result(timeout=300)
+    finally:
+        eng.stop()
+    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
+    return [r.output for r in reqs], eng
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_llm_chunked_prefill_matches_cpu(pipelined, monkeypatch):
+    """Prompts arriving while others decode go in 5-token chunks, each chunk in
+    one pass with the live sequences' next feeds (mixed steps): the same
+    greedy outputs (and command counts) as whole prompt passes, the KV pool
+    fully returned."""
+    ref, _ = _run_chunked("0", pipelined, monkeypatch)
+    got, eng = _run_chunked("5", pipelined, monkeypatch)
+    assert eng.stats.get("mixed_steps", 0) >= 3
+    for a, b, n in zip(got, ref, (2, 1, 1, 3, 1, 4)):
+        assert len(json.loads(a)["commands"]) == n
+    assert got == ref

@@ -441,6 +441,40 @@ def test_bench_dp2_shared_gpu():
     assert out["command_count_match_rate"] == 1.0
 
 
+def test_llm_chunked_prefill_gpu(monkeypatch):
+    """Prompts arriving while others decode go in chunks, each chunk in one
+    pass with the live sequences' next feeds (hand-written prompt-pass GEMMs),
+    after a drain of the pipelined graph steps: every request completes with
+    the expected command count, KV blocks and sequence slots all returned."""
+    import time as _t
+    monkeypatch.setenv("LOQA_CHUNK_PREFILL", "16")
+    monkeypatch.setenv("LOQA_INLINE_PREFILL", "0")
+    cfg = llama_config("test-tiny")
+    eng = LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True)
+    assert eng.chunk_prefill == 16 and eng.pipelined
+    n_list = [2, 3, 1, 4, 2, 1]
+    tok = eng.tok
+    reqs = [GenRequest(tok.encode(f"Voice command: turn on the lights {i}", bos=True),
+                       multi_command_schema(n, min_response_tokens=3)) for i, n in enumerate(n_list)]
+    eng.warmup_graphs()
+    eng.start()
+    try:
+        fa = eng.submit_batch(reqs[:3])
+        t0 = _t.time()
+        while not all(r.t_first for r in reqs[:3]) and _t.time() - t0 < 60:
+            _t.sleep(0.001)
+        fb = eng.submit_batch(reqs[3:])
+        fa.result(timeout=120)
+        fb.result(timeout=120)
+    finally:
+        eng.stop()
+    assert eng.stats.get("mixed_steps", 0) > 0
+    for r, n in zip(reqs, n_list):
+        assert len(json.loads(r.output)["commands"]) == n
+    assert eng.kv.pool.free_blocks() == eng.kv.num_blocks
+    assert sorted(eng._free_seq_slots) == list(range(8))
+
+
 def test_placed_stream_slot_gpu():
     """Every serving stream is the pool stream at its fixed slot, whatever
     drew pool streams before it, and runs work."""
