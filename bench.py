@@ -556,6 +556,11 @@ def main(argv=None) -> int:
         "llm_prefill": round((llm.stats["prefill_s"] - s0["prefill_s"]) / args.steps * 1e3, 2),
         "llm_decode": round((llm.stats["decode_s"] - s0["decode_s"]) / args.steps * 1e3, 2),
         "llm_decode_steps": (llm.stats["decode_steps"] - s0["decode_steps"]) / args.steps,
+        # chunked prompt passes (LOQA_CHUNK_PREFILL): passes that carry prompt
+        # chunks together with the live sequences' next feeds
+        "llm_mixed": round((llm.stats.get("mixed_s", 0.0) - s0.get("mixed_s", 0.0))
+                           / args.steps * 1e3, 2),
+        "llm_mixed_steps": (llm.stats.get("mixed_steps", 0) - s0.get("mixed_steps", 0)) / args.steps,
     }
     recs = torch.cat(step.records, 0) if step.records else torch.zeros(0, 4)
     total_utts = info.world * B * args.steps

@@ -44,58 +44,10 @@ __device__ __forceinline__ float16v mfma32(const bf16x8& a, const bf16x8& b, con
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvArgs p) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.z;
-  const int t0 = (blockIdx.x * 4 + wave) * 32;   // first output step of this wave
-  const int co0 = blockIdx.y * 32;
+// Epilogue: C[t][co], lane column co = co0 + (lane & 31), rows t over registers.
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const float16v& acc, int b, int t0,
+                                              int co0, int lane) {
   const int r = lane & 31, kh = lane >> 5;
-  const bf16_t* xb = p.x + (size_t)b * p.xb;
-  float16v acc;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-  if (t0 < p.Tq) {
-    // K slices s = tap * nC + c (16 input channels each), taken CONV_U at a
-    // time: every slice's x and w fragments of a group are requested before
-    // the group's first MFMA, so CONV_U x 2 16-byte loads per lane are in
-    // flight instead of one dependent pair per MFMA (the loop was load-latency
-    // bound: 2.4% MFMA busy, profiles/r4_pmc_vits.txt). Same slice order as a
-    // plain tap-major loop, so the sums are unchanged. Loads past the end are
-    // clamped to the last slice and their MFMAs skipped (wave-uniform).
-    const int to = t0 + r;
-    const bool tv = to < p.Tq;
-    const int tbase = to * p.stride - p.pad;
-    const int nC = p.Cin >> 4, KC = p.K * nC;
-    const bf16_t* wrow = p.w + (size_t)(co0 + r) * p.K * p.Cin + 8 * kh;
-    const bf16_t* xcol = xb + 8 * kh;
-    for (int s0 = 0; s0 < KC; s0 += CONV_U) {
-      uint4 av[CONV_U], bv[CONV_U];
-#pragma unroll
-      for (int u = 0; u < CONV_U; ++u) {
-        const int sl = min(s0 + u, KC - 1);
-        const int tap = sl / nC, c = sl - tap * nC;
-        const int ti = tbase + tap * p.dil;
-        const bool ok = tv && ti >= 0 && ti < p.Tin;
-        const uint4 xv = *reinterpret_cast<const uint4*>(xcol + (size_t)(ok ? ti : 0) * p.ldx + 16 * c);
-        av[u] = ok ? xv : make_uint4(0, 0, 0, 0);
-        bv[u] = *reinterpret_cast<const uint4*>(wrow + (size_t)tap * p.Cin + 16 * c);
-      }
-#pragma unroll
-      for (int u = 0; u < CONV_U; ++u) {
-        if (s0 + u >= KC) break;          // wave-uniform
-        uint4 a = av[u];
-        if (p.pre_act == 1) {
-          float f[8];
-          unpack8(a, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : f[j] * p.pre_slope;
-          a = pack8(f);
-        }
-        acc = mfma32(*reinterpret_cast<const bf16x8*>(&a), *reinterpret_cast<const bf16x8*>(&bv[u]), acc);
-      }
-    }
-  }
-  // epilogue: C[t][co], lane column co = co0 + (lane & 31), rows t over registers.
   // Two phases: every row's residual / accumulator element is requested first
   // (clamped addresses, one wait), then the values are finished and stored -
   // a load-use pair per row serialised 16 memory round trips per wave.
@@ -166,6 +118,136 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvArgs p) {
   }
 }
 
+__global__ __launch_bounds__(256) void conv1d_mfma_kernel(ConvArgs p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.z;
+  const int t0 = (blockIdx.x * 4 + wave) * 32;   // first output step of this wave
+  const int co0 = blockIdx.y * 32;
+  const int r = lane & 31, kh = lane >> 5;
+  const bf16_t* xb = p.x + (size_t)b * p.xb;
+  float16v acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  if (t0 < p.Tq) {
+    // K slices s = tap * nC + c (16 input channels each), taken CONV_U at a
+    // time: every slice's x and w fragments of a group are requested before
+    // the group's first MFMA, so CONV_U x 2 16-byte loads per lane are in
+    // flight instead of one dependent pair per MFMA (the loop was load-latency
+    // bound: 2.4% MFMA busy, profiles/r4_pmc_vits.txt). Same slice order as a
+    // plain tap-major loop, so the sums are unchanged. Loads past the end are
+    // clamped to the last slice and their MFMAs skipped (wave-uniform).
+    const int to = t0 + r;
+    const bool tv = to < p.Tq;
+    const int tbase = to * p.stride - p.pad;
+    const int nC = p.Cin >> 4, KC = p.K * nC;
+    const bf16_t* wrow = p.w + (size_t)(co0 + r) * p.K * p.Cin + 8 * kh;
+    const bf16_t* xcol = xb + 8 * kh;
+    for (int s0 = 0; s0 < KC; s0 += CONV_U) {
+      uint4 av[CONV_U], bv[CONV_U];
+#pragma unroll
+      for (int u = 0; u < CONV_U; ++u) {
+        const int sl = min(s0 + u, KC - 1);
+        const int tap = sl / nC, c = sl - tap * nC;
+        const int ti = tbase + tap * p.dil;
+        const bool ok = tv && ti >= 0 && ti < p.Tin;
+        const uint4 xv = *reinterpret_cast<const uint4*>(xcol + (size_t)(ok ? ti : 0) * p.ldx + 16 * c);
+        av[u] = ok ? xv : make_uint4(0, 0, 0, 0);
+        bv[u] = *reinterpret_cast<const uint4*>(wrow + (size_t)tap * p.Cin + 16 * c);
+      }
+#pragma unroll
+      for (int u = 0; u < CONV_U; ++u) {
+        if (s0 + u >= KC) break;          // wave-uniform
+        uint4 a = av[u];
+        if (p.pre_act == 1) {
+          float f[8];
+          unpack8(a, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : f[j] * p.pre_slope;
+          a = pack8(f);
+        }
+        acc = mfma32(*reinterpret_cast<const bf16x8*>(&a), *reinterpret_cast<const bf16x8*>(&bv[u]), acc);
+      }
+    }
+  }
+  conv_epilogue(p, acc, b, t0, co0, lane);
+}
+
+// LDS-staged form for stride-1 convolutions (every VITS conv: the polyphase
+// transposed convolutions run stride 1 with an output stride): the workgroup's
+// 128 output steps need input rows [t0 - pad, t0 + 128 + (K - 1) * dil - pad)
+// of each CC-channel chunk, staged ONCE in LDS (pre-activation applied while
+// staging) and read by all 4 waves at every tap's shifted offset; the
+// 32 x K x CC weight slice is staged once too. The register form above re-reads
+// each input row K times per wave and the weights once per wave from L1 / L2
+// (~1 GB of operand traffic for one 76 800-row HiFi-GAN conv: 2.3% MFMA busy,
+// profiles/r4_pmc_vits.txt). Rows are padded by 16 B so a wave's 32 lanes,
+// reading 16 B each at a fixed row stride, do not all hit the same banks.
+// Same K-slice order (tap-major, then channel) as the register form.
+template <int CC>
+__global__ __launch_bounds__(256) void conv1d_lds_kernel(ConvArgs p) {
+  constexpr int XS = CC + 8;                     // padded row (bf16 elements)
+  constexpr int NC16 = CC / 16;
+  extern __shared__ __attribute__((aligned(16))) bf16_t conv_smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.z;
+  const int tw0 = blockIdx.x * 128;              // first output step of the workgroup
+  const int t0 = tw0 + wave * 32;                // this wave's
+  const int co0 = blockIdx.y * 32;
+  const int r = lane & 31, kh = lane >> 5;
+  const int R = 128 + (p.K - 1) * p.dil;         // staged input rows per chunk
+  bf16_t* xs = conv_smem;                        // [R][XS]
+  bf16_t* ws = conv_smem + (size_t)R * XS;       // [32 * K][XS]
+  const bf16_t* xb = p.x + (size_t)b * p.xb;
+  const int row0 = tw0 - p.pad;                  // input row of staged row 0
+  float16v acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int c0 = 0; c0 < p.Cin; c0 += CC) {
+    __syncthreads();                             // previous chunk's reads are done
+    // input rows: R x CC bf16 in 16-byte pieces, pre-activation applied here
+    for (int i = threadIdx.x; i < R * NC16 * 2; i += 256) {
+      const int row = i / (NC16 * 2), piece = i - row * (NC16 * 2);
+      const int ti = row0 + row;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ti >= 0 && ti < p.Tin) {
+        v = *reinterpret_cast<const uint4*>(xb + (size_t)ti * p.ldx + c0 + 8 * piece);
+        if (p.pre_act == 1) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : f[j] * p.pre_slope;
+          v = pack8(f);
+        }
+      }
+      *reinterpret_cast<uint4*>(xs + (size_t)row * XS + 8 * piece) = v;
+    }
+    // weights: 32 output channels x K taps x CC
+    for (int i = threadIdx.x; i < 32 * p.K * NC16 * 2; i += 256) {
+      const int rowk = i / (NC16 * 2), piece = i - rowk * (NC16 * 2);
+      const int co = rowk / p.K, tap = rowk - co * p.K;
+      const uint4 v = *reinterpret_cast<const uint4*>(
+          p.w + ((size_t)(co0 + co) * p.K + tap) * p.Cin + c0 + 8 * piece);
+      *reinterpret_cast<uint4*>(ws + (size_t)rowk * XS + 8 * piece) = v;
+    }
+    __syncthreads();
+    if (t0 < p.Tq) {
+      const bf16_t* xl = xs + (size_t)(wave * 32 + r) * XS + 8 * kh;
+      const bf16_t* wl = ws + (size_t)r * p.K * XS + 8 * kh;
+      for (int tap = 0; tap < p.K; ++tap) {
+        const bf16_t* xt = xl + (size_t)tap * p.dil * XS;
+        const bf16_t* wt = wl + (size_t)tap * XS;
+#pragma unroll
+        for (int c = 0; c < NC16; ++c) {
+          const uint4 av = *reinterpret_cast<const uint4*>(xt + 16 * c);
+          const uint4 bv = *reinterpret_cast<const uint4*>(wt + 16 * c);
+          acc = mfma32(*reinterpret_cast<const bf16x8*>(&av), *reinterpret_cast<const bf16x8*>(&bv), acc);
+        }
+      }
+    }
+  }
+  if (t0 < p.Tq) conv_epilogue(p, acc, b, t0, co0, lane);
+}
+
 extern "C" int loqa_conv1d(const void* x, long long xb, int ldx, const void* w, const void* bias,
                            void* y, long long yb, int ldy, const void* res, long long rb, int ldr,
                            const void* acc, long long ab, int lda, const int* lens, int B, int Tin,
@@ -182,6 +264,20 @@ extern "C" int loqa_conv1d(const void* x, long long xb, int ldx, const void* w, 
              K, dil, pad, stride, ostride, ophase, Tout, pre_act, pre_slope, post_act, alpha,
              out_pcm16, cout_real};
   dim3 grid((Tq + 127) / 128, Cout / 32, B);
+  if (stride == 1 && Cin % 32 == 0) {
+    // LDS form: 64-channel chunks when the staged rows + weight slice fit in
+    // 64 KiB (two workgroups per CU), else 32-channel chunks
+    const int R = 128 + (K - 1) * dil;
+    auto lds_of = [&](int cc) { return (size_t)(R + 32 * K) * (cc + 8) * sizeof(bf16_t); };
+    if (Cin % 64 == 0 && lds_of(64) <= 64 * 1024) {
+      hipLaunchKernelGGL(conv1d_lds_kernel<64>, grid, dim3(256), lds_of(64), s, p);
+      return (int)hipGetLastError();
+    }
+    if (lds_of(32) <= 64 * 1024) {
+      hipLaunchKernelGGL(conv1d_lds_kernel<32>, grid, dim3(256), lds_of(32), s, p);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL(conv1d_mfma_kernel, grid, dim3(256), 0, s, p);
   return (int)hipGetLastError();
 }

@@ -122,13 +122,15 @@ class LLMEngine:
         # batch directly, its tail fed max_decode_q tokens per step (it shares
         # the decode steps' weight reads instead of a whole pass of its own)
         self.inline_prefill = int(os.environ.get("LOQA_INLINE_PREFILL", "64"))
-        # chunked prompt passes (0: off): while sequences are decoding, a new
-        # prompt goes in chunks of this many tokens, each chunk in ONE pass
-        # together with every live sequence's next feed (a mixed step: the
-        # chunk rides on the decode step's weight reads instead of stalling
-        # the live sequences for a whole prompt pass); with nothing decoding
-        # the whole prompt is one pass (_mixed_step)
-        self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "0"))
+        # chunked prompt passes (0: whole-prompt passes between decode steps):
+        # while sequences are decoding, a new prompt goes in chunks of this many
+        # tokens, each chunk in ONE pass together with every live sequence's
+        # next feed (a mixed step: the live sequences advance during the prompt
+        # pass instead of stalling for it); with nothing decoding the whole
+        # prompt is one pass (_mixed_step). Measured (docs/PERF.md "Round 4"):
+        # 256 -> 19.49-19.64 vs 18.58-19.30 utt/s (4 interleaved pairs); 128
+        # loses (a pass costs 6.7 ms even at 32 rows, so more passes cost more)
+        self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "256"))
         # token budget of one decode step: every live sequence feeds its sampled
         # token plus a jump-forward literal, so without a cap 17+ sequences in a
         # forced run would exceed the fused GEMMs' row limit (ops.MPADS);

@@ -413,8 +413,12 @@ def test_llama_decode_fast_path_matches_generic():
 # ------------------------------------------------------------------ VITS kernels
 @pytest.mark.parametrize("Cin,Cout,K,dil,act,pre", [
     (192, 192, 5, 1, None, None), (64, 32, 7, 3, "relu", 0.1), (512, 256, 3, 1, "tanh", None),
-    (32, 1, 7, 1, "tanh", 0.01), (192, 384, 5, 1, "gated", None)])
+    (32, 1, 7, 1, "tanh", 0.01), (192, 384, 5, 1, "gated", None),
+    (128, 128, 11, 5, None, 0.1), (256, 256, 7, 3, None, 0.1)])
 def test_conv1d_mfma(Cin, Cout, K, dil, act, pre):
+    """Stride-1 convs run the LDS-staged kernel (64- or 32-channel chunks by
+    the 64 KiB budget: the K = 11, dil = 5 case takes 32) vs the fp32 torch
+    reference."""
     B, T = 2, 300
     w = torch.randn(Cout, Cin, K, device=DEV) * (Cin * K) ** -0.5
     b = torch.randn(Cout, device=DEV) * 0.1
