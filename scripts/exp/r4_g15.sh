@@ -3,6 +3,14 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 600 python -u scripts/exp/gemm_sk_bench.py --ms 64,128,192,256 --wms 1500 --grid --only qkv,o,gu,down > gpurun_out/r4_gemm_small_m.jsonl 2> gpurun_out/r4_gemm_small_m.err || { echo GRIDFAIL; tail -20 gpurun_out/r4_gemm_small_m.err; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/r4_gemm_small_m.jsonl"):
+    d = json.loads(l)
+    g = sorted(d["grid"].items(), key=lambda kv: kv[1])[:3]
+    print(f"{d['shape']:>5} M={d['M']:>4} blas={d['hipblaslt_us']:>6} plan{d['plan']}={d['plan_us']:>6} ws={d['ws_us']} best={g}")
+PY
 ab() {  # name env...
   local name=$1; shift
   env "$@" timeout -k 10 300 python bench.py --steps 40 --warmup 5 > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err || { echo "FAIL $name"; tail -20 gpurun_out/ab_$name.err; exit 1; }
