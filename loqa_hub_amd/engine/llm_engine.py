@@ -130,7 +130,7 @@ class LLMEngine:
         # prompt is one pass (_mixed_step). Measured (docs/PERF.md "Round 4"):
         # 256 -> 19.49-19.64 vs 18.58-19.30 utt/s (4 interleaved pairs); 128
         # loses (a pass costs 6.7 ms even at 32 rows, so more passes cost more)
-        self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "256"))
+        self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "320"))
         # token budget of one decode step: every live sequence feeds its sampled
         # token plus a jump-forward literal, so without a cap 17+ sequences in a
         # forced run would exceed the fused GEMMs' row limit (ops.MPADS);

@@ -1698,10 +1698,16 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
 # (scripts/exp/gemm_sk_bench.py --grid, cold weights; profiles/r4_gemm_proj_grid.txt):
 # ("sk", layout, K chunks) = gemm_sk, ("ws", depth) = gemm_ws.
 PROJ_TABLE = {
-    (6144, 4096): [(400, ("sk", 4, 1)), (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],     # Llama qkv
-    (4096, 4096): [(900, ("sk", 4, 1)), (1 << 30, ("sk", 0, 1))],                         # o
-    (28672, 4096): [(384, ("ws", 0)), (900, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],      # gate|up
-    (4096, 14336): [(400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],   # down
+    # the chunked prompt passes (LOQA_CHUNK_PREFILL) also run 64-256 rows:
+    # more K chunks fill the CUs there (profiles/r4_gemm_small_m.txt)
+    (6144, 4096): [(64, ("sk", 4, 4)), (128, ("sk", 4, 2)), (400, ("sk", 4, 1)),
+                   (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],                         # Llama qkv
+    (4096, 4096): [(128, ("sk", 4, 4)), (256, ("sk", 4, 2)), (900, ("sk", 4, 1)),
+                   (1 << 30, ("sk", 0, 1))],                                               # o
+    (28672, 4096): [(256, ("ws", 1)), (384, ("ws", 0)), (900, ("sk", 0, 1)),
+                    (1 << 30, ("sk", 6, 1))],                                              # gate|up
+    (4096, 14336): [(64, ("sk", 4, 8)), (128, ("sk", 5, 8)), (256, ("sk", 5, 4)),
+                    (400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],    # down
     # encoder qkv / fc1: gemm_ws is ~8% faster alone (24.2 / 25.8 vs 26.2 / 28.2
     # us) but its long-lived 512-thread workgroups cost the concurrent decoders
     # more than that (encoder on ws: 18.82 / 19.02 vs 19.15 / 18.99 utt/s)
@@ -1712,6 +1718,15 @@ PROJ_TABLE = {
 }
 
 
+# A/B switch for the small-row entries above (temporary)
+_PROJ_OLD = {
+    (6144, 4096): [(400, ("sk", 4, 1)), (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],
+    (4096, 4096): [(900, ("sk", 4, 1)), (1 << 30, ("sk", 0, 1))],
+    (28672, 4096): [(384, ("ws", 0)), (900, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],
+    (4096, 14336): [(400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],
+} if os.environ.get("LOQA_PROJ_SMALLM", "1") == "0" else None
+
+
 def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
          act: str | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
     """A prompt-pass projection on the fastest hand-written GEMM for its shape
@@ -1720,7 +1735,10 @@ def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Ten
     M = x.shape[0]
     N, K = w.shape
     choice = None
-    for m_max, c in PROJ_TABLE.get((N, K), ()):
+    table = PROJ_TABLE.get((N, K), ())
+    if _PROJ_OLD and (N, K) in _PROJ_OLD:
+        table = _PROJ_OLD[(N, K)]
+    for m_max, c in table:
         if M <= m_max:
             choice = c
             break
