@@ -128,8 +128,9 @@ class LLMEngine:
         # next feed (a mixed step: the live sequences advance during the prompt
         # pass instead of stalling for it); with nothing decoding the whole
         # prompt is one pass (_mixed_step). Measured (docs/PERF.md "Round 4"):
-        # 256 -> 19.49-19.64 vs 18.58-19.30 utt/s (4 interleaved pairs); 128
-        # loses (a pass costs 6.7 ms even at 32 rows, so more passes cost more)
+        # 256 -> 19.49-19.64 vs 18.58-19.30 utt/s (4 interleaved pairs); chunk
+        # sweep 192 / 256 / 320 / 384 / 512 -> 320 best; 128 loses (a pass is
+        # expensive at any row count, so more passes cost more)
         self.chunk_prefill = int(os.environ.get("LOQA_CHUNK_PREFILL", "320"))
         # token budget of one decode step: every live sequence feeds its sampled
         # token plus a jump-forward literal, so without a cap 17+ sequences in a

@@ -1699,7 +1699,9 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
 # ("sk", layout, K chunks) = gemm_sk, ("ws", depth) = gemm_ws.
 PROJ_TABLE = {
     # the chunked prompt passes (LOQA_CHUNK_PREFILL) also run 64-256 rows:
-    # more K chunks fill the CUs there (profiles/r4_gemm_small_m.txt)
+    # more K chunks fill the CUs there (profiles/r4_gemm_small_m.txt; a 32 /
+    # 128-row pass 4.81 / 6.33 vs 6.70 / 7.21 ms, headline neutral:
+    # profiles/r4_ab_proj_small_m.txt)
     (6144, 4096): [(64, ("sk", 4, 4)), (128, ("sk", 4, 2)), (400, ("sk", 4, 1)),
                    (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],                         # Llama qkv
     (4096, 4096): [(128, ("sk", 4, 4)), (256, ("sk", 4, 2)), (900, ("sk", 4, 1)),
@@ -1718,15 +1720,6 @@ PROJ_TABLE = {
 }
 
 
-# A/B switch for the small-row entries above (temporary)
-_PROJ_OLD = {
-    (6144, 4096): [(400, ("sk", 4, 1)), (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],
-    (4096, 4096): [(900, ("sk", 4, 1)), (1 << 30, ("sk", 0, 1))],
-    (28672, 4096): [(384, ("ws", 0)), (900, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],
-    (4096, 14336): [(400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],
-} if os.environ.get("LOQA_PROJ_SMALLM", "1") == "0" else None
-
-
 def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
          act: str | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
     """A prompt-pass projection on the fastest hand-written GEMM for its shape
@@ -1735,10 +1728,7 @@ def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Ten
     M = x.shape[0]
     N, K = w.shape
     choice = None
-    table = PROJ_TABLE.get((N, K), ())
-    if _PROJ_OLD and (N, K) in _PROJ_OLD:
-        table = _PROJ_OLD[(N, K)]
-    for m_max, c in table:
+    for m_max, c in PROJ_TABLE.get((N, K), ()):
         if M <= m_max:
             choice = c
             break
