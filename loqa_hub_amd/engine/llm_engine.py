@@ -169,14 +169,14 @@ class LLMEngine:
         # rank 0 publishes each scheduler iteration's arrivals, followers replay
         self.tp_ctl = None
         self._cells_lock = threading.Lock()
-        # prefill placement (continuous-batching scheduler): the scheduler runs
-        # a step boundary's new prompts on the decode stream between two decode
-        # steps, all arrivals of that boundary in ONE pass (serialised). Two
-        # measured alternatives lost and were removed in round 4 (docs/PERF.md):
-        # a prefill worker stream overlapped with the decode steps (its GEMMs
-        # slowed every concurrent step, 17.9-18.0 vs 18.3-18.5 utt/s) and mixed
-        # steps whose prefill pass also carried the live sequences' next tokens
-        # (the pipeline drain cost what the rider tokens saved).
+        # prompt placement (continuous-batching scheduler): prompt passes run on
+        # the decode stream, serialised with the decode steps; while sequences
+        # decode they are the chunked mixed steps above. Removed in round 4
+        # after measuring (docs/PERF.md): a prefill worker stream overlapped
+        # with the decode steps (its GEMMs slowed every concurrent step,
+        # 17.9-18.0 vs 18.3-18.5 utt/s), round 3's rider variant (one
+        # jump-forward slice per live sequence on a hipBLASLt pass: the drain
+        # cost what the riders saved) and coalescing holds.
         self.stats = {"prefill_tokens": 0, "decode_steps": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "prefix_hit_tokens": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "host_pre_s": 0.0, "gpu_wait_s": 0.0,
