@@ -255,16 +255,19 @@ class VitsGraphRunner:
     B_BUCKETS = (1, 2, 4, 8, 16, 32)
     T_STEP = 64
     F_STEP = 128
+    MAX_AUDIO_GRAPHS = 48      # least recently used audio graphs beyond this are dropped
 
     def __init__(self, model: VitsModel, device, *, max_symbols: int = 512, max_frames: int = 4096):
+        import collections
         self.model = model
         self.device = torch.device(device)
         self.max_symbols = max_symbols
         self.max_frames = max_frames
         self.pool = torch.cuda.graph_pool_handle()
         self._text: dict = {}
-        self._audio: dict = {}
-        self.stats = {"replays": 0, "captures": 0, "eager": 0}
+        # LRU: each audio graph keeps its PCM output (up to tens of MB) alive
+        self._audio: collections.OrderedDict = collections.OrderedDict()
+        self.stats = {"replays": 0, "captures": 0, "eager": 0, "evicted": 0}
 
     def _bucket_b(self, B: int) -> int | None:
         for b in self.B_BUCKETS:
@@ -295,13 +298,21 @@ class VitsGraphRunner:
         return ent
 
     def _audio_graph(self, Bb: int, Tb: int, Fb: int, text_out):
-        ent = self._audio.get((Bb, Tb, Fb))
+        key = (Bb, Tb, Fb)
+        ent = self._audio.get(key)
         if ent is None:
+            while len(self._audio) >= self.MAX_AUDIO_GRAPHS:
+                # the graph and its tensors go back to the shared pool; its text
+                # graph (whose outputs it reads) stays, text graphs are few
+                self._audio.popitem(last=False)
+                self.stats["evicted"] += 1
             seed = torch.zeros(1, dtype=torch.int32, device=self.device)
             stats, cum, flen = text_out
             g, pcm = self._capture(lambda: self.model.audio_phase(stats, cum, flen, Fb,
                                                                   seed_dev=seed))
-            ent = self._audio[(Bb, Tb, Fb)] = (g, seed, pcm)
+            ent = self._audio[key] = (g, seed, pcm)
+        else:
+            self._audio.move_to_end(key)
         return ent
 
     def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
