@@ -31,9 +31,11 @@ def _tp_engine(cfg):
     from ..parallel.tp_serving import build_tp_llm, init_tp
     g = cfg.gpu
     info = init_tp(g.tp)
-    eng = build_tp_llm(llama_config(g.llm_model), info, seed=g.seed, max_seqs=g.max_batch,
+    lcfg = llama_config(g.llm_model)
+    eng = build_tp_llm(lcfg, info, seed=g.seed, max_seqs=g.max_batch,
                        max_seq_len=g.max_seq_len, block_size=g.kv_block,
-                       use_graphs=g.use_graphs, checkpoint=g.llm_checkpoint)
+                       use_graphs=g.use_graphs, checkpoint=g.llm_checkpoint,
+                       tokenizer=g.tokenizer("llm", lcfg.vocab_size))
     return info, eng
 
 

@@ -206,6 +206,20 @@ class GPUConfig:
     tp_fallback_model: str = "llama3-8b"   # a failed TP group degrades to this ("none": off)
     stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
     llm_checkpoint: str = ""
+    # tokenizer.json of a checkpoint ("": the one in / beside the checkpoint;
+    # no checkpoint: the synthetic tokenizer of the random-init weights)
+    stt_tokenizer: str = ""
+    llm_tokenizer: str = ""
+
+    def tokenizer(self, which: str, vocab_size: int):
+        """The tokenizer for ``which`` ("stt" / "llm"): an explicit
+        ``HUB_*_TOKENIZER``, else the checkpoint's own file, else None."""
+        from .engine.tokenizer import find_tokenizer, load_tokenizer
+        explicit = getattr(self, f"{which}_tokenizer")
+        if explicit:
+            return load_tokenizer(explicit, vocab_size)
+        ckpt = getattr(self, f"{which}_checkpoint")
+        return load_tokenizer(ckpt, vocab_size) if find_tokenizer(ckpt) else None
 
 
 @dataclass
@@ -352,6 +366,8 @@ def load(env=None) -> Config:
             tp_fallback_model=env_str(e, "llama3-8b", "HUB_TP_FALLBACK_MODEL"),
             stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
             llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
+            stt_tokenizer=env_str(e, "", "HUB_STT_TOKENIZER"),
+            llm_tokenizer=env_str(e, "", "HUB_LLM_TOKENIZER"),
         ),
         arbitration=ArbitrationConfig(
             window=env_duration(e, 0.300, "ARBITRATION_WINDOW_DURATION"),

@@ -78,7 +78,7 @@ class LLMEngine:
                  max_seq_len: int = 1024, block_size: int = 16, num_blocks: int | None = None,
                  tp: TPGroup | None = None, use_graphs: bool = True, prefill_chunk: int = 8192,
                  weights: LlamaWeights | None = None, fused_decode: bool = True,
-                 compact: bool = False):
+                 compact: bool = False, tokenizer=None):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -92,7 +92,9 @@ class LLMEngine:
                                                    compact=compact)
         self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = LlamaModel(self.weights)
-        self.tok = get_tokenizer(cfg.vocab_size)
+        # a checkpoint's own tokenizer (tokenizer.HFTokenizer), else the
+        # synthetic one of the random-init weights
+        self.tok = tokenizer or get_tokenizer(cfg.vocab_size)
         self.grammar = GrammarTables(self.tok, self.device)
         from .grammar import INTENTS
         self.grammar.trie(INTENTS)

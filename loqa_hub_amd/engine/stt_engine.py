@@ -68,7 +68,7 @@ class STTEngine:
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
                  block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
                  fused: bool = True, weights: WhisperWeights | None = None,
-                 contended_tuning: bool = False):
+                 contended_tuning: bool = False, tokenizer=None):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -82,7 +82,7 @@ class STTEngine:
             self.weights = weights or WhisperWeights(cfg, self.device, seed=seed)
         self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = WhisperModel(self.weights)
-        self.tok = get_tokenizer(cfg.vocab_size)
+        self.tok = tokenizer or get_tokenizer(cfg.vocab_size)
         self.sot = [self.tok.token_id(s) for s in
                     ("<|startoftranscript|>", "<|en|>", "<|transcribe|>", "<|notimestamps|>")]
         self.eot = self.tok.token_id("<|endoftext|>")

@@ -167,3 +167,96 @@ class SyntheticTokenizer:
             b = t - self.byte_base
             return chr(b) if 32 <= b < 127 else ""
         return self.strings[t] if self.n_special <= t < self.n_real else ""
+
+
+# ---------------------------------------------------------------------------
+# Real checkpoints: the Hugging Face ``tokenizer.json`` shipped with them
+TOKENIZER_FILE = "tokenizer.json"
+_BOS_NAMES = ("<|begin_of_text|>", "<s>", "<|startoftext|>")
+_EOS_NAMES = ("<|end_of_text|>", "<|eot_id|>", "</s>", "<|endoftext|>")
+
+
+def find_tokenizer(path: str) -> str | None:
+    """``tokenizer.json`` for a checkpoint: ``path`` itself, or the file in
+    ``path`` (a checkpoint directory) or beside it (a single safetensors file)."""
+    import os
+    if not path:
+        return None
+    if os.path.isfile(path) and os.path.basename(path) == TOKENIZER_FILE:
+        return path
+    d = path if os.path.isdir(path) else os.path.dirname(os.path.abspath(path))
+    f = os.path.join(d, TOKENIZER_FILE)
+    return f if os.path.isfile(f) else None
+
+
+def load_tokenizer(path: str, vocab_size: int) -> "HFTokenizer":
+    f = find_tokenizer(path)
+    if f is None:
+        raise FileNotFoundError(f"no {TOKENIZER_FILE} at or beside {path!r}")
+    return HFTokenizer(f, vocab_size)
+
+
+class HFTokenizer:
+    """A checkpoint's own tokenizer (``tokenizers`` library, Rust; the file is
+    JSON: nothing in it executes) behind the interface the engines and the
+    grammar use (``SyntheticTokenizer``'s): ``encode`` / ``decode``,
+    ``token_id`` of a one-token string, and ``token_text`` - the exact text a
+    token adds after any other token. ``token_text`` is what the constrained
+    decoder concatenates into its JSON, so it must keep a SentencePiece
+    token's leading space that ``decode([t])`` alone would strip: every token
+    is decoded behind a fixed anchor token and the anchor's text is cut off.
+    Special / added tokens and ids past the file's vocabulary have no text
+    (the grammar never allows them)."""
+
+    def __init__(self, file: str, vocab_size: int):
+        from tokenizers import Tokenizer
+        self._t = Tokenizer.from_file(file)
+        n = self._t.get_vocab_size(with_added_tokens=True)
+        if n > vocab_size:
+            raise ValueError(f"{file}: {n} tokens exceed the model's vocabulary of {vocab_size}")
+        self.vocab_size = vocab_size
+        self.n_special = 0
+        self.n_real = n
+        self._added = {int(i): t for i, t in self._t.get_added_tokens_decoder().items()}
+        self.bos = next((i for i in map(self._t.token_to_id, _BOS_NAMES) if i is not None), None)
+        self.eos = next((i for i in map(self._t.token_to_id, _EOS_NAMES) if i is not None), None)
+        anchor = self._anchor()
+        a_text = self._t.decode([anchor], skip_special_tokens=False)
+        texts = self._t.decode_batch([[anchor, i] for i in range(n)], skip_special_tokens=False)
+        self._text = []
+        for i, s in enumerate(texts):
+            ok = i not in self._added and s.startswith(a_text) and "�" not in s
+            self._text.append(s[len(a_text):] if ok else "")
+        self._by_text: dict[str, int] = {}
+        for i in range(n - 1, -1, -1):      # lowest id wins
+            if self._text[i]:
+                self._by_text[self._text[i]] = i
+
+    def _anchor(self) -> int:
+        for s in ("a", "x", "the", "A"):
+            ids = self._t.encode(s, add_special_tokens=False).ids
+            if len(ids) == 1 and ids[0] not in self._added:
+                return ids[0]
+        return next(i for i in range(self._t.get_vocab_size()) if i not in self._added)
+
+    def token_id(self, s: str) -> int:
+        i = self._t.token_to_id(s)
+        if i is not None and (i in self._added or self._text[i] == s):
+            return i
+        ids = self._t.encode(s, add_special_tokens=False).ids
+        if len(ids) == 1 and self._text[ids[0]] == s:
+            return ids[0]
+        if s in self._by_text:
+            return self._by_text[s]
+        raise KeyError(f"{s!r} is not one token of this tokenizer")
+
+    def encode(self, text: str, bos: bool = False) -> list[int]:
+        ids = self._t.encode(text, add_special_tokens=False).ids
+        return ([self.bos] if bos and self.bos is not None else []) + ids
+
+    def decode(self, ids) -> str:
+        return self._t.decode([int(t) for t in ids if 0 <= int(t) < self.n_real],
+                              skip_special_tokens=True)
+
+    def token_text(self, t: int) -> str:
+        return self._text[t] if 0 <= t < self.n_real else ""

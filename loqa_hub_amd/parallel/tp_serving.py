@@ -59,7 +59,7 @@ def init_tp(tp: int) -> DistInfo:
 
 def build_tp_llm(lcfg, info: DistInfo, *, seed: int = 0, max_seqs: int = 64,
                  max_seq_len: int = 1024, block_size: int = 16, use_graphs: bool = True,
-                 compact: bool = False, checkpoint: str = ""):
+                 compact: bool = False, checkpoint: str = "", tokenizer=None):
     """This rank's engine of the TP group: custom all-reduce, Megatron shard of
     the seeded (or ``checkpoint``) weights, and the lock-step control ring."""
     from ..engine.llm_engine import LLMEngine
@@ -72,7 +72,7 @@ def build_tp_llm(lcfg, info: DistInfo, *, seed: int = 0, max_seqs: int = 64,
         weights = loader.load_llama(lcfg, checkpoint, info.device, tp=tp)
     eng = LLMEngine(lcfg, info.device, seed=seed, max_seqs=max_seqs, max_seq_len=max_seq_len,
                     block_size=block_size, tp=tp, use_graphs=use_graphs, weights=weights,
-                    compact=compact)
+                    compact=compact, tokenizer=tokenizer)
     eng.tp_ctl = TPControl(info.rank, info.world, control_tag(), dist.group.WORLD)
     eng.tp_ctl.start_heartbeat()
     return eng

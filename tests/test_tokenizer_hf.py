@@ -1,0 +1,128 @@
+"""A checkpoint's own ``tokenizer.json`` behind the engines (``engine/tokenizer.py``
+``HFTokenizer``): byte-level BPE (the Llama-3 / Whisper kind) and SentencePiece-
+style Metaspace BPE (the TinyLlama / Llama-2 kind), both trained here from a
+small corpus with the ``tokenizers`` library (no network, no downloaded
+vocabulary). Parity of a real checkpoint's token ids is unpinned: none of the
+reference's files hold a tokenizer."""
+import json
+import os
+
+import pytest
+import torch
+
+from loqa_hub_amd.config import GPUConfig
+from loqa_hub_amd.engine.grammar import GrammarTables, multi_command_schema
+from loqa_hub_amd.engine.tokenizer import HFTokenizer, find_tokenizer, load_tokenizer
+from loqa_hub_amd.llm.commands import parse_multi_command_response
+from loqa_hub_amd.llm.prompts import build_multi_command_prompt
+
+tk = pytest.importorskip("tokenizers")
+
+CORPUS = [build_multi_command_prompt(t) for t in (
+    "turn on the kitchen lights and play music in the bedroom",
+    "turn off the tv then dim the living room lamp",
+    "hello what time is it 95 percent 0123456789")] * 20
+
+WHISPER_SPECIALS = ["<|endoftext|>", "<|startoftranscript|>", "<|en|>", "<|transcribe|>",
+                    "<|notimestamps|>"]
+
+
+def _byte_level(path, vocab=600, specials=("<|begin_of_text|>", "<|end_of_text|>")):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    t = Tokenizer(models.BPE())
+    t.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    t.decoder = decoders.ByteLevel()
+    t.train_from_iterator(CORPUS, trainers.BpeTrainer(
+        vocab_size=vocab, special_tokens=list(specials),
+        initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    os.makedirs(path, exist_ok=True)
+    t.save(os.path.join(path, "tokenizer.json"))
+    return os.path.join(path, "tokenizer.json")
+
+
+def _metaspace(path, vocab=500):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    t = Tokenizer(models.BPE(unk_token="<unk>"))
+    t.pre_tokenizer = pre_tokenizers.Metaspace()
+    t.decoder = decoders.Metaspace()
+    alphabet = [chr(c) for c in range(32, 127)]
+    t.train_from_iterator(CORPUS, trainers.BpeTrainer(vocab_size=vocab, initial_alphabet=alphabet,
+                                                      special_tokens=["<unk>", "<s>", "</s>"]))
+    os.makedirs(path, exist_ok=True)
+    t.save(os.path.join(path, "tokenizer.json"))
+    return os.path.join(path, "tokenizer.json")
+
+
+@pytest.mark.parametrize("kind", ["byte_level", "metaspace"])
+def test_hf_tokenizer_interface(tmp_path, kind):
+    f = (_byte_level if kind == "byte_level" else _metaspace)(str(tmp_path / kind))
+    tok = HFTokenizer(f, 4096)
+    text = 'Voice command: "turn on the lights" {"confidence": 0.95}'
+    ids = tok.encode(text, bos=True)
+    assert ids[0] == tok.bos and tok.bos is not None and tok.eos is not None
+    assert tok.decode(ids) == text
+    # the texts the constrained decoder concatenates rebuild the input exactly
+    # (a SentencePiece tokenizer adds its one leading space)
+    joined = "".join(tok.token_text(t) for t in ids[1:])
+    assert joined == (text if kind == "byte_level" else " " + text)
+    for s in ['"', "0", "9", "{"]:
+        assert tok.token_text(tok.token_id(s)) == s
+    assert tok.token_text(tok.bos) == "" and tok.token_text(4095) == ""
+    with pytest.raises(ValueError):
+        HFTokenizer(f, 100)      # a file larger than the model's vocabulary
+
+
+def test_find_tokenizer(tmp_path):
+    f = _byte_level(str(tmp_path / "ckpt"))
+    ckpt = tmp_path / "ckpt" / "model.safetensors"
+    ckpt.write_bytes(b"")
+    assert find_tokenizer(str(tmp_path / "ckpt")) == f
+    assert find_tokenizer(str(ckpt)) == f
+    assert find_tokenizer(f) == f
+    assert find_tokenizer(str(tmp_path)) is None and find_tokenizer("") is None
+    with pytest.raises(FileNotFoundError):
+        load_tokenizer(str(tmp_path), 4096)
+    g = GPUConfig(llm_checkpoint=str(ckpt))
+    assert isinstance(g.tokenizer("llm", 4096), HFTokenizer)
+    assert g.tokenizer("stt", 4096) is None            # no checkpoint: synthetic tokenizer
+    g = GPUConfig(stt_tokenizer=f)
+    assert isinstance(g.tokenizer("stt", 4096), HFTokenizer)
+
+
+@pytest.mark.parametrize("kind", ["byte_level", "metaspace"])
+def test_llm_engine_with_checkpoint_tokenizer_cpu(tmp_path, kind):
+    """The constrained decoder on a real tokenizer: grammar tables from its
+    vocabulary, prompts through its BPE, valid multi-command JSON out."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    f = (_byte_level if kind == "byte_level" else _metaspace)(str(tmp_path / kind))
+    tok = load_tokenizer(f, 4096)
+    GrammarTables(tok)
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=4,
+                    max_seq_len=768, use_graphs=False, tokenizer=tok)
+    assert eng.tok is tok
+    reqs = [GenRequest(tok.encode(build_multi_command_prompt("turn on the lights and play music"),
+                                  bos=True), multi_command_schema(n)) for n in (1, 2)]
+    eng.generate(reqs)
+    for n, r in zip((1, 2), reqs):
+        assert len(parse_multi_command_response(r.output, "x").commands) == n
+        json.loads(r.output)
+
+
+def test_stt_engine_with_checkpoint_tokenizer_cpu(tmp_path):
+    """Whisper's special tokens come from the file; a teacher-forced
+    transcript round-trips through the file's BPE."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    f = _byte_level(str(tmp_path / "whisper"), specials=WHISPER_SPECIALS)
+    tok = load_tokenizer(f, 4096)
+    eng = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4,
+                    tokenizer=tok)
+    assert eng.sot == [tok.token_id(s) for s in WHISPER_SPECIALS[1:]]
+    assert eng.eot == tok.token_id("<|endoftext|>") == 0
+    utts = make_batch(0, 2, [1, 2])
+    reqs = [STTRequest(u.pcm, transcript=u.text) for u in utts]
+    eng.transcribe(reqs)
+    for r, u in zip(reqs, utts):
+        assert r.text == u.text
