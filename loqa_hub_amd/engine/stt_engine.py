@@ -68,7 +68,7 @@ class STTEngine:
     def __init__(self, cfg: WhisperConfig, device, *, seed: int = 0, max_batch: int = 64,
                  block_size: int = 16, use_graphs: bool = True, fast_decode: bool = True,
                  fused: bool = True, weights: WhisperWeights | None = None,
-                 contended_tuning: bool = False, tokenizer=None):
+                 contended_tuning: bool = False, tokenizer=None, language: str = "en"):
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -83,8 +83,15 @@ class STTEngine:
         self.weights.max_wgs = self.max_wgs or ops.MAX_DECODE_WGS
         self.model = WhisperModel(self.weights)
         self.tok = tokenizer or get_tokenizer(cfg.vocab_size)
-        self.sot = [self.tok.token_id(s) for s in
-                    ("<|startoftranscript|>", "<|en|>", "<|transcribe|>", "<|notimestamps|>")]
+        # start-of-transcript prompt; the language token follows STT_LANGUAGE
+        # (the reference passes it to its STT service)
+        try:
+            lang = self.tok.token_id(f"<|{language}|>")
+        except KeyError:
+            raise ValueError(f"STT language {language!r}: no <|{language}|> token in the "
+                             "tokenizer (a multilingual Whisper tokenizer.json has one)") from None
+        self.sot = [self.tok.token_id("<|startoftranscript|>"), lang,
+                    self.tok.token_id("<|transcribe|>"), self.tok.token_id("<|notimestamps|>")]
         self.eot = self.tok.token_id("<|endoftext|>")
         self.block_size = block_size
         self.max_blocks = (cfg.n_text_ctx + block_size - 1) // block_size

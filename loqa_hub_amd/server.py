@@ -103,7 +103,8 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
         lw = loader.load_llama(lcfg, g.llm_checkpoint, device) if (g.llm_checkpoint and llm is None) \
             else None
     stt = STTEngine(scfg, device, seed=g.seed, max_batch=g.max_batch, use_graphs=g.use_graphs,
-                    weights=sw, tokenizer=g.tokenizer("stt", scfg.vocab_size))
+                    weights=sw, tokenizer=g.tokenizer("stt", scfg.vocab_size),
+                    language=cfg.stt.language)
     if llm is None:
         llm = LLMEngine(lcfg, device, seed=g.seed, max_seqs=g.max_batch, weights=lw,
                         max_seq_len=g.max_seq_len, block_size=g.kv_block, use_graphs=g.use_graphs,

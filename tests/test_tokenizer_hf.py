@@ -24,7 +24,7 @@ CORPUS = [build_multi_command_prompt(t) for t in (
     "hello what time is it 95 percent 0123456789")] * 20
 
 WHISPER_SPECIALS = ["<|endoftext|>", "<|startoftranscript|>", "<|en|>", "<|transcribe|>",
-                    "<|notimestamps|>"]
+                    "<|notimestamps|>", "<|de|>"]
 
 
 def _byte_level(path, vocab=600, specials=("<|begin_of_text|>", "<|end_of_text|>")):
@@ -119,10 +119,17 @@ def test_stt_engine_with_checkpoint_tokenizer_cpu(tmp_path):
     tok = load_tokenizer(f, 4096)
     eng = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4,
                     tokenizer=tok)
-    assert eng.sot == [tok.token_id(s) for s in WHISPER_SPECIALS[1:]]
+    assert eng.sot == [tok.token_id(s) for s in WHISPER_SPECIALS[1:5]]
     assert eng.eot == tok.token_id("<|endoftext|>") == 0
     utts = make_batch(0, 2, [1, 2])
     reqs = [STTRequest(u.pcm, transcript=u.text) for u in utts]
     eng.transcribe(reqs)
     for r, u in zip(reqs, utts):
         assert r.text == u.text
+    # STT_LANGUAGE picks the language token of the start-of-transcript prompt
+    de = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=2,
+                   tokenizer=tok, language="de", weights=eng.weights)
+    assert de.sot[1] == tok.token_id("<|de|>") and de.sot[0] == eng.sot[0]
+    with pytest.raises(ValueError):
+        STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=2,
+                  tokenizer=tok, language="fr", weights=eng.weights)
