@@ -137,12 +137,12 @@ class VoicePipeline:
             j.n_expected = n
             prompt = build_multi_command_prompt(text)
             schema = multi_command_schema(n, min_response_tokens=self.min_response_tokens)
-            r = GenRequest(tok.encode(prompt, bos=True), schema, on_tokens=j.on_tokens)
+            r = GenRequest(tok.encode_prompt(prompt), schema, on_tokens=j.on_tokens)
             r.kind = "multi"  # type: ignore[attr-defined]
         else:
             j.n_expected = 1
             schema = single_command_schema(max_response_tokens=12)
-            r = GenRequest(tok.encode(build_prompt(text), bos=True), schema, on_tokens=j.on_tokens)
+            r = GenRequest(tok.encode_prompt(build_prompt(text)), schema, on_tokens=j.on_tokens)
             r.kind = "single"  # type: ignore[attr-defined]
         return r
 

@@ -117,6 +117,10 @@ class SyntheticTokenizer:
             return SPECIALS.index(s)
         return self._lookup[s]
 
+    def encode_prompt(self, text: str) -> list[int]:
+        """A whole LLM prompt (no chat template for the random-init weights)."""
+        return self.encode(text, bos=True)
+
     def encode(self, text: str, bos: bool = False) -> list[int]:
         out = [self.bos] if bos else []
         pos = 0
@@ -220,6 +224,7 @@ class HFTokenizer:
         self._added = {int(i): t for i, t in self._t.get_added_tokens_decoder().items()}
         self.bos = next((i for i in map(self._t.token_to_id, _BOS_NAMES) if i is not None), None)
         self.eos = next((i for i in map(self._t.token_to_id, _EOS_NAMES) if i is not None), None)
+        self._chat = self._chat_template(file)
         anchor = self._anchor()
         a_text = self._t.decode([anchor], skip_special_tokens=False)
         texts = self._t.decode_batch([[anchor, i] for i in range(n)], skip_special_tokens=False)
@@ -231,6 +236,48 @@ class HFTokenizer:
         for i in range(n - 1, -1, -1):      # lowest id wins
             if self._text[i]:
                 self._by_text[self._text[i]] = i
+
+    def _chat_template(self, file: str):
+        """The checkpoint's chat template (``tokenizer_config.json`` beside
+        ``tokenizer.json``), compiled in a sandboxed Jinja environment, or None.
+        The reference sends its prompts to Ollama's ``/api/generate`` without
+        ``raw``, which wraps them in the model's template; a real instruct
+        checkpoint here gets the same (``encode_prompt``)."""
+        import json
+        import os
+        cfg_file = os.path.join(os.path.dirname(file), "tokenizer_config.json")
+        if not os.path.isfile(cfg_file):
+            return None
+        with open(cfg_file, encoding="utf-8") as fh:
+            cfg = json.load(fh)
+        tpl = cfg.get("chat_template")
+        if isinstance(tpl, list):        # named templates: the default one
+            tpl = next((t.get("template") for t in tpl if t.get("name") == "default"), None)
+        if not isinstance(tpl, str) or not tpl:
+            return None
+        from jinja2.sandbox import ImmutableSandboxedEnvironment
+
+        def raise_exception(msg):
+            raise ValueError(f"chat template: {msg}")
+
+        env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
+        env.globals["raise_exception"] = raise_exception
+
+        def tok_str(k):
+            v = cfg.get(k)
+            return v.get("content", "") if isinstance(v, dict) else (v or "")
+        return env.from_string(tpl), tok_str("bos_token"), tok_str("eos_token")
+
+    def encode_prompt(self, text: str) -> list[int]:
+        """A whole LLM prompt: as the user turn of the checkpoint's chat
+        template (followed by the assistant header) when it has one - the
+        template writes its own BOS - else the text after BOS."""
+        if self._chat is None:
+            return self.encode(text, bos=True)
+        tpl, bos, eos = self._chat
+        s = tpl.render(messages=[{"role": "user", "content": text}], add_generation_prompt=True,
+                       bos_token=bos, eos_token=eos)
+        return self.encode(s)
 
     def _anchor(self) -> int:
         for s in ("a", "x", "the", "A"):

@@ -96,7 +96,7 @@ class GPUBackend:
         for prompt, kind, n, _ in batch:
             schema = (multi_command_schema(max(1, n), min_response_tokens=self.min_response_tokens)
                       if kind == "multi" else single_command_schema())
-            reqs.append(GenRequest(tok.encode(prompt, bos=True), schema))
+            reqs.append(GenRequest(tok.encode_prompt(prompt), schema))
         try:
             await asyncio.get_running_loop().run_in_executor(None, self.engine.generate, reqs)
         except Exception as e:

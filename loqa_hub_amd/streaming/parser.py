@@ -166,7 +166,7 @@ class GPUStreamingBackend:
 
         def push(ids):                                  # engine thread
             loop.call_soon_threadsafe(ch.try_put, (tok.decode(ids), False))
-        req = GenRequest(tok.encode(prompt, bos=True), single_command_schema(), on_tokens=push)
+        req = GenRequest(tok.encode_prompt(prompt), single_command_schema(), on_tokens=push)
 
         async def run():
             try:

@@ -133,3 +133,38 @@ def test_stt_engine_with_checkpoint_tokenizer_cpu(tmp_path):
     with pytest.raises(ValueError):
         STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=2,
                   tokenizer=tok, language="fr", weights=eng.weights)
+
+
+LLAMA3_TEMPLATE = (
+    "{{ bos_token }}{% for m in messages %}<|start_header_id|>{{ m['role'] }}<|end_header_id|>\n\n"
+    "{{ m['content'] | trim }}<|eot_id|>{% endfor %}"
+    "{% if add_generation_prompt %}<|start_header_id|>assistant<|end_header_id|>\n\n{% endif %}")
+
+
+def test_chat_template_prompt_cpu(tmp_path):
+    """A checkpoint with a chat template gets its prompts wrapped as the user
+    turn (as Ollama's /api/generate does for the reference); the decoder still
+    emits valid multi-command JSON after the assistant header."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    specials = ("<|begin_of_text|>", "<|end_of_text|>", "<|start_header_id|>", "<|end_header_id|>",
+                "<|eot_id|>")
+    f = _byte_level(str(tmp_path / "chat"), specials=specials)
+    with open(tmp_path / "chat" / "tokenizer_config.json", "w") as fh:
+        json.dump({"chat_template": LLAMA3_TEMPLATE, "bos_token": "<|begin_of_text|>",
+                   "eos_token": {"content": "<|eot_id|>"}}, fh)
+    tok = load_tokenizer(f, 4096)
+    text = build_multi_command_prompt("turn on the lights")
+    ids = tok.encode_prompt(text)
+    hdr, end = tok.token_id("<|start_header_id|>"), tok.token_id("<|end_header_id|>")
+    assert ids[0] == tok.bos and ids[1] == hdr and ids.count(hdr) == 2 and ids[-1] == tok.encode("\n\n")[-1]
+    assert tok.decode(ids) == "user\n\n" + text.strip() + "assistant\n\n"
+    assert end in ids and tok.token_id("<|eot_id|>") in ids
+    # a tokenizer without a template: BOS + text
+    plain = load_tokenizer(_byte_level(str(tmp_path / "plain")), 4096)
+    assert plain.encode_prompt("hi") == [plain.bos] + plain.encode("hi")
+    eng = LLMEngine(llama_config("test-tiny"), torch.device("cpu"), seed=0, max_seqs=2,
+                    max_seq_len=768, use_graphs=False, tokenizer=tok)
+    reqs = [GenRequest(ids, multi_command_schema(2))]
+    eng.generate(reqs)
+    assert len(parse_multi_command_response(reqs[0].output, "x").commands) == 2
