@@ -93,6 +93,16 @@ class STTEngine:
         self.sot = [self.tok.token_id("<|startoftranscript|>"), lang,
                     self.tok.token_id("<|transcribe|>"), self.tok.token_id("<|notimestamps|>")]
         self.eot = self.tok.token_id("<|endoftext|>")
+        # a checkpoint's tokenizer: greedy decoding never emits its special /
+        # timestamp tokens or the generation config's suppress_tokens (as the
+        # reference's STT service decodes); one packed mask row for every
+        # sequence. The synthetic tokenizer of the random-init weights: none.
+        self._sup = self._sup_rows = None
+        if hasattr(self.tok, "sampling_mask"):
+            from ..ops.reference import pack_mask
+            self._sup = pack_mask(self.tok.sampling_mask(keep=(self.eot,))[None]).to(self.device)
+            self._sup_rows = torch.zeros(max(256, 2 * max_batch), dtype=torch.int32,
+                                         device=self.device)
         self.block_size = block_size
         self.max_blocks = (cfg.n_text_ctx + block_size - 1) // block_size
         self.kv = PagedKVCache(cfg.dec_layers, cfg.n_heads, cfg.head_dim,
@@ -311,6 +321,11 @@ class STTEngine:
             return self.self_splits
         return max(1, min(self.self_splits, (ctx + self.SPLIT_KEYS - 1) // self.SPLIT_KEYS))
 
+    def _argmax(self, logits: torch.Tensor) -> torch.Tensor:
+        if self._sup is None:
+            return ops.masked_argmax(logits)
+        return ops.masked_argmax(logits, self._sup, self._sup_rows[: logits.shape[0]])
+
     def _fast_forward(self, dev: dict, max_q: int, B_pad: int, ctx: int | None = None) -> torch.Tensor:
         ns = self._self_splits(ctx)
         if self.fused and dev["tokens"].numel() <= 64:
@@ -319,13 +334,13 @@ class STTEngine:
                                        self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
                                        dev["enc_lens"], dev["logit_idx"], self.ws, self.scratch,
                                        ns, self.SPLIT_KEYS, self.cross_split_keys)
-            return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
+            return self._argmax(logits[:B_pad, : self.cfg.vocab_size])
         logits = decode_step_fast(self.model, dev["tokens"], dev["positions"], dev["slots"],
                                   dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
                                   self.kv.k, self.kv.v, self.xkv, dev["enc_starts"],
                                   dev["enc_lens"], dev["logit_idx"], self.ws, ns,
                                   self.SPLIT_KEYS)
-        return ops.masked_argmax(logits[:B_pad, : self.cfg.vocab_size])
+        return self._argmax(logits[:B_pad, : self.cfg.vocab_size])
 
     def _graph(self, B_pad: int, T_pad: int, ctx: int) -> dict:
         """Captured decode step for (sequence bucket, token bucket, context
@@ -523,7 +538,7 @@ class STTEngine:
             dev(toks, torch.int32), dev(pos, torch.int32), dev(slots, torch.int32),
             dev(cu, torch.int32), dev(ctx, torch.int32), dev(bt, torch.int32), max_q, max_ctx,
             self.kv.k, self.kv.v, self.xkv, enc_starts, enc_lens, dev(lidx, torch.int64), self.ws)
-        return ops.masked_argmax(logits).cpu().numpy()
+        return self._argmax(logits).cpu().numpy()
 
     # ----------------------------------------------------------- admission
     def _admit(self, reqs: list[STTRequest], slots: list[int],

@@ -225,6 +225,14 @@ class HFTokenizer:
         self.bos = next((i for i in map(self._t.token_to_id, _BOS_NAMES) if i is not None), None)
         self.eos = next((i for i in map(self._t.token_to_id, _EOS_NAMES) if i is not None), None)
         self._chat = self._chat_template(file)
+        # generation_config.json beside the file (Whisper: suppress_tokens)
+        import json
+        import os
+        gc = os.path.join(os.path.dirname(file), "generation_config.json")
+        self.generation_config = {}
+        if os.path.isfile(gc):
+            with open(gc, encoding="utf-8") as fh:
+                self.generation_config = json.load(fh)
         anchor = self._anchor()
         a_text = self._t.decode([anchor], skip_special_tokens=False)
         texts = self._t.decode_batch([[anchor, i] for i in range(n)], skip_special_tokens=False)
@@ -307,3 +315,20 @@ class HFTokenizer:
 
     def token_text(self, t: int) -> str:
         return self._text[t] if 0 <= t < self.n_real else ""
+
+    def sampling_mask(self, keep: tuple = ()):
+        """bool [vocab_size]: the tokens free (unconstrained) sampling may
+        emit: not the added / special tokens (Whisper's task, language and
+        timestamp tokens) except ``keep``, not the ``suppress_tokens`` of the
+        checkpoint's generation config, not the padding ids past the file."""
+        import torch
+        m = torch.zeros(self.vocab_size, dtype=torch.bool)
+        m[: self.n_real] = True
+        for i in self._added:
+            m[i] = False
+        for i in self.generation_config.get("suppress_tokens") or ():
+            if 0 <= int(i) < self.vocab_size:
+                m[int(i)] = False
+        for i in keep:
+            m[i] = True
+        return m

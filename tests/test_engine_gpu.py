@@ -494,3 +494,22 @@ def test_placed_stream_slot_gpu():
         y = (x * x).sum()
     s.synchronize()
     assert y.item() == 4.0 * 4096
+
+
+def test_stt_suppression_checkpoint_tokenizer_gpu(tmp_path):
+    """The suppression mask of a checkpoint tokenizer on the graph-replayed
+    Whisper decode (masked argmax kernel, one mask row for every sequence)."""
+    from test_tokenizer_hf import WHISPER_SPECIALS, _byte_level
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.engine.tokenizer import load_tokenizer
+    f = _byte_level(str(tmp_path / "whisper"), vocab=3000, specials=WHISPER_SPECIALS)
+    with open(tmp_path / "whisper" / "generation_config.json", "w") as fh:
+        json.dump({"suppress_tokens": list(range(300, 2900))}, fh)
+    tok = load_tokenizer(f, 4096)
+    eng = STTEngine(whisper_config("test-whisper"), "cuda", seed=0, max_batch=4, tokenizer=tok)
+    utts = make_batch(0, 3, [1, 2])
+    reqs = [STTRequest(u.pcm, max_new_tokens=12) for u in utts]
+    eng.transcribe(reqs)
+    allowed = set(tok.sampling_mask(keep=(eng.eot,)).nonzero().flatten().tolist())
+    toks = [t for r in reqs for t in r.tokens]
+    assert toks and set(toks) <= allowed

@@ -168,3 +168,27 @@ def test_chat_template_prompt_cpu(tmp_path):
     reqs = [GenRequest(ids, multi_command_schema(2))]
     eng.generate(reqs)
     assert len(parse_multi_command_response(reqs[0].output, "x").commands) == 2
+
+
+def test_stt_suppression_with_checkpoint_tokenizer_cpu(tmp_path):
+    """Greedy Whisper decoding on a checkpoint tokenizer never emits its
+    special tokens (other than end-of-text) or the generation config's
+    suppress_tokens; random weights would otherwise hit them."""
+    from loqa_hub_amd.engine.stt_engine import STTEngine, STTRequest
+    from loqa_hub_amd.engine.synthetic import make_batch
+    from loqa_hub_amd.models.configs import whisper_config
+    f = _byte_level(str(tmp_path / "whisper"), vocab=3000, specials=WHISPER_SPECIALS)
+    suppressed = list(range(300, 2900))
+    with open(tmp_path / "whisper" / "generation_config.json", "w") as fh:
+        json.dump({"suppress_tokens": suppressed}, fh)
+    tok = load_tokenizer(f, 4096)
+    m = tok.sampling_mask(keep=(tok.token_id("<|endoftext|>"),))
+    assert not m[300:2900].any() and not m[tok.n_real:].any() and m[0] and not m[1:6].any()
+    eng = STTEngine(whisper_config("test-whisper"), torch.device("cpu"), seed=0, max_batch=4,
+                    tokenizer=tok)
+    utts = make_batch(0, 3, [1, 2])
+    reqs = [STTRequest(u.pcm, max_new_tokens=12) for u in utts]
+    eng.transcribe(reqs)
+    allowed = set(m.nonzero().flatten().tolist())
+    toks = [t for r in reqs for t in r.tokens]
+    assert toks and set(toks) <= allowed
