@@ -240,9 +240,13 @@ class HFTokenizer:
         for i, s in enumerate(texts):
             ok = i not in self._added and s.startswith(a_text) and "�" not in s
             self._text.append(s[len(a_text):] if ok else "")
+        # text -> id for token_id: a vocabulary piece before a byte-fallback
+        # token (SentencePiece "<0x22>" also decodes to '"'; a model emits
+        # the piece), then the lowest id
         self._by_text: dict[str, int] = {}
-        for i in range(n - 1, -1, -1):      # lowest id wins
-            if self._text[i]:
+        byte_fb = re.compile(r"<0x[0-9A-Fa-f]{2}>")
+        for i in sorted(range(n), key=lambda i: (bool(byte_fb.fullmatch(self._t.id_to_token(i) or "")), i)):
+            if self._text[i] and self._text[i] not in self._by_text:
                 self._by_text[self._text[i]] = i
 
     def _chat_template(self, file: str):

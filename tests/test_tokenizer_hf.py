@@ -192,3 +192,24 @@ def test_stt_suppression_with_checkpoint_tokenizer_cpu(tmp_path):
     allowed = set(m.nonzero().flatten().tolist())
     toks = [t for r in reqs for t in r.tokens]
     assert toks and set(toks) <= allowed
+
+
+def test_byte_fallback_tokens_rank_after_pieces(tmp_path):
+    """SentencePiece byte-fallback tokens (<0x22>, regular vocabulary entries
+    ahead of the pieces, as in Llama-2 / TinyLlama files) decode to the same
+    text as the real piece; token_id returns the piece (what a model emits)."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers
+    vocab = {"<unk>": 0, "<s>": 1, "</s>": 2}
+    for b in range(256):
+        vocab[f"<0x{b:02X}>"] = len(vocab)
+    for c in ["\u2581"] + [chr(c) for c in range(33, 127)]:
+        vocab[c] = len(vocab)
+    t = Tokenizer(models.BPE(vocab=vocab, merges=[], unk_token="<unk>", byte_fallback=True))
+    t.pre_tokenizer = pre_tokenizers.Metaspace()
+    t.decoder = decoders.Sequence([decoders.ByteFallback(), decoders.Metaspace()])
+    t.add_special_tokens(["<unk>", "<s>", "</s>"])
+    os.makedirs(tmp_path / "bf", exist_ok=True)
+    t.save(str(tmp_path / "bf" / "tokenizer.json"))
+    tok = HFTokenizer(str(tmp_path / "bf" / "tokenizer.json"), 4096)
+    assert tok.token_text(vocab["<0x22>"]) == '"'             # same text as the piece
+    assert tok.token_id('"') == vocab['"'] and tok.token_id("0") == vocab["0"]
