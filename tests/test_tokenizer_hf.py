@@ -213,3 +213,36 @@ def test_byte_fallback_tokens_rank_after_pieces(tmp_path):
     tok = HFTokenizer(str(tmp_path / "bf" / "tokenizer.json"), 4096)
     assert tok.token_text(vocab["<0x22>"]) == '"'             # same text as the piece
     assert tok.token_id('"') == vocab['"'] and tok.token_id("0") == vocab["0"]
+
+
+def test_hub_processor_uses_checkpoint_and_tokenizer_cpu(tmp_path):
+    """HUB_LLM_CHECKPOINT pointing at a safetensors directory with a
+    tokenizer.json: the served processor's engine loads both, and an
+    utterance runs through the hub path on them."""
+    import asyncio
+
+    import numpy as np
+
+    from loqa_hub_amd import config as cfgmod
+    from loqa_hub_amd.models import loader
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import LlamaWeights
+    from loqa_hub_amd.server import build_gpu_processor
+    ck = tmp_path / "llm"
+    os.makedirs(ck)
+    w = LlamaWeights(llama_config("test-tiny"), torch.device("cpu"), seed=5)
+    loader.save_llama(w, str(ck / "model.safetensors"))
+    _byte_level(str(ck))
+
+    async def go():
+        cfg = cfgmod.load({"HUB_STT_MODEL": "test-whisper", "HUB_LLM_MODEL": "test-tiny",
+                           "HUB_MAX_BATCH": "2", "HUB_USE_GRAPHS": "false",
+                           "HUB_LLM_CHECKPOINT": str(ck), "HUB_TTS_BACKEND": "none"})
+        proc = build_gpu_processor(cfg, None, device="cpu", bridge=False)
+        eng = proc.pipeline.llm
+        assert isinstance(eng.tok, HFTokenizer)
+        assert torch.equal(eng.weights.layers[0]["wqkv"].float(), w.layers[0]["wqkv"].float())
+        pcm = np.random.default_rng(0).standard_normal(16000).astype(np.float32) * 0.1
+        r = await proc.process("r0", "q0", pcm, 16000)
+        assert r.command in ("voice_command_success", "no_speech", "error", "confirmation_needed")
+    asyncio.run(go())
