@@ -22,6 +22,16 @@
 // Epilogues as gemm_sk.hip: bf16 (+ f32 bias, GELU), SwiGLU (a wave's 64
 // features = 32 gate + the matching 32 up rows, permuted at staging), residual
 // add in place (+ bias), one rounding.
+//
+// Split-K (S > 1): the K range is cut into S chunks, each its own workgroup,
+// summed inside the launch by the tile's last arriving chunk (gemm_sk.hip's
+// protocol: partial stores -> vmcnt(0) -> agent release -> relaxed ticket; the
+// last arriver takes an agent acquire and adds the S partials in fixed chunk
+// order). A workgroup's operand ingestion is (BM + 128) x K/S: at ~300 rows
+// the activation block dominates it, so fewer K per workgroup is what lets
+// more workgroups than 128-feature tiles share the pass (down: 32 tiles x 8
+// chunks). Chunk-major workgroup order: the workgroups of one K chunk (one
+// activation slice, L2-resident) run together.
 #include "common.h"
 
 #define WS_BK 64
@@ -36,6 +46,9 @@ struct GemmWsParams {
   const float* bias;              // [N] f32 or null (bf16 / resid)
   void* y; long long ldy;         // bf16 output (WS_RESID: the residual, updated in place)
   int bm;                         // rows per workgroup (multiple of 64, <= 64 * FM of the launch)
+  int S;                          // K chunks (>= 1)
+  float* ws;                      // S > 1: [tiles][S][bm * 128] f32 partials
+  int* counters;                  // S > 1: [tiles] ints, zero on entry (left zero)
 };
 
 template <int N>
@@ -63,10 +76,14 @@ __global__ __launch_bounds__(512) void gemm_ws_kernel(GemmWsParams p) {
   const int wn = wave % WN, wm = wave / WN;
   const int M = p.M, N = p.N;
   const int mblocks = (M + p.bm - 1) / p.bm;
+  const int tiles = mblocks * (N / BN), S = p.S;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int mb = id % mblocks, nb = id / mblocks;   // a weight tile's row blocks adjacent
+  const int s = id / tiles, tile = id - s * tiles;
+  const int mb = tile % mblocks, nb = tile / mblocks;   // a weight tile's row blocks adjacent
   const int m0 = mb * p.bm, n0 = nb * BN;
-  const int nt = p.K / WS_BK;
+  const int KT = p.K / WS_BK;
+  const int kt0 = (int)(((long long)s * KT) / S), kt1 = (int)(((long long)(s + 1) * KT) / S);
+  const int nt = kt1 - kt0;
   const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(p.w);
 
@@ -83,7 +100,7 @@ __global__ __launch_bounds__(512) void gemm_ws_kernel(GemmWsParams p) {
     } else {
       row = n0 + r;
     }
-    wsrc[i] = W + (size_t)row * p.K + c * 8;
+    wsrc[i] = W + (size_t)row * p.K + (size_t)kt0 * WS_BK + c * 8;
   }
   const bf16_t* xsrc[IX];
 #pragma unroll
@@ -91,7 +108,7 @@ __global__ __launch_bounds__(512) void gemm_ws_kernel(GemmWsParams p) {
     const int r = 8 * (wave * IX + i) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = min(m0 + min(r, p.bm - 1), M - 1);
-    xsrc[i] = X + (size_t)m * p.ldx + c * 8;
+    xsrc[i] = X + (size_t)m * p.ldx + (size_t)kt0 * WS_BK + c * 8;
   }
   auto stage_w = [&](int kt) {
     unsigned char* dst = wl + (kt % NBW) * WSTAGE;
@@ -193,6 +210,53 @@ __global__ __launch_bounds__(512) void gemm_ws_kernel(GemmWsParams p) {
     compute(t);
   }
 
+  // ---- split-K: publish this chunk's partial, the tile's last arriver sums them
+  if (S > 1) {
+    constexpr int PER_WAVE = FN * FM * 256;      // floats per wave partial (16 B per lane per fragment)
+    float* mine = p.ws + (((size_t)tile * S + s) * NW + wave) * PER_WAVE;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        *reinterpret_cast<float4v*>(mine + ((i * FM + j) * 64 + lane) * 4) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);     // every wave is past its last LDS read
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == S - 1;
+      if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // fixed chunk order 0..S-1, this workgroup's own partial read back too:
+    // the sum does not depend on which chunk arrived last
+    constexpr int GI = 16 / FM >= FN ? FN : (16 / FM >= 2 ? 2 : 1);
+    static_assert(FN % GI == 0, "fragment groups");
+    for (int c = 0; c < S; ++c) {
+      const float* theirs = p.ws + (((size_t)tile * S + c) * NW + wave) * PER_WAVE;
+#pragma unroll
+      for (int i0 = 0; i0 < FN; i0 += GI) {
+        float4v v[GI][FM];
+#pragma unroll
+        for (int i = 0; i < GI; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j)
+            v[i][j] = *reinterpret_cast<const float4v*>(theirs + (((i0 + i) * FM + j) * 64 + lane) * 4);
+#pragma unroll
+        for (int i = 0; i < GI; ++i)
+#pragma unroll
+          for (int j = 0; j < FM; ++j) acc[i0 + i][j] = c == 0 ? v[i][j] : acc[i0 + i][j] + v[i][j];
+      }
+    }
+  }
+
   // ---- epilogue: acc[i][j] = C[n = n0 + TN wn + 16 i + 4 fq + r][m = m0 + TM wm + 16 j + fr]
   bf16_t* Y = reinterpret_cast<bf16_t*>(p.y);
   const int mend = min(M, m0 + p.bm);
@@ -252,7 +316,7 @@ __global__ __launch_bounds__(512) void gemm_ws_kernel(GemmWsParams p) {
 
 template <int FM, int NBW, int NBX>
 static int ws_launch(const GemmWsParams& p, hipStream_t st) {
-  const int grid = ((p.M + p.bm - 1) / p.bm) * (p.N / 128);
+  const int grid = ((p.M + p.bm - 1) / p.bm) * (p.N / 128) * p.S;
   switch (p.epi) {
     case WS_SWIGLU:
       hipLaunchKernelGGL((gemm_ws_kernel<FM, NBW, NBX, WS_SWIGLU>), dim3(grid), dim3(512), 0, st, p);
@@ -271,8 +335,9 @@ static int ws_launch(const GemmWsParams& p, hipStream_t st) {
 extern "C" int loqa_gemm_ws(const GemmWsParams* p, int depth, hipStream_t st) {
   if (!p || p->M <= 0 || p->epi < 0 || p->epi > 2 || !p->x || !p->w || !p->y) return (int)hipErrorInvalidValue;
   if (p->N % 128 || p->K % WS_BK || p->K < WS_BK || p->ldx % 8 || p->ldy % 4 || p->bm < 64 || p->bm % 64 ||
-      p->bm > 384 || depth < 0 || depth > 1)
+      p->bm > 384 || depth < 0 || depth > 1 || p->S < 1 || p->S > p->K / WS_BK)
     return (int)hipErrorInvalidValue;
+  if (p->S > 1 && (!p->ws || !p->counters)) return (int)hipErrorInvalidValue;
   if ((p->epi == WS_SWIGLU && (p->bias || p->act)) || (p->epi == WS_RESID && p->act))
     return (int)hipErrorInvalidValue;
   const int fm = p->bm / 64;

@@ -1650,10 +1650,11 @@ def gemm_ws_rows(M: int, depth: int = 0) -> int:
 def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
             act: str | None = None, residual: torch.Tensor | None = None,
             out: torch.Tensor | None = None, depth: int | None = None,
-            bm: int | None = None) -> torch.Tensor:
+            bm: int | None = None, splits: int = 1) -> torch.Tensor:
     """Y = X W^T on the row-resident weight-streaming GEMM: a workgroup owns
     128 output features x all the rows of its row block (up to 384), so every
-    weight byte is read once. Epilogues as :func:`gemm_sk`."""
+    weight byte is read once; ``splits`` K chunks per tile, summed in-launch.
+    Epilogues as :func:`gemm_sk`."""
     N, K = w.shape
     M = x.shape[0]
     assert x.shape[1] == K, (x.shape, w.shape)
@@ -1688,7 +1689,13 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
         assert y.shape == (M, cols) and y.stride(1) == 1
     p.y, p.ldy = ptr(y), y.stride(0)
     p.bm = gemm_ws_rows(M, depth) if bm is None else bm
-    check(kernels().loqa_gemm_ws(ctypes.byref(p), depth, stream_ptr(x)), "gemm_ws")
+    p.S = splits
+    st = stream_ptr(x)
+    if splits > 1:
+        tiles = -(-M // p.bm) * (N // 128)
+        ws, cnt = _sk_workspace(x.device, st, tiles * splits * p.bm * 128, tiles)
+        p.ws, p.counters = ptr(ws), ptr(cnt)
+    check(kernels().loqa_gemm_ws(ctypes.byref(p), depth, st), "gemm_ws")
     return y
 
 
@@ -1696,7 +1703,7 @@ def gemm_ws(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.
 # Projection dispatch for prompt passes (prefill, Whisper encoder): the
 # hand-written GEMM measured fastest per (N, K) and row count
 # (scripts/exp/gemm_sk_bench.py --grid, cold weights; profiles/r4_gemm_proj_grid.txt):
-# ("sk", layout, K chunks) = gemm_sk, ("ws", depth) = gemm_ws.
+# ("sk", layout, K chunks) = gemm_sk, ("ws", depth[, K chunks]) = gemm_ws.
 PROJ_TABLE = {
     # the chunked prompt passes (LOQA_CHUNK_PREFILL) also run 64-256 rows:
     # more K chunks fill the CUs there (profiles/r4_gemm_small_m.txt; a 32 /
@@ -1706,10 +1713,17 @@ PROJ_TABLE = {
                    (900, ("sk", 5, 1)), (1 << 30, ("sk", 0, 1))],                         # Llama qkv
     (4096, 4096): [(128, ("sk", 4, 4)), (256, ("sk", 4, 2)), (900, ("sk", 4, 1)),
                    (1 << 30, ("sk", 0, 1))],                                               # o
-    (28672, 4096): [(256, ("ws", 1)), (384, ("ws", 0)), (900, ("sk", 0, 1)),
+    (28672, 4096): [(256, ("ws", 1)), (384, ("ws", 0)), (900, ("ws", 0)),
                     (1 << 30, ("sk", 6, 1))],                                              # gate|up
+    # 400-1000 rows (whole-prompt passes of two or three prompts, nothing
+    # decoding): down on the weight-streaming GEMM with K chunks, gate|up on it
+    # unsplit (600 rows: 94 vs 118 us, 160 vs 196 us; profiles/r4_ws_splitk.txt).
+    # At 300-400 rows, the chunked passes beside the decoders, the split-K
+    # weight-streaming down is faster alone (79 vs 121 us at 340 rows) but
+    # neutral end to end (19.03 vs 19.07 utt/s, 3 interleaved pairs): kept on sk
     (4096, 14336): [(64, ("sk", 4, 8)), (128, ("sk", 5, 8)), (256, ("sk", 5, 4)),
-                    (400, ("sk", 8, 3)), (900, ("sk", 0, 3)), (1 << 30, ("sk", 6, 3))],    # down
+                    (400, ("sk", 8, 3)), (700, ("ws", 0, 4)), (1000, ("ws", 0, 2)),
+                    (1 << 30, ("sk", 6, 3))],                                              # down
     # encoder qkv / fc1: gemm_ws is ~8% faster alone (24.2 / 25.8 vs 26.2 / 28.2
     # us) but its long-lived 512-thread workgroups cost the concurrent decoders
     # more than that (encoder on ws: 18.82 / 19.02 vs 19.15 / 18.99 utt/s)
@@ -1733,7 +1747,8 @@ def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Ten
             choice = c
             break
     if choice is not None and choice[0] == "ws" and N % 128 == 0:
-        return gemm_ws(x, w, epi=epi, bias=bias, act=act, residual=residual, depth=choice[1])
+        return gemm_ws(x, w, epi=epi, bias=bias, act=act, residual=residual, depth=choice[1],
+                       splits=choice[2] if len(choice) > 2 else 1)
     if choice is not None and choice[0] == "sk" and N % SK_LAYOUTS[choice[1]][0] == 0:
         return gemm_sk(x, w, epi=epi, bias=bias, act=act, residual=residual, layout=choice[1],
                        splits=choice[2])

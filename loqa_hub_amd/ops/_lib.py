@@ -74,6 +74,7 @@ class GemmWsParams(ctypes.Structure):
         ("M", c_int), ("N", c_int), ("K", c_int),
         ("epi", c_int), ("act", c_int), ("bias", c_void_p),
         ("y", c_void_p), ("ldy", c_ll), ("bm", c_int),
+        ("S", c_int), ("ws", c_void_p), ("counters", c_void_p),
     ]
 
 

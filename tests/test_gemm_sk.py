@@ -124,3 +124,31 @@ def test_gemm_ws_gpu_matches_fp32(depth):
     ref = ops._sk_ref(x.cpu(), w.cpu(), "bf16", None, None)
     for bm in (64, 128, 192, 256) + ((320, 384) if depth == 0 else ()):
         assert _rel(ops.gemm_ws(x, w, depth=depth, bm=bm), ref) < 1e-2, bm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [0, 1])
+def test_gemm_ws_splitk_gpu_matches_fp32(depth):
+    """Weight-streaming GEMM with the K range split over workgroups and summed
+    in-launch: every epilogue, ragged M, uneven K chunks, against the fp32
+    reference; the split result does not depend on which chunk lands last
+    (two launches bitwise equal); counters left zero for the next launch."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(20 + depth)
+    for M, N, K, S in ((300, 384, 1024, 4), (17, 256, 640, 3), (300, 256, 14336 // 8, 7),
+                       (129, 128, 512, 8), (64, 512, 256, 2)):
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+        b = torch.randn(N, device=dev) * 0.1
+        y = ops.gemm_ws(x, w, bias=b, act="gelu", depth=depth, splits=S)
+        assert _rel(y, ops._sk_ref(x.cpu(), w.cpu(), "bf16", b.cpu(), None, "gelu")) < 1e-2, (M, N, K, S)
+        assert torch.equal(y, ops.gemm_ws(x, w, bias=b, act="gelu", depth=depth, splits=S))
+        res = torch.randn(M, N, device=dev).bfloat16()
+        rr = ops._sk_ref(x.cpu(), w.cpu(), "resid", b.cpu(), res.cpu())
+        ops.gemm_ws(x, w, epi="resid", residual=res, bias=b, depth=depth, splits=S)
+        assert _rel(res, rr) < 1e-2, (M, N, K, S, "resid")
+        sw = ops.gemm_ws(x, w, epi="swiglu", depth=depth, splits=S)
+        assert _rel(sw, ops._sk_ref(x.cpu(), w.cpu(), "swiglu", None, None)) < 2e-2, (M, N, K, S)
+    torch.cuda.synchronize()
+    for (_, st), (_, cnt) in ops._SK_WS.items():
+        assert int(cnt.abs().sum()) == 0
