@@ -27,11 +27,10 @@ log = logging.getLogger("loqa.main")
 
 def _tp_engine(cfg):
     """HUB_TP > 1: this rank's TP engine (rank 0: the leader, served below)."""
-    from ..models.configs import llama_config
     from ..parallel.tp_serving import build_tp_llm, init_tp
     g = cfg.gpu
     info = init_tp(g.tp)
-    lcfg = llama_config(g.llm_model)
+    lcfg = g.llm_config()
     eng = build_tp_llm(lcfg, info, seed=g.seed, max_seqs=g.max_batch,
                        max_seq_len=g.max_seq_len, block_size=g.kv_block,
                        use_graphs=g.use_graphs, checkpoint=g.llm_checkpoint,

@@ -211,6 +211,19 @@ class GPUConfig:
     stt_tokenizer: str = ""
     llm_tokenizer: str = ""
 
+    def llm_config(self):
+        """The intent model's shape: the checkpoint's own config.json when it
+        has one (any Llama-family checkpoint), else the named ``HUB_LLM_MODEL``."""
+        from .models.configs import checkpoint_config, llama_config, llama_config_from_hf
+        d = checkpoint_config(self.llm_checkpoint)
+        return llama_config_from_hf(d, self.llm_model) if d else llama_config(self.llm_model)
+
+    def stt_config(self):
+        """As ``llm_config`` for the Whisper checkpoint / ``HUB_STT_MODEL``."""
+        from .models.configs import checkpoint_config, whisper_config, whisper_config_from_hf
+        d = checkpoint_config(self.stt_checkpoint)
+        return whisper_config_from_hf(d, self.stt_model) if d else whisper_config(self.stt_model)
+
     def tokenizer(self, which: str, vocab_size: int):
         """The tokenizer for ``which`` ("stt" / "llm"): an explicit
         ``HUB_*_TOKENIZER``, else the checkpoint's own file, else None."""

@@ -23,6 +23,9 @@ class LlamaConfig:
     norm_eps: float = 1e-5
     tie_embeddings: bool = False
     max_positions: int = 8192
+    # Llama-3.1-style RoPE frequency scaling: (factor, low_freq_factor,
+    # high_freq_factor, original_max_positions), or None
+    rope_scaling: tuple | None = None
 
     @property
     def qkv_dim(self) -> int:
@@ -37,8 +40,10 @@ class LlamaConfig:
 
 LLAMA_CONFIGS = {
     "tinyllama": LlamaConfig("tinyllama-1.1b", 2048, 22, 32, 4, 64, 5632, 32000, rope_theta=10000.0),
-    "llama3.2-1b": LlamaConfig("llama-3.2-1b", 2048, 16, 32, 8, 64, 8192, 128256, tie_embeddings=True),
-    "llama3.2-3b": LlamaConfig("llama-3.2-3b", 3072, 28, 24, 8, 128, 8192, 128256, tie_embeddings=True),
+    "llama3.2-1b": LlamaConfig("llama-3.2-1b", 2048, 16, 32, 8, 64, 8192, 128256, tie_embeddings=True,
+                               rope_scaling=(32.0, 1.0, 4.0, 8192)),
+    "llama3.2-3b": LlamaConfig("llama-3.2-3b", 3072, 28, 24, 8, 128, 8192, 128256, tie_embeddings=True,
+                               rope_scaling=(32.0, 1.0, 4.0, 8192)),
     "llama3-8b": LlamaConfig("llama-3-8b", 4096, 32, 32, 8, 128, 14336, 128256),
     "llama3-70b": LlamaConfig("llama-3-70b", 8192, 80, 64, 8, 128, 28672, 128256),
     # small shapes for CPU tests / smoke
@@ -119,3 +124,51 @@ def whisper_config(name: str, **over) -> WhisperConfig:
 def vits_config(name: str, **over) -> VitsConfig:
     c = VITS_CONFIGS[name]
     return replace(c, **over) if over else c
+
+
+# --------------------------------------------------------------------------
+# A checkpoint's own config.json (Hugging Face naming): any Llama-family or
+# Whisper checkpoint, not only the named sizes above
+def llama_config_from_hf(d: dict, name: str = "checkpoint") -> LlamaConfig:
+    H = int(d["num_attention_heads"])
+    D = int(d.get("head_dim") or int(d["hidden_size"]) // H)
+    rs = d.get("rope_scaling") or None
+    scaling = None
+    if rs:
+        kind = rs.get("rope_type", rs.get("type"))
+        if kind != "llama3":
+            raise ValueError(f"{name}: rope_scaling type {kind!r} is not supported")
+        scaling = (float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),
+                   float(rs.get("high_freq_factor", 4.0)),
+                   int(rs.get("original_max_position_embeddings", 8192)))
+    return LlamaConfig(name, int(d["hidden_size"]), int(d["num_hidden_layers"]), H,
+                       int(d.get("num_key_value_heads", H)), D, int(d["intermediate_size"]),
+                       int(d["vocab_size"]), rope_theta=float(d.get("rope_theta", 10000.0)),
+                       norm_eps=float(d.get("rms_norm_eps", 1e-5)),
+                       tie_embeddings=bool(d.get("tie_word_embeddings", False)),
+                       max_positions=min(int(d.get("max_position_embeddings", 8192)), 8192),
+                       rope_scaling=scaling)
+
+
+def whisper_config_from_hf(d: dict, name: str = "checkpoint") -> WhisperConfig:
+    c = WhisperConfig(name, int(d["num_mel_bins"]), int(d["d_model"]), int(d["encoder_layers"]),
+                      int(d["decoder_layers"]), int(d["encoder_attention_heads"]),
+                      int(d["vocab_size"]), n_audio_ctx=int(d.get("max_source_positions", 1500)),
+                      n_text_ctx=int(d.get("max_target_positions", 448)))
+    if int(d.get("encoder_ffn_dim", c.ffn_dim)) != c.ffn_dim:
+        raise ValueError(f"{name}: encoder_ffn_dim {d['encoder_ffn_dim']} != 4 * d_model")
+    return c
+
+
+def checkpoint_config(path: str):
+    """The config.json dict in (or beside) a checkpoint, or None."""
+    import json
+    import os
+    if not path:
+        return None
+    d = path if os.path.isdir(path) else os.path.dirname(os.path.abspath(path))
+    f = os.path.join(d, "config.json")
+    if not os.path.isfile(f):
+        return None
+    with open(f, encoding="utf-8") as fh:
+        return json.load(fh)

@@ -164,7 +164,8 @@ class LlamaWeights:
         vs = slice(r * self.v, (r + 1) * self.v)
         self.lm_head = self.embed[vs] if cfg.tie_embeddings else \
             rnd(("lm_head",), self.v, d, row0=r * self.v)
-        self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device)
+        self.cos_sin = rope_cos_sin(D, cfg.max_positions, cfg.rope_theta, device=device,
+                                    scaling=cfg.rope_scaling)
         self._finalize()
 
     def _compact_layer(self, L: dict) -> dict:
@@ -224,7 +225,8 @@ class LlamaWeights:
         self.layers = layers
         self.final_norm = final_norm
         self.lm_head = self.embed if (cfg.tie_embeddings or lm_head is None) else lm_head
-        self.cos_sin = rope_cos_sin(cfg.head_dim, cfg.max_positions, cfg.rope_theta, device=device)
+        self.cos_sin = rope_cos_sin(cfg.head_dim, cfg.max_positions, cfg.rope_theta, device=device,
+                                    scaling=cfg.rope_scaling)
         if tp is not None and tp.world > 1:
             self.decode_layers, self.lm_head_p = [], None
             return cls.shard(self, tp)

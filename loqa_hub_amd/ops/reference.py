@@ -50,9 +50,21 @@ def gelu_bias_(x, bias=None, pos=None):
     return x
 
 
-def rope_cos_sin(head_dim: int, max_pos: int, theta: float, device=None) -> torch.Tensor:
-    """[max_pos, D/2, 2] f32 table of (cos, sin) for NeoX rotate-half RoPE."""
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, device=None,
+                 scaling: tuple | None = None) -> torch.Tensor:
+    """[max_pos, D/2, 2] f32 table of (cos, sin) for NeoX rotate-half RoPE.
+    ``scaling`` = (factor, low_freq_factor, high_freq_factor, original max
+    positions): Llama-3.1 frequency scaling - wavelengths longer than
+    original / low are divided by ``factor``, shorter than original / high
+    kept, and the band between interpolated."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling is not None:
+        factor, low, high, orig = scaling
+        wavelen = 2 * math.pi / inv
+        smooth = ((orig / wavelen - low) / (high - low)).clamp(0.0, 1.0)
+        inv = torch.where(wavelen > orig / low, inv / factor,
+                          torch.where(wavelen < orig / high, inv,
+                                      (1 - smooth) * inv / factor + smooth * inv))
     ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
     return torch.stack([ang.cos(), ang.sin()], dim=-1).float().to(device)
 

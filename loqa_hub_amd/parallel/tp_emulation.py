@@ -113,7 +113,8 @@ class TPEmulation:
             hf = ops.rmsnorm(residual, w0.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
         else:
             hf = ops.rmsnorm(residual.index_select(0, meta.logit_idx), w0.final_norm, cfg.norm_eps)
-        return [ops.skinny_gemm(hf, w.lm_head_p, 1, max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
+        return [ops.skinny_gemm(hf, w.lm_head_p, 1,
+                                max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
                 for w in ws]
 
     @staticmethod

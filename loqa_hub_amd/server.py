@@ -91,11 +91,11 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
     from .engine.llm_engine import LLMEngine
     from .engine.pipeline import VoicePipeline
     from .engine.stt_engine import STTEngine
-    from .models.configs import llama_config, whisper_config
+    from .models.configs import llama_config
     from .streaming.components import tts_options_from
     from .transport.voice_processor import GPUVoiceProcessor
     g = cfg.gpu
-    scfg, lcfg = whisper_config(g.stt_model), llama_config(g.llm_model)
+    scfg, lcfg = g.stt_config(), g.llm_config()
     sw = lw = None
     if g.stt_checkpoint or (g.llm_checkpoint and llm is None):
         from .models import loader

@@ -104,7 +104,8 @@ def main() -> int:
            "rank_step_ms_local_collectives": round(step_ms, 3),
            "rank_step_weight_TBps": round(shard_bytes / (step_ms * 1e-3) / 1e12, 2),
            "collectives_per_step": n_coll, "xgmi_us_per_collective": [lo, hi],
-           "projected_step_ms": [round(step_ms + n_coll * lo / 1e3, 3), round(step_ms + n_coll * hi / 1e3, 3)],
+           "projected_step_ms": [round(step_ms + n_coll * lo / 1e3, 3),
+                                 round(step_ms + n_coll * hi / 1e3, 3)],
            "init_s": round(t_init, 1)}
     print(json.dumps(out), flush=True)
     return 0

@@ -75,3 +75,52 @@ def test_broadcast_state_gloo(tmp_path):
     assert a.keys() == b.keys() and len(a) == 8
     for k in a:
         assert a[k].dtype == b[k].dtype and torch.equal(a[k], b[k]), k
+
+
+def test_checkpoint_config_json_cpu(tmp_path):
+    """A checkpoint's config.json (Hugging Face keys) sets the model shape:
+    Llama-3.2-style with llama3 RoPE scaling, and Whisper; GPUConfig prefers it
+    over the named model."""
+    import json as _json
+
+    import pytest
+    import math
+
+    from loqa_hub_amd.config import GPUConfig
+    from loqa_hub_amd.models.configs import (checkpoint_config, llama_config,
+                                             llama_config_from_hf, whisper_config,
+                                             whisper_config_from_hf)
+    from loqa_hub_amd.ops.reference import rope_cos_sin
+    d = {"hidden_size": 2048, "num_hidden_layers": 16, "num_attention_heads": 32,
+         "num_key_value_heads": 8, "intermediate_size": 8192, "vocab_size": 128256,
+         "rope_theta": 500000.0, "rms_norm_eps": 1e-5, "tie_word_embeddings": True,
+         "max_position_embeddings": 131072,
+         "rope_scaling": {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                          "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}}
+    c = llama_config_from_hf(d, "x")
+    ref = llama_config("llama3.2-1b")
+    for k in ("d_model", "n_layers", "n_heads", "n_kv_heads", "head_dim", "ffn_dim", "vocab_size",
+              "rope_theta", "tie_embeddings", "rope_scaling"):
+        assert getattr(c, k) == getattr(ref, k), k
+    # scaled table: short wavelengths untouched, long ones slowed 32x
+    plain = rope_cos_sin(64, 16, 500000.0)
+    sc = rope_cos_sin(64, 16, 500000.0, scaling=c.rope_scaling)
+    assert torch.equal(sc[:, 0], plain[:, 0])
+    ang_p, ang_s = math.atan2(plain[1, -1, 1], plain[1, -1, 0]), math.atan2(sc[1, -1, 1], sc[1, -1, 0])
+    assert abs(ang_s * 32 - ang_p) < 1e-6
+    with pytest.raises(ValueError):
+        llama_config_from_hf(dict(d, rope_scaling={"type": "yarn", "factor": 4.0}))
+    w = {"num_mel_bins": 128, "d_model": 1280, "encoder_layers": 32, "decoder_layers": 32,
+         "encoder_attention_heads": 20, "vocab_size": 51866, "encoder_ffn_dim": 5120,
+         "max_source_positions": 1500, "max_target_positions": 448}
+    assert whisper_config_from_hf(w, "whisper-large-v3") == whisper_config("whisper-large-v3")
+    os.makedirs(tmp_path / "ck")
+    with open(tmp_path / "ck" / "config.json", "w") as fh:
+        _json.dump(d, fh)
+    assert checkpoint_config(str(tmp_path / "ck")) == d
+    assert checkpoint_config(str(tmp_path / "ck" / "model.safetensors")) == d
+    assert checkpoint_config(str(tmp_path)) is None
+    g = GPUConfig(llm_model="tinyllama", llm_checkpoint=str(tmp_path / "ck"))
+    assert g.llm_config().d_model == 2048 and g.llm_config().rope_scaling == (32.0, 1.0, 4.0, 8192)
+    assert GPUConfig(llm_model="tinyllama").llm_config() == llama_config("tinyllama")
+    assert GPUConfig(stt_model="whisper-base").stt_config() == whisper_config("whisper-base")

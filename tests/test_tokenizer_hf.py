@@ -233,13 +233,18 @@ def test_hub_processor_uses_checkpoint_and_tokenizer_cpu(tmp_path):
     w = LlamaWeights(llama_config("test-tiny"), torch.device("cpu"), seed=5)
     loader.save_llama(w, str(ck / "model.safetensors"))
     _byte_level(str(ck))
+    with open(ck / "config.json", "w") as fh:     # the shape comes from the checkpoint
+        json.dump({"hidden_size": 256, "num_hidden_layers": 2, "num_attention_heads": 4,
+                   "num_key_value_heads": 2, "intermediate_size": 512, "vocab_size": 4096,
+                   "tie_word_embeddings": True, "max_position_embeddings": 2048}, fh)
 
     async def go():
-        cfg = cfgmod.load({"HUB_STT_MODEL": "test-whisper", "HUB_LLM_MODEL": "test-tiny",
+        cfg = cfgmod.load({"HUB_STT_MODEL": "test-whisper", "HUB_LLM_MODEL": "llama3-8b",
                            "HUB_MAX_BATCH": "2", "HUB_USE_GRAPHS": "false",
                            "HUB_LLM_CHECKPOINT": str(ck), "HUB_TTS_BACKEND": "none"})
         proc = build_gpu_processor(cfg, None, device="cpu", bridge=False)
         eng = proc.pipeline.llm
+        assert eng.cfg.d_model == 256 and eng.cfg.n_layers == 2   # not the named llama3-8b
         assert isinstance(eng.tok, HFTokenizer)
         assert torch.equal(eng.weights.layers[0]["wqkv"].float(), w.layers[0]["wqkv"].float())
         pcm = np.random.default_rng(0).standard_normal(16000).astype(np.float32) * 0.1
