@@ -204,6 +204,9 @@ class GPUConfig:
     use_graphs: bool = True
     seed: int = 0
     tp_fallback_model: str = "llama3-8b"   # a failed TP group degrades to this ("none": off)
+    # the fallback's weights (+ tokenizer in / beside it); required when
+    # llm_checkpoint is set (no silent swap to a random-init model)
+    tp_fallback_checkpoint: str = ""
     stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
     llm_checkpoint: str = ""
     # tokenizer.json of a checkpoint ("": the one in / beside the checkpoint;
@@ -217,6 +220,14 @@ class GPUConfig:
         from .models.configs import checkpoint_config, llama_config, llama_config_from_hf
         d = checkpoint_config(self.llm_checkpoint)
         return llama_config_from_hf(d, self.llm_model) if d else llama_config(self.llm_model)
+
+    def tp_fallback_config(self):
+        """Shape of the TP failover engine: its checkpoint's config.json, else
+        ``HUB_TP_FALLBACK_MODEL``."""
+        from .models.configs import checkpoint_config, llama_config, llama_config_from_hf
+        d = checkpoint_config(self.tp_fallback_checkpoint)
+        return llama_config_from_hf(d, self.tp_fallback_model) if d else \
+            llama_config(self.tp_fallback_model)
 
     def stt_config(self):
         """As ``llm_config`` for the Whisper checkpoint / ``HUB_STT_MODEL``."""
@@ -377,6 +388,7 @@ def load(env=None) -> Config:
             use_graphs=env_bool(e, True, "HUB_USE_GRAPHS"),
             seed=env_int(e, 0, "HUB_SEED"),
             tp_fallback_model=env_str(e, "llama3-8b", "HUB_TP_FALLBACK_MODEL"),
+            tp_fallback_checkpoint=env_str(e, "", "HUB_TP_FALLBACK_CHECKPOINT"),
             stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
             llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
             stt_tokenizer=env_str(e, "", "HUB_STT_TOKENIZER"),

@@ -668,11 +668,14 @@ class LLMEngine:
         t_end = 0.0
         while self._running:
             idle = not live and not waiting and not prefilling
-            items = self._next_items(idle)
-            if items is None:          # TP follower: the leader stopped
-                break
-            waiting += [it for it in items if it is not None]
             try:
+                # inside the try: a leader's heartbeat check or control-ring
+                # publish raises CollectiveError here, and that must reach the
+                # fail-all + _tp_fail path below (an idle hub's follower death)
+                items = self._next_items(idle)
+                if items is None:          # TP follower: the leader stopped
+                    break
+                waiting += [it for it in items if it is not None]
                 new: list[GenRequest] = []
                 active = len(live) + len(prefilling)
                 while waiting and active + len(new) + len(waiting[0][0]) <= cap:
@@ -695,7 +698,9 @@ class LLMEngine:
                             pl.admit(r)
                     live += inl
                     new = [r for r in new if len(r.feed) > self.inline_prefill]
-                if new and self.chunk_prefill > 0:
+                if new and self.chunk_prefill > 0 and not getattr(self.weights, "compact", False):
+                    # (compact weights keep only the fused decode copies: their
+                    # prompts go through _prefill_fused below, not a mixed pass)
                     for r in new:
                         r.chunk_total = len(r.feed)   # type: ignore[attr-defined]
                     prefilling += new

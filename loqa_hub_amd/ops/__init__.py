@@ -1544,7 +1544,21 @@ def gemm_sk_plan(M: int, N: int, K: int, epi: str = "bf16",
     return best
 
 
+_SK_WS_GRAPHS: list = []   # workspaces owned by captured graphs (never reused)
+
+
 def _sk_workspace(dev: torch.device, stream: int, floats: int, tiles: int):
+    """Split-K partials + arrival counters (zero on entry; each tile's reducer
+    re-zeroes its own). Eager launches share one growing workspace per stream
+    (stream order serialises them). A launch being CAPTURED gets a workspace of
+    its own that lives as long as the process: a shared one could be regrown
+    by a later capture, freeing memory an earlier graph still replays into,
+    and two graphs replayed on different streams would race on it."""
+    if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        ws = (torch.empty(floats, dtype=torch.float32, device=dev),
+              torch.zeros(tiles, dtype=torch.int32, device=dev))
+        _SK_WS_GRAPHS.append(ws)
+        return ws
     key = (dev, stream)
     ws = _SK_WS.get(key)
     if ws is None or ws[0].numel() < floats or ws[1].numel() < tiles:

@@ -107,14 +107,26 @@ class TPFailover:
     fits beside the 70B shard in 288 GB) on a thread of its own and swaps it
     into the voice pipeline; until then every utterance fails fast. The
     fallback decodes eagerly (no graph capture while the STT engine serves).
-    ``stats``: ``tp_degraded`` (1 once failed), ``tp_fallback_ready``."""
+    ``stats``: ``tp_degraded`` (1 once failed), ``tp_fallback_ready``.
+
+    Weights: ``checkpoint`` (``HUB_TP_FALLBACK_CHECKPOINT``, with the tokenizer
+    in / beside it or ``tokenizer``) loads a real model. Without one the
+    fallback is the seeded random-init model, which is only acceptable when the
+    TP group itself serves random-init weights: ``require_checkpoint`` (set by
+    the hub when ``HUB_LLM_CHECKPOINT`` is) makes the failover fail CLOSED -
+    utterances keep failing with the STT-failed reply and
+    ``tp_fallback_refused`` is set - instead of publishing a random model's
+    commands on ``loqa.devices.commands.*``."""
 
     def __init__(self, processor, lcfg, device, *, seed: int = 0, max_seqs: int = 64,
-                 max_seq_len: int = 1024, block_size: int = 16, build=None):
+                 max_seq_len: int = 1024, block_size: int = 16, build=None,
+                 checkpoint: str = "", tokenizer=None, require_checkpoint: bool = False):
         self.processor, self.lcfg, self.device = processor, lcfg, device
         self.kw = dict(seed=seed, max_seqs=max_seqs, max_seq_len=max_seq_len,
                        block_size=block_size, use_graphs=False)
         self._build = build
+        self.checkpoint, self.tokenizer = checkpoint, tokenizer
+        self.require_checkpoint = require_checkpoint
         self.error = ""
         self.t_failed = 0.0
         self.ready = threading.Event()
@@ -133,6 +145,13 @@ class TPFailover:
         st = self.processor.stats
         st["tp_degraded"] = 1
         st["tp_fallback_ready"] = 0
+        if self._build is None and self.require_checkpoint and not self.checkpoint:
+            st["tp_fallback_refused"] = 1
+            log.error("tensor-parallel group failed (%s) and no fallback checkpoint is set "
+                      "(HUB_TP_FALLBACK_CHECKPOINT): the primary serves a checkpoint, so the hub "
+                      "will not fall back to random-init weights - utterances fail until restart",
+                      err)
+            return
         log.error("tensor-parallel group failed (%s): serving falls back to %s on %s",
                   err, self.lcfg.name, self.device)
         threading.Thread(target=self._swap, name="tp-failover", daemon=True).start()
@@ -143,7 +162,14 @@ class TPFailover:
                 eng = self._build()
             else:
                 from ..engine.llm_engine import LLMEngine
-                eng = LLMEngine(self.lcfg, self.device, **self.kw)
+                weights, tok = None, self.tokenizer
+                if self.checkpoint:
+                    from ..engine.tokenizer import find_tokenizer, load_tokenizer
+                    from ..models import loader
+                    weights = loader.load_llama(self.lcfg, self.checkpoint, self.device)
+                    if tok is None and find_tokenizer(self.checkpoint):
+                        tok = load_tokenizer(self.checkpoint, self.lcfg.vocab_size)
+                eng = LLMEngine(self.lcfg, self.device, weights=weights, tokenizer=tok, **self.kw)
             old = self.processor.pipeline.llm
             self.processor.pipeline.llm = eng
             self.processor.stats["tp_fallback_ready"] = 1

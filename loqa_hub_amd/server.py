@@ -91,7 +91,6 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
     from .engine.llm_engine import LLMEngine
     from .engine.pipeline import VoicePipeline
     from .engine.stt_engine import STTEngine
-    from .models.configs import llama_config
     from .streaming.components import tts_options_from
     from .transport.voice_processor import GPUVoiceProcessor
     g = cfg.gpu
@@ -124,9 +123,11 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
     if llm.tp.world > 1 and g.tp_fallback_model != "none":
         # a failed TP group degrades to a single-GPU engine
         from .parallel.tp_serving import TPFailover
-        proc.tp_failover = TPFailover(proc, llama_config(g.tp_fallback_model), device, seed=g.seed,
+        proc.tp_failover = TPFailover(proc, g.tp_fallback_config(), device, seed=g.seed,
                                       max_seqs=g.max_batch, max_seq_len=g.max_seq_len,
-                                      block_size=g.kv_block).attach(llm)
+                                      block_size=g.kv_block,
+                                      checkpoint=g.tp_fallback_checkpoint,
+                                      require_checkpoint=bool(g.llm_checkpoint)).attach(llm)
     return proc
 
 

@@ -584,6 +584,33 @@ def test_llm_compact_weights_match_default_cpu():
         assert len(a["commands"]) == len(b["commands"]) == 2
 
 
+def test_llm_compact_weights_scheduler_cpu():
+    """compact weights keep no row-major prompt-pass copies, so the
+    continuous-batching scheduler must not send their prompts (> 64 tokens,
+    the default inline limit) into a mixed pass (model.forward -> KeyError);
+    they go through the fused chunked prefill and produce the same outputs
+    as generate()."""
+    import json
+
+    from loqa_hub_amd.engine.grammar import multi_command_schema
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    cfg = llama_config("test-tiny")
+    eng = LLMEngine(cfg, torch.device("cpu"), seed=4, max_seqs=4, max_seq_len=512,
+                    use_graphs=False, compact=True)
+
+    def reqs():
+        return [GenRequest(list(range(10, 10 + 90 + 9 * i)),
+                           multi_command_schema(1 + i, min_response_tokens=2)) for i in range(3)]
+    ref = [r.output for r in eng.generate(reqs())]
+    try:
+        got = eng.submit_batch(reqs()).result(timeout=120)
+    finally:
+        eng.stop()
+    assert [r.output for r in got] == ref
+    assert [len(json.loads(o)["commands"]) for o in ref] == [1, 2, 3]
+
+
 def test_step_meta_native_matches_python():
     """One-call step metadata (native) against the Python twin."""
     from loqa_hub_amd.engine.kv_cache import NativeBlockPool

@@ -257,3 +257,115 @@ def test_tp_follower_death_fails_over(tmp_path):
     assert res["stats"]["tp_degraded"] == 1 and res["stats"]["tp_fallback_ready"] == 1
     assert res["outs"] == ref                 # the fallback serves correct parses
     print(res["wave1_error"], round(res["detect_s"], 2), res["stats"])
+
+
+def _idle_death_worker(rank, world, port, out_dir):
+    """Rank 1 follows for a moment and dies while the leader is IDLE (nothing
+    submitted): only the leader's heartbeat check can notice. The failover is
+    configured fail-closed (the primary "serves a checkpoint", no fallback
+    checkpoint is set), so it must refuse to swap in random-init weights."""
+    import datetime
+    import threading
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=30))
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import TPGroup
+    from loqa_hub_amd.parallel.tp_control import TPControl
+    from loqa_hub_amd.parallel.tp_serving import TPFailover
+    cfg = llama_config("test-tiny")
+    tp = TPGroup(rank, world, dist.group.WORLD)
+    eng = LLMEngine(cfg, "cpu", max_seqs=4, max_seq_len=256, tp=tp, seed=5)
+    eng.tp_ctl = TPControl(rank, world, f"idle{port}", dist.group.WORLD)
+    eng.tp_ctl.start_heartbeat(0.05)
+    eng.tp_follower_timeout = 1.0
+    if rank != 0:
+        threading.Thread(target=lambda: (time.sleep(1.0), os._exit(9)), daemon=True).start()
+        eng.follow()
+        os._exit(0)
+
+    class Pipe:
+        llm = eng
+
+    class Proc:
+        pipeline = Pipe()
+        stats = {}
+    proc = Proc()
+    fo = TPFailover(proc, cfg, "cpu", seed=5, max_seqs=4, max_seq_len=256,
+                    require_checkpoint=True).attach(eng)
+    eng.start()                       # the scheduler idles, checking heartbeats
+    t0 = time.monotonic()
+    while not proc.stats.get("tp_degraded") and time.monotonic() - t0 < 60:
+        time.sleep(0.05)
+    res = {"detect_s": time.monotonic() - t0, "stats": dict(proc.stats),
+           "sched_alive": eng._sched.is_alive() if eng._sched else False,
+           "fatal": type(getattr(eng, "_fatal", None)).__name__}
+    try:
+        eng.submit_batch(_prompt_reqs(eng)[:1]).result(timeout=5)
+        res["late_ok"] = True
+    except Exception as e:  # noqa: BLE001
+        res["late_error"] = type(e).__name__
+    time.sleep(0.3)
+    res["ready"] = fo.ready.is_set()
+    res["same_engine"] = proc.pipeline.llm is eng
+    with open(os.path.join(out_dir, "idle.json"), "w") as f:
+        json.dump(res, f)
+    sys.stdout.flush()
+    os._exit(0)
+
+
+def test_tp_idle_follower_death_detected_and_fails_closed(tmp_path):
+    """a follower that dies while the leader idles is caught by the
+    heartbeat check inside the scheduler's try (the scheduler thread does not
+    die with the CollectiveError): the group is marked failed, later
+    submissions fail fast, and a failover that would have to invent random
+    weights for a checkpoint-serving hub refuses to."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_death_worker, args=(r, 2, port, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert procs[1].exitcode == 9
+    res = json.load(open(tmp_path / "idle.json"))
+    assert res["stats"].get("tp_degraded") == 1, res
+    assert res["fatal"] == "CollectiveError" and not res["sched_alive"], res
+    assert res["late_error"] == "CollectiveError", res
+    assert res["stats"].get("tp_fallback_refused") == 1 and not res["ready"], res
+    assert res["same_engine"], res
+
+
+def test_tp_failover_loads_fallback_checkpoint(tmp_path):
+    """HUB_TP_FALLBACK_CHECKPOINT: the failover engine carries the checkpoint's
+    weights, not the seeded random init."""
+    from loqa_hub_amd.models import loader
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import LlamaWeights
+    from loqa_hub_amd.parallel.tp_serving import TPFailover
+    cfg = llama_config("test-tiny")
+    w = LlamaWeights(cfg, "cpu", seed=77)
+    path = str(tmp_path / "fb.safetensors")
+    loader.save_llama(w, path)
+
+    class Pipe:
+        llm = None
+
+    class Proc:
+        pipeline = Pipe()
+        stats = {}
+    proc = Proc()
+    fo = TPFailover(proc, cfg, "cpu", seed=5, max_seqs=4, max_seq_len=256, checkpoint=path,
+                    require_checkpoint=True)
+    fo.on_failure(RuntimeError("test"))
+    assert fo.ready.wait(120)
+    eng = proc.pipeline.llm
+    assert torch.equal(eng.weights.embed, w.embed)
+    assert not torch.equal(eng.weights.embed, LlamaWeights(cfg, "cpu", seed=5).embed)
+    assert proc.stats["tp_fallback_ready"] == 1 and "tp_fallback_refused" not in proc.stats
