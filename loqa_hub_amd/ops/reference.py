@@ -515,3 +515,81 @@ def init_uniform4(rows: int, cols: int, ld: int, row0: int, col0: int, s: int,
         h = _fmix32((idx * 4 + k + s) & 0xFFFFFFFF)
         acc += (h >> 8).to(torch.float32) * (1.0 / 16777216.0)
     return ((acc - 2.0) * torch.tensor(scale, dtype=torch.float32)).to(torch.bfloat16)
+
+
+# ------------------------------------------------------------ whole models
+def _causal_attn(q, k, v, G: int, scale: float, q0: int = 0):
+    """q [T, H, D], k / v [L, Hkv, D] (fp32); query i sits at position q0 + i."""
+    k = k.repeat_interleave(G, dim=1)
+    v = v.repeat_interleave(G, dim=1)
+    s = torch.einsum("qhd,khd->hqk", q, k) * scale
+    qpos = torch.arange(q.shape[0], device=q.device) + q0
+    kpos = torch.arange(k.shape[0], device=q.device)
+    s = s.masked_fill(kpos[None, None, :] > qpos[None, :, None], float("-inf"))
+    return torch.einsum("hqk,khd->qhd", torch.softmax(s, dim=-1), v)
+
+
+@torch.no_grad()
+def llama_forward_ref(w, tokens: list[int]) -> torch.Tensor:
+    """fp32 forward of a whole Llama model (``LlamaWeights``, unsharded, with
+    its row-major layer copies) over one sequence at positions 0..T-1; returns
+    fp32 logits [T, V]. Every weight is the model's own bf16 tensor upcast:
+    the oracle of the fused bf16 decode path (tests/test_engine_gpu.py)."""
+    cfg = w.cfg
+    H, Hkv, D, F = w.h, w.hkv, cfg.head_dim, w.f
+    dev = w.embed.device
+    t = torch.tensor(tokens, dtype=torch.long, device=dev)
+    T = t.numel()
+    cs = w.cos_sin[:T].float()
+
+    def rms(x, g):
+        return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + cfg.norm_eps) * g.float()
+    x = w.embed[t].float()
+    for L in w.layers:
+        h = rms(x, L["attn_norm"])
+        qkv = h @ L["wqkv"].float().t()
+        q = apply_rope(qkv[:, : H * D].view(T, H, D), cs)
+        k = apply_rope(qkv[:, H * D:(H + Hkv) * D].view(T, Hkv, D), cs)
+        v = qkv[:, (H + Hkv) * D:].view(T, Hkv, D)
+        a = _causal_attn(q, k, v, H // Hkv, 1.0 / math.sqrt(D)).reshape(T, H * D)
+        x = x + a @ L["wo"].float().t()
+        gu = rms(x, L["mlp_norm"]) @ L["w_gate_up"].float().t()
+        x = x + (torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]) @ L["w_down"].float().t()
+    return rms(x, w.final_norm) @ w.lm_head.float().t()
+
+
+@torch.no_grad()
+def whisper_decoder_ref(w, tokens: list[int], enc: torch.Tensor) -> torch.Tensor:
+    """fp32 Whisper decoder (``WhisperWeights``) over one sequence at positions
+    0..T-1 with cross-attention over the encoder states ``enc`` [T_enc, d];
+    returns fp32 logits [T, vocab] (tied embedding)."""
+    cfg = w.cfg
+    d, H, D = cfg.d_model, cfg.n_heads, cfg.head_dim
+    dev = w.tok_embed.device
+    t = torch.tensor(tokens, dtype=torch.long, device=dev)
+    T = t.numel()
+    e = enc.float()
+
+    def ln(x, g, b):
+        return torch.nn.functional.layer_norm(x, (d,), g.float(), b.float(), 1e-5)
+
+    def lin(x, W, b):
+        return x @ W.float().t() + b.float()
+
+    def gelu(x):
+        return 0.5 * x * (1.0 + torch.erf(x * 0.70710678118654752))
+    x = w.tok_embed[t].float() + w.dec_pos[:T].float()
+    sc = 1.0 / math.sqrt(D)
+    for L in w.dec:
+        qkv = lin(ln(x, L["ln1_w"], L["ln1_b"]), L["wqkv"], L["bqkv"])
+        q, k, v = (qkv[:, i * d:(i + 1) * d].view(T, H, D) for i in range(3))
+        x = x + lin(_causal_attn(q, k, v, 1, sc).reshape(T, d), L["wo"], L["bo"])
+        q = lin(ln(x, L["lnx_w"], L["lnx_b"]), L["xq"], L["xq_b"]).view(T, H, D)
+        kv = lin(e, L["xkv"], L["xkv_b"])
+        Te = e.shape[0]
+        k, v = kv[:, :d].view(Te, H, D), kv[:, d:].view(Te, H, D)
+        p = torch.softmax(torch.einsum("qhd,khd->hqk", q, k) * sc, dim=-1)
+        x = x + lin(torch.einsum("hqk,khd->qhd", p, v).reshape(T, d), L["xo"], L["xo_b"])
+        x = x + lin(gelu(lin(ln(x, L["ln2_w"], L["ln2_b"]), L["fc1"], L["fc1_b"])), L["fc2"],
+                    L["fc2_b"])
+    return ln(x, w.dec_ln_w, w.dec_ln_b) @ w.tok_embed.float().t()

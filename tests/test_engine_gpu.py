@@ -513,3 +513,116 @@ def test_stt_suppression_checkpoint_tokenizer_gpu(tmp_path):
     allowed = set(tok.sampling_mask(keep=(eng.eot,)).nonzero().flatten().tolist())
     toks = [t for r in reqs for t in r.tokens]
     assert toks and set(toks) <= allowed
+
+
+def _rel_max(a: torch.Tensor, b: torch.Tensor) -> float:
+    return float((a - b).abs().max() / b.abs().max())
+
+
+def test_llama3_8b_fused_graph_decode_vs_fp32_gpu():
+    """Llama-3-8B shapes (4 layers + the full 128k lm_head)
+    through the fused, graph-replayed decode step, teacher-forced for 32
+    steps after a 24-token prompt (fed 8 tokens per fused step), against an
+    fp32 torch forward on the same weights (ops.reference.llama_forward_ref):
+    every step's logits within 2e-2 of the fp32 logits' max (relative), and
+    the greedy choice equal except at near-ties."""
+    from loqa_hub_amd.ops import reference as ref
+    cfg = llama_config("llama3-8b", n_layers=4)
+    eng = LLMEngine(cfg, "cuda", seed=3, max_seqs=2, max_seq_len=256, use_graphs=True)
+    w, P, STEPS = eng.weights, 24, 32
+    g = torch.Generator().manual_seed(7)
+    toks = torch.randint(3, cfg.vocab_size, (P + STEPS,), generator=g).tolist()
+    r = GenRequest(toks[:P], [])
+    r.seq_id = 1
+    eng.kv.pool.add_seq(1, [])
+
+    def fused(feed, dev=None):
+        max_q, _, host = eng._meta([r], [feed], True, 1, 16)
+        if dev is None:
+            dev = eng._to_device(host)
+        else:
+            for k, a in host.items():
+                dev[k].copy_(torch.from_numpy(a))
+        return dev, eng._build_meta(dev, max_q, 256, True)
+    for c in range(0, P, 8):                     # the prompt, 8 rows per fused step
+        _, meta = fused(toks[c:c + 8])
+        eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+    dev, meta = fused([toks[P]])                 # step 0 (runs once here as the warm-up)
+    eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+    errs, agree = [], 0
+    for s in range(STEPS):
+        if s > 0:
+            fused([toks[P + s]], dev)
+        graph.replay()
+        torch.cuda.synchronize()
+        got = out[0].float()
+        want = ref.llama_forward_ref(w, toks[: P + s + 1])[-1]
+        errs.append(_rel_max(got, want))
+        top2 = want.topk(2).values
+        agree += int(got.argmax() == want.argmax() or float(top2[0] - top2[1]) < 2e-2 * float(
+            want.abs().max()))
+    print("llama3-8b x4 fused graph decode: max rel logit err per step", max(errs))
+    assert max(errs) <= 2e-2, errs
+    assert agree == STEPS
+
+
+def test_whisper_large_v3_fused_graph_decode_vs_fp32_gpu():
+    """Whisper-large-v3 decoder shapes (2 layers, d 1280, 20
+    heads, 51866 vocab) through the fused, graph-replayed decode step with
+    cross-attention over 1500 encoder rows, teacher-forced (the 4-token SOT
+    prompt, then 16 one-token steps), against an fp32 torch decoder on the
+    same weights (ops.reference.whisper_decoder_ref): per-step logits within
+    2e-2 relative."""
+    from loqa_hub_amd.models.whisper import decode_step_fused
+    from loqa_hub_amd.ops import reference as ref
+    cfg = whisper_config("whisper-large-v3", enc_layers=1, dec_layers=2)
+    eng = STTEngine(cfg, "cuda", seed=2, max_batch=2, use_graphs=False)
+    assert eng.fused
+    g = torch.Generator().manual_seed(5)
+    enc = torch.randn(cfg.n_audio_ctx, cfg.d_model, generator=g).to("cuda", torch.bfloat16)
+    eng.cross_kv(enc)
+    toks = list(eng.sot) + torch.randint(0, 50000, (16,), generator=g).tolist()
+    r = STTRequest(np.zeros(160, np.int16))
+    r.seq_id, r.slot = 1, 0
+    eng.kv.pool.add_seq(1, [])
+
+    def step(feed, dev=None):
+        r.feed = feed
+        max_q, host = eng._host_meta([r], 1, 16)
+        if dev is None:
+            dev = eng._dev(host)
+        else:
+            for k, a in host.items():
+                dev[k].copy_(torch.from_numpy(a))
+        return dev, max_q
+
+    def fwd(dev, max_q):
+        return decode_step_fused(eng.model, dev["tokens"], dev["positions"], dev["slots"],
+                                 dev["cu_q"], dev["ctx_lens"], dev["block_tables"], max_q,
+                                 eng.kv.k, eng.kv.v, eng.xkv, dev["enc_starts"], dev["enc_lens"],
+                                 dev["logit_idx"], eng.ws, eng.scratch, eng.self_splits,
+                                 eng.SPLIT_KEYS, eng.cross_split_keys)
+    V, n0 = cfg.vocab_size, len(eng.sot)
+    errs = []
+    dev, mq = step(toks[:n0])                     # the SOT prompt, eager
+    got = fwd(dev, mq)[0, :V].float()
+    errs.append(_rel_max(got, ref.whisper_decoder_ref(eng.weights, toks[:n0], enc)[-1]))
+    dev, mq = step([toks[n0]])                    # first one-token step (warm-up run)
+    fwd(dev, mq)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = fwd(dev, mq)
+    for s in range(n0, len(toks)):
+        if s > n0:
+            step([toks[s]], dev)
+        graph.replay()
+        torch.cuda.synchronize()
+        want = ref.whisper_decoder_ref(eng.weights, toks[: s + 1], enc)[-1]
+        errs.append(_rel_max(out[0, :V].float(), want))
+    print("whisper-large-v3 x2 fused graph decode: max rel logit err per step", max(errs))
+    assert max(errs) <= 2e-2, errs
