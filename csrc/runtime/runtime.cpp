@@ -34,6 +34,10 @@ struct Slot {
   bool busy = false;        // owned by a producer or in flight
   hipEvent_t done = nullptr;
   bool in_flight = false;
+  // stream-in mode: device mirror of the slot, filled while the relay speaks
+  int16_t* dev = nullptr;
+  int64_t flushed = 0;      // samples already copied to dev (issued on the H2D stream)
+  hipEvent_t flush_ev = nullptr;
 };
 
 struct PcmStager {
@@ -41,6 +45,8 @@ struct PcmStager {
   int64_t cap = 0;  // samples per slot
   std::mutex mu;
   hipStream_t h2d = nullptr;
+  bool own_h2d = false;     // created here (destroyed here) vs set by the caller
+  bool stream_in = false;   // per-chunk copies into the device mirrors
 };
 
 // ------------------------------------------------------------------ BlockPool
@@ -144,6 +150,7 @@ void* loqa_stager_create(int nslots, long long samples_per_slot, int own_stream)
     delete s;
     return nullptr;
   }
+  s->own_h2d = own_stream != 0;
   for (auto& sl : s->slots) {
     if (hipHostMalloc((void**)&sl.host, sizeof(int16_t) * samples_per_slot, hipHostMallocDefault) !=
             hipSuccess ||
@@ -164,9 +171,58 @@ void loqa_stager_destroy(void* h) {
   for (auto& sl : s->slots) {
     if (sl.host) hipHostFree(sl.host);
     if (sl.done) hipEventDestroy(sl.done);
+    if (sl.dev) hipFree(sl.dev);
+    if (sl.flush_ev) hipEventDestroy(sl.flush_ev);
   }
-  if (s->h2d) hipStreamDestroy(s->h2d);
+  if (s->h2d && s->own_h2d) hipStreamDestroy(s->h2d);
   delete s;
+}
+
+// Stream-in mode (SURVEY §2.4 "Host<->device data path"): every slot gets a
+// device mirror, and loqa_stager_flush copies the samples appended since the
+// last flush with hipMemcpyAsync on `stream` - a placed side stream owned by
+// the caller (utils/streams.py "h2d"), so the transfer runs while the relay is
+// still speaking and end of speech only copies the tail. Returns 0 or a HIP
+// error (a failed mirror allocation leaves the mode off).
+int loqa_stager_set_stream(void* h, hipStream_t stream, int stream_in) {
+  auto* s = static_cast<PcmStager*>(h);
+  std::lock_guard<std::mutex> g(s->mu);
+  if (s->h2d && s->own_h2d) return (int)hipErrorInvalidValue;
+  s->h2d = stream;
+  if (stream_in && !s->stream_in) {
+    for (auto& sl : s->slots) {
+      if (!sl.dev) {
+        hipError_t e = hipMalloc((void**)&sl.dev, sizeof(int16_t) * (size_t)s->cap);
+        if (e != hipSuccess) return (int)e;
+        e = hipEventCreateWithFlags(&sl.flush_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return (int)e;
+      }
+    }
+    s->stream_in = true;
+  }
+  return 0;
+}
+
+// Copy the samples appended since the last flush into the slot's device
+// mirror on the H2D stream when at least min_samples are pending. Returns the
+// samples issued (0: below the threshold or not in stream-in mode), or a
+// negative HIP error.
+long long loqa_stager_flush(void* h, int slot, long long min_samples) {
+  auto* s = static_cast<PcmStager*>(h);
+  Slot& sl = s->slots[slot];
+  if (!s->stream_in || !sl.dev) return 0;
+  const long long n = sl.len - sl.flushed;
+  if (n <= 0 || n < min_samples) return 0;
+  hipError_t e = hipMemcpyAsync(sl.dev + sl.flushed, sl.host + sl.flushed, (size_t)n * 2,
+                                hipMemcpyHostToDevice, s->h2d);
+  if (e == hipSuccess) e = hipEventRecord(sl.flush_ev, s->h2d);
+  if (e != hipSuccess) return -(long long)e;
+  sl.flushed = sl.len;
+  return n;
+}
+
+long long loqa_stager_flushed(void* h, int slot) {
+  return static_cast<PcmStager*>(h)->slots[slot].flushed;
 }
 
 // Acquire a free slot (reclaiming slots whose transfer completed). -1 if none.
@@ -182,6 +238,7 @@ int loqa_stager_acquire(void* h) {
     if (!sl.busy) {
       sl.busy = true;
       sl.len = 0;
+      sl.flushed = 0;
       return (int)i;
     }
   }
@@ -210,12 +267,32 @@ const void* loqa_stager_host_ptr(void* h, int slot) {
 // stream (then `wait_stream`, the compute stream, waits for the copy) or, with
 // no own stream, on `wait_stream` itself. The slot is recycled once the copy's
 // event has completed.
+// Stream-in mode: only the samples not yet flushed cross PCIe now (on the H2D
+// stream), `wait_stream` waits for the slot's last flush event, and the
+// mirror is copied device-to-device into dst on `wait_stream`.
 int loqa_stager_upload(void* h, int slot, void* dst, long long max_samples, hipStream_t wait_stream) {
   auto* s = static_cast<PcmStager*>(h);
   Slot& sl = s->slots[slot];
   const long long n = sl.len < max_samples ? sl.len : max_samples;
-  hipStream_t cs = s->h2d ? s->h2d : wait_stream;
   hipError_t e = hipSuccess;
+  if (s->stream_in && sl.dev && sl.flushed > 0) {   // (never flushed: the direct copy below)
+    if (n > sl.flushed) {
+      e = hipMemcpyAsync(sl.dev + sl.flushed, sl.host + sl.flushed, (size_t)(n - sl.flushed) * 2,
+                         hipMemcpyHostToDevice, s->h2d);
+      if (e == hipSuccess) e = hipEventRecord(sl.flush_ev, s->h2d);
+      if (e != hipSuccess) return (int)e;
+      sl.flushed = n;
+    }
+    if (sl.flushed > 0) e = hipStreamWaitEvent(wait_stream, sl.flush_ev, 0);
+    if (e == hipSuccess && n > 0)
+      e = hipMemcpyAsync(dst, sl.dev, (size_t)n * 2, hipMemcpyDeviceToDevice, wait_stream);
+    if (e == hipSuccess) e = hipEventRecord(sl.done, wait_stream);
+    if (e != hipSuccess) return (int)e;
+    std::lock_guard<std::mutex> g(s->mu);
+    sl.in_flight = true;
+    return 0;
+  }
+  hipStream_t cs = s->h2d ? s->h2d : wait_stream;
   if (n > 0) e = hipMemcpyAsync(dst, sl.host, (size_t)n * 2, hipMemcpyHostToDevice, cs);
   if (e != hipSuccess) return (int)e;
   e = hipEventRecord(sl.done, cs);
@@ -224,6 +301,11 @@ int loqa_stager_upload(void* h, int slot, void* dst, long long max_samples, hipS
   std::lock_guard<std::mutex> g(s->mu);
   sl.in_flight = true;
   return (int)e;
+}
+
+// Plain async H2D copy (a slot chain's host-buffered tail).
+int loqa_memcpy_h2d_async(void* dst, const void* src, long long nbytes, hipStream_t stream) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, stream);
 }
 
 void loqa_stager_release(void* h, int slot) {

@@ -255,6 +255,12 @@ class ArbitrationConfig:
     bridge_timeout: float = 2.0
     confirmation_enabled: bool = False
     relay_groups: dict = field(default_factory=dict)  # relay id -> room/group
+    # per_relay_group scope: a relay whose group (static ARBITRATION_RELAY_GROUPS
+    # map) has no other member cannot collide, so it wins at once instead of
+    # waiting out the window ("Single relay: No additional latency (bypass
+    # arbitration)", reference docs/COLLISION_DETECTION.md:203; the reference's
+    # code always waits, audio_service.go:443,494-502, hence opt-in)
+    single_relay_bypass: bool = False
 
 
 @dataclass
@@ -402,6 +408,7 @@ def load(env=None) -> Config:
             bridge_timeout=env_duration(e, 2.0, "BRIDGE_TIMEOUT"),
             confirmation_enabled=env_bool(e, False, "CONFIRMATION_ENABLED"),
             relay_groups=parse_relay_groups(env_str(e, "", "ARBITRATION_RELAY_GROUPS")),
+            single_relay_bypass=env_bool(e, False, "ARBITRATION_SINGLE_RELAY_BYPASS"),
         ),
     )
     try:

@@ -36,7 +36,9 @@ class PipelineJob:
     relay_id: str
     request_id: str
     pcm: np.ndarray
-    transcript_hint: str | None = None     # synthetic ground truth (teacher forcing)
+    # synthetic ground truth (teacher forcing); a list = one text per 30 s
+    # window of a long-form utterance
+    transcript_hint: str | list | None = None
     staged: object = None                  # pinned PCM slot with the samples (relay path)
     on_tokens: object = None               # streaming hook: called with each step's token ids
     # results
@@ -54,6 +56,13 @@ class PipelineJob:
     @property
     def n_commands(self) -> int:
         return len(self.multi.commands) if self.multi else 0
+
+
+def _stt_request(j: PipelineJob) -> STTRequest:
+    h = j.transcript_hint
+    if isinstance(h, (list, tuple)):
+        return STTRequest(j.pcm, transcript=" ".join(h), transcript_windows=list(h), staged=j.staged)
+    return STTRequest(j.pcm, transcript=h, staged=j.staged)
 
 
 class VoicePipeline:
@@ -104,7 +113,7 @@ class VoicePipeline:
             # the samples were produced on the default stream (e.g. an RCCL scatter)
             cur = torch.cuda.current_stream(device_pcm.device)
             cur.wait_stream(torch.cuda.default_stream(device_pcm.device))
-        reqs = [STTRequest(j.pcm, transcript=j.transcript_hint, staged=j.staged) for j in jobs]
+        reqs = [_stt_request(j) for j in jobs]
         self.stt.transcribe(reqs, device_pcm)
         for j, r in zip(jobs, reqs):
             self._stt_post(j, r)
@@ -239,7 +248,7 @@ class VoicePipeline:
         owner = {}
         for j, f in batch:
             j.t["start"] = j.t.get("start", t0)
-            r = STTRequest(j.pcm, transcript=j.transcript_hint, staged=j.staged)
+            r = _stt_request(j)
             reqs.append(r)
             owner[id(r)] = (j, f)
         self.stats["stt_batches"] += 1

@@ -11,6 +11,7 @@ of the same length; only the fed-back token is the reference one.
 """
 from __future__ import annotations
 
+import logging
 import os
 import queue
 import threading
@@ -29,19 +30,37 @@ from .batching import join_futures, plan_step
 from .kv_cache import PagedKVCache
 from .tokenizer import get_tokenizer
 
+log = logging.getLogger("loqa.stt")
+
 N_SAMPLES = 480000  # 30 s @ 16 kHz
 # numpy PCM of direct submissions staged through the pinned stager (False: a
 # one-off pinned tensor copy per request)
 PCM_STAGER = True
+# relay PCM copied to HBM chunk by chunk while the relay speaks (pcm_staging.py)
+PCM_STREAM_IN = os.environ.get("LOQA_PCM_STREAM_IN", "1") != "0"
+# long-form audio: an utterance longer than 30 s is split into
+# 30 s windows, encoded as extra encoder rows of the same batch (one
+# cross-attention slot each) and decoded window after window, each window's
+# decode prompted with the previous window's text (<|startofprev|>, at most
+# PREV_TOKENS tokens, fed 4 per step like the SOT prompt); the texts are joined.
+MAX_WINDOWS = int(os.environ.get("LOQA_STT_MAX_WINDOWS", "20"))
+PREV_TOKENS = int(os.environ.get("LOQA_STT_PREV_TOKENS", "32"))
+
+
+def n_windows(n_samples: int) -> int:
+    return max(1, min(MAX_WINDOWS, -(-n_samples // N_SAMPLES)))
 
 
 @dataclass(eq=False)
 class STTRequest:
     pcm: np.ndarray                   # int16 samples @ 16 kHz
     transcript: str | None = None     # teacher-forcing target (synthetic mode)
-    max_new_tokens: int = 96
+    max_new_tokens: int = 96          # per 30 s window
     staged: object = None             # pinned PCM slot (engine/pcm_staging.py) holding the samples
-    n_samples: int = 0                # samples uploaded (<= 30 s)
+    n_samples: int = 0                # samples uploaded (<= MAX_WINDOWS x 30 s)
+    # teacher-forcing targets per 30 s window of a long-form utterance (else
+    # ``transcript`` is split over the windows by words)
+    transcript_windows: list | None = None
     # outputs
     text: str = ""
     sumsq: float = 0.0
@@ -58,6 +77,14 @@ class STTRequest:
     feed: list[int] = field(default_factory=list)
     step: int = 0
     on_done: object = None
+    # long-form state (engine-owned): windows, the one being decoded, their
+    # cross-attention slots, finished windows' texts / tokens, prompt steps
+    windows: int = 1
+    win: int = 0
+    slots: list = field(default_factory=list)
+    win_texts: list = field(default_factory=list)
+    prev_tokens: list = field(default_factory=list)
+    prompt_steps: int = 1
 
 
 class STTEngine:
@@ -93,6 +120,11 @@ class STTEngine:
         self.sot = [self.tok.token_id("<|startoftranscript|>"), lang,
                     self.tok.token_id("<|transcribe|>"), self.tok.token_id("<|notimestamps|>")]
         self.eot = self.tok.token_id("<|endoftext|>")
+        self.n_prompt_tokens_per_step = len(self.sot)
+        try:
+            self.sop = self.tok.token_id("<|startofprev|>")
+        except KeyError:
+            self.sop = None     # no previous-text prompt for long-form windows
         # a checkpoint's tokenizer: greedy decoding never emits its special /
         # timestamp tokens or the generation config's suppress_tokens (as the
         # reference's STT service decodes); one packed mask row for every
@@ -181,11 +213,29 @@ class STTEngine:
         H2D stream, and this (compute) stream waits on the copies' events.
         ``device_pcm`` (already on the GPU, e.g. scattered by the DP router
         over RCCL) holds the concatenated samples and skips the copies."""
-        lens = [min(self._n_samples(r), N_SAMPLES) for r in reqs]
+        lens = []
+        for r in reqs:
+            n = self._n_samples(r)
+            w = n_windows(n)
+            if n > w * N_SAMPLES:
+                self.stats["long_form_dropped_samples"] = \
+                    self.stats.get("long_form_dropped_samples", 0) + n - w * N_SAMPLES
+                log.error("utterance of %.1f s exceeds %d windows (LOQA_STT_MAX_WINDOWS): "
+                          "the last %.1f s are not transcribed", n / 16000, MAX_WINDOWS,
+                          (n - w * N_SAMPLES) / 16000)
+            lens.append(min(n, w * N_SAMPLES))
+            r.windows = w
         for r, n in zip(reqs, lens):
             r.n_samples = n
         offs = np.zeros(len(reqs) + 1, np.int64)
         offs[1:] = np.cumsum(lens)
+        # one padded 30 s encoder row per window: a request's windows are
+        # consecutive slices of its samples, so the rows' offsets are the
+        # cumulative row lengths
+        row_lens = [min(N_SAMPLES, n - w * N_SAMPLES) for r, n in zip(reqs, lens)
+                    for w in range(r.windows)]
+        row_offs = np.zeros(len(row_lens) + 1, np.int64)
+        row_offs[1:] = np.cumsum(row_lens)
         if device_pcm is not None:
             pcm = device_pcm[: int(offs[-1])]
         elif self.is_gpu:
@@ -209,10 +259,10 @@ class STTEngine:
                 if r.staged is not None:
                     r.staged.release()
                     r.staged = None
-        off_t = torch.from_numpy(offs)
+        off_t = torch.from_numpy(row_offs)
         if self.is_gpu:
             off_t = off_t.pin_memory().to(self.device, non_blocking=True)
-        return ops.pcm16_to_f32_padded(pcm, off_t, N_SAMPLES, offs)
+        return ops.pcm16_to_f32_padded(pcm, off_t, N_SAMPLES, row_offs)
 
     @staticmethod
     def _n_samples(r: STTRequest) -> int:
@@ -226,7 +276,11 @@ class STTEngine:
         """The engine's pinned PCM stager (created on first use)."""
         if getattr(self, "stager", None) is None:
             from .pcm_staging import PcmStager
-            self.stager = PcmStager(2 * self.max_batch + 16, N_SAMPLES)
+            h2d = None
+            if PCM_STREAM_IN:
+                from ..utils.streams import placed_stream
+                h2d = placed_stream(self.device, "h2d")
+            self.stager = PcmStager(2 * self.max_batch + 16, N_SAMPLES, h2d_stream=h2d)
         return self.stager
 
     def new_pcm_slot(self):
@@ -548,11 +602,16 @@ class STTEngine:
         self._encode(reqs, slots, device_pcm)
         self._start_decode(reqs)
 
+    def rows_needed(self, reqs: list[STTRequest]) -> int:
+        """Encoder rows / cross-attention slots of ``reqs`` (one per 30 s window)."""
+        return sum(n_windows(self._n_samples(r)) for r in reqs)
+
     def _encode(self, reqs: list[STTRequest], slots: list[int],
                 device_pcm: torch.Tensor | None = None) -> None:
         """GPU half of admission (any thread with its own stream): PCM upload,
-        log-mel + encoder, cross-attention K|V into the requests' slots; returns
-        once that work is complete (the RMS read-back synchronises)."""
+        log-mel + encoder, cross-attention K|V into the requests' slots (one per
+        30 s window, in order); returns once that work is complete (the RMS
+        read-back synchronises)."""
         tr = tracer()
         dev = self.device if self.is_gpu else None
         t_enc0 = time.perf_counter()
@@ -569,24 +628,57 @@ class STTEngine:
         self.stats["encode_s"] += t1 - t0
         for r in reqs:
             r.t_enc0, r.t_enc1 = t_enc0, t1
-        for i, (r, sl) in enumerate(zip(reqs, slots)):
+        i = 0
+        for r in reqs:
+            w = r.windows
             n = max(1, r.n_samples)
-            r.sumsq = float(ss[i])
-            r.rms = float(np.sqrt(ss[i] / n))
-            r.slot = sl
+            r.sumsq = float(ss[i:i + w].sum())
+            r.rms = float(np.sqrt(r.sumsq / n))
+            r.slots = list(slots[i:i + w])
+            r.slot = r.slots[0]
+            i += w
 
     def _start_decode(self, reqs: list[STTRequest]) -> None:
         """Decoder sequences for encoded requests (scheduler thread)."""
         now = time.perf_counter()
         for r in reqs:
             r.t_dec0 = now
-            r.seq_id = self._next
-            self._next += 1
-            self.kv.pool.add_seq(r.seq_id, [])
-            r.tokens, r.step, r.feed, r.t_done = [], 0, list(self.sot), 0.0
-            r.target = None
-            if r.transcript is not None:
-                r.target = self.tok.encode(" " + r.transcript.strip())[: self.cfg.n_text_ctx - 8] + [self.eot]
+            r.t_done = 0.0
+            r.win_texts, r.prev_tokens = [], []
+            if not r.slots:
+                r.slots = [r.slot]
+            self._begin_window(r, 0)
+
+    def _window_text(self, r: STTRequest, w: int) -> str | None:
+        """Teacher-forcing text of window ``w`` (None: free decoding)."""
+        if r.transcript_windows is not None:
+            return r.transcript_windows[w] if w < len(r.transcript_windows) else ""
+        if r.transcript is None:
+            return None
+        if r.windows == 1:
+            return r.transcript
+        words = r.transcript.split()
+        per = -(-len(words) // r.windows)
+        return " ".join(words[w * per:(w + 1) * per])
+
+    def _begin_window(self, r: STTRequest, w: int) -> None:
+        """A fresh decoder sequence for window ``w`` of ``r`` over its encoder
+        rows; later windows are prompted with the previous windows' text."""
+        r.win = w
+        r.slot = r.slots[w]
+        r.seq_id = self._next
+        self._next += 1
+        self.kv.pool.add_seq(r.seq_id, [])
+        prompt = []
+        if w > 0 and self.sop is not None and r.prev_tokens and PREV_TOKENS > 0:
+            prompt = [self.sop] + r.prev_tokens[-PREV_TOKENS:]
+        r.tokens, r.step, r.feed = [], 0, prompt + list(self.sot)
+        r.prompt_steps = -(-len(r.feed) // len(self.sot))
+        r.target = None
+        text = self._window_text(r, w)
+        if text is not None:
+            room = self.cfg.n_text_ctx - 8 - len(r.feed)
+            r.target = self.tok.encode(" " + text.strip())[:room] + [self.eot]
 
     def _decode_once(self, live: list[STTRequest]) -> list[STTRequest]:
         """One decoder step over ``live`` (at most ``step_tokens`` tokens: a
@@ -613,15 +705,26 @@ class STTEngine:
             r.step += 1
             if t == self.eot or len(r.tokens) >= r.max_new_tokens or \
                     (r.target is not None and r.step >= len(r.target)):
-                done.append(self._finish(r))
+                f = self._finish(r)
+                if f is not None:
+                    done.append(f)
             else:
                 r.feed = [t]
         return done
 
-    def _finish(self, r: STTRequest) -> STTRequest:
-        r.t_done = time.perf_counter()
-        r.text = self.tok.decode([x for x in r.tokens if x != self.eot]).strip()
+    def _finish(self, r: STTRequest) -> STTRequest | None:
+        """Window ``r.win`` of ``r`` is decoded: start the next window (None)
+        or complete the request (its windows' texts joined)."""
+        toks = [x for x in r.tokens if x != self.eot]
+        r.win_texts.append(self.tok.decode(toks).strip())
+        r.prev_tokens = (r.prev_tokens + toks)[-max(PREV_TOKENS, 1):]
         self.kv.pool.free_seq(r.seq_id)
+        if r.win + 1 < r.windows:
+            self.stats["long_form_windows"] = self.stats.get("long_form_windows", 0) + 1
+            self._begin_window(r, r.win + 1)
+            return None
+        r.t_done = time.perf_counter()
+        r.text = " ".join(t for t in r.win_texts if t)
         self.stats["utterances"] += 1
         return r
 
@@ -630,8 +733,9 @@ class STTEngine:
         """Synchronous batch: encode all, decode until every request is done."""
         if not reqs:
             return reqs
-        assert len(reqs) <= self.max_batch, "batch exceeds max_batch"
-        self._admit(reqs, list(range(len(reqs))), device_pcm)
+        rows = self.rows_needed(reqs)
+        assert rows <= self.max_batch, "batch (30 s windows) exceeds max_batch"
+        self._admit(reqs, list(range(rows)), device_pcm)
         t_dec = time.monotonic()
         live, steps = list(reqs), 0
         while live:
@@ -675,11 +779,14 @@ class STTEngine:
             fut.set_exception(self._fatal)
             return fut
         reqs = list(reqs)
-        if len(reqs) > self.max_batch:
-            # admission needs a free slot for every request of an inbox item:
-            # an oversize batch would wait forever, so it goes in max_batch chunks
-            return join_futures([self.submit_batch(reqs[i:i + self.max_batch], on_done)
-                                 for i in range(0, len(reqs), self.max_batch)], reqs)
+        if len(reqs) > 1 and self.rows_needed(reqs) > self.max_batch:
+            # admission needs a free slot for every window of an inbox item: an
+            # oversize batch would wait forever, so it goes in smaller items
+            return join_futures([self.submit_batch([r], on_done) for r in reqs], reqs)
+        if self.rows_needed(reqs) > self.max_batch:
+            fut.set_exception(ValueError(f"utterance needs {self.rows_needed(reqs)} 30 s windows "
+                                         f"> max_batch {self.max_batch}"))
+            return fut
         self._inbox.put((reqs, on_done, fut))
         return fut
 
@@ -726,8 +833,10 @@ class STTEngine:
                     waiting.append(it)
             try:
                 new: list[STTRequest] = []
-                while waiting and len(waiting[0][0]) <= len(self._free_slots) - len(new):
+                n_rows = 0
+                while waiting and self.rows_needed(waiting[0][0]) <= len(self._free_slots) - n_rows:
                     reqs, cb, fut = waiting.pop(0)
+                    n_rows += self.rows_needed(reqs)
                     if not reqs:
                         fut.set_result(reqs)
                         continue
@@ -737,7 +846,7 @@ class STTEngine:
                         r.on_done = cell
                     new += reqs
                 if new:
-                    slots = [self._free_slots.pop(0) for _ in new]
+                    slots = [self._free_slots.pop(0) for _ in range(n_rows)]
                     if enc_pool is not None:
                         encoding.append((new, enc_pool.submit(self._encode, new, slots)))
                     else:
@@ -764,7 +873,7 @@ class STTEngine:
                 if live:
                     finished = pl.pump(live) if pl is not None else self._decode_once(live)
                     for r in finished:
-                        self._free_slots.append(r.slot)
+                        self._free_slots += r.slots or [r.slot]
                         self._free_slots.sort()
                         cell = r.on_done
                         if cell[3] is not None:

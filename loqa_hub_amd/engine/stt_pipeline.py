@@ -57,10 +57,16 @@ class STTPipeline:
         r.pl_end = False           # greedy: the last decided token ended the sequence
 
     def _feed(self, r):
-        """(tokens with DEV placeholders, speculative) of r's next step, or None."""
+        """(tokens with DEV placeholders, speculative) of r's next step, or None.
+        The first ``r.prompt_steps`` steps feed the prompt (the SOT tokens, after
+        a long-form window's previous-text prompt) at most len(SOT) tokens at a
+        time - the captured graphs' per-sequence query limit."""
+        c = self.eng.n_prompt_tokens_per_step
+        ps = r.prompt_steps
         k = r.pl_launched
-        if k == 0:
-            return list(r.feed), False
+        if k < ps:
+            return list(r.feed[k * c:(k + 1) * c]), False
+        k = k - ps + 1                            # 1 = the first step feeding a decoded token
         if r.target is not None:
             if k >= len(r.target):
                 return None                       # every target token is in flight / done
@@ -194,6 +200,9 @@ class STTPipeline:
                 if sp:
                     self.stats["pl_discard"] += 1
                 continue
+            k -= r.prompt_steps - 1              # token index; < 0: a prompt chunk (logits unused)
+            if k < 0:
+                continue
             t = int(r.target[k]) if r.target is not None else int(nxt[b])
             r.tokens.append(t)
             r.step += 1
@@ -202,9 +211,18 @@ class STTPipeline:
             if end:
                 r.pl_end = True
                 if r.pl_fl == 0:
-                    done.append(eng._finish(r))
+                    self._window_end(r, done)
         # a greedy request that ended while a discarded step was in flight
         for r in st.rows:
             if r.pl_end and r.pl_fl == 0 and r.t_done == 0.0 and r not in done:
-                done.append(eng._finish(r))
+                self._window_end(r, done)
         return done
+
+    def _window_end(self, r, done: list) -> None:
+        """r's current window is decoded: r completes, or (long-form) its next
+        window starts as a fresh pipelined sequence."""
+        f = self.eng._finish(r)
+        if f is not None:
+            done.append(f)
+        else:
+            self.admit(r)

@@ -99,3 +99,53 @@ def make_unique(seed: int, counts: list[int], offset: int = 0,
         seen.add(u.text)
         out.append(u)
     return out
+
+
+@dataclass
+class LongUtterance:
+    relay_id: str
+    text: str                 # full transcript
+    window_texts: list        # transcript per 30 s window (teacher forcing)
+    n_commands: int
+    pcm: np.ndarray
+    last_command_start_s: float
+
+
+def make_long_utterance(seed: int, n_commands: int = 3, seconds: float = 45.0,
+                        relay_id: str = "relay-long", sr: int = 16000) -> LongUtterance:
+    """A long-form utterance: the wake word and the first
+    commands, a long pause (low-level noise), then the LAST command after the
+    30 s mark, padded to ``seconds``. Each word's samples are known, so every
+    word is assigned to the 30 s window it starts in (``window_texts``)."""
+    rng = np.random.default_rng(seed * 7907 + 11)
+    text = utterance_text(rng, n_commands)
+    words = text.split()
+    # the last command: from the last joiner on (e.g. "and then turn off ...")
+    last = max(text.rfind(j.strip() + " ") for j in JOINERS if j.strip())
+    n_last = len(text[last:].split())
+    head, tail = words[:-n_last], words[-n_last:]
+    segs, starts = [], []
+    pos = 0
+    for w in head:
+        a = to_pcm16(speechlike(rng, 1))
+        starts.append(pos)
+        segs.append(a)
+        pos += len(a)
+    gap = int(31.5 * sr) - pos
+    if gap > 0:
+        segs.append(to_pcm16(0.003 * rng.standard_normal(gap)))
+        pos += gap
+    t_last = pos / sr
+    for w in tail:
+        a = to_pcm16(speechlike(rng, 1))
+        starts.append(pos)
+        segs.append(a)
+        pos += len(a)
+    if pos < int(seconds * sr):
+        segs.append(to_pcm16(0.003 * rng.standard_normal(int(seconds * sr) - pos)))
+    pcm = np.concatenate(segs)
+    n_win = -(-len(pcm) // (30 * sr))
+    win = [[] for _ in range(n_win)]
+    for w, st in zip(words, starts):
+        win[st // (30 * sr)].append(w)
+    return LongUtterance(relay_id, text, [" ".join(x) for x in win], n_commands, pcm, t_last)

@@ -93,6 +93,9 @@ class SyntheticTokenizer:
         # pre-split into runs of up to three); appended last so earlier ids stay
         for n in range(100):
             add(f"{n:02d}")
+        # Whisper's previous-text prompt marker (long-form windows), appended
+        # after everything else so no earlier id moves
+        add("<|startofprev|>")
         if len(strings) > vocab_size:
             raise ValueError(f"vocab_size {vocab_size} too small for the synthetic tokenizer")
         self.n_real = len(strings)

@@ -168,6 +168,10 @@ _RUNTIME_SIGS = {
     "loqa_stager_host_ptr": ([c_void_p, c_int], c_void_p),
     "loqa_stager_upload": ([c_void_p, c_int, c_void_p, c_ll, c_void_p], c_int),
     "loqa_stager_release": ([c_void_p, c_int], None),
+    "loqa_stager_set_stream": ([c_void_p, c_void_p, c_int], c_int),
+    "loqa_stager_flush": ([c_void_p, c_int, c_ll], c_ll),
+    "loqa_stager_flushed": ([c_void_p, c_int], c_ll),
+    "loqa_memcpy_h2d_async": ([c_void_p, c_void_p, c_ll, c_void_p], c_int),
     "loqa_pool_create": ([c_int, c_int], c_void_p),
     "loqa_pool_destroy": ([c_void_p], None),
     "loqa_pool_debug_hash_mask": ([c_void_p, ctypes.c_ulonglong], None),

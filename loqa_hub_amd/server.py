@@ -248,6 +248,7 @@ class HubServer:
         a = self.cfg.arbitration
         self.audio_service = AudioService(
             self.processor, window_duration=a.window, scope=a.scope, relay_groups=a.relay_groups,
+            single_relay_bypass=a.single_relay_bypass,
             end_of_speech_wait=a.end_of_speech_wait, events_store=self.events,
             audio_publisher=publisher, confirmation_enabled=a.confirmation_enabled,
             transcript_hints=self.transcript_hints)

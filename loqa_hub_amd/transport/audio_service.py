@@ -163,7 +163,7 @@ class AudioService:
                  scope: str = "global", relay_groups: dict[str, str] | None = None,
                  end_of_speech_wait: float = 5.0, result_timeout: float = 30.0,
                  events_store=None, audio_publisher=None, confirmation_enabled: bool = False,
-                 transcript_hints=None):
+                 transcript_hints=None, single_relay_bypass: bool = False):
         self.processor = processor
         self.arbitration_window_duration = window_duration
         self.scope = scope
@@ -177,15 +177,33 @@ class AudioService:
         # utterance's known transcript, which teacher-forces the random-init
         # Whisper decoder; real relays never have one
         self.transcript_hints = transcript_hints
+        # opt-in: a relay alone in its (static) group skips the window
+        # (docs/COLLISION_DETECTION.md:203 of the reference; ArbitrationConfig)
+        self.single_relay_bypass = single_relay_bypass and scope == "per_relay_group"
+        self._group_size: dict[str, int] = {}
+        for g in self.relay_groups.values():
+            self._group_size[g] = self._group_size.get(g, 0) + 1
         self.windows: dict[str, ArbitrationWindow] = {}
         self.active_streams: dict[str, RelayStream] = {}
-        self.stats = {"windows": 0, "arbitrations": 0, "cancelled": 0, "processed": 0, "late": 0}
+        self.stats = {"windows": 0, "arbitrations": 0, "cancelled": 0, "processed": 0, "late": 0,
+                      "bypassed": 0}
 
     # ------------------------------------------------------------ windows
     def window_key(self, relay_id: str) -> str:
         if self.scope == "global":
             return "global"
         return self.relay_groups.get(relay_id, relay_id)
+
+    def can_collide(self, relay_id: str) -> bool:
+        """Whether another relay could join ``relay_id``'s window: always in the
+        global scope; per group, unless the static group map leaves the
+        relay's group with no other member (an unmapped relay is its own
+        group unless some relay is mapped to a group of that name)."""
+        if self.scope == "global":
+            return True
+        key = self.window_key(relay_id)
+        members = self._group_size.get(key, 0) + (0 if relay_id in self.relay_groups else 1)
+        return members > 1
 
     @property
     def arbitration_window(self) -> ArbitrationWindow | None:
@@ -202,6 +220,13 @@ class AudioService:
         self.active_streams[relay_id] = rs
         self.windows[key] = w
         self.stats["windows"] += 1
+        if self.single_relay_bypass and not self.can_collide(relay_id):
+            # nobody can join this window: decide now (the relay wins before
+            # its next chunk is read)
+            self.stats["bypassed"] += 1
+            hublog.log_audio_processing(relay_id, "arbitration_bypassed", reason="single_relay_group")
+            self.perform_arbitration(w)
+            return w
         hublog.log_audio_processing(relay_id, "arbitration_window_started",
                                     window_duration_ms=w.window_duration * 1e3, first_relay=relay_id)
         asyncio.get_running_loop().call_later(w.window_duration, self._close_window, w)

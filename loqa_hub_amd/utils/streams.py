@@ -68,7 +68,10 @@ def aligned_pool_stream(device: torch.device, priority: int, slot: int):
 # implicit placement had depended on the STT upload drawing one pool stream per
 # batch: removing that draw moved the LLM decoder to slot 0 and halved the
 # throughput (19.1 -> 9.8 utt/s). LOQA_SLOT_<ROLE> overrides (search).
-DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3, "tts": 29}
+# The PCM stream-in copies (engine/pcm_staging.py) take the old prefill
+# worker's slot 3: a queue of their own beside the decoders (the copies run on
+# the DMA engine and hold no CU).
+DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3, "tts": 29, "h2d": 3}
 
 
 def init_pools(device: torch.device) -> None:

@@ -125,3 +125,42 @@ def test_grpc_roundtrip():
         finally:
             await server.stop(0)
     asyncio.run(go())
+
+
+def test_single_relay_group_bypasses_window():
+    """ARBITRATION_SINGLE_RELAY_BYPASS (reference docs/COLLISION_DETECTION.md:203,
+    "Single relay: No additional latency"): in the per-group scope a relay
+    whose static group has no other member wins at once, while a relay that
+    shares its room still waits out the window and collides as before."""
+    import time
+
+    async def go():
+        proc = FakeProcessor()
+        svc = AudioService(proc, window_duration=0.5, scope="per_relay_group",
+                           relay_groups={"k1": "kitchen", "k2": "kitchen", "b1": "bedroom"},
+                           single_relay_bypass=True)
+        assert not svc.can_collide("b1") and not svc.can_collide("garage-relay")
+        assert svc.can_collide("k1") and svc.can_collide("k2")
+        t0 = time.monotonic()
+        ctx_b = FakeContext()
+        await svc.StreamAudio(relay_stream("b1", 3000, speech_chunks=2), ctx_b)
+        t_single = time.monotonic() - t0
+        t0 = time.monotonic()
+        ck1, ck2 = FakeContext(), FakeContext()
+        await asyncio.gather(svc.StreamAudio(relay_stream("k1", 2000), ck1),
+                             svc.StreamAudio(relay_stream("k2", 8000, delay=0.02), ck2))
+        t_pair = time.monotonic() - t0
+        return proc, svc, ctx_b, ck1, ck2, t_single, t_pair
+    proc, svc, ctx_b, ck1, ck2, t_single, t_pair = asyncio.run(go())
+    assert ctx_b.sent and ctx_b.sent[-1].success and t_single < 0.3, t_single
+    assert svc.stats["bypassed"] == 1
+    assert t_pair >= 0.5                       # the kitchen pair waited out the window
+    assert ck1.sent[-1].response_text == MSG_CANCELLED and ck2.sent[-1].success
+    # without the opt-in the single relay waits for the window as the reference does
+    async def ref():
+        svc2 = AudioService(FakeProcessor(), window_duration=0.3, scope="per_relay_group",
+                            relay_groups={"b1": "bedroom"})
+        t0 = time.monotonic()
+        await svc2.StreamAudio(relay_stream("b1", 3000, speech_chunks=1), FakeContext())
+        return time.monotonic() - t0
+    assert asyncio.run(ref()) >= 0.3
