@@ -165,7 +165,14 @@ def hub_summary(srv, recs: list, args) -> tuple[float | None, dict]:
     r = np.array(recs, dtype=np.float64).reshape(-1, 4)
     slope = (float(np.polyfit(r[:, 0], r[:, 3], 1)[0])
              if len(r) and len(set(r[:, 0])) >= 2 else None)
+    st = srv.processor.stats
+    gap = (round(1e3 * st["eos_enc_gap_s"] / st["eos_enc_n"], 3)
+           if st.get("eos_enc_n") else None)
     return slope, {"voice_events": srv.events.count(ListOptions()),
+                   "end_of_speech_to_encoder_ms": gap,
+                   "encode_span_ms": (round(1e3 * st["enc_span_s"] / st["eos_enc_n"], 3)
+                                      if st.get("eos_enc_n") and "enc_span_s" in st else None),
+                   "paced": bool(getattr(args, "paced", False)),
                    "audio_service": dict(srv.audio_service.stats),
                    "processor": dict(srv.processor.stats),
                    "latency_ms_p50": round(float(np.median(r[:, 3])), 1) if len(r) else None,
@@ -343,6 +350,9 @@ def main(argv=None) -> int:
                     help="closed: B concurrent closed-loop streams per GPU (continuous batching); "
                          "hub: B simulated relays per GPU over gRPC into the served hub; "
                          "batch: lockstep batches of B")
+    ap.add_argument("--paced", action="store_true",
+                    help="--mode hub: relays send their speech in real time (100 ms chunks "
+                         "every 100 ms); latency is then counted from the end of speech")
     ap.add_argument("--window-ms", type=float, default=300.0,
                     help="--mode hub: arbitration window (the reference's 300 ms)")
     ap.add_argument("--inflight", type=int, default=2,
@@ -505,12 +515,16 @@ def main(argv=None) -> int:
                     yield AudioChunk(relay_id=relay, audio_data=wake, sample_rate=16000,
                                      is_wake_word=True)
                     for o in range(0, max(len(rest), 1), step_b):
+                        if args.paced:          # a real relay: one 100 ms chunk per 100 ms
+                            await asyncio.sleep(step_b / 32000)
                         yield AudioChunk(relay_id=relay, audio_data=rest[o:o + step_b],
                                          sample_rate=16000,
                                          is_end_of_speech=o + step_b >= len(rest))
                 t_s = time.perf_counter()
                 got = [r async for r in call(chunks())]
                 lat = (time.perf_counter() - t_s) * 1e3
+                if args.paced:                  # latency after the relay stopped speaking
+                    lat -= 1e3 * (-(-max(len(rest), 1) // step_b)) * step_b / 32000
                 ok = bool(got) and got[-1].success
                 if record:
                     hub_recs.setdefault(relay, []).append([u.n_commands, float(ok), lat])

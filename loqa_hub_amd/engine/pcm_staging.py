@@ -219,3 +219,50 @@ class PcmStager:
             _lib.runtime().loqa_stager_destroy(self._h)
             self._h = None
 
+
+
+class RegisteredPcm:
+    """A relay's samples in host memory another process wrote - a slot of the
+    DP front end's shared-memory PCM ring (``parallel/dp_serving.py``) that
+    this GPU worker pinned with ``hipHostRegister`` - uploaded straight from
+    there by ``hipMemcpyAsync`` (no pickled bytes, no staging copy). The
+    front end owns the slot and reuses it only after this utterance's result
+    came back, so ``release`` has nothing to return."""
+
+    def __init__(self, view: np.ndarray, host_ptr: int):
+        self.view, self.host_ptr = view, host_ptr
+        self.released = False
+
+    def __len__(self) -> int:
+        return int(self.view.size)
+
+    def numpy(self) -> np.ndarray:
+        return self.view
+
+    def upload(self, dst_ptr: int, max_samples: int, wait_stream: int) -> None:
+        n = min(len(self), max_samples)
+        if n > 0:
+            _lib.check(_lib.runtime().loqa_memcpy_h2d_async(dst_ptr, self.host_ptr, 2 * n,
+                                                              wait_stream), "memcpy_h2d_async")
+        self.released = True
+
+    def release(self) -> None:
+        self.released = True
+
+
+def host_register(addr: int, nbytes: int) -> bool:
+    """Pin ``nbytes`` of existing host memory at ``addr`` for DMA
+    (``hipHostRegister`` on torch's HIP runtime). False if HIP refuses."""
+    from ..utils.hip_runtime import hip_runtime
+    hip = hip_runtime()
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostRegister.restype = ctypes.c_int
+    return hip.hipHostRegister(ctypes.c_void_p(addr), ctypes.c_size_t(nbytes), 0) == 0
+
+
+def host_unregister(addr: int) -> None:
+    from ..utils.hip_runtime import hip_runtime
+    hip = hip_runtime()
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    hip.hipHostUnregister.restype = ctypes.c_int
+    hip.hipHostUnregister(ctypes.c_void_p(addr))

@@ -23,6 +23,16 @@ Failure handling (reference: none beyond service retries):
   reply. ``FAULT_INJECT=gpu_kill:<rank>[@n]`` drives this path.
 
 ``metrics()`` aggregates per-worker counters (D3) for ``/api/metrics``.
+
+PCM transport: each worker owns a ring of ``LOQA_DP_SHM_SLOTS`` 30 s slots in
+POSIX shared memory, created by the front end. At dispatch the front end
+copies the winner's PCM16 into a free slot of the chosen worker and sends only
+(slot, length) over the request queue; the GPU worker has the whole ring
+pinned (``hipHostRegister``) and its STT upload is one ``hipMemcpyAsync``
+straight from the slot (``engine/pcm_staging.RegisteredPcm``). The slot goes
+back to the front end's free list when the utterance's result arrives (or its
+worker dies). Longer utterances, or a full ring, travel as bytes in the queue
+item as before.
 """
 from __future__ import annotations
 
@@ -42,6 +52,44 @@ from ..transport.audio_service import MSG_STT_FAILED, UtteranceResult
 from .dp_router import LeastLoadedRouter
 
 log = logging.getLogger("loqa.dp")
+
+SHM_SLOTS = int(os.environ.get("LOQA_DP_SHM_SLOTS", "48"))
+SHM_SLOT_BYTES = 480000 * 2          # one 30 s window of PCM16
+
+
+class _WorkerPcmRing:
+    """Worker side of its shared-memory PCM ring (mapped, and pinned on a GPU)."""
+
+    def __init__(self, name: str, slot_bytes: int, device: str):
+        from multiprocessing import shared_memory
+        self.shm = shared_memory.SharedMemory(name=name)
+        self.slot_bytes = slot_bytes
+        import ctypes
+        self.addr = ctypes.addressof(ctypes.c_char.from_buffer(self.shm.buf))
+        self.registered = False
+        if device.startswith("cuda"):
+            from ..engine.pcm_staging import host_register
+            self.registered = host_register(self.addr, self.shm.size)
+            if not self.registered:
+                log.warning("hipHostRegister of the PCM ring failed: staging copies instead")
+
+    def samples(self, slot: int, nbytes: int):
+        """(int16 view of the slot, a RegisteredPcm for the GPU upload or None)."""
+        off = slot * self.slot_bytes
+        view = np.frombuffer(self.shm.buf, dtype="<i2", count=nbytes // 2, offset=off)
+        if not self.registered:
+            return view, None
+        from ..engine.pcm_staging import RegisteredPcm
+        return view, RegisteredPcm(view, self.addr + off)
+
+    def close(self) -> None:
+        if self.registered:
+            from ..engine.pcm_staging import host_unregister
+            host_unregister(self.addr)
+        try:
+            self.shm.close()
+        except BufferError:
+            pass                      # a view is still referenced: the OS unmaps at exit
 
 
 # --------------------------------------------------------------- worker side
@@ -142,12 +190,22 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
             resp_q.put(("hb", rank, hb))
             time.sleep(spec.get("heartbeat_s", 0.5))
 
+    ring = None
+    if spec.get("pcm_shm"):
+        ring = _WorkerPcmRing(spec["pcm_shm"][rank], spec["pcm_shm_slot_bytes"], device)
+
     async def handle(item) -> None:
         _, rid, relay_id, request_id, data, sr, hint = item
-        pcm16 = np.frombuffer(data, dtype="<i2")
+        reg = None
+        if isinstance(data, tuple):               # ("shm", slot, nbytes)
+            pcm16, reg = ring.samples(data[1], data[2])
+        else:
+            pcm16 = np.frombuffer(data, dtype="<i2")
         try:
             if takes_pcm16:
                 kw = {"pcm16": pcm16}
+                if reg is not None:
+                    kw = {"pcm_slot": reg}
                 if hint:
                     kw["transcript_hint"] = hint
                 res = await proc.process(relay_id, request_id, np.zeros(0, np.float32), sr, **kw)
@@ -196,6 +254,8 @@ def _worker_main(rank: int, spec: dict, req_q, resp_q) -> None:
         loop.run_until_complete(_close_worker_processor(proc))
     finally:
         state["stop"] = True
+        if ring is not None:
+            ring.close()
 
 
 # --------------------------------------------------------------- front side
@@ -206,6 +266,7 @@ class _Req:
     worker: int = -1
     attempts: int = 0
     session: str = ""
+    shm_slot: int = -1          # slot of the worker's PCM ring holding the samples
 
 
 class _RemoteReply:
@@ -250,10 +311,21 @@ class DPVoiceProcessor:
         self.failures: list[dict] = []
         self._running = False
         self._served = 0
+        self._shm: list = []
+        self._shm_free: list[list[int]] = []
+        self.pcm_shm_sent = 0
+        self.pcm_inline_sent = 0
 
     # lifecycle
     async def start(self) -> None:
         ctx = mp.get_context("spawn")
+        if SHM_SLOTS > 0 and "pcm_shm" not in self.spec:
+            from multiprocessing import shared_memory
+            self._shm = [shared_memory.SharedMemory(create=True, size=SHM_SLOTS * SHM_SLOT_BYTES)
+                         for _ in range(self.n)]
+            self._shm_free = [list(range(SHM_SLOTS)) for _ in range(self.n)]
+            self.spec["pcm_shm"] = [m.name for m in self._shm]
+            self.spec["pcm_shm_slot_bytes"] = SHM_SLOT_BYTES
         self._req_qs = [ctx.Queue() for _ in range(self.n)]
         self._resp_q = ctx.Queue()
         self._procs = [ctx.Process(target=_worker_main, args=(r, self.spec, self._req_qs[r],
@@ -289,6 +361,13 @@ class DPVoiceProcessor:
             if p.is_alive():
                 p.kill()
                 p.join(timeout=5)
+        for m in self._shm:
+            try:
+                m.close()
+                m.unlink()
+            except (FileNotFoundError, BufferError):
+                pass
+        self._shm = []
 
     # routing
     async def process(self, relay_id: str, request_id: str, audio: np.ndarray,
@@ -355,10 +434,28 @@ class DPVoiceProcessor:
             return
         req.worker = w
         self._pending[w].add(rid)
-        self._req_qs[w].put(("utt", rid) + req.args[1:])
+        args = req.args[1:]
+        data = args[2]
+        if self._shm and len(data) <= SHM_SLOT_BYTES and self._shm_free[w]:
+            slot = self._shm_free[w].pop()
+            off = slot * SHM_SLOT_BYTES
+            self._shm[w].buf[off:off + len(data)] = data
+            req.shm_slot = slot
+            args = args[:2] + (("shm", slot, len(data)),) + args[3:]
+            self.pcm_shm_sent += 1
+        else:
+            self.pcm_inline_sent += 1
+        self._req_qs[w].put(("utt", rid) + args)
+
+    def _free_shm(self, req: _Req) -> None:
+        if req.shm_slot >= 0 and req.worker >= 0 and self._shm:
+            self._shm_free[req.worker].append(req.shm_slot)
+        req.shm_slot = -1
 
     def _finish(self, rid: int, res: UtteranceResult) -> None:
         req = self._reqs.pop(rid, None)
+        if req is not None:
+            self._free_shm(req)
         if req is not None and req.session and self.streaming is not None:
             sm = (res.metrics or {}).get("speech", {}).get("streaming")
             self.streaming.end_speech_session(req.session, sm)
@@ -427,6 +524,7 @@ class DPVoiceProcessor:
             req = self._reqs.get(rid)
             if req is None:
                 continue
+            self._free_shm(req)         # the dead worker's slot: its reader is gone
             if req.attempts >= self.max_attempts:
                 self._finish(rid, UtteranceResult(success=False, command="error",
                                                   response_text=MSG_STT_FAILED,
@@ -443,6 +541,8 @@ class DPVoiceProcessor:
                 if isinstance(v, (int, float)) and not isinstance(v, bool):
                     out[k] = out.get(k, 0) + v
         out["served"] = self._served
+        out["pcm_shm_sent"] = self.pcm_shm_sent
+        out["pcm_inline_sent"] = self.pcm_inline_sent
         return out
 
     def metrics(self) -> dict:

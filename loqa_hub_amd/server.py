@@ -266,6 +266,14 @@ class HubServer:
         await site.start()
         self.http_port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
         log.info("HTTP server listening on :%d", self.http_port)
+        # the start-up objects (models, protobuf classes, the composition) are
+        # long-lived: move them out of the cyclic GC's generations and collect
+        # young objects less often, so full collections do not stall the event
+        # loop in the middle of relay traffic (front-end p99, docs/PERF.md)
+        import gc
+        gc.collect()
+        gc.freeze()
+        gc.set_threshold(50000, 20, 100)
 
     async def stop(self) -> None:
         stop = getattr(self.processor, "close", None)

@@ -411,8 +411,14 @@ class AudioService:
             async for chunk in request_iterator:
                 if not relay_id:
                     relay_id = chunk.relay_id
-                hublog.log_audio_processing(relay_id, "received", bytes=len(chunk.audio_data),
-                                            wake_word=chunk.is_wake_word)
+                # per-chunk line at DEBUG (the reference logs it at info through
+                # zap, ~1 us; a Python JSON record costs ~30 us, 5-6k chunks/s at
+                # 64 relays: docs/PERF.md "Round 5", front end); the wake word and
+                # end of speech keep their info lines
+                if hublog.debug_enabled():
+                    hublog.log_audio_processing_debug(relay_id, "received",
+                                                      bytes=len(chunk.audio_data),
+                                                      wake_word=chunk.is_wake_word)
                 data = chunk.audio_data
                 if chunk.is_wake_word:
                     key = self.window_key(relay_id)
@@ -457,9 +463,17 @@ class AudioService:
                 rs.pcm_slot = new_slot()
 
     async def _await_result(self, rs: RelayStream, stream: "_ContextWriter") -> None:
-        deadline = time.monotonic() + self.end_of_speech_wait
-        while rs.status == RelayStatus.CONTENDING and time.monotonic() < deadline:
-            await asyncio.sleep(0.005)
+        if rs.status == RelayStatus.CONTENDING:
+            # the window's decision (the reference polls 50 x 100 ms, :1008-1041)
+            w = self.windows.get(self.window_key(rs.relay_id))
+            if w is not None and rs.relay_id in w.relays:
+                try:
+                    await asyncio.wait_for(w.closed.wait(), self.end_of_speech_wait)
+                except asyncio.TimeoutError:
+                    pass
+            deadline = time.monotonic() + self.end_of_speech_wait
+            while rs.status == RelayStatus.CONTENDING and time.monotonic() < deadline:
+                await asyncio.sleep(0.005)
         if rs.status != RelayStatus.WINNER or rs.result is None:
             return
         try:

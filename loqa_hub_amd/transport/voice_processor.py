@@ -152,6 +152,15 @@ class GPUVoiceProcessor:
                 self.streaming.begin_speech_session(speech.session_id, speech)
         try:
             await self.pipeline.submit(j)
+            if "enc0" in j.t and "start" in j.t:
+                # process() runs at end of speech: the gap until the encoder
+                # (upload + log-mel) starts on this utterance
+                self.stats["eos_enc_gap_s"] = self.stats.get("eos_enc_gap_s", 0.0) + \
+                    j.t["enc0"] - j.t["start"]
+                self.stats["eos_enc_n"] = self.stats.get("eos_enc_n", 0) + 1
+                if "enc1" in j.t:     # upload + log-mel + encoder + cross K|V, synchronised
+                    self.stats["enc_span_s"] = self.stats.get("enc_span_s", 0.0) + \
+                        j.t["enc1"] - j.t["enc0"]
         except Exception as e:  # noqa: BLE001
             if pcm_slot is not None:
                 pcm_slot.release()        # idempotent: a no-op once uploaded

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import json
 import logging
+import logging.handlers
 import os
 import sys
 import time
@@ -61,12 +62,37 @@ def initialize(level: str | None = None, fmt: str | None = None, stream=None) ->
     lg = logging.getLogger(ROOT)
     for h in list(lg.handlers):
         lg.removeHandler(h)
+        if isinstance(h, _DeferredHandler):
+            h.listener.stop()
     h = logging.StreamHandler(stream or sys.stderr)
     h.setFormatter(JSONFormatter() if fmt == "json" else ConsoleFormatter())
+    if os.environ.get("LOQA_LOG_ASYNC", "1") != "0" and stream is None:
+        # formatting + the write happen on a listener thread, not on the
+        # event loop that serves the relays (front-end tail latency)
+        h = _DeferredHandler(h)
     lg.addHandler(h)
     lg.setLevel(_LEVELS.get(level.lower(), logging.INFO))
     lg.propagate = False
     return lg
+
+
+class _DeferredHandler(logging.handlers.QueueHandler):
+    """Enqueue the raw record (the stock QueueHandler formats it in the
+    caller's thread first); a QueueListener thread formats and writes it."""
+
+    def __init__(self, target: logging.Handler):
+        import queue as _q
+        super().__init__(_q.SimpleQueue())
+        self.listener = logging.handlers.QueueListener(self.queue, target,
+                                                       respect_handler_level=True)
+        self.listener.start()
+        import atexit
+        atexit.register(self.listener.stop)
+
+    def prepare(self, record: logging.LogRecord) -> logging.LogRecord:
+        if record.exc_info and not record.exc_text:
+            record.exc_text = logging.Formatter().formatException(record.exc_info)
+        return record
 
 
 def get(name: str = "") -> logging.Logger:
@@ -89,6 +115,15 @@ def log_voice_event(event) -> None:
 def log_audio_processing(relay_id: str, stage: str, **fields) -> None:
     _log(logging.INFO, "Audio processing", component="audio_processing",
          relay_id=sanitize_log_input(relay_id), stage=stage, **fields)
+
+
+def log_audio_processing_debug(relay_id: str, stage: str, **fields) -> None:
+    _log(logging.DEBUG, "Audio processing", component="audio_processing",
+         relay_id=sanitize_log_input(relay_id), stage=stage, **fields)
+
+
+def debug_enabled() -> bool:
+    return logging.getLogger(ROOT).isEnabledFor(logging.DEBUG)
 
 
 def log_nats_event(subject: str, event_type: str, **fields) -> None:

@@ -95,3 +95,57 @@ def test_comm_device_follows_backend():
     assert DistInfo(device=gpu, backend="nccl", world=2).comm_device == gpu
     assert DistInfo(device=gpu, backend="gloo", world=2).comm_device.type == "cpu"
     assert DistInfo().comm_device.type == "cpu"
+
+
+class _Pcm16Processor:
+    """Takes the raw PCM16 (as GPU workers do) and answers with a digest of
+    the samples it received."""
+    takes_pcm16 = True
+
+    def __init__(self, spec):
+        self.rank = spec["rank"]
+        self.stats = {}
+
+    async def process(self, relay_id, request_id, audio, sr, transcript_hint=None, pcm16=None,
+                      pcm_slot=None):
+        import hashlib
+        x = pcm_slot.numpy() if pcm_slot is not None else pcm16
+        await asyncio.sleep(0.005)
+        return UtteranceResult(transcription=hashlib.sha1(np.ascontiguousarray(x).tobytes()).hexdigest(),
+                               response_text=str(x.size))
+
+
+def pcm16_factory(spec, device):
+    return _Pcm16Processor(spec)
+
+
+def test_dp_pcm_shared_memory_ring(monkeypatch):
+    """PCM reaches the workers through their shared-memory
+    rings (only the slot index crosses the queue), byte-exact; slots are
+    recycled when results come back (more utterances than slots); an
+    utterance longer than a slot falls back to inline bytes."""
+    import hashlib
+
+    from loqa_hub_amd.parallel import dp_serving
+    monkeypatch.setattr(dp_serving, "SHM_SLOTS", 3)
+    rng = np.random.default_rng(0)
+    pcms = [rng.integers(-32768, 32767, n).astype("<i2") for n in
+            [1600, 48000, 480000, 16000] * 4 + [480001]]
+
+    async def main():
+        dp = DPVoiceProcessor(dict(device="cpu", factory=pcm16_factory, heartbeat_s=0.1), 2)
+        await dp.start()
+        try:
+            assert len(dp._shm) == 2
+            res = []
+            for k in range(0, len(pcms), 6):          # waves: slots must come back
+                res += await asyncio.wait_for(asyncio.gather(*[
+                    dp.process(f"relay-{i}", f"req-{i}", np.zeros(0, np.float32), 16000,
+                               pcm16=p) for i, p in enumerate(pcms[k:k + 6], k)]), 60)
+            return res, dp.stats, [sorted(f) for f in dp._shm_free]
+        finally:
+            await dp.close()
+    res, st, free = asyncio.run(main())
+    assert [r.transcription for r in res] == [hashlib.sha1(p.tobytes()).hexdigest() for p in pcms]
+    assert st["pcm_shm_sent"] == len(pcms) - 1 and st["pcm_inline_sent"] == 1
+    assert free == [[0, 1, 2], [0, 1, 2]]

@@ -1,0 +1,32 @@
+"""The served DP hub's front end under load: real gRPC relays
+into HubServer -> AudioService (per-group windows) -> DP router -> stub worker
+processes (fixed-latency fake GPU, PCM through the shared-memory ring).
+The full-size run (64 relays, 8 workers) is scripts/frontend_bench.py
+(profiles/r5_frontend_64relays.json); this is a smaller CPU-tier version
+with loose bounds (the CI container's 8 CPUs also run the clients)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "scripts"))
+
+
+def test_frontend_sustains_relay_load():
+    import frontend_bench
+    r = frontend_bench.run(relays=16, workers=4, seconds=5.0, window_ms=200.0, gpu_ms=30.0,
+                           client_procs=1, warm_s=1.5)
+    assert r["success_rate"] == 1.0
+    assert r["utt_per_s"] >= 0.8 * r["ideal_utt_per_s"], r
+    assert r["added_ms_p50"] < 30.0, r
+    assert r["pcm_shm_sent"] > 0 and r["pcm_inline_sent"] == 0, r
+
+
+def test_frontend_single_relay_bypass_load():
+    """Every relay alone in its group: with the bypass opt-in no utterance
+    waits for a window."""
+    import frontend_bench
+    r = frontend_bench.run(relays=8, workers=2, seconds=4.0, window_ms=300.0, gpu_ms=30.0,
+                           client_procs=1, warm_s=1.0, bypass=True)
+    assert r["success_rate"] == 1.0
+    assert r["svc"]["bypassed"] == r["svc"]["windows"] > 0
+    assert r["added_ms_p50"] < 30.0, r          # no 300 ms window in the latency
