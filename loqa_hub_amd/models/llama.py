@@ -340,7 +340,7 @@ class LlamaModel:
         h = ops.rmsnorm(x, w.layers[0]["attn_norm"], cfg.norm_eps)
         split_keys = 256
         num_splits = max(1, (meta.max_ctx + split_keys - 1) // split_keys)
-        if (PREFILL_HW and x.is_cuda and tp.world == 1 and not meta.decode
+        if (PREFILL_HW and x.is_cuda and not meta.decode
                 and not getattr(w, "compact", False) and "wqkv" in L0_KEYS(w)):
             return self._forward_prefill_hw(meta, k_cache, v_cache, attn_ws, x, h)
         for li, L in enumerate(w.layers):
@@ -368,7 +368,9 @@ class LlamaModel:
                             ) -> torch.Tensor:
         """Prompt pass on the hand-written GEMMs (``ops.proj``: per shape the
         measured faster of the split-K tiled GEMM, whose K chunks are summed
-        in-launch, and the row-resident weight-streaming GEMM): per layer qkv
+        in-launch, and the row-resident weight-streaming GEMM; tensor parallel:
+        the same GEMMs on the rank's shards, the row-parallel o / down partials
+        summed by the custom all-reduce - no hipBLASLt on any rank): per layer qkv
         (bf16) -> RoPE + KV append -> flash attention -> o added straight into
         the residual stream (one rounding) -> RMSNorm -> gate|up with the
         SwiGLU epilogue -> down added into the residual -> the next layer's
@@ -376,12 +378,15 @@ class LlamaModel:
         as prefill-GEMM f32 slabs summed by the next norm is 9% faster alone,
         7.73 vs 8.46 ms per 318-token pass, but ~1% slower beside the
         decoders: docs/PERF.md "Round 4".)"""
-        cfg, w = self.cfg, self.w
+        cfg, w, tp = self.cfg, self.w, self.w.tp
         H, Hkv, D = w.h, w.hkv, cfg.head_dim
         residual = x.contiguous()
+        dn = None
         for li, L in enumerate(w.layers):
             if li > 0:
-                h = ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps)
+                # TP: the previous down partials (all-reduced) join the residual here
+                h = (ops.rmsnorm(residual, L["attn_norm"], cfg.norm_eps) if dn is None else
+                     ops.rmsnorm(dn, L["attn_norm"], cfg.norm_eps, residual=residual))
             qkv = ops.proj(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
@@ -389,10 +394,24 @@ class LlamaModel:
                                  head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
                                  block_tables=meta.block_tables, grouped=False, split_keys=256,
                                  num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
-            ops.proj(attn, L["wo"], epi="resid", residual=residual)
-            hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
+            if tp.world == 1:
+                ops.proj(attn, L["wo"], epi="resid", residual=residual)
+                hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)
+            else:
+                # row-parallel o: this rank's partial on the hand-written GEMM,
+                # the custom all-reduce (two-shot over xGMI at prompt sizes),
+                # then residual add + RMSNorm in one kernel
+                o = ops.proj(attn, L["wo"])
+                tp.all_reduce_(o)
+                hn = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             a = ops.proj(hn, L["w_gate_up"], epi="swiglu")
-            ops.proj(a, L["w_down"], epi="resid", residual=residual)
+            if tp.world == 1:
+                ops.proj(a, L["w_down"], epi="resid", residual=residual)
+            else:
+                dn = ops.proj(a, L["w_down"])
+                tp.all_reduce_(dn)
+        if dn is not None:
+            residual.add_(dn)          # one bf16 rounding, as the norm's residual add
         return ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
 
     def _ones(self, x: torch.Tensor) -> torch.Tensor:

@@ -37,6 +37,14 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=0, help="override layer count (0: the model's)")
     ap.add_argument("--xgmi-us", default="3,6",
                     help="extra latency per cross-GPU collective (low,high): flag exchange + xGMI reads")
+    ap.add_argument("--prefill-rows", type=int, default=320,
+                    help="also time this rank's prompt pass over this many tokens (0: skip)")
+    ap.add_argument("--xgmi-gbps", default="40,60",
+                    help="effective GB/s per xGMI link (low,high) for the prompt pass's two-shot "
+                         "all-reduces (7 links per GPU)")
+    ap.add_argument("--steps-per-command", type=float, default=40.0,
+                    help="decode steps per added command (profiles/config5_tp1_r2.json: "
+                         "1035.73 ms / 25.884 ms per step = 40; config5_tp8_share_r3.json: 38)")
     a = ap.parse_args()
     from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
     from loqa_hub_amd.models.configs import llama_config
@@ -107,6 +115,47 @@ def main() -> int:
            "projected_step_ms": [round(step_ms + n_coll * lo / 1e3, 3),
                                  round(step_ms + n_coll * hi / 1e3, 3)],
            "init_s": round(t_init, 1)}
+    spc = a.steps_per_command
+    out["steps_per_added_command"] = spc
+    out["projected_ms_per_added_command"] = [round(spc * v, 1) for v in out["projected_step_ms"]]
+    out["reference_bar_ms_per_added_command"] = 200.0
+    if a.prefill_rows > 0 and "wqkv" in (w.layers[0] if w.layers else {}):
+        # this rank's prompt pass (hand-written GEMMs on its shards; the
+        # row-parallel partials' all-reduces are no-ops on the one-rank handle
+        # and are modelled below: two-shot, 2 (W-1)/W of the tensor per rank
+        # over 7 links)
+        T = a.prefill_rows
+        r = GenRequest(list(range(7, 7 + T)), [])
+        r.seq_id = eng._next_id
+        eng._next_id += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+        mq, mc, hp = eng._meta([r], [r.prompt], decode=False)
+        dp = eng._to_device(hp)
+        pm = eng._build_meta(dp, mq, mc, False)
+
+        def pass_():
+            return eng.model.logits(eng.model.forward(pm, eng.kv.k, eng.kv.v, eng.attn_ws))
+        for _ in range(2):
+            pass_()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pass_()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        pf_ms = sorted(ts)[len(ts) // 2]
+        nbytes = T * cfg.d_model * 2
+        per_rank = 2 * (a.tp - 1) / a.tp * nbytes
+        glo, ghi = (float(v) for v in a.xgmi_gbps.split(","))
+        n_ar = 2 * L
+        ar = [n_ar * (per_rank / (7 * g * 1e9) * 1e3 + lo / 1e3) for g in (ghi, glo)]
+        out["prefill"] = {"rows": T, "rank_pass_ms_local": round(pf_ms, 3),
+                          "allreduces": n_ar, "allreduce_bytes": nbytes,
+                          "projected_pass_ms": [round(pf_ms + ar[0], 2), round(pf_ms + ar[1], 2)],
+                          "gemms": "ops.proj (gemm_sk / gemm_ws), no hipBLASLt"}
     print(json.dumps(out), flush=True)
     return 0
 
