@@ -17,6 +17,10 @@ from loqa_hub_amd import ops  # noqa: E402
 
 LLAMA = {"qkv": (6144, 4096, "bf16"), "o": (4096, 4096, "resid"), "gu": (28672, 4096, "swiglu"),
          "down": (4096, 14336, "resid")}
+# Llama-3-70B TP=8 rank shards (config 5 prompt passes; o / down are partials
+# for the all-reduce, plain bf16 outputs)
+TP70 = {"qkv70": (1280, 8192, "bf16"), "o70": (8192, 1024, "bf16"), "gu70": (7168, 8192, "swiglu"),
+        "down70": (8192, 3584, "bf16")}
 WHISPER = {"enc_qkv": (3840, 1280, "bf16"), "enc_o": (1280, 1280, "resid"),
            "enc_fc1": (5120, 1280, "bf16"), "enc_fc2": (1280, 5120, "resid")}
 
@@ -44,6 +48,7 @@ def main():
     dev = torch.device("cuda", 0)
     cases = [(m, k, v) for m in map(int, a.ms.split(",")) for k, v in LLAMA.items()]
     cases += [(m, k, v) for m in map(int, a.wms.split(",")) for k, v in WHISPER.items()]
+    cases += [(m, k, v) for m in map(int, a.ms.split(",")) for k, v in TP70.items()]
     if a.only:
         cases = [c for c in cases if c[1] in a.only.split(",")]
     for M, name, (N, K, epi) in cases:
@@ -63,7 +68,7 @@ def main():
                 ops.gemm_sk(x, ws[i], epi=epi, layout=lay, splits=s)
         t_plan = timeit(run, n_w)
         ws_t = {}
-        for depth in (0, 1):
+        for depth in ((0, 1) if N % 128 == 0 else ()):
             def run_ws(i, depth=depth):
                 if epi == "resid":
                     ops.gemm_ws(x, ws[i], epi="resid", residual=res, depth=depth)

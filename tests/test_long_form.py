@@ -147,3 +147,33 @@ def test_pcm_stager_uploads_byte_identical_gpu():
             assert np.array_equal(out.cpu().numpy(), pcm), (stream_in, n)
             assert len(slot.slots) == min(3, -(-n // 480000))
         st.close()
+
+
+@pytest.mark.gpu
+def test_dp_pcm_ring_registered_upload_gpu():
+    """The DP worker's side of the shared-memory PCM ring on a GPU: the ring
+    is pinned with hipHostRegister and a slot uploads straight to HBM
+    (RegisteredPcm), byte-identical."""
+    from multiprocessing import shared_memory
+
+    from loqa_hub_amd.parallel.dp_serving import _WorkerPcmRing
+    dev = torch.device("cuda", 0)
+    slot_bytes = 480000 * 2
+    shm = shared_memory.SharedMemory(create=True, size=3 * slot_bytes)
+    try:
+        rng = np.random.default_rng(1)
+        pcm = rng.integers(-32768, 32767, 123457).astype("<i2")
+        b = pcm.tobytes()
+        shm.buf[slot_bytes:slot_bytes + len(b)] = b        # slot 1, as the front end writes it
+        ring = _WorkerPcmRing(shm.name, slot_bytes, "cuda:0")
+        assert ring.registered
+        view, reg = ring.samples(1, len(b))
+        assert reg is not None and np.array_equal(view, pcm)
+        out = torch.empty(pcm.size, dtype=torch.int16, device=dev)
+        reg.upload(out.data_ptr(), pcm.size, torch.cuda.current_stream(dev).cuda_stream)
+        assert np.array_equal(out.cpu().numpy(), pcm)
+        del view, reg
+        ring.close()
+    finally:
+        shm.close()
+        shm.unlink()
