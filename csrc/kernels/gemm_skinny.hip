@@ -16,6 +16,7 @@
 //     go to f32 slabs part[S][Mpad][N] that the NEXT kernel sums in its prologue
 //     (slab_ops.hip) - deterministic, no atomics, no extra launch.
 #include "common.h"
+#include "attn_decode.h"
 #include <stdlib.h>
 
 typedef float float4v_ __attribute__((ext_vector_type(4)));
@@ -412,6 +413,14 @@ struct FusedParams {
   int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
   int wr;                 // waves along the rows (1, or 4 with S == 1; any S with xl)
   int xl;                 // x through LDS (wr == 4; Mpad 32 / 64 / 128)
+  // qkv + decode attention in ONE launch (mode 3, see ATTD below): 0 = off
+  int att;
+  long long q_bytes, kv_bytes;       // sizes of q_out and of one layer's K (= V) cache
+  const int* cu_q; const int* ctx_lens; const int* block_tables;
+  int max_blocks, att_B, split_keys, num_splits;
+  float att_scale; float* part_o; float* part_ml; int* att_counters;
+  void* att_out; long long att_ld;
+  int* att_sync;                     // [ready per kv head | work | exit | error], zeroed, left zero
 };
 
 struct FusedArgs {
@@ -423,7 +432,78 @@ struct FusedArgs {
   bf16_t* residual; float* rowsq_out; float* rowsum_out;                      // EPI_RESID
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
+  AttnDecArgs att; int att_B; int* att_sync; long long q_bytes, kv_bytes;     // ATTD
 };
+
+// ---------------------------------------------------------------------------
+// qkv -> decode attention hand-off (ATTD = head dim, 0 = off; mode EPI_ROPE):
+// the q / K / V rows of the step go out with write-through (sc1) stores and
+// each row tile then bumps its kv head's ready counter (release: sc1 stores,
+// vmcnt(0), relaxed agent atomic - guide §6 Guideline 16). Every workgroup of
+// the grid, once its tiles are done, turns into an attention worker: it takes
+// (split, kv head, sequence) items from a work counter, waits for the item's
+// kv head to be complete ((G + 2) x D / (16 RT) tiles), takes an agent
+// acquire and runs the decode-attention body of attn_decode.h - the launch
+// boundary between qkv and attention disappears and the attention of a head
+// starts as soon as ITS tiles are in. Workers only wait for tiles of the same
+// grid whose workgroups hold no dependency (they are producers that have not
+// yet been dispatched at worst), so every wait ends; the spin is bounded
+// anyway (error word). The last workgroup out resets the counters (graph
+// replays). The attention arithmetic is attn_decode_kernel's, bit for bit.
+#define ATT_SPIN_LIMIT (1 << 20)
+
+__device__ __forceinline__ int att_need(int G, int D, int RT) { return (G + 2) * D / (16 * RT); }
+
+template <int D>
+__device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, int RT, DecSmem<D>& sm, int* sflag) {
+  int* sync = a.att_sync;
+  const int Hkv = a.att.Hkv, Bq = a.att_B, ns = a.att.num_splits;
+  const int n_items = ns * Hkv * Bq;
+  const int need = att_need(a.att.Hq / Hkv, D, RT);
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+      sflag[0] = __hip_atomic_fetch_add(&sync[64], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int item = __builtin_amdgcn_readfirstlane(sflag[0]);   // uniform: scalar tile math
+    if (item >= n_items) break;
+    const int kvh = item % Hkv, rest = item / Hkv;
+    const int b = rest % Bq, split = rest / Bq;
+    if (threadIdx.x == 0) {
+      unsigned spins = __hip_atomic_load(&sync[66], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           ? ATT_SPIN_LIMIT : 0u;
+      while (__hip_atomic_load(&sync[kvh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (++spins > ATT_SPIN_LIMIT) {
+          __hip_atomic_store(&sync[66], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    attn_decode_body<D, 0, 1>(a.att, split, kvh, b, sm);
+  }
+  if (threadIdx.x == 0) {
+    const int e = __hip_atomic_fetch_add(&sync[65], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == (int)(gridDim.x * gridDim.y) - 1) {
+      for (int k = 0; k < Hkv; ++k) __hip_atomic_store(&sync[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[64], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[65], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// an 8-byte store, write-through (sc1) when the attention phase reads it
+template <int SC1>
+__device__ __forceinline__ void st_u2(bf16_t* base, size_t elem, uint2 v, long long nbytes) {
+  if constexpr (SC1) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2_{v.x, v.y}, r, (unsigned)(elem * 2), 0, 16);
+  } else {
+    *reinterpret_cast<uint2*>(base + elem) = v;
+  }
+}
 
 // WR: waves along the rows. WR = 1: the 4 waves split the tile's K range
 // (LDS reduce); WR = 4: every wave owns its own (16 * RT)-row tile over the
@@ -432,8 +512,9 @@ struct FusedArgs {
 // workgroup (L1 hits for the other 3) instead of once per wave, and no
 // cross-wave reduction is needed (measured on cold weights, M = 16: the
 // gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0>
-__global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int ATTD = 0>
+__global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedArgs a) {
+  static_assert(!ATTD || (MODE == EPI_ROPE && !XL), "attention hand-off: qkv (RoPE) mode only");
   constexpr int WK = 4 / WR;                     // waves along K
   constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
   constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
@@ -441,7 +522,11 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   // XL + RoPE at MT 8: the RoPE cos/sin operands (RT * MT * 8 VGPRs) are
   // loaded after the k loop instead of being held through it
   constexpr bool EARLY_EPI = !(XL && MODE == EPI_ROPE && MT > 4);
-  __shared__ __attribute__((aligned(16))) float smem[NSM];
+  // ATTD: the attention phase's LDS aliases the reduce / prologue area (one
+  // __shared__ array; the phase starts behind a workgroup barrier), + a flag word
+  constexpr int ATT_F = ATTD ? (int)(sizeof(DecSmem<ATTD ? ATTD : 64>) / 4) + 4 : 0;
+  constexpr int SMF = NSM > ATT_F ? NSM : ATT_F;
+  __shared__ __attribute__((aligned(16))) float smem[SMF];
   __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   float4v_* red = reinterpret_cast<float4v_*>(smem);
   float* sred = smem;
@@ -652,7 +737,10 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
           __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       t = __shfl(t, 0, 64);
-      if (t != a.S - 1) return;
+      if (t != a.S - 1) {
+        if constexpr (ATTD != 0) goto attn_phase;
+        else return;
+      }
     } else {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -663,7 +751,10 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         sred[0] = (float)t;
       }
       __syncthreads();
-      if ((int)sred[0] != a.S - 1 || wave != 0) return;
+      if ((int)sred[0] != a.S - 1 || wave != 0) {
+        if constexpr (ATTD != 0) goto attn_phase;
+        else return;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // fixed summation order (split 0..S-1) whichever block arrives last
@@ -699,7 +790,8 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = tot[i][j];
   } else if (wk != 0) {
-    return;
+    if constexpr (ATTD != 0) goto attn_phase;
+    else return;
   }
 
   // ---- epilogue (the wk == 0 wave of each row tile): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
@@ -822,15 +914,13 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
           uint2 w2;
           w2.x = pack_bf16x2(ov[0], ov[1]);
           w2.y = pack_bf16x2(ov[2], ov[3]);
-          bf16_t* dst;
           if (!isk) {
-            dst = a.q_out + (size_t)m * a.H * D + head * D;
+            st_u2<ATTD != 0>(a.q_out, (size_t)m * a.H * D + head * D + c, w2, a.q_bytes);
           } else {
             if (slot < 0) continue;
             const int bb = slot / a.blk, o = slot - bb * a.blk;
-            dst = a.kc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D;
+            st_u2<ATTD != 0>(a.kc, (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c, w2, a.kv_bytes);
           }
-          *reinterpret_cast<uint2*>(dst + c) = w2;
         } else {
           if (slot < 0) continue;
           const int bb = slot / a.blk, o = slot - bb * a.blk;
@@ -839,8 +929,21 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
           uint2 w2;
           w2.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
           w2.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-          *reinterpret_cast<uint2*>(a.vc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c) = w2;
+          st_u2<ATTD != 0>(a.vc, (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c, w2, a.kv_bytes);
         }
+      }
+    }
+    if constexpr (ATTD != 0) {
+      // this row tile is in: bump its kv head's ready counter (after the
+      // write-through stores have completed)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        const int pt0 = tile * RT;
+        const int G = a.H / a.Hkv;
+        const int kvh = pt0 < nq_t ? (pt0 / tph) / G
+                        : pt0 < nq_t + nk_t ? (pt0 - nq_t) / tph
+                                            : ((pt0 - nq_t - nk_t) * 16) / D;
+        __hip_atomic_fetch_add(&a.att_sync[kvh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   } else if constexpr (MODE == EPI_ACT) {
@@ -876,6 +979,12 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
         *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq) = w2;
       }
     }
+  }
+  if constexpr (ATTD == 0) return;
+attn_phase:
+  if constexpr (ATTD != 0) {
+    attn_fused_phase<ATTD>(a, RT, *reinterpret_cast<DecSmem<ATTD>*>(smem),
+                           reinterpret_cast<int*>(smem) + (SMF - 1));
   }
 }
 
@@ -998,6 +1107,40 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
   }
 }
 
+// qkv + attention (ATTD): RT 1 / 2, WR 1 / 4, Mpad 16 / 32 / 64, no XL, the
+// plain prefetch-group choice of launch_fused
+template <int RT, int MT, int WR, int NORM, int ATTD>
+static int launch_attd(const FusedArgs& a, hipStream_t st) {
+  constexpr int WK = 4 / WR;
+  dim3 grid(a.N / (16 * RT * WR), a.S);
+  const int kw = a.K / 32 / (a.S * WK);
+  if (MT <= 2 && kw % 4 == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, EPI_ROPE, NORM, 0, ATTD>), grid,
+                       dim3(256), 0, st, a);
+  else if (kw % 2 == 0)
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, WR, EPI_ROPE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, WR, EPI_ROPE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int NORM, int ATTD>
+static int dispatch_attd(const FusedArgs& a, int rt, int wr, hipStream_t st) {
+#define LQ_ATTD_MT(RT_, WR_)                                           \
+  switch (a.Mpad) {                                                    \
+    case 16: return launch_attd<RT_, 1, WR_, NORM, ATTD>(a, st);       \
+    case 32: return launch_attd<RT_, 2, WR_, NORM, ATTD>(a, st);       \
+    default: return launch_attd<RT_, 4, WR_, NORM, ATTD>(a, st);       \
+  }
+  if (rt == 1) {
+    if (wr == 4) { LQ_ATTD_MT(1, 4) }
+    LQ_ATTD_MT(1, 1)
+  }
+  if (wr == 4) { LQ_ATTD_MT(2, 4) }
+  LQ_ATTD_MT(2, 1)
+#undef LQ_ATTD_MT
+}
+
 // mode: 1 silu (out [Mpad, ldo >= N/2]), 2 residual (+bias) + row sum-of-squares
 // (+ row sums), 3 (RoPE if cs) + paged KV append + q, 4 act(bias + x W^T) -> out
 // (act 0 identity, 1 GELU-erf). norm: 1 RMSNorm / 2 LayerNorm of x (the bf16
@@ -1028,6 +1171,43 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->bias, (bf16_t*)p->out, p->ldo, p->act, (bf16_t*)p->residual, p->rowsq_out,
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
+  if (p->att) {
+    // qkv + decode attention in one launch: the attention reads the q rows
+    // this launch writes (row stride H * D) and the paged caches it appends to
+    if (p->mode != EPI_ROPE || p->xl || p->rt > 2 || p->att != p->D || (p->D != 64 && p->D != 128) ||
+        !p->att_sync || !p->block_tables || !p->cu_q || !p->ctx_lens || !p->part_o || !p->part_ml ||
+        !p->att_counters || !p->att_out || p->att_B < 1 || p->Hkv > 64 || p->num_splits < 1 ||
+        p->split_keys % DEC_TILE || p->blk < 16 || (p->blk & (p->blk - 1)) ||
+        p->q_bytes <= 0 || p->kv_bytes <= 0 || p->q_bytes >= (1ll << 31) || p->kv_bytes >= (1ll << 31) ||
+        (p->norm != NORM_RMS && p->norm != NORM_LN) || (p->norm == NORM_LN && p->D != 64))
+      return (int)hipErrorInvalidValue;
+    // the whole grid must be resident at once (workers wait on tiles of the
+    // same grid): <= one workgroup per CU although two fit (launch bounds
+    // 256 x 2), so two such launches on concurrent streams (the Whisper and
+    // Llama decoders) are resident together as well
+    static int ncu = 0;
+    if (ncu <= 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return (int)hipErrorInvalidValue;
+    }
+    if ((long long)(N / (16 * p->rt * p->wr)) * S > ncu) return (int)hipErrorInvalidValue;
+    a.att = AttnDecArgs{a.q_out, (long long)p->H * p->D, a.kc, a.vc, 0, nullptr, p->cu_q, p->ctx_lens,
+                        p->block_tables, p->max_blocks, p->blk, p->H, p->Hkv,
+                        p->att_scale * 1.4426950408889634f, 1, p->split_keys, p->num_splits, p->part_o,
+                        p->part_ml, Mpad, p->att_counters, (bf16_t*)p->att_out, p->att_ld};
+    a.att_B = p->att_B;
+    a.att_sync = p->att_sync;
+    a.q_bytes = p->q_bytes;
+    a.kv_bytes = p->kv_bytes;
+    if (p->D == 128) {
+      if (p->norm == NORM_RMS) return dispatch_attd<NORM_RMS, 128>(a, p->rt, p->wr, st);
+      return (int)hipErrorInvalidValue;
+    }
+    if (p->norm == NORM_RMS) return dispatch_attd<NORM_RMS, 64>(a, p->rt, p->wr, st);
+    return dispatch_attd<NORM_LN, 64>(a, p->rt, p->wr, st);
+  }
   switch (p->mode) {
     case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, p->xl, st);
     case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, p->xl, st);

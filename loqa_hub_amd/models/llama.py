@@ -485,18 +485,33 @@ class LlamaModel:
         # chunked prefill through this path (compact weights) can exceed the
         # grouped kernels' row limit: plain varlen flash attention then
         grouped = (H // Hkv) * meta.max_q <= 128
+        # decode rows (the split-key kernel's <= 32 query rows per kv head): qkv
+        # and attention through skinny_fused(attn=), one launch with FUSE_QKV_ATTN
+        dec_attn = (H // Hkv) * meta.max_q <= 32 and attn_ws is not None
+        ao = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device) if dec_attn else None
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
-            ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True,
-                             eps=cfg.norm_eps,
-                             positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
-                             k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
-                             n_heads=H, n_kv=Hkv, head_dim=D)
-            attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
-                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
-                                 block_tables=meta.block_tables, grouped=grouped,
-                                 split_keys=split_keys, num_splits=num_splits if grouped else 1,
-                                 workspace=attn_ws, max_k=meta.max_ctx)
+            if dec_attn:
+                attn = ops.skinny_fused(
+                    residual, P["wqkv_f"], "rope", scratch, norm=True, eps=cfg.norm_eps,
+                    positions=meta.positions, cos_sin=w.cos_sin, q_out=q, k_cache=k_cache[li],
+                    v_cache=v_cache[li], slots=meta.slots, n_heads=H, n_kv=Hkv, head_dim=D,
+                    attn=dict(cu_q=meta.cu_q, ctx_lens=meta.ctx_lens,
+                              block_tables=meta.block_tables, max_q=meta.max_q,
+                              split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
+                              max_k=meta.max_ctx, out=ao))
+            else:
+                ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True,
+                                 eps=cfg.norm_eps,
+                                 positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
+                                 k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
+                                 n_heads=H, n_kv=Hkv, head_dim=D)
+                attn = ops.attention(q, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                     head_dim=D, causal=True, max_q=meta.max_q,
+                                     ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
+                                     grouped=grouped, split_keys=split_keys,
+                                     num_splits=num_splits if grouped else 1,
+                                     workspace=attn_ws, max_k=meta.max_ctx)
             if tp.world == 1:
                 ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
             else:

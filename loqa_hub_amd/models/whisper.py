@@ -401,13 +401,12 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
         scratch.seed_stats(residual)
     q = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device)
     for i, F in enumerate(w.dec_f):
-        ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5, positions=positions, q_out=q,
-                         k_cache=k_cache[i], v_cache=v_cache[i], slots=slots, n_heads=H, n_kv=H,
-                         head_dim=D)
-        a = ops.attention(q, k_cache[i], v_cache[i], cu_q, n_heads=H, n_kv=H, head_dim=D,
-                          causal=True, max_q=max_q, ctx_lens=ctx_lens, block_tables=block_tables,
-                          grouped=True, split_keys=split_keys, num_splits=self_splits,
-                          workspace=ws)
+        a = ops.skinny_fused(residual, F["qkv"], "rope", scratch, eps=1e-5, positions=positions,
+                             q_out=q, k_cache=k_cache[i], v_cache=v_cache[i], slots=slots,
+                             n_heads=H, n_kv=H, head_dim=D,
+                             attn=dict(cu_q=cu_q, ctx_lens=ctx_lens, block_tables=block_tables,
+                                       max_q=max_q, split_keys=split_keys,
+                                       num_splits=self_splits, workspace=ws))
         ops.skinny_fused(a, F["o"], "resid", scratch, residual=residual, row_sums=True)
         xq = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5)
         kv = xkv[i]

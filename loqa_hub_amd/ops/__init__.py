@@ -166,6 +166,10 @@ class AttnWorkspace:
         # split-arrival tickets of the decode kernel's in-launch combine, one per
         # (sequence, kv head); the last arriving split resets its counter
         self.counters = torch.zeros(max_tokens * n_heads, dtype=torch.int32, device=device)
+        # hand-off words of the fused qkv + attention launch (skinny_fused(attn=)):
+        # per-kv-head ready counts [0, 64), work 64, exit 65, error 66; zero on
+        # entry and left zero (the error word is sticky)
+        self.sync = torch.zeros(128, dtype=torch.int32, device=device)
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Tensor, *,
@@ -1166,7 +1170,8 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
                  residual: torch.Tensor | None = None, positions=None, cos_sin=None, q_out=None,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
-                 row_sums: bool = False, wr: int | None = None, xl: int | None = None) -> torch.Tensor:
+                 row_sums: bool = False, wr: int | None = None, xl: int | None = None,
+                 attn: dict | None = None) -> torch.Tensor:
     """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32,
     64 or 128 (``xl``: activations staged through LDS, 4 waves along rows,
     required at Mpad 128; chosen by the tuner at 64).
@@ -1181,7 +1186,33 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     "resid": residual += x W^T (+ bias) in place, writes per-tile row sums of
     squares (and row sums with ``row_sums``);
     "rope": q -> q_out, k (RoPE'd when ``cos_sin``) and v -> paged caches
-    (``perm_rope_qkv`` order); "act": returns act(x W^T + bias) bf16 [Mpad, N]."""
+    (``perm_rope_qkv`` order); "act": returns act(x W^T + bias) bf16 [Mpad, N].
+
+    ``attn`` (mode "rope"): the step's causal decode attention over the paged
+    caches (keys of :func:`attention`: cu_q, ctx_lens, block_tables, max_q,
+    split_keys, num_splits, workspace, max_k, scale, out) follows the GEMM and
+    its output is returned. With ``FUSE_QKV_ATTN`` and a supported shape both
+    run in ONE launch (the GEMM's workgroups turn into attention workers as
+    their tiles complete, gemm_skinny.hip ATTD), bit-identical to the two
+    launches; otherwise the two launches."""
+    if attn is not None:
+        assert mode == "rope"
+        fused = _gpu(x) and _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache,
+                                       n_heads, n_kv, head_dim, attn, norm)
+        if not fused:
+            skinny_fused(x, wp, mode, scratch, splits=splits, norm=norm, eps=eps,
+                         rowsq_tiles=rowsq_tiles, rt=rt, positions=positions, cos_sin=cos_sin,
+                         q_out=q_out, k_cache=k_cache, v_cache=v_cache, slots=slots,
+                         n_heads=n_heads, n_kv=n_kv, head_dim=head_dim, bias=bias, colsum=colsum,
+                         wr=wr, xl=xl)
+            return attention(q_out, k_cache, v_cache, attn["cu_q"], n_heads=n_heads, n_kv=n_kv,
+                             head_dim=head_dim, causal=True, max_q=attn["max_q"],
+                             ctx_lens=attn["ctx_lens"], block_tables=attn["block_tables"],
+                             scale=attn.get("scale"), grouped=True,
+                             split_keys=attn["split_keys"], num_splits=attn["num_splits"],
+                             workspace=attn["workspace"], out=attn.get("out"),
+                             max_k=attn.get("max_k"))
+        splits, rt, wr, xl = fused
     if isinstance(wp, FusedLinear):
         lin = wp
         wp = lin.wp
@@ -1251,10 +1282,71 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
     p.rt, p.wr, p.xl = rt, wr, int(bool(xl))
+    if attn is not None:
+        ws = attn["workspace"]
+        bt = attn["block_tables"]
+        aout = attn.get("out")
+        if aout is None:
+            aout = torch.empty(Mpad, n_heads * head_dim, dtype=torch.bfloat16, device=x.device)
+        p.att, p.q_bytes, p.kv_bytes = head_dim, q_out.numel() * 2, k_cache.numel() * 2
+        p.cu_q, p.ctx_lens, p.block_tables = ptr(attn["cu_q"]), ptr(attn["ctx_lens"]), ptr(bt)
+        p.max_blocks, p.att_B = bt.shape[1], attn["cu_q"].numel() - 1
+        p.split_keys, p.num_splits = attn["split_keys"], attn["num_splits"]
+        sc = attn.get("scale")
+        p.att_scale = sc if sc is not None else 1.0 / math.sqrt(head_dim)
+        p.part_o, p.part_ml, p.att_counters = ptr(ws.part_o), ptr(ws.part_ml), ptr(ws.counters)
+        p.att_out, p.att_ld, p.att_sync = ptr(aout), aout.stride(0), ptr(ws.sync)
+        check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused(attn)")
+        return aout
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out
     return q_out if mode == "rope" else residual
+
+
+# qkv + decode attention in one launch (skinny_fused(attn=...)): off by default
+# until it measures faster in the pipeline (docs/PERF.md)
+FUSE_QKV_ATTN = os.environ.get("LOQA_FUSE_QKV_ATTN", "0") == "1"
+_NUM_CUS: list = []
+
+
+def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, attn, norm):
+    """(splits, rt, wr, xl) of a supported fused qkv + attention launch, or None."""
+    if not FUSE_QKV_ATTN:
+        return None
+    lin = wp if isinstance(wp, FusedLinear) else None
+    w = lin.wp if lin is not None else wp
+    nrm = _NORMS[lin.norm if (lin is not None and norm is None) else norm]
+    Mpad, K = x.shape
+    N = w.shape[0] * 16
+    tuned = _FSPLITS.get(("rope", N, K, Mpad))
+    free = splits is None and rt is None and wr is None and xl is None
+    S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
+    rt = rt or (tuned[1] if tuned else 2)
+    if xl is None:
+        xl = tuned[3] if (tuned and not splits and len(tuned) > 3) else 0
+    if wr is None:
+        wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
+    if wr != 1 and (S != 1 or N % (64 * rt)):
+        wr = 1
+    if not _NUM_CUS:
+        _NUM_CUS.append(torch.cuda.get_device_properties(x.device).multi_processor_count)
+    if free and (xl or (N // (16 * rt * wr)) * S > _NUM_CUS[0]):
+        # the tuned layout would not be resident at once: 32-row tiles, no split
+        S, rt, wr, xl = 1, 2, 1, 0
+    G = H // Hkv
+    bt, ws = attn["block_tables"], attn["workspace"]
+    ok = (Mpad in (16, 32, 64) and not xl and rt in (1, 2) and D in (64, 128)
+          and (nrm == 1 or (nrm == 2 and D == 64)) and Hkv <= 64 and G * attn["max_q"] <= 32
+          and attn["split_keys"] % 32 == 0 and bt is not None and k_cache.dim() == 4
+          and k_cache.shape[2] >= 16 and k_cache.shape[2] & (k_cache.shape[2] - 1) == 0
+          and q_out.is_contiguous() and q_out.shape[1] == H * D and q_out.numel() * 2 < (1 << 31)
+          and k_cache.numel() * 2 < (1 << 31) and ws.max_splits >= attn["num_splits"]
+          and ws.max_tokens >= Mpad and (attn["cu_q"].numel() - 1) * Hkv <= ws.counters.numel()
+          and (N // (16 * rt * wr)) * S <= _NUM_CUS[0])
+    if ok and attn.get("max_k") is not None:
+        assert attn["max_k"] <= bt.shape[1] * k_cache.shape[2], "context exceeds block table"
+    return (S, rt, wr, 0) if ok else None
 
 
 def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, positions,
@@ -1745,6 +1837,12 @@ PROJ_TABLE = {
     (1280, 1280): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc o
     (5120, 1280): [(2000, ("sk", 0, 1)), (1 << 30, ("sk", 6, 1))],                        # enc fc1
     (1280, 5120): [(2000, ("sk", 4, 1)), (1 << 30, ("sk", 5, 1))],                        # enc fc2
+    # Llama-3-70B TP=8 shards, prompt passes of ~320 rows (grid search,
+    # profiles/r5_tp70_shard_grid.jsonl): the planner's (4, 2) / (5, 1) picks
+    # were 38.1 / 85.3 us, these 27.2 / 69.7 us (hipBLASLt 28.1 / 69.8); o and
+    # down shards keep the planner's (5, 1) (15.2 / 37.6 us)
+    (1280, 8192): [(512, ("sk", 4, 4))],                                                   # qkv/8
+    (7168, 8192): [(512, ("sk", 4, 1))],                                                   # gate|up/8
 }
 
 

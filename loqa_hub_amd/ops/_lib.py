@@ -40,6 +40,12 @@ class FusedParams(ctypes.Structure):
         ("vc", c_void_p), ("slots", c_void_p),
         ("H", c_int), ("Hkv", c_int), ("D", c_int), ("blk", c_int),
         ("rt", c_int), ("wr", c_int), ("xl", c_int),
+        ("att", c_int), ("q_bytes", c_ll), ("kv_bytes", c_ll),
+        ("cu_q", c_void_p), ("ctx_lens", c_void_p), ("block_tables", c_void_p),
+        ("max_blocks", c_int), ("att_B", c_int), ("split_keys", c_int), ("num_splits", c_int),
+        ("att_scale", c_float), ("part_o", c_void_p), ("part_ml", c_void_p),
+        ("att_counters", c_void_p), ("att_out", c_void_p), ("att_ld", c_ll),
+        ("att_sync", c_void_p),
     ]
 
 

@@ -29,4 +29,6 @@ def test_frontend_single_relay_bypass_load():
                            client_procs=1, warm_s=1.0, bypass=True)
     assert r["success_rate"] == 1.0
     assert r["svc"]["bypassed"] == r["svc"]["windows"] > 0
-    assert r["added_ms_p50"] < 30.0, r          # no 300 ms window in the latency
+    # no 300 ms window in the latency (the bound leaves room for a loaded CI
+    # host: an unloaded run measures a few ms)
+    assert r["added_ms_p50"] < 150.0, r
