@@ -19,6 +19,7 @@
 //   end barrier (same flags, second set) so no peer overwrites a slot that is
 //   still being read.
 #include "common.h"
+#include <stdlib.h>
 
 #define CAR_MAX_WORLD 8
 #define CAR_BLOCKS 32          // blocks of the one-/two-shot kernels
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(256) void car_twoshot_kernel(CarPeers peers, const 
 #define CAR_SYS 17            // buffer-op cache policy: sc0 | sc1 (system coherent)
 
 typedef unsigned car_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_car __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t car_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
@@ -288,6 +290,42 @@ __device__ __forceinline__ float car_row_butterfly(float sq, int vpr) {
   return sq;
 }
 
+// LEAN: the phase-2 publish without the system-scope release fences (an L2
+// write-back each): everything a peer reads here lives in the uncached IPC
+// region and is stored with system-coherent (sc0 | sc1) buffer stores, so
+// draining this rank's stores (vmcnt(0)) before the flag store already orders
+// data before flag; peers read with sc0 | sc1 loads, so no acquire is needed.
+template <int LEAN>
+__device__ __forceinline__ bool car_publish_wait(const CarPeers& peers, int rank, int world, int blk,
+                                                 unsigned e) {
+  if constexpr (!LEAN) {
+    return car_barrier(peers, rank, world, 2, blk, e);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int q = 0; q < world; ++q)
+        st_sys(&reinterpret_cast<CarSignals*>(peers.base[q])->mid[blk][rank], e);
+    }
+    bool ok = true;
+    if (threadIdx.x < world) {
+      CarSignals* me = reinterpret_cast<CarSignals*>(peers.base[rank]);
+      const unsigned* f = &me->mid[blk][threadIdx.x];
+      unsigned spins = ld_sys(&me->error) ? CAR_SPIN_LIMIT : 0u;
+      while ((int)(ld_sys(f) - e) < 0) {
+        if (++spins > CAR_SPIN_LIMIT) {
+          st_sys(&me->error, 1u);
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    return __syncthreads_and(ok);
+  }
+}
+
+template <int LEAN>
 __global__ __launch_bounds__(256) void car_resid_kernel(CarPeers peers, long long in_off, long long res_off,
                                                         long long st_off, bf16_t* __restrict__ residual,
                                                         float* __restrict__ rowsq_out, int Mpad, int d,
@@ -321,17 +359,26 @@ __global__ __launch_bounds__(256) void car_resid_kernel(CarPeers peers, long lon
         uint2 o;
         sq = car_resid_math(rv, v, world, o);
         *reinterpret_cast<uint2*>(residual + el) = o;
-        *reinterpret_cast<uint2*>(rmine + el) = o;
+        if constexpr (LEAN)
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_car{o.x, o.y}, car_rsrc(rmine, res_bytes),
+                                                (unsigned)(el * 2), 0, CAR_SYS);
+        else
+          *reinterpret_cast<uint2*>(rmine + el) = o;
       }
       sq = car_row_butterfly(sq, vpr);
       if (cv == 0 && act) {
-        smine[(size_t)blk * Mpad + m] = sq;
+        if constexpr (LEAN)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq), car_rsrc(smine, st_bytes),
+                                                (unsigned)(((size_t)blk * Mpad + m) * 4), 0, CAR_SYS);
+        else
+          smine[(size_t)blk * Mpad + m] = sq;
         rowsq_out[((size_t)rank * nblk + blk) * Mpad + m] = sq;
       }
     }
-    // phase 2: publish (release at system scope, as car_barrier), then gather
-    // every other rank's rounded sub-slice b and its statistics
-    ok = car_barrier(peers, rank, world, 2, blk, e);
+    // phase 2: publish (release at system scope, as car_barrier; LEAN: see
+    // car_publish_wait), then gather every other rank's rounded sub-slice b
+    // and its statistics
+    ok = car_publish_wait<LEAN>(peers, rank, world, blk, e);
     if (ok) {
       const int vb = cw >> 3;                          // bf16x8 vectors per row of a sub-slice
       for (int q = 0; q < world; ++q) {
@@ -572,7 +619,12 @@ extern "C" int loqa_car_resid(void* hp, int which, void* residual, float* rowsq_
     return (int)hipErrorInvalidValue;
   for (int q = 0; q < h->world; ++q)
     if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(car_resid_kernel, dim3(nblk), dim3(256), 0, s, h->peers,
+  static int lean = -1;
+  if (lean < 0) {
+    const char* ev = getenv("LOQA_CAR_LEAN");
+    lean = ev ? atoi(ev) : 0;
+  }
+  hipLaunchKernelGGL(lean ? car_resid_kernel<1> : car_resid_kernel<0>, dim3(nblk), dim3(256), 0, s, h->peers,
                      (long long)car_in_off(h, which), (long long)car_res_off(h, which),
                      (long long)car_st_off(h, which), (bf16_t*)residual, rowsq_out, Mpad, d, h->rank,
                      h->world);

@@ -421,6 +421,9 @@ struct FusedParams {
   float att_scale; float* part_o; float* part_ml; int* att_counters;
   void* att_out; long long att_ld;
   int* att_sync;                     // [ready per kv head | work | exit | error], zeroed, left zero
+  // mode 4 (act) + att: attention over contiguous K / V rows (Whisper
+  // cross-attention over the encoder output): q = this GEMM's output
+  const void* att_k; const void* att_v; long long att_kv_stride; const int* att_kv_start;
 };
 
 struct FusedArgs {
@@ -433,10 +436,13 @@ struct FusedArgs {
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
   AttnDecArgs att; int att_B; int* att_sync; long long q_bytes, kv_bytes;     // ATTD
+  int att_need;                                 // ready tiles per kv head
 };
 
 // ---------------------------------------------------------------------------
-// qkv -> decode attention hand-off (ATTD = head dim, 0 = off; mode EPI_ROPE):
+// qkv -> decode attention hand-off (ATTD = head dim, 0 = off; mode EPI_ROPE;
+// mode EPI_ACT: a q projection -> attention over contiguous K / V rows, the
+// Whisper cross-attention, where only the q tiles are waited for):
 // the q / K / V rows of the step go out with write-through (sc1) stores and
 // each row tile then bumps its kv head's ready counter (release: sc1 stores,
 // vmcnt(0), relaxed agent atomic - guide §6 Guideline 16). Every workgroup of
@@ -452,14 +458,12 @@ struct FusedArgs {
 // replays). The attention arithmetic is attn_decode_kernel's, bit for bit.
 #define ATT_SPIN_LIMIT (1 << 20)
 
-__device__ __forceinline__ int att_need(int G, int D, int RT) { return (G + 2) * D / (16 * RT); }
-
 template <int D>
-__device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, int RT, DecSmem<D>& sm, int* sflag) {
+__device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, DecSmem<D>& sm, int* sflag) {
   int* sync = a.att_sync;
   const int Hkv = a.att.Hkv, Bq = a.att_B, ns = a.att.num_splits;
   const int n_items = ns * Hkv * Bq;
-  const int need = att_need(a.att.Hq / Hkv, D, RT);
+  const int need = a.att_need;
   for (;;) {
     __syncthreads();
     if (threadIdx.x == 0)
@@ -514,7 +518,8 @@ __device__ __forceinline__ void st_u2(bf16_t* base, size_t elem, uint2 v, long l
 // gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
 template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int ATTD = 0>
 __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedArgs a) {
-  static_assert(!ATTD || (MODE == EPI_ROPE && !XL), "attention hand-off: qkv (RoPE) mode only");
+  static_assert(!ATTD || ((MODE == EPI_ROPE || MODE == EPI_ACT) && !XL),
+                "attention hand-off: qkv (RoPE) or q projection (act) mode");
   constexpr int WK = 4 / WR;                     // waves along K
   constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
   constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
@@ -976,14 +981,21 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
         uint2 w2;
         w2.x = pack_bf16x2(o[0], o[1]);
         w2.y = pack_bf16x2(o[2], o[3]);
-        *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq) = w2;
+        st_u2<ATTD != 0>(a.out, (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq, w2, a.q_bytes);
+      }
+    }
+    if constexpr (ATTD != 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        const int kvh = ((tile * 16 * RT) / ATTD) / (a.att.Hq / a.att.Hkv);
+        __hip_atomic_fetch_add(&a.att_sync[kvh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
   if constexpr (ATTD == 0) return;
 attn_phase:
   if constexpr (ATTD != 0) {
-    attn_fused_phase<ATTD>(a, RT, *reinterpret_cast<DecSmem<ATTD>*>(smem),
+    attn_fused_phase<ATTD>(a, *reinterpret_cast<DecSmem<ATTD>*>(smem),
                            reinterpret_cast<int*>(smem) + (SMF - 1));
   }
 }
@@ -1109,28 +1121,28 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
 
 // qkv + attention (ATTD): RT 1 / 2, WR 1 / 4, Mpad 16 / 32 / 64, no XL, the
 // plain prefetch-group choice of launch_fused
-template <int RT, int MT, int WR, int NORM, int ATTD>
+template <int RT, int MT, int WR, int MODE, int NORM, int ATTD>
 static int launch_attd(const FusedArgs& a, hipStream_t st) {
   constexpr int WK = 4 / WR;
   dim3 grid(a.N / (16 * RT * WR), a.S);
   const int kw = a.K / 32 / (a.S * WK);
   if (MT <= 2 && kw % 4 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, EPI_ROPE, NORM, 0, ATTD>), grid,
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM, 0, ATTD>), grid,
                        dim3(256), 0, st, a);
   else if (kw % 2 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, WR, EPI_ROPE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, WR, MODE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, WR, EPI_ROPE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, WR, MODE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
-template <int NORM, int ATTD>
+template <int MODE, int NORM, int ATTD>
 static int dispatch_attd(const FusedArgs& a, int rt, int wr, hipStream_t st) {
 #define LQ_ATTD_MT(RT_, WR_)                                           \
   switch (a.Mpad) {                                                    \
-    case 16: return launch_attd<RT_, 1, WR_, NORM, ATTD>(a, st);       \
-    case 32: return launch_attd<RT_, 2, WR_, NORM, ATTD>(a, st);       \
-    default: return launch_attd<RT_, 4, WR_, NORM, ATTD>(a, st);       \
+    case 16: return launch_attd<RT_, 1, WR_, MODE, NORM, ATTD>(a, st);       \
+    case 32: return launch_attd<RT_, 2, WR_, MODE, NORM, ATTD>(a, st);       \
+    default: return launch_attd<RT_, 4, WR_, MODE, NORM, ATTD>(a, st);       \
   }
   if (rt == 1) {
     if (wr == 4) { LQ_ATTD_MT(1, 4) }
@@ -1172,13 +1184,20 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   if (p->att) {
-    // qkv + decode attention in one launch: the attention reads the q rows
-    // this launch writes (row stride H * D) and the paged caches it appends to
-    if (p->mode != EPI_ROPE || p->xl || p->rt > 2 || p->att != p->D || (p->D != 64 && p->D != 128) ||
-        !p->att_sync || !p->block_tables || !p->cu_q || !p->ctx_lens || !p->part_o || !p->part_ml ||
+    // GEMM + decode attention in one launch. rope: the attention reads the q
+    // rows this launch writes (row stride H * D) and the paged caches it
+    // appends to; act: q = the output rows (stride ldo), K / V contiguous rows
+    // at per-sequence starts (cross-attention, not causal)
+    const bool rope = p->mode == EPI_ROPE;
+    if ((!rope && p->mode != EPI_ACT) || p->xl || p->rt > 2 || p->att != p->D ||
+        (p->D != 64 && p->D != 128) || p->H % p->Hkv ||
+        !p->att_sync || !p->cu_q || !p->ctx_lens || !p->part_o || !p->part_ml ||
         !p->att_counters || !p->att_out || p->att_B < 1 || p->Hkv > 64 || p->num_splits < 1 ||
-        p->split_keys % DEC_TILE || p->blk < 16 || (p->blk & (p->blk - 1)) ||
-        p->q_bytes <= 0 || p->kv_bytes <= 0 || p->q_bytes >= (1ll << 31) || p->kv_bytes >= (1ll << 31) ||
+        p->split_keys % DEC_TILE || p->q_bytes <= 0 || p->q_bytes >= (1ll << 31) ||
+        (rope && (!p->block_tables || p->blk < 16 || (p->blk & (p->blk - 1)) || p->kv_bytes <= 0 ||
+                  p->kv_bytes >= (1ll << 31))) ||
+        (!rope && (p->act > 1 || N != p->H * p->D || !p->att_k || !p->att_v || !p->att_kv_start ||
+                   p->att_kv_stride % 8 || p->ldo % 8)) ||
         (p->norm != NORM_RMS && p->norm != NORM_LN) || (p->norm == NORM_LN && p->D != 64))
       return (int)hipErrorInvalidValue;
     // the whole grid must be resident at once (workers wait on tiles of the
@@ -1193,20 +1212,35 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
         return (int)hipErrorInvalidValue;
     }
     if ((long long)(N / (16 * p->rt * p->wr)) * S > ncu) return (int)hipErrorInvalidValue;
-    a.att = AttnDecArgs{a.q_out, (long long)p->H * p->D, a.kc, a.vc, 0, nullptr, p->cu_q, p->ctx_lens,
-                        p->block_tables, p->max_blocks, p->blk, p->H, p->Hkv,
-                        p->att_scale * 1.4426950408889634f, 1, p->split_keys, p->num_splits, p->part_o,
-                        p->part_ml, Mpad, p->att_counters, (bf16_t*)p->att_out, p->att_ld};
+    const float sl2 = p->att_scale * 1.4426950408889634f;
+    const int G = p->H / p->Hkv, tile_rows = 16 * p->rt;
+    if (rope)
+      a.att = AttnDecArgs{a.q_out, (long long)p->H * p->D, a.kc, a.vc, 0, nullptr, p->cu_q, p->ctx_lens,
+                          p->block_tables, p->max_blocks, p->blk, p->H, p->Hkv, sl2, 1, p->split_keys,
+                          p->num_splits, p->part_o, p->part_ml, Mpad, p->att_counters,
+                          (bf16_t*)p->att_out, p->att_ld};
+    else
+      a.att = AttnDecArgs{a.out, p->ldo, (const bf16_t*)p->att_k, (const bf16_t*)p->att_v,
+                          p->att_kv_stride, p->att_kv_start, p->cu_q, p->ctx_lens, nullptr, 0, 0, p->H,
+                          p->Hkv, sl2, 0, p->split_keys, p->num_splits, p->part_o, p->part_ml, Mpad,
+                          p->att_counters, (bf16_t*)p->att_out, p->att_ld};
+    // tiles per kv head: its G q heads (+ its k and v rows in rope mode)
+    a.att_need = (rope ? G + 2 : G) * p->D / tile_rows;
     a.att_B = p->att_B;
     a.att_sync = p->att_sync;
     a.q_bytes = p->q_bytes;
     a.kv_bytes = p->kv_bytes;
-    if (p->D == 128) {
-      if (p->norm == NORM_RMS) return dispatch_attd<NORM_RMS, 128>(a, p->rt, p->wr, st);
-      return (int)hipErrorInvalidValue;
+    if (rope) {
+      if (p->D == 128) {
+        if (p->norm == NORM_RMS) return dispatch_attd<EPI_ROPE, NORM_RMS, 128>(a, p->rt, p->wr, st);
+        return (int)hipErrorInvalidValue;
+      }
+      if (p->norm == NORM_RMS) return dispatch_attd<EPI_ROPE, NORM_RMS, 64>(a, p->rt, p->wr, st);
+      return dispatch_attd<EPI_ROPE, NORM_LN, 64>(a, p->rt, p->wr, st);
     }
-    if (p->norm == NORM_RMS) return dispatch_attd<NORM_RMS, 64>(a, p->rt, p->wr, st);
-    return dispatch_attd<NORM_LN, 64>(a, p->rt, p->wr, st);
+    // act mode: the Whisper q projection (LayerNorm prologue, D = 64) only
+    if (p->D == 64 && p->norm == NORM_LN) return dispatch_attd<EPI_ACT, NORM_LN, 64>(a, p->rt, p->wr, st);
+    return (int)hipErrorInvalidValue;
   }
   switch (p->mode) {
     case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, p->xl, st);

@@ -68,10 +68,14 @@ def _build_lib(name: str, sources: list[str], headers: list[str], flags: list[st
 
     with ThreadPoolExecutor(max_workers=min(8, len(sources))) as ex:
         objs = list(ex.map(compile_one, sources))
-    cmd = [hipcc, *flags, "-shared", "-fPIC", *objs, "-o", out]
+    # link next to the target and rename over it: a reader (a running process,
+    # a tree snapshot) never sees a half-written library
+    tmp = out + ".tmp"
+    cmd = [hipcc, *flags, "-shared", "-fPIC", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
     with open(stamp, "w") as f:
         f.write(digest)
     return out

@@ -408,11 +408,12 @@ def decode_step_fused(model: "WhisperModel", tokens: torch.Tensor, positions: to
                                        max_q=max_q, split_keys=split_keys,
                                        num_splits=self_splits, workspace=ws))
         ops.skinny_fused(a, F["o"], "resid", scratch, residual=residual, row_sums=True)
-        xq = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5)
         kv = xkv[i]
-        a = ops.attention(xq, kv, kv[:, d:], cu_q, n_heads=H, n_kv=H, head_dim=D, causal=False,
-                          max_q=max_q, cu_k=enc_starts, ctx_lens=enc_lens, grouped=True,
-                          split_keys=cross_split_keys, num_splits=enc_splits, workspace=ws)
+        a = ops.skinny_fused(residual, F["xq"], "act", scratch, eps=1e-5, n_heads=H, n_kv=H,
+                             head_dim=D,
+                             attn=dict(cu_q=cu_q, ctx_lens=enc_lens, kv_start=enc_starts, k=kv,
+                                       v=kv[:, d:], max_q=max_q, split_keys=cross_split_keys,
+                                       num_splits=enc_splits, workspace=ws))
         ops.skinny_fused(a, F["xo"], "resid", scratch, residual=residual, row_sums=True)
         m = ops.skinny_fused(residual, F["fc1"], "act", scratch, act="gelu", eps=1e-5)
         ops.skinny_fused(m, F["fc2"], "resid", scratch, residual=residual, row_sums=True)

@@ -1196,22 +1196,34 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     their tiles complete, gemm_skinny.hip ATTD), bit-identical to the two
     launches; otherwise the two launches."""
     if attn is not None:
-        assert mode == "rope"
-        fused = _gpu(x) and _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache,
-                                       n_heads, n_kv, head_dim, attn, norm)
+        assert mode in ("rope", "act")
+        rope = mode == "rope"
+        if not rope and out is None:
+            out = torch.empty(x.shape[0], wp.shape[0] * 16 if not isinstance(wp, FusedLinear)
+                              else wp.N, dtype=torch.bfloat16, device=x.device)
+        fused = _gpu(x) and _attd_plan(x, wp, scratch, splits, rt, wr, xl,
+                                       q_out if rope else out, k_cache if rope else attn["k"],
+                                       n_heads, n_kv, head_dim, attn, norm, mode, act)
         if not fused:
-            skinny_fused(x, wp, mode, scratch, splits=splits, norm=norm, eps=eps,
-                         rowsq_tiles=rowsq_tiles, rt=rt, positions=positions, cos_sin=cos_sin,
-                         q_out=q_out, k_cache=k_cache, v_cache=v_cache, slots=slots,
-                         n_heads=n_heads, n_kv=n_kv, head_dim=head_dim, bias=bias, colsum=colsum,
-                         wr=wr, xl=xl)
-            return attention(q_out, k_cache, v_cache, attn["cu_q"], n_heads=n_heads, n_kv=n_kv,
-                             head_dim=head_dim, causal=True, max_q=attn["max_q"],
-                             ctx_lens=attn["ctx_lens"], block_tables=attn["block_tables"],
+            qq = skinny_fused(x, wp, mode, scratch, splits=splits, norm=norm, eps=eps,
+                              rowsq_tiles=rowsq_tiles, rt=rt, positions=positions, cos_sin=cos_sin,
+                              q_out=q_out, k_cache=k_cache, v_cache=v_cache, slots=slots,
+                              n_heads=n_heads, n_kv=n_kv, head_dim=head_dim, bias=bias,
+                              colsum=colsum, wr=wr, xl=xl, out=out, act=act)
+            if rope:
+                return attention(q_out, k_cache, v_cache, attn["cu_q"], n_heads=n_heads,
+                                 n_kv=n_kv, head_dim=head_dim, causal=True, max_q=attn["max_q"],
+                                 ctx_lens=attn["ctx_lens"], block_tables=attn["block_tables"],
+                                 scale=attn.get("scale"), grouped=True,
+                                 split_keys=attn["split_keys"], num_splits=attn["num_splits"],
+                                 workspace=attn["workspace"], out=attn.get("out"),
+                                 max_k=attn.get("max_k"))
+            return attention(qq, attn["k"], attn["v"], attn["cu_q"], n_heads=n_heads, n_kv=n_kv,
+                             head_dim=head_dim, causal=False, max_q=attn["max_q"],
+                             cu_k=attn["kv_start"], ctx_lens=attn["ctx_lens"],
                              scale=attn.get("scale"), grouped=True,
                              split_keys=attn["split_keys"], num_splits=attn["num_splits"],
-                             workspace=attn["workspace"], out=attn.get("out"),
-                             max_k=attn.get("max_k"))
+                             workspace=attn["workspace"], out=attn.get("out"))
         splits, rt, wr, xl = fused
     if isinstance(wp, FusedLinear):
         lin = wp
@@ -1284,13 +1296,20 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.rt, p.wr, p.xl = rt, wr, int(bool(xl))
     if attn is not None:
         ws = attn["workspace"]
-        bt = attn["block_tables"]
+        bt = attn.get("block_tables")
         aout = attn.get("out")
         if aout is None:
             aout = torch.empty(Mpad, n_heads * head_dim, dtype=torch.bfloat16, device=x.device)
-        p.att, p.q_bytes, p.kv_bytes = head_dim, q_out.numel() * 2, k_cache.numel() * 2
-        p.cu_q, p.ctx_lens, p.block_tables = ptr(attn["cu_q"]), ptr(attn["ctx_lens"]), ptr(bt)
-        p.max_blocks, p.att_B = bt.shape[1], attn["cu_q"].numel() - 1
+        if mode == "rope":
+            p.att, p.q_bytes, p.kv_bytes = head_dim, q_out.numel() * 2, k_cache.numel() * 2
+            p.block_tables, p.max_blocks = ptr(bt), bt.shape[1]
+        else:
+            p.att, p.q_bytes, p.kv_bytes = head_dim, out.numel() * 2, 0
+            k, v = attn["k"], attn["v"]
+            p.att_k, p.att_v, p.att_kv_stride = ptr(k), ptr(v), k.stride(0)
+            p.att_kv_start = ptr(attn["kv_start"])
+        p.cu_q, p.ctx_lens = ptr(attn["cu_q"]), ptr(attn["ctx_lens"])
+        p.att_B = attn["cu_q"].numel() - 1
         p.split_keys, p.num_splits = attn["split_keys"], attn["num_splits"]
         sc = attn.get("scale")
         p.att_scale = sc if sc is not None else 1.0 / math.sqrt(head_dim)
@@ -1310,8 +1329,11 @@ FUSE_QKV_ATTN = os.environ.get("LOQA_FUSE_QKV_ATTN", "0") == "1"
 _NUM_CUS: list = []
 
 
-def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, attn, norm):
-    """(splits, rt, wr, xl) of a supported fused qkv + attention launch, or None."""
+def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, attn, norm,
+               mode="rope", act="none"):
+    """(splits, rt, wr, xl) of a supported fused GEMM + attention launch, or
+    None. rope: qkv + paged causal attention; act: q projection + attention
+    over contiguous K / V rows (``k_cache`` = the K rows)."""
     if not FUSE_QKV_ATTN:
         return None
     lin = wp if isinstance(wp, FusedLinear) else None
@@ -1319,7 +1341,7 @@ def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, at
     nrm = _NORMS[lin.norm if (lin is not None and norm is None) else norm]
     Mpad, K = x.shape
     N = w.shape[0] * 16
-    tuned = _FSPLITS.get(("rope", N, K, Mpad))
+    tuned = _FSPLITS.get((mode, N, K, Mpad))
     free = splits is None and rt is None and wr is None and xl is None
     S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
     rt = rt or (tuned[1] if tuned else 2)
@@ -1335,16 +1357,24 @@ def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, at
         # the tuned layout would not be resident at once: 32-row tiles, no split
         S, rt, wr, xl = 1, 2, 1, 0
     G = H // Hkv
-    bt, ws = attn["block_tables"], attn["workspace"]
-    ok = (Mpad in (16, 32, 64) and not xl and rt in (1, 2) and D in (64, 128)
-          and (nrm == 1 or (nrm == 2 and D == 64)) and Hkv <= 64 and G * attn["max_q"] <= 32
-          and attn["split_keys"] % 32 == 0 and bt is not None and k_cache.dim() == 4
-          and k_cache.shape[2] >= 16 and k_cache.shape[2] & (k_cache.shape[2] - 1) == 0
-          and q_out.is_contiguous() and q_out.shape[1] == H * D and q_out.numel() * 2 < (1 << 31)
-          and k_cache.numel() * 2 < (1 << 31) and ws.max_splits >= attn["num_splits"]
+    ws = attn["workspace"]
+    ok = (Mpad in (16, 32, 64) and not xl and rt in (1, 2) and D in (64, 128) and H % Hkv == 0
+          and Hkv <= 64 and G * attn["max_q"] <= 32 and attn["split_keys"] % 32 == 0
+          and q_out.numel() * 2 < (1 << 31) and ws.max_splits >= attn["num_splits"]
           and ws.max_tokens >= Mpad and (attn["cu_q"].numel() - 1) * Hkv <= ws.counters.numel()
           and (N // (16 * rt * wr)) * S <= _NUM_CUS[0])
-    if ok and attn.get("max_k") is not None:
+    if mode == "rope":
+        bt = attn["block_tables"]
+        ok = ok and ((nrm == 1 and D in (64, 128)) or (nrm == 2 and D == 64)) \
+            and bt is not None and k_cache.dim() == 4 and k_cache.shape[2] >= 16 \
+            and k_cache.shape[2] & (k_cache.shape[2] - 1) == 0 and q_out.is_contiguous() \
+            and q_out.shape[1] == H * D and k_cache.numel() * 2 < (1 << 31)
+    else:
+        v = attn["v"]
+        ok = ok and nrm == 2 and D == 64 and act in ("none", "gelu") and N == H * D \
+            and q_out.stride(0) % 8 == 0 and k_cache.stride(0) == v.stride(0) \
+            and k_cache.stride(0) % 8 == 0 and attn.get("kv_start") is not None
+    if ok and mode == "rope" and attn.get("max_k") is not None:
         assert attn["max_k"] <= bt.shape[1] * k_cache.shape[2], "context exceeds block table"
     return (S, rt, wr, 0) if ok else None
 

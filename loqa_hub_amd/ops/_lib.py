@@ -46,6 +46,7 @@ class FusedParams(ctypes.Structure):
         ("att_scale", c_float), ("part_o", c_void_p), ("part_ml", c_void_p),
         ("att_counters", c_void_p), ("att_out", c_void_p), ("att_ld", c_ll),
         ("att_sync", c_void_p),
+        ("att_k", c_void_p), ("att_v", c_void_p), ("att_kv_stride", c_ll), ("att_kv_start", c_void_p),
     ]
 
 

@@ -197,3 +197,71 @@ def test_fused_qkv_attention_cpu_falls_back():
         for h in range(H):
             v = vc[blkid, h // G, off].float()
             assert torch.allclose(a[b, h * D:(h + 1) * D].float(), v, atol=1e-2)
+
+
+def _xcase(Mpad, max_q, seed=0, n_audio=1500):
+    """Whisper large-v3 cross-attention step: q projection (LayerNorm
+    prologue + bias) of the decoder rows, K / V = per-utterance encoder rows."""
+    H, D, K = 20, 64, 1280
+    g = torch.Generator().manual_seed(seed)
+    dev = torch.device("cuda", 0)
+    w = (torch.randn(K, K, generator=g) * 0.02).bfloat16()
+    nw = (torch.rand(K, generator=g) + 0.5).bfloat16()
+    nb_ = (torch.randn(K, generator=g) * 0.1).bfloat16()
+    bias = (torch.randn(K, generator=g) * 0.1).bfloat16()
+    lin = ops.FusedLinear(w.to(dev), norm="ln", norm_w=nw.to(dev), norm_b=nb_.to(dev),
+                          bias=bias.to(dev))
+    B = max(1, Mpad // max_q - (1 if Mpad // max_q > 2 else 0))
+    qlens = [max_q if b % 3 else max(1, max_q // 2) for b in range(B)]
+    cu = [0]
+    for q in qlens:
+        cu.append(cu[-1] + q)
+    kv = (torch.randn(B * n_audio, 2 * K, generator=g) * 0.5).bfloat16().to(dev)
+    return dict(H=H, D=D, K=K, lin=lin, x=torch.randn(Mpad, K, generator=g).bfloat16().to(dev),
+                kv=kv, cu_q=torch.tensor(cu, dtype=torch.int32, device=dev),
+                starts=torch.arange(B, dtype=torch.int32, device=dev) * n_audio,
+                lens=torch.full((B,), n_audio, dtype=torch.int32, device=dev), max_q=max_q, B=B)
+
+
+def _xrun(c, fuse, *, S, rt, wr, ws, scr, split_keys=512):
+    ops.FUSE_QKV_ATTN = fuse
+    Mpad = c["x"].shape[0]
+    out = torch.empty(Mpad, c["K"], dtype=torch.bfloat16, device=c["x"].device)
+    ns = -(-1500 // split_keys)
+    scr.seed_stats(c["x"])
+    a = ops.skinny_fused(
+        c["x"], c["lin"], "act", scr, splits=S, rt=rt, wr=wr, xl=0, eps=1e-5, rowsq_tiles=1,
+        out=out, n_heads=c["H"], n_kv=c["H"], head_dim=c["D"],
+        attn=dict(cu_q=c["cu_q"], ctx_lens=c["lens"], kv_start=c["starts"], k=c["kv"],
+                  v=c["kv"][:, c["K"]:], max_q=c["max_q"], split_keys=split_keys, num_splits=ns,
+                  workspace=ws))
+    torch.cuda.synchronize()
+    T = int(c["cu_q"][-1])
+    return out[:T].clone(), a[:T].clone()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Mpad", [16, 32, 64])
+@pytest.mark.parametrize("rt,wr,S", [(1, 1, 1), (2, 1, 1), (1, 1, 2), (1, 4, 1), (2, 4, 1)])
+@pytest.mark.parametrize("max_q", [1, 4])
+def test_fused_xq_cross_attention_bitwise_gpu(restore_flag, Mpad, rt, wr, S, max_q):
+    """The Whisper cross-attention hand-off (act mode: q projection ->
+    attention over the encoder rows) equals the two launches bit for bit."""
+    c = _xcase(Mpad, max_q, seed=Mpad + max_q)
+    dev = c["x"].device
+    ws = ops.AttnWorkspace(dev, 64, c["H"], c["D"], 64)
+    scr = ops.FusedScratch(dev)
+    ops.FUSE_QKV_ATTN = True
+    plan = ops._attd_plan(c["x"], c["lin"], scr, S, rt, wr, 0,
+                          torch.empty(Mpad, c["K"], dtype=torch.bfloat16, device=dev), c["kv"],
+                          c["H"], c["H"], c["D"],
+                          dict(cu_q=c["cu_q"], ctx_lens=c["lens"], kv_start=c["starts"],
+                               k=c["kv"], v=c["kv"][:, c["K"]:], max_q=c["max_q"],
+                               split_keys=512, num_splits=3, workspace=ws), None, "act", "none")
+    assert plan is not None, "the fused launch must be the path under test"
+    base = _xrun(c, False, S=S, rt=rt, wr=wr, ws=ws, scr=scr)
+    fused = _xrun(c, True, S=S, rt=rt, wr=wr, ws=ws, scr=scr)
+    for name, a, b in zip(("xq", "attn"), fused, base):
+        assert torch.equal(a, b), (name, float((a.float() - b.float()).abs().max()))
+    assert int(ws.sync.abs().sum()) == 0, ws.sync[:80].tolist()
+    assert int(ws.counters.abs().sum()) == 0
