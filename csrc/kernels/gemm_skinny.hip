@@ -424,6 +424,7 @@ struct FusedParams {
   // mode 4 (act) + att: attention over contiguous K / V rows (Whisper
   // cross-attention over the encoder output): q = this GEMM's output
   const void* att_k; const void* att_v; long long att_kv_stride; const int* att_kv_start;
+  int att_workers;                   // >= the GEMM's blocks: the rest are attention-only blocks
 };
 
 struct FusedArgs {
@@ -437,6 +438,8 @@ struct FusedArgs {
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
   AttnDecArgs att; int att_B; int* att_sync; long long q_bytes, kv_bytes;     // ATTD
   int att_need;                                 // ready tiles per kv head
+  int gemm_x;                                   // GEMM blocks along x (the rest: attention only)
+  int att_extra_x;                              // attention-only blocks along x
 };
 
 // ---------------------------------------------------------------------------
@@ -516,23 +519,22 @@ __device__ __forceinline__ void st_u2(bf16_t* base, size_t elem, uint2 v, long l
 // workgroup (L1 hits for the other 3) instead of once per wave, and no
 // cross-wave reduction is needed (measured on cold weights, M = 16: the
 // gate|up stream went from 48 us to 39 us). WR > 1 requires S == 1.
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int ATTD = 0>
-__global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedArgs a) {
-  static_assert(!ATTD || ((MODE == EPI_ROPE || MODE == EPI_ACT) && !XL),
-                "attention hand-off: qkv (RoPE) or q projection (act) mode");
+template <int RT, int MT, int WR>
+struct FusedSmem {
+  static constexpr int WK = 4 / WR;
+  static constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
+  static constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
+};
+
+// One (16 * RT * WR)-row output tile of the fused GEMM (a workgroup's whole
+// GEMM work; `return` = this workgroup's GEMM part is done)
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int ATTD>
+__device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs) {
   constexpr int WK = 4 / WR;                     // waves along K
-  constexpr int NRED = WK > 1 ? WR * (WK - 1) * RT * MT * 64 : 1;
-  constexpr int NSM = NRED * 4 > 1024 ? NRED * 4 : 1024;   // floats: reduce / prologue / ticket
   static_assert(!XL || WR == 4, "XL needs the 4 waves along rows");
   // XL + RoPE at MT 8: the RoPE cos/sin operands (RT * MT * 8 VGPRs) are
   // loaded after the k loop instead of being held through it
   constexpr bool EARLY_EPI = !(XL && MODE == EPI_ROPE && MT > 4);
-  // ATTD: the attention phase's LDS aliases the reduce / prologue area (one
-  // __shared__ array; the phase starts behind a workgroup barrier), + a flag word
-  constexpr int ATT_F = ATTD ? (int)(sizeof(DecSmem<ATTD ? ATTD : 64>) / 4) + 4 : 0;
-  constexpr int SMF = NSM > ATT_F ? NSM : ATT_F;
-  __shared__ __attribute__((aligned(16))) float smem[SMF];
-  __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   float4v_* red = reinterpret_cast<float4v_*>(smem);
   float* sred = smem;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -742,10 +744,7 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
           __hip_atomic_store(&a.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       t = __shfl(t, 0, 64);
-      if (t != a.S - 1) {
-        if constexpr (ATTD != 0) goto attn_phase;
-        else return;
-      }
+      if (t != a.S - 1) return;
     } else {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -756,10 +755,7 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
         sred[0] = (float)t;
       }
       __syncthreads();
-      if ((int)sred[0] != a.S - 1 || wave != 0) {
-        if constexpr (ATTD != 0) goto attn_phase;
-        else return;
-      }
+      if ((int)sred[0] != a.S - 1 || wave != 0) return;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // fixed summation order (split 0..S-1) whichever block arrives last
@@ -795,8 +791,7 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = tot[i][j];
   } else if (wk != 0) {
-    if constexpr (ATTD != 0) goto attn_phase;
-    else return;
+    return;
   }
 
   // ---- epilogue (the wk == 0 wave of each row tile): acc[i][j] = C[n0 + 4*(lane>>4) + r][m] for i = tile half
@@ -992,9 +987,26 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
       }
     }
   }
-  if constexpr (ATTD == 0) return;
-attn_phase:
-  if constexpr (ATTD != 0) {
+}
+
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int ATTD = 0>
+__global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedArgs a) {
+  static_assert(!ATTD || ((MODE == EPI_ROPE || MODE == EPI_ACT) && !XL),
+                "attention hand-off: qkv (RoPE) or q projection (act) mode");
+  constexpr int NSM = FusedSmem<RT, MT, WR>::NSM;
+  // ATTD: the attention phase's LDS aliases the reduce / prologue area (one
+  // __shared__ array; the phase starts behind a workgroup barrier), + a flag word
+  constexpr int ATT_F = ATTD ? (int)(sizeof(DecSmem<ATTD ? ATTD : 64>) / 4) + 4 : 0;
+  constexpr int SMF = NSM > ATT_F ? NSM : ATT_F;
+  __shared__ __attribute__((aligned(16))) float smem[SMF];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
+  if constexpr (ATTD == 0) {
+    skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, 0>(a, smem, xs);
+  } else {
+    // blocks past the GEMM's (gemm_x) are attention workers only: dispatched
+    // after every GEMM block of their XCD, they never hold a slot a producer
+    // waits for
+    if ((int)blockIdx.x < a.gemm_x) skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, ATTD>(a, smem, xs);
     attn_fused_phase<ATTD>(a, *reinterpret_cast<DecSmem<ATTD>*>(smem),
                            reinterpret_cast<int*>(smem) + (SMF - 1));
   }
@@ -1124,7 +1136,7 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
 template <int RT, int MT, int WR, int MODE, int NORM, int ATTD>
 static int launch_attd(const FusedArgs& a, hipStream_t st) {
   constexpr int WK = 4 / WR;
-  dim3 grid(a.N / (16 * RT * WR), a.S);
+  dim3 grid(a.gemm_x + a.att_extra_x, a.S);
   const int kw = a.K / 32 / (a.S * WK);
   if (MT <= 2 && kw % 4 == 0)
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM, 0, ATTD>), grid,
@@ -1227,6 +1239,8 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
     // tiles per kv head: its G q heads (+ its k and v rows in rope mode)
     a.att_need = (rope ? G + 2 : G) * p->D / tile_rows;
     a.att_B = p->att_B;
+    a.gemm_x = N / (16 * p->rt * p->wr);
+    a.att_extra_x = p->att_workers > a.gemm_x * S ? (p->att_workers - a.gemm_x * S + S - 1) / S : 0;
     a.att_sync = p->att_sync;
     a.q_bytes = p->q_bytes;
     a.kv_bytes = p->kv_bytes;

@@ -1310,6 +1310,9 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
             p.att_kv_start = ptr(attn["kv_start"])
         p.cu_q, p.ctx_lens = ptr(attn["cu_q"]), ptr(attn["ctx_lens"])
         p.att_B = attn["cu_q"].numel() - 1
+        # one attention worker per (split, kv head, sequence) item, as the
+        # standalone kernel's grid: the GEMM's blocks plus attention-only ones
+        p.att_workers = min(ATTD_MAX_WORKERS, attn["num_splits"] * n_kv * p.att_B)
         p.split_keys, p.num_splits = attn["split_keys"], attn["num_splits"]
         sc = attn.get("scale")
         p.att_scale = sc if sc is not None else 1.0 / math.sqrt(head_dim)
@@ -1326,6 +1329,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
 # qkv + decode attention in one launch (skinny_fused(attn=...)): off by default
 # until it measures faster in the pipeline (docs/PERF.md)
 FUSE_QKV_ATTN = os.environ.get("LOQA_FUSE_QKV_ATTN", "0") == "1"
+ATTD_MAX_WORKERS = int(os.environ.get("LOQA_ATTD_WORKERS", "2048"))
 _NUM_CUS: list = []
 
 

@@ -47,6 +47,7 @@ class FusedParams(ctypes.Structure):
         ("att_counters", c_void_p), ("att_out", c_void_p), ("att_ld", c_ll),
         ("att_sync", c_void_p),
         ("att_k", c_void_p), ("att_v", c_void_p), ("att_kv_stride", c_ll), ("att_kv_start", c_void_p),
+        ("att_workers", c_int),
     ]
 
 

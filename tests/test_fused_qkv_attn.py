@@ -19,7 +19,28 @@ SHAPES = {
 }
 
 
-def _case(shape, Mpad, max_q, seed=0, blk=16, nb=512):
+def _layout(Mpad, max_q, g, blk=16):
+    """Sequences of one decode step: q lengths, prior contexts, block tables."""
+    B = max(1, Mpad // max_q - (1 if Mpad // max_q > 2 else 0))   # some padded rows
+    qlens = [max_q if b % 3 else max(1, max_q // 2) for b in range(B)]
+    prior = [int(x) for x in torch.randint(1, 700, (B,), generator=g)]
+    prior[0] = 1                       # a sequence at its first decoded token
+    ctx = [p + q for p, q in zip(prior, qlens)]
+    max_blocks = max(-(-c // blk) for c in ctx) + 1
+    nb = B * max_blocks + 16
+    blocks = torch.randperm(nb, generator=g)[: B * max_blocks].view(B, max_blocks).int()
+    return B, qlens, prior, ctx, blocks, nb
+
+
+def test_decode_layout_builder_cpu():
+    for Mpad in (16, 32, 64):
+        for max_q in (1, 4):
+            B, qlens, prior, ctx, blocks, nb = _layout(Mpad, max_q, torch.Generator().manual_seed(1))
+            assert sum(qlens) <= Mpad and blocks.shape[0] == B and int(blocks.max()) < nb
+            assert all(-(-c // 16) <= blocks.shape[1] for c in ctx)
+
+
+def _case(shape, Mpad, max_q, seed=0, blk=16):
     H, Hkv, D, K, norm = SHAPES[shape]
     g = torch.Generator().manual_seed(seed)
     dev = torch.device("cuda", 0)
@@ -34,15 +55,9 @@ def _case(shape, Mpad, max_q, seed=0, blk=16, nb=512):
         bias = (torch.randn(N, generator=g) * 0.1).bfloat16()
         lin = ops.FusedLinear(w.to(dev), norm="ln", norm_w=nw.to(dev), norm_b=nb_.to(dev),
                               bias=bias.to(dev), perm=perm.to(dev))
-    B = max(1, Mpad // max_q - (1 if Mpad // max_q > 2 else 0))   # some padded rows
-    qlens = [max_q if b % 3 else max(1, max_q // 2) for b in range(B)]
+    B, qlens, prior, ctx, blocks, nb = _layout(Mpad, max_q, g, blk)
     T = sum(qlens)
     assert T <= Mpad and (H // Hkv) * max_q <= 32
-    prior = [int(x) for x in torch.randint(1, 700, (B,), generator=g)]
-    prior[0] = 1                       # a sequence at its first decoded token
-    ctx = [p + q for p, q in zip(prior, qlens)]
-    max_blocks = max(-(-c // blk) for c in ctx) + 1
-    blocks = torch.randperm(nb, generator=g)[: B * max_blocks].view(B, max_blocks).int()
     kc = (torch.randn(nb, Hkv, blk, D, generator=g) * 0.5).bfloat16()
     vc = (torch.randn(nb, Hkv, blk, D, generator=g) * 0.5).bfloat16()
     pos, slots = [], []
@@ -216,7 +231,8 @@ def _xcase(Mpad, max_q, seed=0, n_audio=1500):
     cu = [0]
     for q in qlens:
         cu.append(cu[-1] + q)
-    kv = (torch.randn(B * n_audio, 2 * K, generator=g) * 0.5).bfloat16().to(dev)
+    gd = torch.Generator(device=dev).manual_seed(seed)
+    kv = (torch.randn(B * n_audio, 2 * K, generator=gd, device=dev) * 0.5).bfloat16()
     return dict(H=H, D=D, K=K, lin=lin, x=torch.randn(Mpad, K, generator=g).bfloat16().to(dev),
                 kv=kv, cu_q=torch.tensor(cu, dtype=torch.int32, device=dev),
                 starts=torch.arange(B, dtype=torch.int32, device=dev) * n_audio,
