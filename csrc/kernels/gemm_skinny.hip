@@ -439,7 +439,7 @@ struct FusedArgs {
   AttnDecArgs att; int att_B; int* att_sync; long long q_bytes, kv_bytes;     // ATTD
   int att_need;                                 // ready tiles per kv head
   int gemm_x;                                   // GEMM blocks along x (the rest: attention only)
-  int att_extra_x;                              // attention-only blocks along x
+  int att_extra;                                // attention-only blocks (after the GEMM's)
 };
 
 // ---------------------------------------------------------------------------
@@ -529,7 +529,8 @@ struct FusedSmem {
 // One (16 * RT * WR)-row output tile of the fused GEMM (a workgroup's whole
 // GEMM work; `return` = this workgroup's GEMM part is done)
 template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int ATTD>
-__device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs) {
+__device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs, const int bx,
+                                                  const int by) {
   constexpr int WK = 4 / WR;                     // waves along K
   static_assert(!XL || WR == 4, "XL needs the 4 waves along rows");
   // XL + RoPE at MT 8: the RoPE cos/sin operands (RT * MT * 8 VGPRs) are
@@ -539,8 +540,8 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
   float* sred = smem;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave % WR, wk = wave / WR;
-  const int tile = blockIdx.x * WR + wr;         // (16 * RT)-row output tile
-  const int s = blockIdx.y;
+  const int tile = bx * WR + wr;                 // (16 * RT)-row output tile
+  const int s = by;                              // K split
   const int KS = a.K >> 5;
   const int kw = KS / (a.S * WK);
   const int ks0 = (s * WK + wk) * kw;
@@ -724,7 +725,7 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
     // WR == 1: wave 0 holds the workgroup's tile; XL (WR == 4): every wave
     // publishes and tickets its own tile.
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        a.part, 0, (int)((size_t)gridDim.x * WR * a.S * RT * MT * 64 * 16), 0x00020000);
+        a.part, 0, (int)((size_t)(a.N / (16 * RT * WR)) * WR * a.S * RT * MT * 64 * 16), 0x00020000);
     const int slab0 = tile * a.S * RT * MT;
     if (WR > 1 || wave == 0) {
 #pragma unroll
@@ -1001,12 +1002,15 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
   __shared__ __attribute__((aligned(16))) float smem[SMF];
   __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   if constexpr (ATTD == 0) {
-    skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, 0>(a, smem, xs);
+    skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, 0>(a, smem, xs, blockIdx.x, blockIdx.y);
   } else {
-    // blocks past the GEMM's (gemm_x) are attention workers only: dispatched
-    // after every GEMM block of their XCD, they never hold a slot a producer
-    // waits for
-    if ((int)blockIdx.x < a.gemm_x) skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, ATTD>(a, smem, xs);
+    // 1-D grid: blocks [0, gemm_x * S) are the GEMM's (x fastest, then the K
+    // split), the rest attention workers only. Dispatched in linear order,
+    // every GEMM block of an XCD is placed before any attention-only block
+    // of that XCD, so those never hold a slot a producer waits for
+    const int id = blockIdx.x;
+    if (id < a.gemm_x * a.S)
+      skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, ATTD>(a, smem, xs, id % a.gemm_x, id / a.gemm_x);
     attn_fused_phase<ATTD>(a, *reinterpret_cast<DecSmem<ATTD>*>(smem),
                            reinterpret_cast<int*>(smem) + (SMF - 1));
   }
@@ -1136,7 +1140,7 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
 template <int RT, int MT, int WR, int MODE, int NORM, int ATTD>
 static int launch_attd(const FusedArgs& a, hipStream_t st) {
   constexpr int WK = 4 / WR;
-  dim3 grid(a.gemm_x + a.att_extra_x, a.S);
+  dim3 grid(a.gemm_x * a.S + a.att_extra);
   const int kw = a.K / 32 / (a.S * WK);
   if (MT <= 2 && kw % 4 == 0)
     hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM, 0, ATTD>), grid,
@@ -1240,7 +1244,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
     a.att_need = (rope ? G + 2 : G) * p->D / tile_rows;
     a.att_B = p->att_B;
     a.gemm_x = N / (16 * p->rt * p->wr);
-    a.att_extra_x = p->att_workers > a.gemm_x * S ? (p->att_workers - a.gemm_x * S + S - 1) / S : 0;
+    a.att_extra = p->att_workers > a.gemm_x * S ? p->att_workers - a.gemm_x * S : 0;
     a.att_sync = p->att_sync;
     a.q_bytes = p->q_bytes;
     a.kv_bytes = p->kv_bytes;
