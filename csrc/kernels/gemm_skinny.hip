@@ -484,7 +484,7 @@ __device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, DecSmem<D>&
           __hip_atomic_store(&sync[66], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(8);   // ~0.2 us between polls: hundreds of pollers share a line
       }
     }
     __syncthreads();

@@ -70,7 +70,66 @@ def bench(shape, Mpad, max_q, fuse, rt, wr, S, ctx_scale=1.0):
     return round(ts[len(ts) // 2], 2), c["B"], c["max_ctx"]
 
 
+def bench_x(Mpad, max_q, fuse, rt, wr, S):
+    from tests.test_fused_qkv_attn import _xcase
+    c = _xcase(Mpad, max_q, seed=1)
+    dev = c["x"].device
+    ws = ops.AttnWorkspace(dev, 64, c["H"], c["D"], 64)
+    scr = ops.FusedScratch(dev)
+    scr.seed_stats(c["x"])
+    out = torch.empty(Mpad, c["K"], dtype=torch.bfloat16, device=dev)
+    ao = torch.empty(Mpad, c["K"], dtype=torch.bfloat16, device=dev)
+    lins = [c["lin"]]
+    import copy
+    for _ in range(LAYERS - 1):
+        l2 = copy.copy(c["lin"])
+        l2.wp = c["lin"].wp.clone()
+        lins.append(l2)
+    ops.FUSE_QKV_ATTN = fuse
+
+    def step():
+        for lin in lins:
+            ops.skinny_fused(c["x"], lin, "act", scr, splits=S, rt=rt, wr=wr, xl=0, eps=1e-5,
+                             rowsq_tiles=1, out=out, n_heads=c["H"], n_kv=c["H"], head_dim=c["D"],
+                             attn=dict(cu_q=c["cu_q"], ctx_lens=c["lens"], kv_start=c["starts"],
+                                       k=c["kv"], v=c["kv"][:, c["K"]:], max_q=max_q,
+                                       split_keys=512, num_splits=3, workspace=ws, out=ao))
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(20):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1000 / LAYERS)
+    ts.sort()
+    assert int(ws.sync.abs().sum()) == 0, ws.sync[:80].tolist()
+    return round(ts[len(ts) // 2], 2), c["B"]
+
+
 def main():
+    for Mpad, max_q in ((16, 1), (16, 4), (32, 1)):
+        for rt, wr, S in ((1, 1, 1), (2, 1, 1)):
+            r = {"shape": "whisper_cross", "Mpad": Mpad, "max_q": max_q, "rt": rt, "wr": wr, "S": S}
+            r["two_launch_us"], r["B"] = bench_x(Mpad, max_q, False, rt, wr, S)
+            r["fused_us"] = bench_x(Mpad, max_q, True, rt, wr, S)[0]
+            print(json.dumps(r), flush=True)
+    main_self()
+
+
+def main_self():
     res = []
     for shape, Mpad, max_q in (("llama", 16, 1), ("llama", 32, 1), ("llama", 16, 4),
                                ("whisper", 16, 1), ("whisper", 32, 1), ("whisper", 64, 4)):
