@@ -37,12 +37,29 @@ struct AttnDecArgs {
   const int* kv_start; const int* cu_q; const int* ctx_lens; const int* block_tables;
   int max_blocks, blk, Hq, Hkv; float scale_log2; int causal, split_keys, num_splits;
   float* part_o; float* part_ml; int total_q; int* counters; bf16_t* out; long long o_stride;
+  // SC1 bodies (the fused GEMM's attention workers): byte sizes of q and of
+  // one K (= V) cache, for the write-through-coherent buffer loads
+  long long q_bytes, kv_bytes;
 };
+
+// 16-byte load; SC1: a buffer load with the sc1 policy (reads what another
+// workgroup stored write-through in this launch, without an L2-invalidating
+// acquire fence - guide §6 Guideline 16)
+template <int SC1>
+__device__ __forceinline__ uint4 ld16(const bf16_t* base, size_t elem, long long nbytes) {
+  if constexpr (SC1) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), 0, (int)nbytes, 0x00020000);
+    const u32x4_ v = __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(elem * 2), 0, 16);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(base + elem);
+  }
+}
 
 // One workgroup's work item (split, kv head, sequence) - the body of the
 // standalone kernel, whose grid is (splits, kv heads, sequences); 256
 // threads, 4 waves.
-template <int D, int PF, int LOOP = 0>
+template <int D, int PF, int LOOP = 0, int SC1 = 0>
 __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int split, const int kvh,
                                                  const int b, DecSmem<D>& sm) {
   const bf16_t* __restrict__ q = A.q;
@@ -108,7 +125,8 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
     const bf16_t* qr = q + (size_t)(q0 + (row_valid ? qi : 0)) * q_stride + (size_t)head * D;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      uint4 v = row_valid ? *reinterpret_cast<const uint4*>(qr + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      uint4 v = row_valid ? ld16<SC1>(q, (size_t)(qr - q) + 16 * s + 8 * h, A.q_bytes)
+                          : make_uint4(0, 0, 0, 0);
       qf[s] = *reinterpret_cast<bf16x8*>(&v);
     }
   }
@@ -146,13 +164,16 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
     const size_t off = row_off(ok ? key : kt);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      kraw[s] = ok ? *reinterpret_cast<const uint4*>(kc + off + 16 * s + 8 * h) : make_uint4(0, 0, 0, 0);
+      kraw[s] = ok ? (SC1 && paged ? ld16<SC1>(kc, off + 16 * s + 8 * h, A.kv_bytes)
+                                   : ld16<0>(kc, off + 16 * s + 8 * h, 0))
+                   : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = lane + 64 * i;
       const int kr = c / CH, cc = (c - kr * CH) * 8;
       const int k2 = kt + kr;
-      vraw[i] = k2 < kend ? *reinterpret_cast<const uint4*>(vc + row_off(k2) + cc)
+      vraw[i] = k2 < kend ? (SC1 && paged ? ld16<SC1>(vc, row_off(k2) + cc, A.kv_bytes)
+                                          : ld16<0>(vc, row_off(k2) + cc, 0))
                           : make_uint4(0, 0, 0, 0);
     }
   };

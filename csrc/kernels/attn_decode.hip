@@ -53,7 +53,7 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   const AttnDecArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, kv_stride,
                       kv_start, cu_q, ctx_lens, block_tables, max_blocks, blk, Hq, Hkv, sl2, causal,
                       split_keys, num_splits, part_o, part_ml, total_q, counters, (bf16_t*)o,
-                      o_stride};
+                      o_stride, 0, 0};
   if (D == 128)
     hipLaunchKernelGGL((attn_decode_kernel<128, 0>), grid, dim3(256), 0, s, a);
   else

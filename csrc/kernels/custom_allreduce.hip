@@ -621,8 +621,10 @@ extern "C" int loqa_car_resid(void* hp, int which, void* residual, float* rowsq_
     if (!h->peers.base[q]) return (int)hipErrorInvalidValue;
   static int lean = -1;
   if (lean < 0) {
+    // default on: 7.46 -> 6.69 ms per config-5 rank step, multi-process TP
+    // tests bitwise (profiles/r5_config5_lean_allreduce.txt)
     const char* ev = getenv("LOQA_CAR_LEAN");
-    lean = ev ? atoi(ev) : 0;
+    lean = ev ? atoi(ev) : 1;
   }
   hipLaunchKernelGGL(lean ? car_resid_kernel<1> : car_resid_kernel<0>, dim3(nblk), dim3(256), 0, s, h->peers,
                      (long long)car_in_off(h, which), (long long)car_res_off(h, which),

@@ -451,8 +451,10 @@ struct FusedArgs {
 // vmcnt(0), relaxed agent atomic - guide §6 Guideline 16). Every workgroup of
 // the grid, once its tiles are done, turns into an attention worker: it takes
 // (split, kv head, sequence) items from a work counter, waits for the item's
-// kv head to be complete ((G + 2) x D / (16 RT) tiles), takes an agent
-// acquire and runs the decode-attention body of attn_decode.h - the launch
+// kv head to be complete ((G + 2) x D / (16 RT) tiles) and runs the
+// decode-attention body of attn_decode.h, reading the handed-off rows with
+// sc1 loads (an agent acquire fence here invalidated the L2 under every
+// concurrent kernel: measured 45 vs 30 us per layer alone) - the launch
 // boundary between qkv and attention disappears and the attention of a head
 // starts as soon as ITS tiles are in. Workers only wait for tiles of the same
 // grid whose workgroups hold no dependency (they are producers that have not
@@ -488,8 +490,10 @@ __device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, DecSmem<D>&
       }
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    attn_decode_body<D, 0, 1>(a.att, split, kvh, b, sm);
+    // no acquire fence (on this chip an agent-scope acquire invalidates the
+    // L2 under every other workgroup's feet): the handed-off q / K / V rows
+    // are read with sc1 buffer loads instead
+    attn_decode_body<D, 0, 1, 1>(a.att, split, kvh, b, sm);
   }
   if (threadIdx.x == 0) {
     const int e = __hip_atomic_fetch_add(&sync[65], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -1234,12 +1238,12 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
       a.att = AttnDecArgs{a.q_out, (long long)p->H * p->D, a.kc, a.vc, 0, nullptr, p->cu_q, p->ctx_lens,
                           p->block_tables, p->max_blocks, p->blk, p->H, p->Hkv, sl2, 1, p->split_keys,
                           p->num_splits, p->part_o, p->part_ml, Mpad, p->att_counters,
-                          (bf16_t*)p->att_out, p->att_ld};
+                          (bf16_t*)p->att_out, p->att_ld, p->q_bytes, p->kv_bytes};
     else
       a.att = AttnDecArgs{a.out, p->ldo, (const bf16_t*)p->att_k, (const bf16_t*)p->att_v,
                           p->att_kv_stride, p->att_kv_start, p->cu_q, p->ctx_lens, nullptr, 0, 0, p->H,
                           p->Hkv, sl2, 0, p->split_keys, p->num_splits, p->part_o, p->part_ml, Mpad,
-                          p->att_counters, (bf16_t*)p->att_out, p->att_ld};
+                          p->att_counters, (bf16_t*)p->att_out, p->att_ld, p->q_bytes, 0};
     // tiles per kv head: its G q heads (+ its k and v rows in rope mode)
     a.att_need = (rope ? G + 2 : G) * p->D / tile_rows;
     a.att_B = p->att_B;
