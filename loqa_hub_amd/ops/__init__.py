@@ -1029,6 +1029,36 @@ def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F:
     return z
 
 
+# ------------------------------------------------------ Infinity Cache prefetch
+# Weight prefetch into the die-level cache on a side stream during the decode
+# layer's latency-bound phases (csrc/kernels/l3_prefetch.hip); off by default
+# until measured (docs/PERF.md)
+L3_PREFETCH = os.environ.get("LOQA_L3_PREFETCH", "0") == "1"
+L3_PREFETCH_WGS = int(os.environ.get("LOQA_L3_PREFETCH_WGS", "128"))
+_L3_SINKS: dict = {}
+
+
+def l3_prefetch(tensors: list, wgs: int | None = None) -> None:
+    """Read ``tensors`` (device, contiguous; <= 8) front to back on the current
+    stream so their bytes sit in the Infinity Cache for a later consumer. A
+    pure read - nothing waits for it. No-op off the GPU."""
+    ts = [t.wp if isinstance(t, FusedLinear) else t for t in tensors if t is not None]
+    if not ts or not _gpu(ts[0]):
+        return
+    assert len(ts) <= 8
+    dev = ts[0].device
+    sink = _L3_SINKS.get(dev)
+    if sink is None:
+        sink = _L3_SINKS[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
+    for t in ts:
+        assert t.is_contiguous() and (t.numel() * t.element_size()) % 16 == 0
+    n = len(ts)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    sizes = (ctypes.c_longlong * n)(*[t.numel() * t.element_size() for t in ts])
+    check(kernels().loqa_l3_prefetch(ptrs, sizes, n, wgs or L3_PREFETCH_WGS, ptr(sink),
+                                     torch.cuda.current_stream(dev).cuda_stream), "l3_prefetch")
+
+
 # ------------------------------------------------------------ fused decode GEMMs
 class FusedScratch:
     """Device state shared by the fused decode GEMMs of one engine: split-K
