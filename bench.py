@@ -100,7 +100,8 @@ async def _start_hub(args, pipe, nats_port: int, info):
     db = os.path.join(tempfile.mkdtemp(prefix="loqa-bench-"), "hub.db")
     cfg = cfgmod.load({"LOQA_DB_PATH": db, "NATS_URL": f"nats://127.0.0.1:{nats_port}",
                        "ARBITRATION_SCOPE": "per_relay_group",
-                       "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms"})
+                       "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms",
+                       "ARBITRATION_SINGLE_RELAY_BYPASS": "true" if args.bypass else "false"})
     hints: dict[str, str] = {}
     srv = HubServer(cfg, skills_dir=os.path.join(os.path.dirname(db), "skills"),
                     skills_config_store=os.path.join(os.path.dirname(db), "skillcfg"),
@@ -205,6 +206,7 @@ def run_hub_dp(args) -> int:
                        "NATS_URL": f"nats://127.0.0.1:{port}",
                        "ARBITRATION_SCOPE": "per_relay_group",
                        "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms",
+                       "ARBITRATION_SINGLE_RELAY_BYPASS": "true" if args.bypass else "false",
                        "HUB_STT_MODEL": args.stt, "HUB_LLM_MODEL": args.llm,
                        "HUB_TTS_MODEL": args.tts_model, "HUB_MAX_BATCH": str(max(B, 8)),
                        "HUB_TTS_BACKEND": "gpu" if args.tts else "none",
@@ -353,6 +355,9 @@ def main(argv=None) -> int:
     ap.add_argument("--paced", action="store_true",
                     help="--mode hub: relays send their speech in real time (100 ms chunks "
                          "every 100 ms); latency is then counted from the end of speech")
+    ap.add_argument("--bypass", action="store_true",
+                    help="--mode hub: a relay alone in its group wins at once (opt-in "
+                         "ARBITRATION_SINGLE_RELAY_BYPASS; every bench relay is its own group)")
     ap.add_argument("--window-ms", type=float, default=300.0,
                     help="--mode hub: arbitration window (the reference's 300 ms)")
     ap.add_argument("--inflight", type=int, default=2,

@@ -657,3 +657,14 @@ def test_hip_runtime_is_torchs_copy():
     with open("/proc/self/maps") as f:
         copies = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
     assert len(copies) == 1, copies
+
+
+def test_bench_cpu_smoke_hub_mode_bypass():
+    """--mode hub --bypass: every bench relay is alone in its group, so no
+    utterance waits for the arbitration window (the window here is 5 s: a
+    run that waited would time out of the smoke's budget)."""
+    out = _run([sys.executable, "bench.py", "--cpu-smoke", "--mode", "hub", "--steps", "1",
+                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "5000", "--bypass"])
+    svc = out["hub"]["audio_service"]
+    assert out["queue_success_rate"] == 1.0 and svc["processed"] == 2
+    assert svc.get("bypassed", 0) == svc.get("windows", 0) > 0
