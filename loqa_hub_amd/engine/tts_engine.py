@@ -82,6 +82,31 @@ class VitsTTSEngine:
         self.stats["samples"] += int(n.sum())
         return [pcm[b, : int(n[b])].copy() for b in range(len(texts))]
 
+    # phrase lengths (characters) and batch sizes the warm-up synthesizes: the
+    # HIP-graph buckets (batch, symbols, frames) a served reply stream hits
+    WARMUP_CHARS = (6, 12, 24, 40, 64, 96, 140)
+    WARMUP_BATCHES = (1, 2, 4)
+
+    def warmup_graphs(self) -> int:
+        """Capture the graph buckets of typical reply phrases before serving
+        (a capture costs an eager run plus the capture itself: taken lazily, the
+        first minutes of serving pay them inside the replies). Returns the
+        number of captures made. No-op without graphs."""
+        if not self.use_graphs:
+            return 0
+        base = "turning on the kitchen lights and the living room music now "
+        seed = self._seed
+        for B in self.WARMUP_BATCHES:
+            for n in self.WARMUP_CHARS:
+                text = (base * (n // len(base) + 1))[:n]
+                self.synthesize_batch([text] * B)
+        self._seed = seed                 # the served replies' noise seeds as without warm-up
+        caps = self._runner.stats["captures"] if self._runner is not None else 0
+        for k in ("batches", "phrases", "samples", "gpu_s", "launch_s"):
+            self.stats[k] = 0 if k in ("batches", "phrases", "samples") else 0.0
+        self.stats["warmup_captures"] = caps
+        return caps
+
     def _stream_ctx(self):
         """VITS runs on its own explicitly placed pool stream (a fixed hardware
         queue beside the decoders, docs/PERF.md "Stream placement"), never on

@@ -112,6 +112,8 @@ def build_gpu_processor(cfg: Config, nats, device: str = "cuda:0", tts=None, *, 
         tts = build_tts(cfg, device)
     pipe = VoicePipeline(stt, llm, nats)
     pipe.warmup()
+    if tts is not None and hasattr(tts, "warmup_graphs"):
+        tts.warmup_graphs()         # VITS graph buckets of typical replies
     sc = cfg.streaming
     proc = GPUVoiceProcessor(pipe, tts=tts, max_batch=min(g.max_batch, 64),
                              bridge=build_bridge(skills, tts) if bridge else None,
