@@ -16,6 +16,8 @@ GPU engines are built lazily by ``build_gpu_processor`` so a CPU-only hub
 """
 from __future__ import annotations
 
+import os
+
 import asyncio
 import logging
 
@@ -49,7 +51,11 @@ def build_tts(cfg: Config, device: str = "cuda:0"):
     if b == "gpu":
         from .engine.tts_engine import VitsTTSEngine
         from .models.configs import vits_config
-        return VitsTTSEngine(vits_config(cfg.gpu.tts_model), device, seed=cfg.gpu.seed)
+        # phrases arriving within this window share one synthesis (a VITS call
+        # at 1-2 phrases is launch / latency bound)
+        win = float(os.environ.get("LOQA_TTS_BATCH_WINDOW_MS", "3")) / 1e3
+        return VitsTTSEngine(vits_config(cfg.gpu.tts_model), device, seed=cfg.gpu.seed,
+                             batch_window=win)
     if b in ("http", "openai"):
         from .llm.tts import OpenAITTSClient
         return OpenAITTSClient(cfg.tts)
