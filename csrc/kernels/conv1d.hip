@@ -202,33 +202,67 @@ __global__ __launch_bounds__(256) void conv1d_lds_kernel(ConvArgs p) {
   float16v acc;
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  // A chunk's operands go global -> registers -> LDS: every 16-byte piece of
+  // the chunk is requested before any is stored (a load-store pair per loop
+  // trip serialised one memory round trip per trip, 4-8 per chunk), and the
+  // NEXT chunk's pieces are requested right after this chunk's are stored, so
+  // their latency hides under this chunk's MFMAs (staged rows R <= 256 and
+  // K <= 16, checked on the host).
+  constexpr int PPR = NC16 * 2;                  // 16-byte pieces per staged row
+  constexpr int XMAX = PPR;                      // 256 rows x PPR pieces / 256 threads
+  constexpr int WMAX = 16 * PPR / 8;             // 32 x 16 taps x PPR pieces / 256 threads
+  const int nx = R * PPR, nw = 32 * p.K * PPR;
+  uint4 xv[XMAX], wv[WMAX];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < XMAX; ++j) {
+      const int i = threadIdx.x + j * 256;
+      const int row = i / PPR, piece = i - row * PPR;
+      const int ti = row0 + row;
+      xv[j] = (i < nx && ti >= 0 && ti < p.Tin)
+                  ? *reinterpret_cast<const uint4*>(xb + (size_t)ti * p.ldx + c0 + 8 * piece)
+                  : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < WMAX; ++j) {
+      const int i = threadIdx.x + j * 256;
+      const int rowk = i / PPR, piece = i - rowk * PPR;
+      const int co = rowk / p.K, tap = rowk - co * p.K;
+      wv[j] = i < nw ? *reinterpret_cast<const uint4*>(
+                           p.w + ((size_t)(co0 + co) * p.K + tap) * p.Cin + c0 + 8 * piece)
+                     : make_uint4(0, 0, 0, 0);
+    }
+  };
+  load_chunk(0);
   for (int c0 = 0; c0 < p.Cin; c0 += CC) {
     __syncthreads();                             // previous chunk's reads are done
-    // input rows: R x CC bf16 in 16-byte pieces, pre-activation applied here
-    for (int i = threadIdx.x; i < R * NC16 * 2; i += 256) {
-      const int row = i / (NC16 * 2), piece = i - row * (NC16 * 2);
-      const int ti = row0 + row;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ti >= 0 && ti < p.Tin) {
-        v = *reinterpret_cast<const uint4*>(xb + (size_t)ti * p.ldx + c0 + 8 * piece);
+    // input rows: R x CC bf16, pre-activation applied while storing
+#pragma unroll
+    for (int j = 0; j < XMAX; ++j) {
+      const int i = threadIdx.x + j * 256;
+      if (i < nx) {
+        const int row = i / PPR, piece = i - row * PPR;
+        uint4 v = xv[j];
         if (p.pre_act == 1) {
           float f[8];
           unpack8(v, f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = f[j] > 0.f ? f[j] : f[j] * p.pre_slope;
+          for (int q = 0; q < 8; ++q) f[q] = f[q] > 0.f ? f[q] : f[q] * p.pre_slope;
           v = pack8(f);
         }
+        *reinterpret_cast<uint4*>(xs + (size_t)row * XS + 8 * piece) = v;
       }
-      *reinterpret_cast<uint4*>(xs + (size_t)row * XS + 8 * piece) = v;
     }
     // weights: 32 output channels x K taps x CC
-    for (int i = threadIdx.x; i < 32 * p.K * NC16 * 2; i += 256) {
-      const int rowk = i / (NC16 * 2), piece = i - rowk * (NC16 * 2);
-      const int co = rowk / p.K, tap = rowk - co * p.K;
-      const uint4 v = *reinterpret_cast<const uint4*>(
-          p.w + ((size_t)(co0 + co) * p.K + tap) * p.Cin + c0 + 8 * piece);
-      *reinterpret_cast<uint4*>(ws + (size_t)rowk * XS + 8 * piece) = v;
+#pragma unroll
+    for (int j = 0; j < WMAX; ++j) {
+      const int i = threadIdx.x + j * 256;
+      if (i < nw) {
+        const int rowk = i / PPR, piece = i - rowk * PPR;
+        *reinterpret_cast<uint4*>(ws + (size_t)rowk * XS + 8 * piece) = wv[j];
+      }
     }
+    if (c0 + CC < p.Cin) load_chunk(c0 + CC);    // lands during this chunk's MFMAs
     __syncthreads();
     if (t0 < p.Tq) {
       const bf16_t* xl = xs + (size_t)(wave * 32 + r) * XS + 8 * kh;
@@ -264,7 +298,7 @@ extern "C" int loqa_conv1d(const void* x, long long xb, int ldx, const void* w, 
              K, dil, pad, stride, ostride, ophase, Tout, pre_act, pre_slope, post_act, alpha,
              out_pcm16, cout_real};
   dim3 grid((Tq + 127) / 128, Cout / 32, B);
-  if (stride == 1 && Cin % 32 == 0) {
+  if (stride == 1 && Cin % 32 == 0 && 128 + (K - 1) * dil <= 256 && K <= 16) {
     // LDS form: 64-channel chunks when the staged rows + weight slice fit in
     // 64 KiB (two workgroups per CU), else 32-channel chunks
     const int R = 128 + (K - 1) * dil;
