@@ -209,6 +209,7 @@ class GPUConfig:
     tp_fallback_checkpoint: str = ""
     stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
     llm_checkpoint: str = ""
+    tts_checkpoint: str = ""          # HF VITS / MMS-TTS dir; "" = the random-init HUB_TTS_MODEL
     # tokenizer.json of a checkpoint ("": the one in / beside the checkpoint;
     # no checkpoint: the synthetic tokenizer of the random-init weights)
     stt_tokenizer: str = ""
@@ -397,6 +398,7 @@ def load(env=None) -> Config:
             tp_fallback_checkpoint=env_str(e, "", "HUB_TP_FALLBACK_CHECKPOINT"),
             stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
             llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
+            tts_checkpoint=env_str(e, "", "HUB_TTS_CHECKPOINT"),
             stt_tokenizer=env_str(e, "", "HUB_STT_TOKENIZER"),
             llm_tokenizer=env_str(e, "", "HUB_LLM_TOKENIZER"),
         ),

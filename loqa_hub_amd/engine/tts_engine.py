@@ -31,11 +31,21 @@ def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
 
 
 class VitsTTSEngine:
-    def __init__(self, cfg: VitsConfig, device, *, seed: int = 0, batch_window: float = 0.003,
-                 max_batch: int = 32, use_graphs: bool = True):
-        self.cfg = cfg
+    def __init__(self, cfg: VitsConfig | None, device, *, seed: int = 0, batch_window: float = 0.003,
+                 max_batch: int = 32, use_graphs: bool = True, checkpoint: str | None = None):
+        """``checkpoint``: a Hugging Face VITS / MMS-TTS directory (config.json,
+        safetensors, vocab.json; models/loader.py ``load_vits``) — its config
+        and vocabulary replace ``cfg`` and the character table; None: the
+        random-init voice of ``cfg``."""
         self.device = torch.device(device)
-        self.model = VitsModel(VitsWeights(cfg, self.device, seed=seed))
+        self.vocab = None
+        if checkpoint:
+            from ..models.loader import load_vits
+            cfg, weights, self.vocab = load_vits(checkpoint, self.device)
+        else:
+            weights = VitsWeights(cfg, self.device, seed=seed)
+        self.cfg = cfg
+        self.model = VitsModel(weights)
         # bucketed HIP-graph replay (models/vits.py VitsGraphRunner), built
         # lazily on the placed TTS stream
         self.use_graphs = use_graphs and self.device.type == "cuda"
@@ -54,7 +64,7 @@ class VitsTTSEngine:
                          ) -> list[np.ndarray]:
         """Synchronous batched synthesis -> PCM16 arrays."""
         speeds = speeds or [1.0] * len(texts)
-        ids = [text_to_ids(t, self.cfg.n_symbols) for t in texts]
+        ids = [text_to_ids(t, self.cfg.n_symbols, self.vocab) for t in texts]
         T = max(len(i) for i in ids)
         arr = np.zeros((len(ids), T), np.int64)
         for b, i in enumerate(ids):

@@ -102,6 +102,19 @@ class VitsConfig:
     resblock_dilations: tuple = ((1, 3, 5), (1, 3, 5), (1, 3, 5))
     sample_rate: int = 22050
     window: int = 4
+    # checkpoints (public VITS / MMS-TTS): the stochastic duration predictor
+    # and the sampling constants of the published models
+    sdp: bool = False
+    sdp_filter: int = 192
+    sdp_flows: int = 4
+    sdp_bins: int = 10
+    sdp_tail: float = 5.0
+    sdp_kernel: int = 3
+    noise_scale: float = 0.667
+    noise_scale_duration: float = 0.8
+    speaking_rate: float = 1.0
+    upsample_kernels: tuple = ()          # () -> 2r for r > 2, else 4
+    leaky_slope: float = 0.1
 
 
 VITS_CONFIGS = {
@@ -158,6 +171,30 @@ def whisper_config_from_hf(d: dict, name: str = "checkpoint") -> WhisperConfig:
     if int(d.get("encoder_ffn_dim", c.ffn_dim)) != c.ffn_dim:
         raise ValueError(f"{name}: encoder_ffn_dim {d['encoder_ffn_dim']} != 4 * d_model")
     return c
+
+
+def vits_config_from_hf(d: dict, name: str = "checkpoint") -> VitsConfig:
+    """A Hugging Face VITS / MMS-TTS config.json (``VitsConfig`` field names)."""
+    return VitsConfig(
+        name, n_symbols=d["vocab_size"], hidden=d["hidden_size"], filter_channels=d["ffn_dim"],
+        n_heads=d["num_attention_heads"], enc_layers=d["num_hidden_layers"],
+        kernel_size=d.get("ffn_kernel_size", 3), flow_layers=d.get("prior_encoder_num_flows", 4),
+        wn_layers=d.get("prior_encoder_num_wavenet_layers", 4), inter_channels=d["flow_size"],
+        upsample_rates=tuple(d["upsample_rates"]), upsample_initial=d["upsample_initial_channel"],
+        resblock_kernels=tuple(d["resblock_kernel_sizes"]),
+        resblock_dilations=tuple(tuple(x) for x in d["resblock_dilation_sizes"]),
+        sample_rate=d.get("sampling_rate", 16000), window=d.get("window_size", 4),
+        sdp=bool(d.get("use_stochastic_duration_prediction", True)),
+        sdp_filter=d.get("duration_predictor_filter_channels", 256),
+        sdp_flows=d.get("duration_predictor_num_flows", 4),
+        sdp_bins=d.get("duration_predictor_flow_bins", 10),
+        sdp_tail=float(d.get("duration_predictor_tail_bound", 5.0)),
+        sdp_kernel=d.get("duration_predictor_kernel_size", 3),
+        noise_scale=float(d.get("noise_scale", 0.667)),
+        noise_scale_duration=float(d.get("noise_scale_duration", 0.8)),
+        speaking_rate=float(d.get("speaking_rate", 1.0)),
+        upsample_kernels=tuple(d.get("upsample_kernel_sizes", ())),
+        leaky_slope=float(d.get("leaky_relu_slope", 0.1)))
 
 
 def checkpoint_config(path: str):

@@ -264,3 +264,147 @@ def broadcast_state(state: dict[str, torch.Tensor] | None, src: int = 0, group=N
                 out[k] = flat[off:off + numel].view(shape) if rank != src else state[k]
                 off += numel
     return out
+
+
+# ----------------------------------------------------------------------- VITS
+def _wn(sd: dict, pre: str) -> torch.Tensor:
+    """A conv weight, folding a weight-norm pair (``parametrizations.weight.
+    original0/1`` or ``weight_g / weight_v``) into the plain weight:
+    w = g * v / ||v|| with the norm over every dim but the first."""
+    if pre + ".weight" in sd:
+        return sd[pre + ".weight"].float()
+    for g_key, v_key in ((".parametrizations.weight.original0", ".parametrizations.weight.original1"),
+                         (".weight_g", ".weight_v")):
+        if pre + g_key in sd:
+            g, v = sd[pre + g_key].float(), sd[pre + v_key].float()
+            n = v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
+            return g * v / n
+    raise KeyError(pre + ".weight")
+
+
+def _dds(sd: dict, pre: str) -> dict:
+    layers = []
+    i = 0
+    while f"{pre}.convs_dilated.{i}.weight" in sd:
+        layers.append({"dw_w": sd[f"{pre}.convs_dilated.{i}.weight"].float(),
+                       "dw_b": sd[f"{pre}.convs_dilated.{i}.bias"].float(),
+                       "pw_w": sd[f"{pre}.convs_pointwise.{i}.weight"].float(),
+                       "pw_b": sd[f"{pre}.convs_pointwise.{i}.bias"].float(),
+                       "n1_w": sd[f"{pre}.norms_1.{i}.weight"].float(),
+                       "n1_b": sd[f"{pre}.norms_1.{i}.bias"].float(),
+                       "n2_w": sd[f"{pre}.norms_2.{i}.weight"].float(),
+                       "n2_b": sd[f"{pre}.norms_2.{i}.bias"].float()})
+        i += 1
+    return {"layers": layers}
+
+
+def vits_from_state_dict(cfg, sd: dict[str, torch.Tensor], device):
+    """``VitsWeights`` from a Hugging Face VITS / MMS-TTS state dict
+    (``VitsModel`` naming; single speaker). The training-only posterior
+    encoder and the duration predictor's posterior flows are not read."""
+    from . import vits as V
+    from .. import ops
+    if cfg.upsample_kernels and any(k % r for k, r in zip(cfg.upsample_kernels, cfg.upsample_rates)):
+        raise ValueError("upsample kernel sizes must be multiples of their rates (polyphase form)")
+    dev = torch.device(device)
+    w = V.VitsWeights.__new__(V.VitsWeights)
+    w.cfg = cfg
+    f = lambda k: sd[k].float()                                   # noqa: E731
+    bf = lambda t: t.to(torch.bfloat16) if t is not None else None  # noqa: E731
+    conv = lambda wt, b=None, gated=False: ops.ConvWeight(bf(wt), bf(b), gated=gated)  # noqa: E731
+    H = cfg.hidden
+    w.emb = bf(f("text_encoder.embed_tokens.weight"))
+    w.enc = []
+    for i in range(cfg.enc_layers):
+        p = f"text_encoder.encoder.layers.{i}."
+        qkv_w = torch.cat([f(p + f"attention.{n}_proj.weight") for n in "qkv"])[:, :, None]
+        qkv_b = torch.cat([f(p + f"attention.{n}_proj.bias") for n in "qkv"])
+        w.enc.append({
+            "qkv": conv(qkv_w, qkv_b),
+            "o": conv(f(p + "attention.out_proj.weight")[:, :, None], f(p + "attention.out_proj.bias")),
+            "emb_k": bf(f(p + "attention.emb_rel_k")[0]), "emb_v": bf(f(p + "attention.emb_rel_v")[0]),
+            "ln1_w": bf(f(p + "layer_norm.weight")), "ln1_b": bf(f(p + "layer_norm.bias")),
+            "ffn1": conv(f(p + "feed_forward.conv_1.weight"), f(p + "feed_forward.conv_1.bias")),
+            "ffn2": conv(f(p + "feed_forward.conv_2.weight"), f(p + "feed_forward.conv_2.bias")),
+            "ln2_w": bf(f(p + "final_layer_norm.weight")), "ln2_b": bf(f(p + "final_layer_norm.bias"))})
+    w.proj = conv(f("text_encoder.project.weight"), f("text_encoder.project.bias"))
+    dp = "duration_predictor."
+    w.from_checkpoint = True          # durations unclamped, as the published models
+    if cfg.sdp:
+        # stochastic duration predictor (fp32: it runs at the symbol count)
+        flows = [{"kind": "affine", "translate": f(dp + "flows.0.translate"),
+                  "log_scale": f(dp + "flows.0.log_scale")}]
+        for j in range(1, cfg.sdp_flows + 1):
+            q = f"{dp}flows.{j}."
+            flows.append({"kind": "conv", "pre_w": f(q + "conv_pre.weight"),
+                          "pre_b": f(q + "conv_pre.bias"), "dds": _dds(sd, q + "conv_dds"),
+                          "proj_w": f(q + "conv_proj.weight"), "proj_b": f(q + "conv_proj.bias")})
+        w.sdp = {"pre_w": f(dp + "conv_pre.weight"), "pre_b": f(dp + "conv_pre.bias"),
+                 "dds": _dds(sd, dp + "conv_dds"),
+                 "proj_w": f(dp + "conv_proj.weight"), "proj_b": f(dp + "conv_proj.bias"),
+                 "flows": flows}
+        w.dp = None
+    else:
+        # deterministic predictor: (k conv + ReLU + LayerNorm) x2 -> 1x1, the
+        # random-init voice's own structure
+        w.sdp = None
+        w.dp = {"c1": conv(f(dp + "conv_1.weight"), f(dp + "conv_1.bias")),
+                "ln1_w": bf(f(dp + "norm_1.weight")), "ln1_b": bf(f(dp + "norm_1.bias")),
+                "c2": conv(f(dp + "conv_2.weight"), f(dp + "conv_2.bias")),
+                "ln2_w": bf(f(dp + "norm_2.weight")), "ln2_b": bf(f(dp + "norm_2.bias")),
+                "proj": conv(f(dp + "proj.weight"), f(dp + "proj.bias"))}
+    # prior flow: mean-only coupling layers over WaveNets
+    w.flows = []
+    for i in range(cfg.flow_layers):
+        p = f"flow.flows.{i}."
+        wn = []
+        for j in range(cfg.wn_layers):
+            last = j == cfg.wn_layers - 1
+            rs_w, rs_b = _wn(sd, p + f"wavenet.res_skip_layers.{j}"), f(p + f"wavenet.res_skip_layers.{j}.bias")
+            wn.append({"in": conv(_wn(sd, p + f"wavenet.in_layers.{j}"), f(p + f"wavenet.in_layers.{j}.bias"),
+                                  gated=True),
+                       "res": None if last else conv(rs_w[:H], rs_b[:H]),
+                       "skip": conv(rs_w if last else rs_w[H:], rs_b if last else rs_b[H:])})
+        w.flows.append({"pre": conv(f(p + "conv_pre.weight"), f(p + "conv_pre.bias")), "wn": wn,
+                        "post": conv(f(p + "conv_post.weight"), f(p + "conv_post.bias"))})
+    # HiFi-GAN generator
+    w.conv_pre = conv(_wn(sd, "decoder.conv_pre"), f("decoder.conv_pre.bias"))
+    w.ups, w.res = [], []
+    nk = len(cfg.resblock_kernels)
+    for i, r in enumerate(cfg.upsample_rates):
+        ut = _wn(sd, f"decoder.upsampler.{i}")
+        k = ut.shape[2]
+        w.ups.append(ops.ConvTransposeWeight(bf(ut), bf(f(f"decoder.upsampler.{i}.bias")), r, (k - r) // 2))
+        blocks = []
+        for j, dils in enumerate(cfg.resblock_dilations):
+            rb = f"decoder.resblocks.{i * nk + j}."
+            blocks.append([(conv(_wn(sd, rb + f"convs1.{m}"), f(rb + f"convs1.{m}.bias")),
+                            conv(_wn(sd, rb + f"convs2.{m}"), f(rb + f"convs2.{m}.bias")), d)
+                           for m, d in enumerate(dils)])
+        w.res.append(blocks)
+    w.conv_post = conv(_wn(sd, "decoder.conv_post"))
+    w.last_channels = w.conv_post.Cin
+    if dev.type != "cpu":
+        torch.cuda.synchronize(dev)
+    return w
+
+
+def load_vits(path: str, device, cfg=None):
+    """(VitsConfig, VitsWeights, vocab or None) of a Hugging Face VITS /
+    MMS-TTS checkpoint directory (config.json + *.safetensors [+ vocab.json])."""
+    import json
+    from .configs import checkpoint_config, vits_config_from_hf
+    if cfg is None:
+        d = checkpoint_config(path)
+        if d is None:
+            raise FileNotFoundError(f"no config.json for the VITS checkpoint {path}")
+        if d.get("num_speakers", 1) > 1 or d.get("wavenet_dilation_rate", 1) != 1:
+            raise ValueError("only single-speaker VITS with WaveNet dilation rate 1 is supported")
+        cfg = vits_config_from_hf(d, os.path.basename(os.path.normpath(path)))
+    sd = read_safetensors(path, device, dtype=torch.float32)
+    vocab = None
+    vf = os.path.join(path if os.path.isdir(path) else os.path.dirname(path), "vocab.json")
+    if os.path.exists(vf):
+        with open(vf, encoding="utf-8") as fh:
+            vocab = json.load(fh)
+    return cfg, vits_from_state_dict(cfg, sd, device), vocab

@@ -38,10 +38,15 @@ SYMBOLS = ("_;:,.!?¡¿—…\"«»“” " + "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefg
              + "ɹɺɾɻʀʁɽʂʃʈʧʉʊʋⱱʌɣɤʍχʎʏʑʐʒʔʡʕʢǀǁǂǃˈˌːˑʼʴʰʱʲʷˠˤ˞↓↑→↗↘'̩'ᵻ")
 
 
-def text_to_ids(text: str, n_symbols: int) -> list[int]:
-    """Character-level symbol ids with VITS's blank interspersing (id 0)."""
-    table = {c: i for i, c in enumerate(SYMBOLS[:n_symbols])}
-    ids = [table.get(c, table[" "]) for c in text]
+def text_to_ids(text: str, n_symbols: int, vocab: dict | None = None) -> list[int]:
+    """Character-level symbol ids with VITS's blank interspersing (id 0).
+    ``vocab`` (a checkpoint's vocab.json, character -> id): lower-cased text,
+    characters outside it dropped, as the MMS-TTS character tokenizers do."""
+    if vocab is not None:
+        ids = [vocab[c] for c in text.lower() if c in vocab]
+    else:
+        table = {c: i for i, c in enumerate(SYMBOLS[:n_symbols])}
+        ids = [table.get(c, table[" "]) for c in text]
     out = [0]
     for i in ids:
         out += [i, 0]
@@ -112,6 +117,7 @@ class VitsWeights:
             ch = co
         self.conv_post = ops.ConvWeight(_rnd(g, dev, 1, ch, 7, std=(ch * 7) ** -0.5), None)
         self.last_channels = ch
+        self.sdp = None          # checkpoints: the stochastic duration predictor (loader)
 
 
 class VitsModel:
@@ -121,6 +127,15 @@ class VitsModel:
     def __init__(self, w: VitsWeights):
         self.w = w
         self.cfg = w.cfg
+        self._sdp = None
+        if getattr(w, "sdp", None) is not None:
+            from .vits_sdp import StochasticDurationPredictor
+            self._sdp = StochasticDurationPredictor(w.sdp, kernel=w.cfg.sdp_kernel,
+                                                    bins=w.cfg.sdp_bins, tail=w.cfg.sdp_tail)
+        # random-init voice: the VITS default; checkpoints: their config's
+        self.noise_scale = (w.cfg.noise_scale if getattr(w, "from_checkpoint", False)
+                            else self.NOISE_SCALE)
+        self.noise_scale_duration = w.cfg.noise_scale_duration
 
     # ------------------------------------------------------------------ text
     def encode_text(self, ids: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
@@ -147,6 +162,8 @@ class VitsModel:
 
     def durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale: float = 1.0
                   ) -> torch.Tensor:
+        if self._sdp is not None:
+            return self._sdp_durations(x, lens, length_scale)
         d = self.w.dp
         Fd = d["c1"].Cout
         T = x.shape[1]
@@ -156,11 +173,26 @@ class VitsModel:
         h = ops.conv1d(h, d["c2"], act="relu", lens=lens)
         h = ops.layernorm(h.view(-1, Fd), d["ln2_w"], d["ln2_b"], 1e-5).view_as(h)
         logw = ops.conv1d(h, d["proj"], lens=lens)[..., 0].float()
-        dur = torch.ceil(torch.exp(logw) * length_scale)
-        dur = dur.clamp(1, self.MAX_FRAMES_PER_SYMBOL)
+        dur = torch.ceil(torch.exp(logw) * length_scale / self.cfg.speaking_rate)
+        if not getattr(self.w, "from_checkpoint", False):
+            dur = dur.clamp(1, self.MAX_FRAMES_PER_SYMBOL)
         T = x.shape[1]
         valid = torch.arange(T, device=x.device)[None, :] < lens[:, None].long()
         return (dur * valid).to(torch.int32)
+
+    def _sdp_durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale) -> torch.Tensor:
+        """Checkpoint voices: frames per symbol from the stochastic duration
+        predictor, ceil(exp(log w) * length_scale), as the published models
+        (no clamp; an all-zero phrase gets one frame)."""
+        B, T, _ = x.shape
+        mask = torch.arange(T, device=x.device)[None, :] < lens[:, None].long()
+        noise = torch.randn(B, 2, T, device=x.device) * self.noise_scale_duration
+        logw = self._sdp.log_durations(x, mask, noise)
+        ls = length_scale / self.cfg.speaking_rate
+        dur = torch.ceil(torch.exp(logw) * ls) * mask
+        first = (dur.sum(1, keepdim=True) == 0) & mask[:, :1]
+        dur[:, :1] = torch.where(first, torch.ones_like(dur[:, :1]), dur[:, :1])
+        return dur.to(torch.int32)
 
     # ------------------------------------------------------------------ flow
     def flow_reverse(self, z: torch.Tensor, flen: torch.Tensor) -> torch.Tensor:
@@ -184,19 +216,20 @@ class VitsModel:
     def decode(self, z: torch.Tensor, pcm_lens: torch.Tensor | None = None) -> torch.Tensor:
         """z [B, F, C] -> PCM16 [B, F * hop]."""
         w, cfg = self.w, self.cfg
+        sl = cfg.leaky_slope
         x = ops.conv1d(z, w.conv_pre)
         for i, ct in enumerate(w.ups):
-            x = ops.conv_transpose1d(x, ct, pre_slope=0.1)
+            x = ops.conv_transpose1d(x, ct, pre_slope=sl)
             xs = None
             nb = len(w.res[i])
             for blocks in w.res[i]:
                 xb = x
                 for j, (c1, c2, d) in enumerate(blocks):
-                    t = ops.conv1d(xb, c1, dil=d, pre_slope=0.1)
+                    t = ops.conv1d(xb, c1, dil=d, pre_slope=sl)
                     if j < len(blocks) - 1:
-                        xb = ops.conv1d(t, c2, pre_slope=0.1, res=xb)
+                        xb = ops.conv1d(t, c2, pre_slope=sl, res=xb)
                     else:  # last pair of the block: xs += (conv + xb) / nb
-                        xs = ops.conv1d(t, c2, pre_slope=0.1, res=xb, alpha=1.0 / nb, acc=xs,
+                        xs = ops.conv1d(t, c2, pre_slope=sl, res=xb, alpha=1.0 / nb, acc=xs,
                                         out=xs)
             x = xs
         pcm = ops.conv1d(x, w.conv_post, pre_slope=0.01, act="tanh", pcm16=True, lens=pcm_lens)
@@ -215,7 +248,7 @@ class VitsModel:
     def audio_phase(self, stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F: int,
                     seed: int = 0, seed_dev: torch.Tensor | None = None) -> torch.Tensor:
         """Prior sample over F frames + reverse flow + vocoder -> PCM16 [B, F * hop]."""
-        z = ops.expand_sample(stats, cum, flen, F, self.NOISE_SCALE, seed, seed_dev=seed_dev)
+        z = ops.expand_sample(stats, cum, flen, F, self.noise_scale, seed, seed_dev=seed_dev)
         z = self.flow_reverse(z, flen)
         return self.decode(z, (flen * self.hop).to(torch.int32))
 

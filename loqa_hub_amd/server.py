@@ -41,7 +41,8 @@ log = logging.getLogger("loqa.server")
 
 def build_tts(cfg: Config, device: str = "cuda:0"):
     """The reply voice (``audio_service.go:180-195``) from ``HUB_TTS_BACKEND``:
-    ``gpu`` -> on-device VITS (``HUB_TTS_MODEL``) on the serving GPU,
+    ``gpu`` -> on-device VITS (``HUB_TTS_CHECKPOINT``, else the random-init
+    ``HUB_TTS_MODEL``) on the serving GPU,
     ``http`` / ``openai`` -> the OpenAI-compatible client (``TTS_URL``; its
     connection is tested in ``HubServer.start`` with the reference's
     fallback rule), ``none`` -> text-only replies."""
@@ -54,8 +55,9 @@ def build_tts(cfg: Config, device: str = "cuda:0"):
         # phrases arriving within this window share one synthesis (a VITS call
         # at 1-2 phrases is launch / latency bound)
         win = float(os.environ.get("LOQA_TTS_BATCH_WINDOW_MS", "3")) / 1e3
-        return VitsTTSEngine(vits_config(cfg.gpu.tts_model), device, seed=cfg.gpu.seed,
-                             batch_window=win)
+        ckpt = cfg.gpu.tts_checkpoint or None
+        return VitsTTSEngine(None if ckpt else vits_config(cfg.gpu.tts_model), device,
+                             seed=cfg.gpu.seed, batch_window=win, checkpoint=ckpt)
     if b in ("http", "openai"):
         from .llm.tts import OpenAITTSClient
         return OpenAITTSClient(cfg.tts)

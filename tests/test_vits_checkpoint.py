@@ -1,0 +1,203 @@
+"""Hugging Face VITS / MMS-TTS checkpoints through ``models/loader.load_vits``:
+component parity against transformers' ``VitsModel`` (the oracle, fp32, run on
+the CPU here) on a small random checkpoint written with ``save_pretrained``.
+
+Compared piecewise, since the two sample differently: the text encoder
+(hidden states and prior statistics), the stochastic duration predictor
+(log durations from the same hidden states and the same noise), and the
+reverse flow + HiFi-GAN vocoder (waveform from the same prior latents).
+Our weights are bf16 on the conv path, so tolerances are bf16-sized; the
+duration predictor runs fp32 and is held to fp32 tolerances."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+transformers = pytest.importorskip("transformers")
+
+from loqa_hub_amd.models.loader import load_vits          # noqa: E402
+from loqa_hub_amd.models.vits import VitsModel, text_to_ids  # noqa: E402
+
+VOCAB = {c: i for i, c in enumerate("_ abcdefghijklmnopqrstuvwxyz.,'?!-")}
+
+
+def _hf_model(sdp: bool = True, seed: int = 0):
+    from transformers import VitsConfig, VitsModel as HFVits
+    torch.manual_seed(seed)
+    cfg = VitsConfig(
+        vocab_size=len(VOCAB), hidden_size=32, num_hidden_layers=2, num_attention_heads=2,
+        window_size=4, ffn_dim=64, ffn_kernel_size=3, flow_size=32, spectrogram_bins=33,
+        prior_encoder_num_flows=2, prior_encoder_num_wavenet_layers=2,
+        posterior_encoder_num_wavenet_layers=1, upsample_initial_channel=256,
+        upsample_rates=[8, 8, 2, 2], upsample_kernel_sizes=[16, 16, 4, 4],
+        resblock_kernel_sizes=[3, 7, 11], resblock_dilation_sizes=[[1, 3, 5]] * 3,
+        duration_predictor_num_flows=2, depth_separable_num_layers=2,
+        use_stochastic_duration_prediction=sdp, noise_scale=0.667, noise_scale_duration=0.8,
+        sampling_rate=16000)
+    m = HFVits(cfg).eval()
+    with torch.no_grad():
+        # the zero-initialised parts (affine flow, biases, coupling post convs)
+        # get values, so every path of the port is exercised
+        for name, p in m.named_parameters():
+            if name.startswith("posterior_encoder") or "post_" in name:
+                continue
+            if name.endswith(("translate", "log_scale")):
+                p.normal_(0.0, 0.3)
+            elif name.endswith(".bias"):
+                p.normal_(0.0, 0.05)
+            elif "flow.flows" in name and "conv_post" in name:
+                p.normal_(0.0, 0.05)
+            elif "norm" in name and name.endswith("weight"):
+                p.normal_(1.0, 0.1)
+    return m
+
+
+DEVICES = ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)]
+
+
+@pytest.fixture(scope="module")
+def ckpt_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("mms_tts")
+    m = _hf_model()
+    m.save_pretrained(str(d), safe_serialization=True)
+    (d / "vocab.json").write_text(json.dumps(VOCAB))
+    return m, d
+
+
+@pytest.fixture(scope="module", params=DEVICES)
+def ckpt(request, ckpt_dir):
+    """(HF model on the CPU, our config, our weights on the device, vocab, dir):
+    the GPU variant runs the HIP conv / attention kernels against the same
+    fp32 CPU oracle."""
+    m, d = ckpt_dir
+    cfg, w, vocab = load_vits(str(d), request.param)
+    return m, cfg, w, vocab, d
+
+
+def _ids(vocab, texts):
+    ids = [text_to_ids(t, 0, vocab) for t in texts]
+    T = max(map(len, ids))
+    arr = torch.zeros(len(ids), T, dtype=torch.int64)
+    for b, i in enumerate(ids):
+        arr[b, :len(i)] = torch.tensor(i)
+    return arr, torch.tensor([len(i) for i in ids], dtype=torch.int32)
+
+
+def _close(a, b, rtol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= rtol * max(scale, 1e-6), (err, scale)
+
+
+def test_config_and_vocab(ckpt):
+    _, cfg, w, vocab, _ = ckpt
+    assert cfg.sdp and cfg.hidden == 32 and cfg.sample_rate == 16000
+    assert cfg.upsample_kernels == (16, 16, 4, 4) and vocab == VOCAB
+    assert w.sdp is not None and w.dp is None and len(w.sdp["flows"]) == 3
+    assert text_to_ids("Hi!", 0, vocab) == [0, VOCAB["h"], 0, VOCAB["i"], 0, VOCAB["!"], 0]
+    assert text_to_ids("h#i", 0, vocab) == [0, VOCAB["h"], 0, VOCAB["i"], 0]   # unknowns dropped
+
+
+def _dev(w):
+    return w.emb.device
+
+
+def test_text_encoder_parity(ckpt):
+    m, cfg, w, vocab, _ = ckpt
+    ids, lens = _ids(vocab, ["turn on the kitchen lights", "hello there"])
+    mask = (torch.arange(ids.shape[1])[None] < lens[:, None].long())
+    with torch.no_grad():
+        out = m.text_encoder(input_ids=ids, padding_mask=mask[..., None].float(),
+                             attention_mask=mask.long())
+        stats, x = VitsModel(w).encode_text(ids.to(_dev(w)), lens.to(_dev(w)))
+        stats, x = stats.cpu(), x.cpu()
+    C = cfg.inter_channels
+    mk = mask[..., None]
+    _close(x.float() * mk, out.last_hidden_state * mk, 0.05)
+    _close(stats[..., :C].float() * mk, out.prior_means * mk, 0.05)
+    _close(stats[..., C:].float() * mk, out.prior_log_variances * mk, 0.05)
+
+
+def test_stochastic_duration_predictor_parity(ckpt):
+    m, cfg, w, vocab, _ = ckpt
+    ids, lens = _ids(vocab, ["what is the weather", "play music in the living room"])
+    B, T = ids.shape
+    mask = (torch.arange(T)[None] < lens[:, None].long())
+    with torch.no_grad():
+        h = m.text_encoder(input_ids=ids, padding_mask=mask[..., None].float(),
+                           attention_mask=mask.long()).last_hidden_state
+        torch.manual_seed(7)
+        ref = m.duration_predictor(h.transpose(1, 2), mask[:, None].float(), reverse=True,
+                                   noise_scale=0.8)[:, 0]
+        torch.manual_seed(7)
+        noise = torch.randn(B, 2, T) * 0.8
+        dv = _dev(w)
+        ours = VitsModel(w)._sdp.log_durations(h.to(dv), mask.to(dv), noise.to(dv)).cpu()
+    torch.testing.assert_close(ours * mask, ref * mask, rtol=1e-4, atol=1e-4)
+    # the spline actually moved the values (not an identity pass-through)
+    assert (ref * mask).abs().max() > 0.05
+
+
+def test_flow_and_vocoder_parity(ckpt):
+    m, cfg, w, _, _ = ckpt
+    torch.manual_seed(3)
+    B, F, C = 2, 40, cfg.inter_channels
+    flen = torch.tensor([40, 29], dtype=torch.int32)
+    fmask = (torch.arange(F)[None] < flen[:, None].long())
+    z = torch.randn(B, F, C) * fmask[..., None]
+    model = VitsModel(w)
+    hop = model.hop
+    with torch.no_grad():
+        lat = m.flow(z.transpose(1, 2), fmask[:, None].float(), None, reverse=True)
+        ref = m.decoder(lat * fmask[:, None].float(), None)[:, 0]            # [B, F * hop]
+        dv = _dev(w)
+        zz = model.flow_reverse(z.to(torch.bfloat16).to(dv).contiguous(), flen.to(dv))
+        _close(zz.float().cpu() * fmask[..., None], lat.transpose(1, 2) * fmask[..., None], 0.05)
+        pcm = model.decode(zz, (flen * hop).to(torch.int32).to(dv)).float().cpu() / 32767.0
+    for b in range(B):
+        n = int(flen[b]) * hop
+        a, r = pcm[b, :n], ref[b, :n]
+        corr = torch.corrcoef(torch.stack([a, r]))[0, 1].item()
+        rel = ((a - r).norm() / r.norm()).item()
+        # bf16 through ~40 convs, then a saturating tanh: RMS, not max, error
+        assert corr > 0.995 and rel < 0.05, (corr, rel)
+
+
+def test_engine_serves_checkpoint(ckpt):
+    """The served path: the engine loads the directory itself; on the GPU the
+    stochastic predictor (its noise draw included) runs inside the captured
+    text-phase graph, replayed for a second batch of the same bucket."""
+    from loqa_hub_amd.engine.tts_engine import VitsTTSEngine
+    _, cfg, w, _, d = ckpt
+    dv = _dev(w)
+    eng = VitsTTSEngine(None, dv, checkpoint=str(d), use_graphs=dv.type == "cuda")
+    assert eng.cfg.sample_rate == 16000 and eng.vocab == VOCAB
+    hop = eng.model.hop
+    for texts in (["turn on the lights", "ok"], ["dim the hallway", "yes please"]):
+        pcm = eng.synthesize_batch(texts)
+        assert all(len(p) > 0 and len(p) % hop == 0 for p in pcm)
+        assert np.abs(pcm[0].astype(np.int32)).max() > 0
+    if dv.type == "cuda":
+        assert eng.stats["graph_replays"] == 2 and eng.stats["graph_captures"] >= 2
+
+
+def test_deterministic_predictor_checkpoint(tmp_path):
+    m = _hf_model(sdp=False, seed=1)
+    m.save_pretrained(str(tmp_path), safe_serialization=True)
+    cfg, w, vocab = load_vits(str(tmp_path), "cpu")
+    assert not cfg.sdp and w.sdp is None and vocab is None
+    ids, lens = _ids({c: i for i, c in enumerate("_ abcdefghijklmnopqrstuvwxyz.,'?!-")},
+                     ["good morning"])
+    mask = (torch.arange(ids.shape[1])[None] < lens[:, None].long())
+    with torch.no_grad():
+        h = m.text_encoder(input_ids=ids, padding_mask=mask[..., None].float(),
+                           attention_mask=mask.long()).last_hidden_state
+        ref = m.duration_predictor(h.transpose(1, 2), mask[:, None].float())[:, 0]
+        model = VitsModel(w)
+        _, x = model.encode_text(ids, lens)
+        dur = model.durations(x, lens)
+    want = torch.ceil(torch.exp(ref) * mask)
+    # bf16 hidden states: a ceil may land one frame either side
+    assert (dur.float() - want).abs().max() <= 1
