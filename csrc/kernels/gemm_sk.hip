@@ -173,7 +173,10 @@ __global__ __launch_bounds__(64 * WN * WM) void gemm_sk_kernel(GemmSkParams p) {
     }
   for (int t = 0; t < nt; ++t) {
     // stage t has landed once at most (issued - t - 1) newer stages are pending
-    if (NBUF >= 3 && issued - t - 1 >= 1) sk_wait_vm<IPW * (NBUF >= 3 ? NBUF - 2 : 0)>();
+    // (up to NBUF - 2 in steady state; fewer in the last iterations)
+    const int newer = issued - t - 1;
+    if (NBUF >= 4 && newer >= 2) sk_wait_vm<IPW * 2>();
+    else if (NBUF >= 3 && newer >= 1) sk_wait_vm<IPW>();
     else sk_wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     // the buffer refilled here was last read in iteration t - 1, which every
@@ -342,6 +345,11 @@ static int sk_launch(const GemmSkParams& p, hipStream_t st) {
 //   6: 256 x 256, 2 x 4 waves of 128 x 64, 2 stages (128 KB)
 //   7:  64 x  64, 2 x 2 waves of 32 x 32, 2 stages (32 KB)
 //   8: 256 x  64, 3 stages (120 KB)
+//   9: 256 x 128, 3 stages (144 KB): two 48 KB stages in flight per CU
+//  10: 128 x 128, 4 stages (128 KB)
+//  11: 128 x  64, 4 stages (96 KB)
+// (short-K shapes - the Whisper encoder's K = 1280, 20 stages - are bound by
+// the bytes one CU keeps in flight: a deeper ring is the lever there)
 extern "C" int loqa_gemm_sk(const GemmSkParams* p, hipStream_t st) {
   if (!p || p->M <= 0 || p->S < 1 || p->epi < 0 || p->epi > 2 || !p->x || !p->w || !p->y)
     return (int)hipErrorInvalidValue;
@@ -358,15 +366,19 @@ extern "C" int loqa_gemm_sk(const GemmSkParams* p, hipStream_t st) {
     case 6: return sk_launch<2, 4, 8, 4, 2>(*p, st);
     case 7: return sk_launch<2, 2, 2, 2, 2>(*p, st);
     case 8: return sk_launch<4, 1, 4, 4, 3>(*p, st);
+    case 9: return sk_launch<4, 2, 4, 4, 3>(*p, st);
+    case 10: return sk_launch<2, 2, 4, 4, 4>(*p, st);
+    case 11: return sk_launch<2, 2, 4, 2, 4>(*p, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
 
 // tile geometry of a layout (features, rows) for the host-side planner
 extern "C" int loqa_gemm_sk_dims(int layout, int* bn, int* bm) {
-  static const int dims[9][2] = {{128, 128}, {128, 64}, {256, 64}, {256, 128}, {128, 64},
-                                 {128, 128}, {256, 256}, {64, 64}, {256, 64}};
-  if (layout < 0 || layout > 8) return (int)hipErrorInvalidValue;
+  static const int dims[12][2] = {{128, 128}, {128, 64}, {256, 64}, {256, 128}, {128, 64},
+                                  {128, 128}, {256, 256}, {64, 64}, {256, 64}, {256, 128},
+                                  {128, 128}, {128, 64}};
+  if (layout < 0 || layout > 11) return (int)hipErrorInvalidValue;
   *bn = dims[layout][0];
   *bm = dims[layout][1];
   return 0;

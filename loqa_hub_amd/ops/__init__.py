@@ -1652,7 +1652,8 @@ _SK_EPI = {"bf16": 0, "swiglu": 1, "resid": 2}
 # = 1.0; 64 x 32 tiles read 1.5x the LDS per MFMA; 128 x 64 0.75x)
 SK_LAYOUTS = {0: (128, 128, 2, 1.0), 1: (128, 64, 3, 0.85), 2: (256, 64, 2, 1.0),
               3: (256, 128, 1, 1.0), 4: (128, 64, 2, 0.9), 5: (128, 128, 1, 1.05),
-              6: (256, 256, 1, 1.15), 7: (64, 64, 4, 0.6), 8: (256, 64, 1, 1.05)}
+              6: (256, 256, 1, 1.15), 7: (64, 64, 4, 0.6), 8: (256, 64, 1, 1.05),
+              9: (256, 128, 1, 1.1), 10: (128, 128, 1, 1.1), 11: (128, 64, 1, 0.95)}
 SK_CUS = 256
 _SK_WS: dict = {}
 
@@ -1905,9 +1906,19 @@ PROJ_TABLE = {
     # profiles/r5_tp70_shard_grid.jsonl): the planner's (4, 2) / (5, 1) picks
     # were 38.1 / 85.3 us, these 27.2 / 69.7 us (hipBLASLt 28.1 / 69.8); o and
     # down shards keep the planner's (5, 1) (15.2 / 37.6 us)
-    (1280, 8192): [(512, ("sk", 4, 4))],                                                   # qkv/8
-    (7168, 8192): [(512, ("sk", 4, 1))],                                                   # gate|up/8
+    # deeper LDS rings (layouts 9 / 11, profiles/r5_sk_grid_deep.jsonl): 25.6 /
+    # 62.9 us vs 26.9 / 68.9 (a TP rank runs no decoder beside its prompt pass)
+    (1280, 8192): [(512, ("sk", 11, 4))],                                                  # qkv/8
+    (7168, 8192): [(512, ("sk", 9, 3))],                                                   # gate|up/8
 }
+# the 8B prompt-pass projections at ~300 rows on the 4-stage rings (qkv 32.7 ->
+# 30.3, o 32.0 -> 30.2, down 76.3 -> 73.4 us alone; one workgroup per CU
+# instead of two beside the decoders): LOQA_SK_DEEP
+SK_DEEP = os.environ.get("LOQA_SK_DEEP", "0") == "1"
+if SK_DEEP:
+    PROJ_TABLE[(6144, 4096)].insert(2, (400, ("sk", 11, 1)))
+    PROJ_TABLE[(4096, 4096)].insert(2, (400, ("sk", 11, 1)))
+    PROJ_TABLE[(4096, 14336)][3] = (400, ("sk", 9, 4))
 
 
 def proj(x: torch.Tensor, w: torch.Tensor, *, epi: str = "bf16", bias: torch.Tensor | None = None,
