@@ -52,7 +52,7 @@ class VitsTTSEngine:
         self._runner: VitsGraphRunner | None = None
         self.batch_window = batch_window
         self.max_batch = max_batch
-        self._pending: list[tuple[str, float, asyncio.Future]] = []
+        self._pending: list[tuple[str, float, int, asyncio.Future]] = []
         self._flusher: asyncio.Task | None = None
         self._gpu_lock = threading.Lock()
         self._stream = None            # the placed TTS stream (utils/streams.py), created lazily
@@ -60,9 +60,28 @@ class VitsTTSEngine:
         self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0, "launch_s": 0.0}
 
     # ---------------------------------------------------------------- batch
-    def synthesize_batch(self, texts: list[str], speeds: list[float] | None = None
-                         ) -> list[np.ndarray]:
-        """Synchronous batched synthesis -> PCM16 arrays."""
+    # ---------------------------------------------------------------- voices
+    def voices(self) -> list[str]:
+        """Voice names: the model name (one speaker), else ``name:<id>`` per
+        speaker of a multi-speaker checkpoint."""
+        n = self.model.n_speakers
+        return [self.cfg.name] if n == 1 else [f"{self.cfg.name}:{i}" for i in range(n)]
+
+    def speaker_id(self, voice: str | None) -> int:
+        """Speaker of a voice name (``name:<id>``, ``<id>`` or a listed name);
+        anything else (the reference's default ``af_bella``, "") -> speaker 0."""
+        n = self.model.n_speakers
+        if n == 1 or not voice:
+            return 0
+        v = voice.rsplit(":", 1)[-1]
+        if v.isdigit() and int(v) < n:
+            return int(v)
+        return 0
+
+    def synthesize_batch(self, texts: list[str], speeds: list[float] | None = None,
+                         speakers: list[int] | None = None) -> list[np.ndarray]:
+        """Synchronous batched synthesis -> PCM16 arrays (``speakers``: speaker
+        ids per text, multi-speaker voices)."""
         speeds = speeds or [1.0] * len(texts)
         ids = [text_to_ids(t, self.cfg.n_symbols, self.vocab) for t in texts]
         T = max(len(i) for i in ids)
@@ -78,8 +97,11 @@ class VitsTTSEngine:
             if self.use_graphs and self._runner is None:
                 self._runner = VitsGraphRunner(self.model, self.device)
             synth = self._runner.synthesize if self._runner is not None else self.model.synthesize
+            spk = None
+            if self.model.n_speakers > 1:
+                spk = torch.tensor(speakers or [0] * len(texts), dtype=torch.int64, device=self.device)
             pcm, n = synth(torch.from_numpy(arr).to(self.device), lens, seed=self._seed,
-                           length_scale=ls)
+                           length_scale=ls, speakers=spk)
             t1 = time.perf_counter()
             pcm, n = pcm.cpu().numpy(), n.cpu().numpy()
             t2 = time.perf_counter()
@@ -136,9 +158,10 @@ class VitsTTSEngine:
             raise ValueError("text cannot be empty")
         faults().check("tts_error")
         speed = options.speed if options and options.speed > 0 else 1.0
+        spk = self.speaker_id(options.voice if options else None)
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        self._pending.append((text, speed, fut))
+        self._pending.append((text, speed, spk, fut))
         if len(self._pending) >= self.max_batch or self._flusher is None or self._flusher.done():
             self._flusher = loop.create_task(self._flush())
         pcm = await fut
@@ -155,18 +178,19 @@ class VitsTTSEngine:
             batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
             try:
                 outs = await asyncio.get_running_loop().run_in_executor(
-                    None, self.synthesize_batch, [t for t, _, _ in batch], [s for _, s, _ in batch])
+                    None, self.synthesize_batch, [t for t, _, _, _ in batch],
+                    [s for _, s, _, _ in batch], [k for _, _, k, _ in batch])
             except Exception as e:  # noqa: BLE001
                 for *_, f in batch:
                     if not f.done():
                         f.set_exception(e)
                 continue
-            for (_, _, f), pcm in zip(batch, outs):
+            for (_, _, _, f), pcm in zip(batch, outs):
                 if not f.done():
                     f.set_result(pcm)
 
     async def get_available_voices(self) -> list[str]:
-        return [self.cfg.name]
+        return self.voices()
 
     async def close(self) -> None:
         return None

@@ -115,6 +115,10 @@ class VitsConfig:
     speaking_rate: float = 1.0
     upsample_kernels: tuple = ()          # () -> 2r for r > 2, else 4
     leaky_slope: float = 0.1
+    # multi-speaker checkpoints (VCTK-style): a speaker embedding conditions
+    # the duration predictor, every flow WaveNet layer and the vocoder input
+    n_speakers: int = 1
+    speaker_dim: int = 0
 
 
 VITS_CONFIGS = {
@@ -194,7 +198,9 @@ def vits_config_from_hf(d: dict, name: str = "checkpoint") -> VitsConfig:
         noise_scale_duration=float(d.get("noise_scale_duration", 0.8)),
         speaking_rate=float(d.get("speaking_rate", 1.0)),
         upsample_kernels=tuple(d.get("upsample_kernel_sizes", ())),
-        leaky_slope=float(d.get("leaky_relu_slope", 0.1)))
+        leaky_slope=float(d.get("leaky_relu_slope", 0.1)),
+        n_speakers=int(d.get("num_speakers", 1)),
+        speaker_dim=int(d.get("speaker_embedding_size", 0)) if d.get("num_speakers", 1) > 1 else 0)
 
 
 def checkpoint_config(path: str):

@@ -300,8 +300,9 @@ def _dds(sd: dict, pre: str) -> dict:
 
 def vits_from_state_dict(cfg, sd: dict[str, torch.Tensor], device):
     """``VitsWeights`` from a Hugging Face VITS / MMS-TTS state dict
-    (``VitsModel`` naming; single speaker). The training-only posterior
-    encoder and the duration predictor's posterior flows are not read."""
+    (``VitsModel`` naming; single or multi speaker). The training-only
+    posterior encoder and the duration predictor's posterior flows are not
+    read."""
     from . import vits as V
     from .. import ops
     if cfg.upsample_kernels and any(k % r for k, r in zip(cfg.upsample_kernels, cfg.upsample_rates)):
@@ -367,6 +368,21 @@ def vits_from_state_dict(cfg, sd: dict[str, torch.Tensor], device):
                        "skip": conv(rs_w if last else rs_w[H:], rs_b if last else rs_b[H:])})
         w.flows.append({"pre": conv(f(p + "conv_pre.weight"), f(p + "conv_pre.bias")), "wn": wn,
                         "post": conv(f(p + "conv_post.weight"), f(p + "conv_post.bias"))})
+    # speaker conditioning (multi-speaker checkpoints): the embedding table and
+    # the 1x1 projections of a speaker vector g, applied per row (fp32, tiny)
+    w.spk = None
+    if cfg.n_speakers > 1:
+        lin = lambda pre: (_wn(sd, pre)[:, :, 0].contiguous(), f(pre + ".bias"))  # noqa: E731
+        w.spk = {"emb": f("embed_speaker.weight"), "dp": lin(dp + "cond"),
+                 "flows": [lin(f"flow.flows.{i}.wavenet.cond_layer") for i in range(cfg.flow_layers)],
+                 "dec": lin("decoder.cond")}
+        # the WaveNet input convs without the fused gate: the speaker term is
+        # added between the conv and tanh / sigmoid
+        for i, fl in enumerate(w.flows):
+            p = f"flow.flows.{i}."
+            for j, layer in enumerate(fl["wn"]):
+                layer["in_plain"] = conv(_wn(sd, p + f"wavenet.in_layers.{j}"),
+                                         f(p + f"wavenet.in_layers.{j}.bias"))
     # HiFi-GAN generator
     w.conv_pre = conv(_wn(sd, "decoder.conv_pre"), f("decoder.conv_pre.bias"))
     w.ups, w.res = [], []
@@ -398,8 +414,8 @@ def load_vits(path: str, device, cfg=None):
         d = checkpoint_config(path)
         if d is None:
             raise FileNotFoundError(f"no config.json for the VITS checkpoint {path}")
-        if d.get("num_speakers", 1) > 1 or d.get("wavenet_dilation_rate", 1) != 1:
-            raise ValueError("only single-speaker VITS with WaveNet dilation rate 1 is supported")
+        if d.get("wavenet_dilation_rate", 1) != 1:
+            raise ValueError("only VITS with WaveNet dilation rate 1 is supported")
         cfg = vits_config_from_hf(d, os.path.basename(os.path.normpath(path)))
     sd = read_safetensors(path, device, dtype=torch.float32)
     vocab = None

@@ -123,6 +123,7 @@ class VitsWeights:
 class VitsModel:
     NOISE_SCALE = 0.667
     MAX_FRAMES_PER_SYMBOL = 12
+    MAX_SDP_FRAMES = 100
 
     def __init__(self, w: VitsWeights):
         self.w = w
@@ -136,6 +137,24 @@ class VitsModel:
         self.noise_scale = (w.cfg.noise_scale if getattr(w, "from_checkpoint", False)
                             else self.NOISE_SCALE)
         self.noise_scale_duration = w.cfg.noise_scale_duration
+        self.spk = getattr(w, "spk", None)        # multi-speaker conditioning (loader)
+
+    @property
+    def n_speakers(self) -> int:
+        return self.cfg.n_speakers if self.spk is not None else 1
+
+    def speaker_vec(self, spk: torch.Tensor | None) -> torch.Tensor | None:
+        """Speaker ids [B] (int64, device) -> embeddings g [B, gin] f32; None
+        for single-speaker voices."""
+        if self.spk is None:
+            return None
+        if spk is None:
+            raise ValueError("a multi-speaker voice needs speaker ids")
+        return self.spk["emb"][spk].float()
+
+    def _proj(self, key, g: torch.Tensor, i: int | None = None) -> torch.Tensor:
+        wgt, b = self.spk[key] if i is None else self.spk[key][i]
+        return torch.nn.functional.linear(g, wgt, b)
 
     # ------------------------------------------------------------------ text
     def encode_text(self, ids: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
@@ -160,14 +179,16 @@ class VitsModel:
             x = (x * mask).contiguous()
         return ops.conv1d(x, w.proj, lens=lens), x
 
-    def durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale: float = 1.0
-                  ) -> torch.Tensor:
+    def durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale: float = 1.0,
+                  g: torch.Tensor | None = None) -> torch.Tensor:
         if self._sdp is not None:
-            return self._sdp_durations(x, lens, length_scale)
+            return self._sdp_durations(x, lens, length_scale, g)
         d = self.w.dp
         Fd = d["c1"].Cout
         T = x.shape[1]
         mask = (torch.arange(T, device=x.device)[None, :] < lens[:, None].long())[..., None]
+        if g is not None:     # the speaker term on the predictor's input
+            x = ((x.float() + self._proj("dp", g)[:, None, :]) * mask).to(torch.bfloat16)
         h = ops.conv1d(x, d["c1"], act="relu", lens=lens)
         h = ops.layernorm(h.view(-1, Fd), d["ln1_w"], d["ln1_b"], 1e-5).view_as(h) * mask
         h = ops.conv1d(h, d["c2"], act="relu", lens=lens)
@@ -180,31 +201,45 @@ class VitsModel:
         valid = torch.arange(T, device=x.device)[None, :] < lens[:, None].long()
         return (dur * valid).to(torch.int32)
 
-    def _sdp_durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale) -> torch.Tensor:
+    def _sdp_durations(self, x: torch.Tensor, lens: torch.Tensor, length_scale,
+                       g: torch.Tensor | None = None) -> torch.Tensor:
         """Checkpoint voices: frames per symbol from the stochastic duration
         predictor, ceil(exp(log w) * length_scale), as the published models
         (no clamp; an all-zero phrase gets one frame)."""
         B, T, _ = x.shape
         mask = torch.arange(T, device=x.device)[None, :] < lens[:, None].long()
         noise = torch.randn(B, 2, T, device=x.device) * self.noise_scale_duration
-        logw = self._sdp.log_durations(x, mask, noise)
+        logw = self._sdp.log_durations(x, mask, noise,
+                                       None if g is None else self._proj("dp", g))
         ls = length_scale / self.cfg.speaking_rate
-        dur = torch.ceil(torch.exp(logw) * ls) * mask
+        # guard only (a trained predictor stays far below it): one symbol may
+        # not claim more than MAX_SDP_FRAMES frames (~1.6 s at 16 kHz / hop 256)
+        dur = torch.ceil(torch.exp(logw) * ls).clamp(max=self.MAX_SDP_FRAMES) * mask
         first = (dur.sum(1, keepdim=True) == 0) & mask[:, :1]
         dur[:, :1] = torch.where(first, torch.ones_like(dur[:, :1]), dur[:, :1])
         return dur.to(torch.int32)
 
     # ------------------------------------------------------------------ flow
-    def flow_reverse(self, z: torch.Tensor, flen: torch.Tensor) -> torch.Tensor:
+    def flow_reverse(self, z: torch.Tensor, flen: torch.Tensor,
+                     g: torch.Tensor | None = None) -> torch.Tensor:
         cfg, w = self.cfg, self.w
-        half = cfg.inter_channels // 2
-        for fl in reversed(w.flows):
+        half, H = cfg.inter_channels // 2, cfg.hidden
+        nf = len(w.flows)
+        for k, fl in enumerate(reversed(w.flows)):
             z = z.flip(-1).contiguous()          # Flip (its own inverse)
             x0, x1 = z[..., :half], z[..., half:]
             h = ops.conv1d(x0, fl["pre"], lens=flen)
             skip = None
-            for layer in fl["wn"]:
-                acts = ops.conv1d(h, layer["in"], act="gated", lens=flen)
+            gc = None if g is None else self._proj("flows", g, nf - 1 - k)   # [B, 2H * layers]
+            for li, layer in enumerate(fl["wn"]):
+                if gc is None:
+                    acts = ops.conv1d(h, layer["in"], act="gated", lens=flen)
+                else:
+                    # multi-speaker: the speaker term enters between the conv
+                    # and the gate, so the fused gate epilogue is not used
+                    a = ops.conv1d(h, layer["in_plain"], lens=flen).float()
+                    a = a + gc[:, None, 2 * H * li:2 * H * (li + 1)]
+                    acts = (torch.tanh(a[..., :H]) * torch.sigmoid(a[..., H:])).to(torch.bfloat16)
                 skip = ops.conv1d(acts, layer["skip"], acc=skip, lens=flen)   # skip += conv
                 if layer["res"] is not None:
                     h = ops.conv1d(acts, layer["res"], res=h, lens=flen)      # h += conv
@@ -213,11 +248,14 @@ class VitsModel:
         return z
 
     # --------------------------------------------------------------- decoder
-    def decode(self, z: torch.Tensor, pcm_lens: torch.Tensor | None = None) -> torch.Tensor:
+    def decode(self, z: torch.Tensor, pcm_lens: torch.Tensor | None = None,
+               g: torch.Tensor | None = None) -> torch.Tensor:
         """z [B, F, C] -> PCM16 [B, F * hop]."""
         w, cfg = self.w, self.cfg
         sl = cfg.leaky_slope
         x = ops.conv1d(z, w.conv_pre)
+        if g is not None:
+            x = (x.float() + self._proj("dec", g)[:, None, :]).to(torch.bfloat16)
         for i, ct in enumerate(w.ups):
             x = ops.conv_transpose1d(x, ct, pre_slope=sl)
             xs = None
@@ -236,35 +274,40 @@ class VitsModel:
         return pcm[..., 0]
 
     # ---------------------------------------------------------------- full
-    def text_phase(self, ids: torch.Tensor, lens: torch.Tensor, length_scale
+    def text_phase(self, ids: torch.Tensor, lens: torch.Tensor, length_scale,
+                   spk: torch.Tensor | None = None
                    ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Text encoder + durations -> (stats, cum, flen); ``length_scale`` a
-        float or a device scalar (graph replay)."""
+        float or a device scalar (graph replay); ``spk`` speaker ids [B]
+        (multi-speaker voices)."""
         stats, x = self.encode_text(ids, lens)
-        dur = self.durations(x, lens, length_scale)
+        dur = self.durations(x, lens, length_scale, self.speaker_vec(spk))
         cum = torch.cumsum(dur, dim=1, dtype=torch.int32).contiguous()
         return stats, cum, cum[:, -1].contiguous()
 
     def audio_phase(self, stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F: int,
-                    seed: int = 0, seed_dev: torch.Tensor | None = None) -> torch.Tensor:
+                    seed: int = 0, seed_dev: torch.Tensor | None = None,
+                    spk: torch.Tensor | None = None) -> torch.Tensor:
         """Prior sample over F frames + reverse flow + vocoder -> PCM16 [B, F * hop]."""
+        g = self.speaker_vec(spk)
         z = ops.expand_sample(stats, cum, flen, F, self.noise_scale, seed, seed_dev=seed_dev)
-        z = self.flow_reverse(z, flen)
-        return self.decode(z, (flen * self.hop).to(torch.int32))
+        z = self.flow_reverse(z, flen, g)
+        return self.decode(z, (flen * self.hop).to(torch.int32), g)
 
     @property
     def hop(self) -> int:
         return int(math.prod(self.cfg.upsample_rates))
 
     def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
-                   length_scale: float = 1.0, frame_step: int = 1
-                   ) -> tuple[torch.Tensor, torch.Tensor]:
+                   length_scale: float = 1.0, frame_step: int = 1,
+                   speakers: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
         """ids [B, T] -> (PCM16 [B, S], samples per utterance [B]). The frame
-        count is rounded up to ``frame_step`` (the graph runner's buckets)."""
-        stats, cum, flen = self.text_phase(ids, lens, length_scale)
+        count is rounded up to ``frame_step`` (the graph runner's buckets).
+        ``speakers``: speaker ids [B] of a multi-speaker voice."""
+        stats, cum, flen = self.text_phase(ids, lens, length_scale, speakers)
         F = int(flen.max().item())
         F = -(-F // frame_step) * frame_step
-        return self.audio_phase(stats, cum, flen, F, seed), flen * self.hop
+        return self.audio_phase(stats, cum, flen, F, seed, spk=speakers), flen * self.hop
 
 
 class VitsGraphRunner:
@@ -326,11 +369,13 @@ class VitsGraphRunner:
             ids = torch.zeros(Bb, Tb, dtype=torch.int64, device=self.device)
             lens = torch.ones(Bb, dtype=torch.int32, device=self.device)
             ls = torch.ones(1, dtype=torch.float32, device=self.device)
-            g, out = self._capture(lambda: self.model.text_phase(ids, lens, ls))
-            ent = self._text[(Bb, Tb)] = (g, ids, lens, ls, out)
+            spk = (torch.zeros(Bb, dtype=torch.int64, device=self.device)
+                   if self.model.n_speakers > 1 else None)
+            g, out = self._capture(lambda: self.model.text_phase(ids, lens, ls, spk))
+            ent = self._text[(Bb, Tb)] = (g, ids, lens, ls, out, spk)
         return ent
 
-    def _audio_graph(self, Bb: int, Tb: int, Fb: int, text_out):
+    def _audio_graph(self, Bb: int, Tb: int, Fb: int, text_out, spk):
         key = (Bb, Tb, Fb)
         ent = self._audio.get(key)
         if ent is None:
@@ -342,37 +387,45 @@ class VitsGraphRunner:
             seed = torch.zeros(1, dtype=torch.int32, device=self.device)
             stats, cum, flen = text_out
             g, pcm = self._capture(lambda: self.model.audio_phase(stats, cum, flen, Fb,
-                                                                  seed_dev=seed))
+                                                                  seed_dev=seed, spk=spk))
             ent = self._audio[key] = (g, seed, pcm)
         else:
             self._audio.move_to_end(key)
         return ent
 
     def synthesize(self, ids: torch.Tensor, lens: torch.Tensor, *, seed: int = 0,
-                   length_scale: float = 1.0) -> tuple[torch.Tensor, torch.Tensor]:
-        """As ``VitsModel.synthesize``; shapes outside the buckets run eagerly."""
+                   length_scale: float = 1.0, speakers: torch.Tensor | None = None
+                   ) -> tuple[torch.Tensor, torch.Tensor]:
+        """As ``VitsModel.synthesize``; shapes outside the buckets run eagerly.
+        ``speakers``: device speaker ids [B] (multi-speaker voices; written
+        into the bucket's id buffer before the replays)."""
         B, T = ids.shape
         Bb = self._bucket_b(B)
         Tb = -(-T // self.T_STEP) * self.T_STEP
         if Bb is None or Tb > self.max_symbols:
             self.stats["eager"] += 1
             return self.model.synthesize(ids, lens, seed=seed, length_scale=length_scale,
-                                         frame_step=self.F_STEP)
-        g1, s_ids, s_lens, s_ls, text_out = self._text_graph(Bb, Tb)
+                                         frame_step=self.F_STEP, speakers=speakers)
+        g1, s_ids, s_lens, s_ls, text_out, s_spk = self._text_graph(Bb, Tb)
         s_ids.zero_()
         s_ids[:B, :T].copy_(ids)
         s_lens.fill_(1)
         s_lens[:B].copy_(lens)
         s_ls.fill_(float(length_scale))
+        if s_spk is not None:
+            s_spk.zero_()
+            if speakers is not None:
+                s_spk[:B].copy_(speakers)
         g1.replay()
         stats, cum, flen = text_out
         F = int(flen[:B].max().item())
         Fb = -(-F // self.F_STEP) * self.F_STEP
         if Fb > self.max_frames:
             self.stats["eager"] += 1
-            pcm = self.model.audio_phase(stats[:B], cum[:B], flen[:B].contiguous(), Fb, seed)
+            pcm = self.model.audio_phase(stats[:B], cum[:B], flen[:B].contiguous(), Fb, seed,
+                                         spk=None if s_spk is None else s_spk[:B])
             return pcm, flen[:B] * self.model.hop
-        g2, s_seed, pcm = self._audio_graph(Bb, Tb, Fb, text_out)
+        g2, s_seed, pcm = self._audio_graph(Bb, Tb, Fb, text_out, s_spk)
         s_seed.fill_(seed & 0x7FFFFFFF)
         g2.replay()
         self.stats["replays"] += 1

@@ -108,13 +108,18 @@ class StochasticDurationPredictor:
     def __init__(self, p: dict, *, kernel: int = 3, bins: int = 10, tail: float = 5.0):
         self.p, self.kernel, self.bins, self.tail = p, kernel, bins, tail
 
-    def log_durations(self, h: torch.Tensor, mask: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
+    def log_durations(self, h: torch.Tensor, mask: torch.Tensor, noise: torch.Tensor,
+                      cond: torch.Tensor | None = None) -> torch.Tensor:
         """h [B, T, H] text hidden states, mask [B, T] bool, noise [B, 2, T]
-        (already scaled by the noise scale) -> log durations [B, T]."""
+        (already scaled by the noise scale), cond [B, H] (multi-speaker: the
+        projected speaker vector, added after the input conv) -> log
+        durations [B, T]."""
         p, k = self.p, self.kernel
         m = mask[:, None, :].float()
         x = h.float().transpose(1, 2)
         x = F.conv1d(x, p["pre_w"], p["pre_b"])
+        if cond is not None:
+            x = x + cond[:, :, None]
         x = dds_conv(x, m, p["dds"], k)
         cond = F.conv1d(x, p["proj_w"], p["proj_b"]) * m
         z = noise.float() * m

@@ -22,10 +22,11 @@ from loqa_hub_amd.models.vits import VitsModel, text_to_ids  # noqa: E402
 VOCAB = {c: i for i, c in enumerate("_ abcdefghijklmnopqrstuvwxyz.,'?!-")}
 
 
-def _hf_model(sdp: bool = True, seed: int = 0):
+def _hf_model(sdp: bool = True, seed: int = 0, speakers: int = 1):
     from transformers import VitsConfig, VitsModel as HFVits
     torch.manual_seed(seed)
-    cfg = VitsConfig(
+    extra = {"num_speakers": speakers, "speaker_embedding_size": 16} if speakers > 1 else {}
+    cfg = VitsConfig(**extra,
         vocab_size=len(VOCAB), hidden_size=32, num_hidden_layers=2, num_attention_heads=2,
         window_size=4, ffn_dim=64, ffn_kernel_size=3, flow_size=32, spectrogram_bins=33,
         prior_encoder_num_flows=2, prior_encoder_num_wavenet_layers=2,
@@ -42,7 +43,9 @@ def _hf_model(sdp: bool = True, seed: int = 0):
         for name, p in m.named_parameters():
             if name.startswith("posterior_encoder") or "post_" in name:
                 continue
-            if name.endswith(("translate", "log_scale")):
+            if "cond" in name or "embed_speaker" in name:
+                p.normal_(0.0, 0.3 if "embed_speaker" in name else 0.1)
+            elif name.endswith(("translate", "log_scale")):
                 p.normal_(0.0, 0.3)
             elif name.endswith(".bias"):
                 p.normal_(0.0, 0.05)
@@ -201,3 +204,101 @@ def test_deterministic_predictor_checkpoint(tmp_path):
     want = torch.ceil(torch.exp(ref) * mask)
     # bf16 hidden states: a ceil may land one frame either side
     assert (dur.float() - want).abs().max() <= 1
+
+
+# ------------------------------------------------------------ multi-speaker
+@pytest.fixture(scope="module")
+def ckpt_ms_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("vits_ms")
+    m = _hf_model(seed=2, speakers=3)
+    m.save_pretrained(str(d), safe_serialization=True)
+    (d / "vocab.json").write_text(json.dumps(VOCAB))
+    return m, d
+
+
+@pytest.fixture(scope="module", params=DEVICES)
+def ckpt_ms(request, ckpt_ms_dir):
+    m, d = ckpt_ms_dir
+    cfg, w, vocab = load_vits(str(d), request.param)
+    return m, cfg, w, vocab, d
+
+
+def test_multi_speaker_duration_parity(ckpt_ms):
+    """Speaker-conditioned stochastic duration predictor vs the oracle."""
+    m, cfg, w, vocab, _ = ckpt_ms
+    assert cfg.n_speakers == 3 and cfg.speaker_dim == 16 and w.spk is not None
+    ids, lens = _ids(vocab, ["what is the weather", "lights off"])
+    B, T = ids.shape
+    mask = (torch.arange(T)[None] < lens[:, None].long())
+    spk = torch.tensor([2, 1])
+    with torch.no_grad():
+        h = m.text_encoder(input_ids=ids, padding_mask=mask[..., None].float(),
+                           attention_mask=mask.long()).last_hidden_state
+        g = m.embed_speaker(spk).unsqueeze(-1)
+        torch.manual_seed(11)
+        ref = m.duration_predictor(h.transpose(1, 2), mask[:, None].float(), global_conditioning=g,
+                                   reverse=True, noise_scale=0.8)[:, 0]
+        torch.manual_seed(11)
+        noise = torch.randn(B, 2, T) * 0.8
+        dv = _dev(w)
+        model = VitsModel(w)
+        gv = model.speaker_vec(spk.to(dv))
+        ours = model._sdp.log_durations(h.to(dv), mask.to(dv), noise.to(dv),
+                                        model._proj("dp", gv)).cpu()
+        # the speaker moves the durations (a conditioning actually applied)
+        torch.manual_seed(11)
+        ref0 = m.duration_predictor(h.transpose(1, 2), mask[:, None].float(),
+                                    global_conditioning=m.embed_speaker(torch.tensor([0, 0])).unsqueeze(-1),
+                                    reverse=True, noise_scale=0.8)[:, 0]
+    torch.testing.assert_close(ours * mask, ref * mask, rtol=1e-4, atol=1e-4)
+    assert ((ref - ref0) * mask).abs().max() > 1e-3
+
+
+def test_multi_speaker_flow_and_vocoder_parity(ckpt_ms):
+    m, cfg, w, _, _ = ckpt_ms
+    torch.manual_seed(5)
+    B, F, C = 2, 36, cfg.inter_channels
+    flen = torch.tensor([36, 36], dtype=torch.int32)
+    fmask = torch.ones(B, F, dtype=torch.bool)
+    z = torch.randn(B, F, C)
+    spk = torch.tensor([0, 2])
+    model = VitsModel(w)
+    hop = model.hop
+    dv = _dev(w)
+    with torch.no_grad():
+        g = m.embed_speaker(spk).unsqueeze(-1)
+        lat = m.flow(z.transpose(1, 2), fmask[:, None].float(), g, reverse=True)
+        ref = m.decoder(lat, g)[:, 0]
+        gv = model.speaker_vec(spk.to(dv))
+        zz = model.flow_reverse(z.to(torch.bfloat16).to(dv).contiguous(), flen.to(dv), gv)
+        _close(zz.float().cpu(), lat.transpose(1, 2), 0.05)
+        pcm = model.decode(zz, (flen * hop).to(torch.int32).to(dv), gv).float().cpu() / 32767.0
+    for b in range(B):
+        a, r = pcm[b], ref[b]
+        corr = torch.corrcoef(torch.stack([a, r]))[0, 1].item()
+        rel = ((a - r).norm() / r.norm()).item()
+        assert corr > 0.995 and rel < 0.05, (b, corr, rel)
+
+
+def test_multi_speaker_engine_voices(ckpt_ms):
+    """Voices map to speakers; one batch mixes speakers (graph replay on the
+    GPU), and a speaker's audio does not depend on its batch neighbours'."""
+    from loqa_hub_amd.engine.tts_engine import VitsTTSEngine
+    _, cfg, w, _, d = ckpt_ms
+    dv = _dev(w)
+    eng = VitsTTSEngine(None, dv, checkpoint=str(d), use_graphs=dv.type == "cuda")
+    name = eng.cfg.name
+    assert eng.voices() == [f"{name}:0", f"{name}:1", f"{name}:2"]
+    assert eng.speaker_id(f"{name}:2") == 2 and eng.speaker_id("1") == 1
+    assert eng.speaker_id("af_bella") == 0 and eng.speaker_id("") == 0 and eng.speaker_id("9") == 0
+    eng.model.noise_scale = 0.0            # deterministic: compare rows across batches
+    eng.model.noise_scale_duration = 0.0
+    mixed = eng.synthesize_batch(["turn on the lights", "turn on the lights"], speakers=[0, 2])
+    alone = eng.synthesize_batch(["turn on the lights"], speakers=[2])
+    assert len(mixed[1]) == len(alone[0])
+    # the batch's frame padding differs (its longest row), and the vocoder's
+    # receptive field reaches a few frames into it: compare away from the end
+    k = int(0.8 * len(alone[0]))
+    a, b = mixed[1][:k].astype(np.float64), alone[0][:k].astype(np.float64)
+    assert np.corrcoef(a, b)[0, 1] > 0.999
+    assert not np.array_equal(mixed[0], mixed[1])      # different speakers, different audio
