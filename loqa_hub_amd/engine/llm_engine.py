@@ -113,7 +113,7 @@ class LLMEngine:
         self.attn_ws = ops.AttnWorkspace(self.device, 128, self.weights.h, cfg.head_dim,
                                          (max_seq_len + 127) // 128) if self.is_gpu else None
         # decode-attention keys per split (>= 128: the workspace holds max_seq_len / 128 splits)
-        self.attn_split_keys = max(128, int(os.environ.get("LOQA_LLM_ATTN_SPLIT_KEYS", "128")) // 32 * 32)
+        self.attn_split_keys = max(32, int(os.environ.get("LOQA_LLM_ATTN_SPLIT_KEYS", "128")) // 32 * 32)
         self.use_graphs = use_graphs and self.is_gpu
         # fused-epilogue decode GEMMs (single GPU, <= 32 tokens per step)
         self.fused_decode = fused_decode and self.weights.fused
