@@ -40,7 +40,15 @@ struct AttnDecArgs {
   // SC1 bodies (the fused GEMM's attention workers): byte sizes of q and of
   // one K (= V) cache, for the write-through-coherent buffer loads
   long long q_bytes, kv_bytes;
+  int prio;      // wave issue priority of the launch (loqa_set_launch_prio), 0 = default
 };
+
+// Launch priority of the calling host thread: kernels launched (or captured)
+// by a thread that set it run their waves at s_setprio 3, so a latency-bound
+// decoder sharing the CUs with a bandwidth-bound one wins the per-SIMD issue
+// arbitration (MI355X_MICROARCH.md: priority, then age). Thread-local: the
+// STT and LLM schedulers launch from their own threads.
+extern thread_local int g_loqa_launch_prio;
 
 // 16-byte load; SC1: a buffer load with the sc1 policy (reads what another
 // workgroup stored write-through in this launch, without an L2-invalidating

@@ -25,8 +25,13 @@
 // K/V addresses need no per-lane dependent lookup.
 #include "attn_decode.h"
 
+thread_local int g_loqa_launch_prio = 0;
+
+extern "C" void loqa_set_launch_prio(int prio) { g_loqa_launch_prio = prio; }
+
 template <int D, int PF>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnDecArgs a) {
+  if (a.prio) __builtin_amdgcn_s_setprio(3);     // kernel argument: wave-uniform
   __shared__ __attribute__((aligned(16))) DecSmem<D> sm;
   attn_decode_body<D, PF>(a, blockIdx.x, blockIdx.y, blockIdx.z, sm);
 }
@@ -53,7 +58,7 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   const AttnDecArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, kv_stride,
                       kv_start, cu_q, ctx_lens, block_tables, max_blocks, blk, Hq, Hkv, sl2, causal,
                       split_keys, num_splits, part_o, part_ml, total_q, counters, (bf16_t*)o,
-                      o_stride, 0, 0};
+                      o_stride, 0, 0, g_loqa_launch_prio};
   if (D == 128)
     hipLaunchKernelGGL((attn_decode_kernel<128, 0>), grid, dim3(256), 0, s, a);
   else

@@ -440,6 +440,7 @@ struct FusedArgs {
   int att_need;                                 // ready tiles per kv head
   int gemm_x;                                   // GEMM blocks along x (the rest: attention only)
   int att_extra;                                // attention-only blocks (after the GEMM's)
+  int prio;                                     // s_setprio 3 for the launch (attn_decode.h)
 };
 
 // ---------------------------------------------------------------------------
@@ -1005,6 +1006,7 @@ __global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedAr
   constexpr int SMF = NSM > ATT_F ? NSM : ATT_F;
   __shared__ __attribute__((aligned(16))) float smem[SMF];
   __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
+  if (a.prio) __builtin_amdgcn_s_setprio(3);     // kernel argument: wave-uniform
   if constexpr (ATTD == 0) {
     skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, 0>(a, smem, xs, blockIdx.x, blockIdx.y);
   } else {
@@ -1203,6 +1205,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->bias, (bf16_t*)p->out, p->ldo, p->act, (bf16_t*)p->residual, p->rowsq_out,
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
+  a.prio = g_loqa_launch_prio;
   if (p->att) {
     // GEMM + decode attention in one launch. rope: the attention reads the q
     // rows this launch writes (row stride H * D) and the paged caches it

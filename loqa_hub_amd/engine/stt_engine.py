@@ -796,6 +796,10 @@ class STTEngine:
                 from ..utils.streams import placed_stream
                 torch.cuda.set_device(self.device)
                 torch.cuda.set_stream(placed_stream(self.device, "stt", stream_priority))
+                if os.environ.get("LOQA_STT_WAVE_PRIO", "0") == "1":
+                    # the latency-bound decoder's waves win issue arbitration
+                    # against co-resident LLM GEMM waves (set per thread)
+                    ops.set_launch_priority(1)
         except Exception as e:  # noqa: BLE001 - never leave submitters waiting
             self._fatal = e
             while True:

@@ -1358,6 +1358,14 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
 
 # qkv + decode attention in one launch (skinny_fused(attn=...)): off by default
 # until it measures faster in the pipeline (docs/PERF.md)
+def set_launch_priority(prio: int) -> None:
+    """Wave issue priority (s_setprio 3) of the decode attention and fused
+    GEMM kernels this host THREAD launches or captures from now on (0 =
+    default); the STT decoder thread sets it under ``LOQA_STT_WAVE_PRIO``."""
+    if torch.cuda.is_available():
+        kernels().loqa_set_launch_prio(int(prio))
+
+
 FUSE_QKV_ATTN = os.environ.get("LOQA_FUSE_QKV_ATTN", "0") == "1"
 ATTD_MAX_WORKERS = int(os.environ.get("LOQA_ATTD_WORKERS", "2048"))
 _NUM_CUS: list = []

@@ -154,6 +154,7 @@ _CAR_SIGS = {
     "loqa_car_create": ([c_int, c_int, c_ll, c_ll], c_void_p),
     "loqa_car_inbuf": ([c_void_p, c_int], c_void_p),
     "loqa_l3_prefetch": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
+    "loqa_set_launch_prio": ([c_int], None),
     "loqa_car_resid": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "loqa_car_argmax": ([c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
                         c_int),
