@@ -1897,11 +1897,12 @@ PROJ_TABLE = {
     # 400-1000 rows (whole-prompt passes of two or three prompts, nothing
     # decoding): down on the weight-streaming GEMM with K chunks, gate|up on it
     # unsplit (600 rows: 94 vs 118 us, 160 vs 196 us; profiles/r4_ws_splitk.txt).
-    # At 300-400 rows, the chunked passes beside the decoders, the split-K
-    # weight-streaming down is faster alone (79 vs 121 us at 340 rows) but
-    # neutral end to end (19.03 vs 19.07 utt/s, 3 interleaved pairs): kept on sk
+    # At 300-400 rows, the chunked passes beside the Whisper decoder, the split-K
+    # weight-streaming down too: round 4's 3 pairs read neutral (19.03 vs 19.07),
+    # round 5's 5 interleaved pairs all favour it - mixed pass 13.0 -> 12.4 ms,
+    # +1.2% utt/s (profiles/r5_ab_down_ws.txt)
     (4096, 14336): [(64, ("sk", 4, 8)), (128, ("sk", 5, 8)), (256, ("sk", 5, 4)),
-                    (400, ("sk", 8, 3)), (700, ("ws", 0, 4)), (1000, ("ws", 0, 2)),
+                    (400, ("ws", 0, 4)), (700, ("ws", 0, 4)), (1000, ("ws", 0, 2)),
                     (1 << 30, ("sk", 6, 3))],                                              # down
     # encoder qkv / fc1: gemm_ws is ~8% faster alone (24.2 / 25.8 vs 26.2 / 28.2
     # us) but its long-lived 512-thread workgroups cost the concurrent decoders
@@ -1923,6 +1924,14 @@ PROJ_TABLE = {
 # 30.3, o 32.0 -> 30.2, down 76.3 -> 73.4 us alone; one workgroup per CU
 # instead of two beside the decoders): LOQA_SK_DEEP
 SK_DEEP = os.environ.get("LOQA_SK_DEEP", "0") == "1"
+# experiment override of the <= 400-row (chunked prompt pass) pick of a shape:
+# "NxK:sk,layout,chunks;NxK:ws,depth,chunks"
+for _ov in filter(None, os.environ.get("LOQA_PROJ_OVERRIDE", "").split(";")):
+    _shape, _pick = _ov.split(":")
+    _n, _k = map(int, _shape.split("x"))
+    _kind, *_args = _pick.split(",")
+    PROJ_TABLE[(_n, _k)] = [(400, (_kind, *map(int, _args)))] + [
+        e for e in PROJ_TABLE.get((_n, _k), []) if e[0] > 400]
 if SK_DEEP:
     PROJ_TABLE[(6144, 4096)].insert(2, (400, ("sk", 11, 1)))
     PROJ_TABLE[(4096, 4096)].insert(2, (400, ("sk", 11, 1)))
