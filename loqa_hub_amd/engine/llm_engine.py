@@ -113,7 +113,7 @@ class LLMEngine:
         self.attn_ws = ops.AttnWorkspace(self.device, 128, self.weights.h, cfg.head_dim,
                                          (max_seq_len + 127) // 128) if self.is_gpu else None
         # decode-attention keys per split (>= 128: the workspace holds max_seq_len / 128 splits)
-        self.attn_split_keys = max(32, int(os.environ.get("LOQA_LLM_ATTN_SPLIT_KEYS", "128")) // 32 * 32)
+        self.attn_split_keys = max(128, int(os.environ.get("LOQA_LLM_ATTN_SPLIT_KEYS", "128")) // 32 * 32)
         self.use_graphs = use_graphs and self.is_gpu
         # fused-epilogue decode GEMMs (single GPU, <= 32 tokens per step)
         self.fused_decode = fused_decode and self.weights.fused
@@ -859,6 +859,27 @@ class LLMEngine:
         self._running = True
         self._schedule(stream_priority)
 
+    MIXED_SPLIT = os.environ.get("LOQA_MIXED_SPLIT_ATTN", "1") != "0"
+
+    def _mixed_split(self, kinds: list[int], feeds: list[list[int]], host: dict):
+        """(live sequences, their rows, longest feed, longest context) when a
+        mixed pass's attention can run as grouped decode attention for the
+        leading live sequences + flash prefill for the prompt chunks (adds
+        ``cu_tail`` to ``host``), else None."""
+        nd = sum(1 for k in kinds if k == 0)
+        if (not self.MIXED_SPLIT or nd == 0 or nd == len(kinds)
+                or any(k != 0 for k in kinds[:nd])):
+            return None
+        dq = max(len(f) for f in feeds[:nd])
+        cu = host["cu_q"]
+        rd = int(cu[nd])
+        ws = self.attn_ws            # None on the CPU (reference attention)
+        if dq > self.max_decode_q or (ws is not None and (
+                rd > ws.max_tokens or nd * self.weights.hkv > ws.counters.numel())):
+            return None
+        host["cu_tail"] = (cu[nd:len(kinds) + 1] - cu[nd]).astype(np.int32)
+        return nd, rd, dq, max(int(host["ctx_lens"][:nd].max()), 1)
+
     def _mixed_step(self, live: list[GenRequest], prefilling: list[GenRequest]
                     ) -> list[GenRequest]:
         """One pass over every live sequence's whole next feed plus the next
@@ -893,8 +914,12 @@ class LLMEngine:
             budget -= n
         max_q, max_ctx, host = self._meta(rows, feeds, decode=False)
         host["mask_rows"] = np.array([r.grammar.mask_row() for r in rows], np.int32)
+        split = self._mixed_split(kinds, feeds, host)
         dev = self._to_device(host)
         meta = self._build_meta(dev, max_q, max_ctx, False)
+        if split is not None:
+            meta.split = split + (dev["cu_tail"],)
+            self.stats["mixed_split"] = self.stats.get("mixed_split", 0) + 1
         nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
         now = time.perf_counter()
         joined: list[GenRequest] = []

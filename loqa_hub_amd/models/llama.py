@@ -39,6 +39,12 @@ class StepMeta:
     max_q: int
     max_ctx: int
     decode: bool                # grouped (small-q) attention path
+    # a mixed prompt pass whose leading sequences are live decoders: (their
+    # count, their rows, their longest feed, their longest context, the prompt
+    # sequences' cu_q relative to the first prompt row) - the two groups get
+    # their own attention launches (grouped decode attention reads each kv
+    # head's cache once; the flash prefill kernel would re-read it per q head)
+    split: tuple | None = None
 
 
 class TPGroup:
@@ -349,12 +355,15 @@ class LlamaModel:
             qkv = ops.linear(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
-            attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
-                                 head_dim=D, causal=True, max_q=meta.max_q,
-                                 ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
-                                 grouped=meta.decode, split_keys=split_keys,
-                                 num_splits=num_splits if meta.decode else 1,
-                                 workspace=attn_ws, max_k=meta.max_ctx)
+            if meta.split is not None:
+                attn = self._prompt_attention(meta, qkv, k_cache[li], v_cache[li], attn_ws)
+            else:
+                attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
+                                     head_dim=D, causal=True, max_q=meta.max_q,
+                                     ctx_lens=meta.ctx_lens, block_tables=meta.block_tables,
+                                     grouped=meta.decode, split_keys=split_keys,
+                                     num_splits=num_splits if meta.decode else 1,
+                                     workspace=attn_ws, max_k=meta.max_ctx)
             o = tp.all_reduce_(ops.linear(attn, L["wo"]))
             h = ops.rmsnorm(o, L["mlp_norm"], cfg.norm_eps, residual=residual)
             gu = ops.linear(h, L["w_gate_up"])
@@ -363,6 +372,34 @@ class LlamaModel:
         sel_mlp = mlp_out.index_select(0, meta.logit_idx)
         return ops.rmsnorm(sel_mlp.contiguous(), w.final_norm, cfg.norm_eps,
                            residual=sel_res.contiguous())
+
+    def _prompt_attention(self, meta: StepMeta, qkv: torch.Tensor, kc: torch.Tensor,
+                          vc: torch.Tensor, attn_ws) -> torch.Tensor:
+        """Attention of a prompt (or mixed) pass. A mixed pass (``meta.split``)
+        runs its leading live-decoder rows on the grouped split-key decode
+        kernel - each kv head's cache read once for its G q heads - and the
+        prompt chunk rows on the flash prefill kernel, which would otherwise
+        take a 128-row query tile per decoder row and head and re-read that
+        sequence's whole cache per q head (G = 4 times)."""
+        w = self.w
+        H, Hkv, D = w.h, w.hkv, self.cfg.head_dim
+        if meta.split is None:
+            return ops.attention(qkv, kc, vc, meta.cu_q, n_heads=H, n_kv=Hkv, head_dim=D,
+                                 causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
+                                 block_tables=meta.block_tables, grouped=False, split_keys=256,
+                                 num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
+        nd, rd, dq, dctx, cu_tail = meta.split
+        attn = torch.empty(qkv.shape[0], H * D, dtype=torch.bfloat16, device=qkv.device)
+        ns, sk = ops.decode_attn_splits(dctx, nd * Hkv, 128, getattr(w, "max_wgs", None))
+        ops.attention(qkv[:rd], kc, vc, meta.cu_q[:nd + 1], n_heads=H, n_kv=Hkv, head_dim=D,
+                      causal=True, max_q=dq, ctx_lens=meta.ctx_lens[:nd],
+                      block_tables=meta.block_tables[:nd], grouped=True, split_keys=sk,
+                      num_splits=ns, workspace=attn_ws, out=attn[:rd], max_k=dctx)
+        ops.attention(qkv[rd:], kc, vc, cu_tail, n_heads=H, n_kv=Hkv, head_dim=D, causal=True,
+                      max_q=meta.max_q, ctx_lens=meta.ctx_lens[nd:],
+                      block_tables=meta.block_tables[nd:], grouped=False, split_keys=256,
+                      num_splits=1, workspace=attn_ws, out=attn[rd:], max_k=meta.max_ctx)
+        return attn
 
     def _forward_prefill_hw(self, meta: StepMeta, k_cache, v_cache, attn_ws, x, h
                             ) -> torch.Tensor:
@@ -390,10 +427,7 @@ class LlamaModel:
             qkv = ops.proj(h, L["wqkv"])
             ops.rope_kv_append(qkv, meta.positions, w.cos_sin, k_cache[li], v_cache[li], meta.slots,
                                H, Hkv, D)
-            attn = ops.attention(qkv, k_cache[li], v_cache[li], meta.cu_q, n_heads=H, n_kv=Hkv,
-                                 head_dim=D, causal=True, max_q=meta.max_q, ctx_lens=meta.ctx_lens,
-                                 block_tables=meta.block_tables, grouped=False, split_keys=256,
-                                 num_splits=1, workspace=attn_ws, max_k=meta.max_ctx)
+            attn = self._prompt_attention(meta, qkv, k_cache[li], v_cache[li], attn_ws)
             if tp.world == 1:
                 ops.proj(attn, L["wo"], epi="resid", residual=residual)
                 hn = ops.rmsnorm(residual, L["mlp_norm"], cfg.norm_eps)

@@ -214,6 +214,8 @@ def test_llm_chunked_prefill_matches_cpu(pipelined, monkeypatch):
     ref, _ = _run_chunked("0", pipelined, monkeypatch)
     got, eng = _run_chunked("5", pipelined, monkeypatch)
     assert eng.stats.get("mixed_steps", 0) >= 3
+    # the live decoders' rows took the grouped decode attention (meta.split)
+    assert eng.stats.get("mixed_split", 0) >= 1
     for a, b, n in zip(got, ref, (2, 1, 1, 3, 1, 4)):
         assert len(json.loads(a)["commands"]) == n
     assert got == ref
