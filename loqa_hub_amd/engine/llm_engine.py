@@ -891,9 +891,11 @@ class LLMEngine:
         drained first (its in-flight steps retired), so every feed is
         host-known. Returns the requests that finished their prompt."""
         pl = self._pl
+        t_a = time.perf_counter()
         if pl is not None:
             pl.drain()
             live = [r for r in live if not r.done]
+        t_b = time.perf_counter()
         rows: list[GenRequest] = []
         feeds: list[list[int]] = []
         kinds: list[int] = []          # 0 live sequence, 1 last prompt chunk, 2 prompt chunk
@@ -920,7 +922,16 @@ class LLMEngine:
         if split is not None:
             meta.split = split + (dev["cu_tail"],)
             self.stats["mixed_split"] = self.stats.get("mixed_split", 0) + 1
-        nxt = self._forward_sample(meta, dev["mask_rows"]).cpu().numpy()
+        t_c = time.perf_counter()
+        nxt = self._forward_sample(meta, dev["mask_rows"])
+        t_d = time.perf_counter()
+        nxt = nxt.cpu().numpy()
+        t_e = time.perf_counter()
+        # where a mixed pass's wall time goes: draining the pipelined steps,
+        # host metadata, host-side launches, waiting for the GPU
+        for k, v in (("mixed_drain_s", t_b - t_a), ("mixed_meta_s", t_c - t_b),
+                     ("mixed_launch_s", t_d - t_c), ("mixed_wait_s", t_e - t_d)):
+            self.stats[k] = self.stats.get(k, 0.0) + v
         now = time.perf_counter()
         joined: list[GenRequest] = []
         n_dec = 0
