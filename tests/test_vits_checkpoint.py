@@ -302,3 +302,53 @@ def test_multi_speaker_engine_voices(ckpt_ms):
     a, b = mixed[1][:k].astype(np.float64), alone[0][:k].astype(np.float64)
     assert np.corrcoef(a, b)[0, 1] > 0.999
     assert not np.array_equal(mixed[0], mixed[1])      # different speakers, different audio
+
+
+# ------------------------------------------------------------- full size
+@pytest.mark.gpu
+def test_mms_size_checkpoint_gpu(tmp_path):
+    """A checkpoint of the public MMS-TTS shape (transformers' VitsConfig
+    defaults: hidden 192, 6 layers, 4 flows, 512-channel HiFi-GAN at 16 kHz,
+    stochastic duration predictor), random weights: the loader, the duration
+    predictor and the flow + vocoder through the HIP kernels against the fp32
+    oracle, and the served engine's graph replays."""
+    from transformers import VitsConfig, VitsModel as HFVits
+    from loqa_hub_amd.engine.tts_engine import VitsTTSEngine
+    torch.manual_seed(0)
+    m = HFVits(VitsConfig()).eval()
+    m.save_pretrained(str(tmp_path), safe_serialization=True)
+    vocab = {c: i for i, c in enumerate("_ '-abcdefghijklmnopqrstuvwxyz0123456")}
+    (tmp_path / "vocab.json").write_text(json.dumps(vocab))
+    dev = torch.device("cuda", 0)
+    cfg, w, voc = load_vits(str(tmp_path), dev)
+    assert cfg.hidden == 192 and cfg.sample_rate == 16000 and cfg.sdp
+    model = VitsModel(w)
+    ids, lens = _ids(voc, ["turn on the kitchen lights please", "good night"])
+    B, T = ids.shape
+    mask = (torch.arange(T)[None] < lens[:, None].long())
+    with torch.no_grad():
+        h = m.text_encoder(input_ids=ids, padding_mask=mask[..., None].float(),
+                           attention_mask=mask.long()).last_hidden_state
+        torch.manual_seed(3)
+        ref = m.duration_predictor(h.transpose(1, 2), mask[:, None].float(), reverse=True,
+                                   noise_scale=0.8)[:, 0]
+        torch.manual_seed(3)
+        noise = torch.randn(B, 2, T) * 0.8
+        ours = model._sdp.log_durations(h.to(dev), mask.to(dev), noise.to(dev)).cpu()
+        torch.testing.assert_close(ours * mask, ref * mask, rtol=1e-3, atol=1e-3)
+        F = 48
+        flen = torch.tensor([F, F], dtype=torch.int32)
+        z = torch.randn(B, F, cfg.inter_channels)
+        lat = m.flow(z.transpose(1, 2), torch.ones(B, 1, F), None, reverse=True)
+        wav = m.decoder(lat, None)[:, 0]
+        zz = model.flow_reverse(z.to(torch.bfloat16).to(dev).contiguous(), flen.to(dev))
+        pcm = model.decode(zz, (flen * model.hop).to(torch.int32).to(dev)).float().cpu() / 32767.0
+    for b in range(B):
+        corr = torch.corrcoef(torch.stack([pcm[b], wav[b]]))[0, 1].item()
+        rel = ((pcm[b] - wav[b]).norm() / wav[b].norm()).item()
+        assert corr > 0.99 and rel < 0.1, (b, corr, rel)
+    eng = VitsTTSEngine(None, dev, checkpoint=str(tmp_path))
+    for texts in (["turn on the lights", "done"], ["play some music", "ok then"]):
+        out = eng.synthesize_batch(texts)
+        assert all(len(p) > 0 and len(p) % model.hop == 0 for p in out)
+    assert eng.stats["graph_replays"] == 2
