@@ -860,6 +860,7 @@ class LLMEngine:
         self._schedule(stream_priority)
 
     MIXED_SPLIT = os.environ.get("LOQA_MIXED_SPLIT_ATTN", "1") != "0"
+    CHUNK_FIT = os.environ.get("LOQA_CHUNK_FIT", "0") == "1"
 
     def _mixed_split(self, kinds: list[int], feeds: list[list[int]], host: dict):
         """(live sequences, their rows, longest feed, longest context) when a
@@ -906,6 +907,10 @@ class LLMEngine:
                 feeds.append(list(f))
                 kinds.append(0)
         budget = self.chunk_prefill if rows else self.prefill_chunk
+        if rows and self.CHUNK_FIT:
+            # the pass's row count (live feeds + chunk) = the chunk size, a
+            # multiple of 64: the prompt GEMMs' row blocks carry no padding
+            budget = max(64, budget - sum(len(f) for f in feeds))
         for r in prefilling:
             if budget <= 0:
                 break
