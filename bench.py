@@ -303,7 +303,10 @@ def run_hub_dp(args) -> int:
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": ("synthetic speech-like PCM16 over gRPC relays, every utterance a distinct "
                  "transcript + random-init weights (teacher-forced STT, grammar-constrained LLM)"),
-        "config": {"model": f"{args.stt} + {args.llm}" + (f" + {args.tts_model}" if args.tts else ""),
+        "config": {"model": f"{args.stt} + {args.llm}" + (
+            f" + {args.tts_model}" if args.tts and not os.environ.get("HUB_TTS_CHECKPOINT") else
+            f" + VITS checkpoint {os.path.basename(os.path.normpath(os.environ['HUB_TTS_CHECKPOINT']))}"
+            if args.tts else ""),
                    "global_batch": N * B, "seq_len": 1500, "parallelism": f"dp{N}",
                    "commands_mix": mix, "baseline_config": 4, "mode": "hub",
                    "served": "front end + one worker process per GPU",
