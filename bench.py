@@ -343,8 +343,8 @@ def main(argv=None) -> int:
     # 8 utterances per stream: a whole number of passes over the 4-way command
     # mix for every stream (5 ends on an unbalanced tail: measured 17.4-17.5
     # vs 18.7-18.9 utt/s at 4, 8 and 12)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch-per-gpu", type=int, default=8)
     ap.add_argument("--stt", default="whisper-large-v3")
     ap.add_argument("--llm", default="llama3-8b")
