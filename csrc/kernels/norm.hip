@@ -23,6 +23,15 @@ __global__ __launch_bounds__(NORM_THREADS) void rmsnorm_kernel(
   const int nvec = d >> 3;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)src * d);
   uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * d) : nullptr;
+  // the norm weight does not depend on the statistics: requested with the row,
+  // so the scale pass does not wait for a second memory round trip
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  uint4 wpre[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = threadIdx.x + i * NORM_THREADS;
+    wpre[i] = c < nvec ? wr[c] : make_uint4(0, 0, 0, 0);
+  }
   float v[MAXV][8];
   float ss = 0.f;
 #pragma unroll
@@ -47,14 +56,13 @@ __global__ __launch_bounds__(NORM_THREADS) void rmsnorm_kernel(
   }
   ss = block_sum(ss, scratch);
   const float inv = rsqrtf(ss / (float)d + eps);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
   uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * d);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * NORM_THREADS;
     if (c < nvec) {
       float wf[8], o[8];
-      unpack8(wr[c], wf);
+      unpack8(wpre[i], wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * wf[j];
       yr[c] = pack8(o);
@@ -73,6 +81,15 @@ __global__ __launch_bounds__(NORM_THREADS) void layernorm_kernel(
   const int nvec = d >> 3;
   const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)src * d);
   uint4* rr = residual ? reinterpret_cast<uint4*>(residual + (size_t)row * d) : nullptr;
+  const uint4* wr = reinterpret_cast<const uint4*>(w);
+  const uint4* br = reinterpret_cast<const uint4*>(b);
+  uint4 wpre[MAXV], bpre[MAXV];     // requested with the row (see rmsnorm_kernel)
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = threadIdx.x + i * NORM_THREADS;
+    wpre[i] = c < nvec ? wr[c] : make_uint4(0, 0, 0, 0);
+    bpre[i] = c < nvec ? br[c] : make_uint4(0, 0, 0, 0);
+  }
   float v[MAXV][8];
   float s = 0.f;
 #pragma unroll
@@ -107,16 +124,14 @@ __global__ __launch_bounds__(NORM_THREADS) void layernorm_kernel(
     }
   }
   const float inv = rsqrtf(block_sum(q, scratch) / (float)d + eps);
-  const uint4* wr = reinterpret_cast<const uint4*>(w);
-  const uint4* br = reinterpret_cast<const uint4*>(b);
   uint4* yr = reinterpret_cast<uint4*>(y + (size_t)row * d);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * NORM_THREADS;
     if (c < nvec) {
       float wf[8], bf[8], o[8];
-      unpack8(wr[c], wf);
-      unpack8(br[c], bf);
+      unpack8(wpre[i], wf);
+      unpack8(bpre[i], bf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * inv * wf[j] + bf[j];
       yr[c] = pack8(o);
