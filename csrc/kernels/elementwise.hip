@@ -149,11 +149,105 @@ __global__ void rope_kv_append_kernel(bf16_t* __restrict__ qkv, int stride,
   }
 }
 
+// Same operation, every load of the row issued before any store: the loop form
+// above reads, rotates and writes one 4-element group per trip, and its
+// in-place q stores keep the compiler from hoisting the next trip's loads, so
+// a thread pays one memory round trip per group (5 at Llama-3-8B's 40 heads).
+// Here each thread holds up to RK groups (and its V piece) in registers.
+template <int RK>
+__global__ __launch_bounds__(128) void rope_kv_append_batched_kernel(
+    bf16_t* __restrict__ qkv, int stride, const int* __restrict__ positions,
+    const float2* __restrict__ cs, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+    const int* __restrict__ slots, int Hq, int Hkv, int D, int blk) {
+  const int t = blockIdx.x;
+  bf16_t* row = qkv + (size_t)t * stride;
+  const int half = D >> 1, pv = half >> 2, dv = D >> 3;
+  const int nq = Hq * pv, nk = Hkv * pv;
+  uint2 lo[RK], hi[RK];
+#pragma unroll
+  for (int k = 0; k < RK; ++k) {
+    const int i = threadIdx.x + k * 128;
+    lo[k] = hi[k] = make_uint2(0u, 0u);
+    if (i < nq + nk) {
+      const bool isk = i >= nq;
+      const int ii = isk ? i - nq : i;
+      const int h = ii / pv, c = (ii - h * pv) * 4;
+      const bf16_t* base = row + (isk ? Hq * D : 0) + h * D;
+      lo[k] = *reinterpret_cast<const uint2*>(base + c);
+      hi[k] = *reinterpret_cast<const uint2*>(base + c + half);
+    }
+  }
+  const int slot = slots ? slots[t] : -1;
+  const bool vok = slot >= 0 && (int)threadIdx.x < Hkv * dv;
+  uint4 vv = make_uint4(0u, 0u, 0u, 0u);
+  if (vok) {
+    const int h = threadIdx.x / dv, c = (threadIdx.x - h * dv) * 8;
+    vv = *reinterpret_cast<const uint4*>(row + (Hq + Hkv) * D + h * D + c);
+  }
+  const float2* csr = cs ? cs + (size_t)positions[t] * half : nullptr;
+  float2 e[RK][4];
+#pragma unroll
+  for (int k = 0; k < RK; ++k) {
+    const int i = threadIdx.x + k * 128;
+    const int ii = i >= nq ? i - nq : i;
+    const int c = (ii - (ii / pv) * pv) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      e[k][j] = (csr && i < nq + nk) ? csr[c + j] : make_float2(1.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < RK; ++k) {
+    const int i = threadIdx.x + k * 128;
+    if (i >= nq + nk) break;
+    const bool isk = i >= nq;
+    const int ii = isk ? i - nq : i;
+    const int h = ii / pv, c = (ii - h * pv) * 4;
+    uint2 l = lo[k], u = hi[k];
+    if (csr) {
+      float a[4] = {__uint_as_float(l.x << 16), __uint_as_float(l.x & 0xffff0000u),
+                    __uint_as_float(l.y << 16), __uint_as_float(l.y & 0xffff0000u)};
+      float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                    __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+      float ra[4], rb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ra[j] = a[j] * e[k][j].x - b[j] * e[k][j].y;
+        rb[j] = b[j] * e[k][j].x + a[j] * e[k][j].y;
+      }
+      l.x = pack_bf16x2(ra[0], ra[1]);
+      l.y = pack_bf16x2(ra[2], ra[3]);
+      u.x = pack_bf16x2(rb[0], rb[1]);
+      u.y = pack_bf16x2(rb[2], rb[3]);
+    }
+    if (!isk) {
+      bf16_t* base = row + h * D;
+      *reinterpret_cast<uint2*>(base + c) = l;
+      *reinterpret_cast<uint2*>(base + c + half) = u;
+    } else if (slot >= 0) {
+      const int b = slot / blk, o = slot - b * blk;
+      bf16_t* dst = kc + (((size_t)b * Hkv + h) * blk + o) * D;
+      *reinterpret_cast<uint2*>(dst + c) = l;
+      *reinterpret_cast<uint2*>(dst + c + half) = u;
+    }
+  }
+  if (vok) {
+    const int b = slot / blk, o = slot - b * blk;
+    const int h = threadIdx.x / dv, c = (threadIdx.x - h * dv) * 8;
+    *reinterpret_cast<uint4*>(vc + (((size_t)b * Hkv + h) * blk + o) * D + c) = vv;
+  }
+}
+
 extern "C" int loqa_rope_kv_append(void* qkv, int stride, const int* positions, const void* cs,
                                    void* kc, void* vc, const int* slots, int T, int Hq, int Hkv,
                                    int D, int blk, hipStream_t s) {
   if (T <= 0) return 0;
   if (D % 8 != 0 || stride < (Hq + 2 * Hkv) * D || (cs && !positions)) return (int)hipErrorInvalidValue;
+  if ((Hq + Hkv) * (D / 8) <= 8 * 128 && Hkv * (D / 8) <= 128) {
+    hipLaunchKernelGGL(rope_kv_append_batched_kernel<8>, dim3(T), dim3(128), 0, s, (bf16_t*)qkv,
+                       stride, positions, (const float2*)cs, (bf16_t*)kc, (bf16_t*)vc, slots, Hq,
+                       Hkv, D, blk);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(rope_kv_append_kernel, dim3(T), dim3(128), 0, s, (bf16_t*)qkv, stride,
                      positions, (const float2*)cs, (bf16_t*)kc, (bf16_t*)vc, slots, Hq, Hkv, D,
                      blk);

@@ -101,8 +101,11 @@ def test_silu_mul_and_gelu():
     assert _rel(y, y2) < 1e-2
 
 
-def test_rope_kv_append():
-    H, Hkv, D, blk, T = 8, 2, 128, 16, 21
+@pytest.mark.parametrize("H,Hkv", [(8, 2), (32, 8), (72, 8)])
+def test_rope_kv_append(H, Hkv):
+    """(8, 2) / (32, 8): the batched-load kernel; (72, 8): the per-group loop
+    (more groups than 8 per thread)."""
+    D, blk, T = 128, 16, 21
     qkv = torch.randn(T, (H + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
     pos = torch.randint(0, 500, (T,), device=DEV, dtype=torch.int32)
     cs = ref.rope_cos_sin(D, 1024, 500000.0, device=DEV)
