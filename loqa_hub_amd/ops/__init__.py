@@ -1109,7 +1109,9 @@ class FusedLinear:
         if bias is not None:
             b = b + bias.float()
         if norm == "ln" and norm_b is not None:
-            b = b + w.float() @ norm_b.float()
+            # W @ beta as a multiply + row sum (load time; keeps rocBLAS's GEMV
+            # out of the process, so a kernel trace holds no vendor BLAS at all)
+            b = b + (w.float() * norm_b.float()[None, :]).sum(1)
         self.colsum = wb.float().sum(1) if norm == "ln" else None
         self.has_bias = bias is not None or (norm == "ln" and norm_b is not None)
         if perm is not None:
