@@ -1929,11 +1929,17 @@ SK_DEEP = os.environ.get("LOQA_SK_DEEP", "0") == "1"
 # experiment override of the <= 400-row (chunked prompt pass) pick of a shape:
 # "NxK:sk,layout,chunks;NxK:ws,depth,chunks"
 for _ov in filter(None, os.environ.get("LOQA_PROJ_OVERRIDE", "").split(";")):
-    _shape, _pick = _ov.split(":")
-    _n, _k = map(int, _shape.split("x"))
-    _kind, *_args = _pick.split(",")
-    PROJ_TABLE[(_n, _k)] = [(400, (_kind, *map(int, _args)))] + [
-        e for e in PROJ_TABLE.get((_n, _k), []) if e[0] > 400]
+    try:
+        _shape, _pick = _ov.split(":")
+        _n, _k = map(int, _shape.split("x"))
+        _kind, *_args = _pick.split(",")
+        if _kind not in ("sk", "ws"):
+            raise ValueError(_kind)
+        PROJ_TABLE[(_n, _k)] = [(400, (_kind, *map(int, _args)))] + [
+            e for e in PROJ_TABLE.get((_n, _k), []) if e[0] > 400]
+    except ValueError:
+        import warnings
+        warnings.warn(f"LOQA_PROJ_OVERRIDE: ignoring malformed entry {_ov!r}")
 if SK_DEEP:
     PROJ_TABLE[(6144, 4096)].insert(2, (400, ("sk", 11, 1)))
     PROJ_TABLE[(4096, 4096)].insert(2, (400, ("sk", 11, 1)))
