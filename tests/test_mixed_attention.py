@@ -79,3 +79,27 @@ def test_mixed_split_attention_gpu():
     for name, o in (("split", got), ("single", one)):
         err = (o.float().cpu() - ref).abs().max().item()
         assert err < 2e-2 * scale, (name, err, scale)
+
+
+def test_mixed_split_planning_cpu():
+    """``LLMEngine._mixed_split``: the live decoders must lead the pass, fit the
+    grouped kernel's query rows and the workspace; otherwise one flash launch."""
+    from types import SimpleNamespace
+    from loqa_hub_amd.engine.llm_engine import LLMEngine
+
+    def plan(kinds, feeds, max_q=8, ws_tokens=128, ws_counters=4096, on=True):
+        cu = np.concatenate([[0], np.cumsum([len(f) for f in feeds])]).astype(np.int32)
+        host = {"cu_q": cu, "ctx_lens": np.arange(10, 10 + len(feeds), dtype=np.int32)}
+        eng = SimpleNamespace(MIXED_SPLIT=on, max_decode_q=max_q, weights=SimpleNamespace(hkv=8),
+                              attn_ws=SimpleNamespace(max_tokens=ws_tokens,
+                                                      counters=torch.zeros(ws_counters)))
+        return LLMEngine._mixed_split(eng, kinds, feeds, host), host
+
+    sp, host = plan([0, 0, 2], [[1], [2, 3], list(range(40))])
+    assert sp == (2, 3, 2, 11) and host["cu_tail"].tolist() == [0, 40]
+    assert plan([0, 0, 1], [[1], list(range(9)), [5] * 7])[0] is None        # feed > 8 rows
+    assert plan([1, 2], [[1] * 5, [2] * 5])[0] is None                       # no live decoder
+    assert plan([0, 0], [[1], [2]])[0] is None                               # nothing to prefill
+    assert plan([0, 1], [[1], [2] * 5], ws_tokens=0)[0] is None               # workspace too small
+    assert plan([0, 1], [[1], [2] * 5], on=False)[0] is None                  # LOQA_MIXED_SPLIT_ATTN=0
+    assert plan([0, 1], [[1], [2] * 5], ws_counters=4)[0] is None             # counters too few
