@@ -16,12 +16,18 @@ Prints ONE JSON line (rank 0). ``value`` = utterances/s over all GPUs;
 ms-per-added-command (both BASELINE.md definitions) is reported alongside.
 Random-init weights, synthetic speech-like audio (no network / checkpoints).
 
-Modes: ``closed`` (default, the headline): B closed-loop streams per GPU
-submit straight into the voice pipeline. ``hub``: the SERVED path - a
-``HubServer`` per GPU with B simulated relays streaming PCM16 chunks over
-real gRPC, per-relay-group arbitration (window ``--window-ms``; the
-reference's is 300 ms), the GPU voice processor, voice-event writes to
-SQLite and the command queue on NATS. ``batch``: lockstep batches of B.
+Modes: ``hub`` (default, the headline - BASELINE config 4 is "64 concurrent
+gRPC audio streams"): the SERVED path, the reference's hot path
+(``audio_service.go:926-1043``) - a ``HubServer`` per GPU (per rank under
+torchrun) with B simulated relays, each a closed loop of gRPC ``StreamAudio``
+calls (wake-word chunk, 100 ms PCM16 chunks, end of speech), per-relay-group
+arbitration with the single-relay bypass (every bench relay is alone in its
+group; ``--no-bypass`` waits out the window), the GPU voice processor,
+voice-event writes to SQLite and the command queue on NATS. After the timed
+steps, ``--window-steps`` more run with the reference's 300 ms window
+(``window_300ms``, a secondary field). ``closed``: B closed-loop streams per
+GPU submit straight into the voice pipeline (no gRPC). ``batch``: lockstep
+batches of B.
 
 ``--gpus N`` must match the launch: under torchrun WORLD_SIZE must equal N
 (else exit 2); without torchrun and N > 1 the bench launches
@@ -336,6 +342,23 @@ def relaunch(n: int, argv: list[str]) -> int:
     return subprocess.call(cmd)
 
 
+def rank_device_problem(args) -> str | None:
+    """Fail-fast check before any collective: every rank of a GPU run needs a
+    GPU of its own (LOCAL_RANK < visible devices; device_count() does not
+    initialise the GPU). None when the launch is sound."""
+    if args.cpu_smoke:
+        return None
+    n_dev = torch.cuda.device_count()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    share = os.environ.get("LOQA_DIST_SHARE_GPU", "0") == "1"
+    if n_dev == 0:
+        return "no GPU visible (HIP_VISIBLE_DEVICES?) and --cpu-smoke not given"
+    if not share and local >= n_dev:
+        return (f"rank {os.environ.get('RANK', '0')} (LOCAL_RANK {local}) has no GPU: "
+                f"{n_dev} visible for --gpus {args.gpus} (one rank per GPU)")
+    return None
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=None,
@@ -351,18 +374,23 @@ def main(argv=None) -> int:
     ap.add_argument("--mix", default="1,2,3,4", help="commands per utterance, cycled")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--mode", choices=["closed", "hub", "batch"], default="closed",
-                    help="closed: B concurrent closed-loop streams per GPU (continuous batching); "
-                         "hub: B simulated relays per GPU over gRPC into the served hub; "
-                         "batch: lockstep batches of B")
+    ap.add_argument("--mode", choices=["closed", "hub", "batch"], default="hub",
+                    help="hub (default): B simulated relays per GPU over gRPC into the served "
+                         "hub; closed: B concurrent closed-loop streams per GPU straight into "
+                         "the pipeline (continuous batching); batch: lockstep batches of B")
     ap.add_argument("--paced", action="store_true",
                     help="--mode hub: relays send their speech in real time (100 ms chunks "
                          "every 100 ms); latency is then counted from the end of speech")
-    ap.add_argument("--bypass", action="store_true",
-                    help="--mode hub: a relay alone in its group wins at once (opt-in "
-                         "ARBITRATION_SINGLE_RELAY_BYPASS; every bench relay is its own group)")
+    ap.add_argument("--bypass", dest="bypass", action="store_true", default=True,
+                    help="--mode hub (default on): a relay alone in its group wins at once "
+                         "(ARBITRATION_SINGLE_RELAY_BYPASS; every bench relay is its own group)")
+    ap.add_argument("--no-bypass", dest="bypass", action="store_false",
+                    help="--mode hub: every relay waits out the arbitration window")
     ap.add_argument("--window-ms", type=float, default=300.0,
                     help="--mode hub: arbitration window (the reference's 300 ms)")
+    ap.add_argument("--window-steps", type=int, default=4,
+                    help="--mode hub with bypass: utterances per relay timed afterwards with the "
+                         "bypass off (the window_300ms secondary field; 0: skip)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="--mode batch: batches in flight (2: next batch's STT overlaps the decode)")
     ap.add_argument("--cpu-smoke", action="store_true", help="tiny models on CPU (plumbing test)")
@@ -387,6 +415,10 @@ def main(argv=None) -> int:
     if int(world_env or "1") != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: launch one rank per "
               f"GPU (torchrun --nproc-per-node {args.gpus})", file=sys.stderr)
+        return 2
+    bad = rank_device_problem(args)
+    if bad:
+        print(f"bench.py: {bad}", file=sys.stderr)
         return 2
     if args.cpu_smoke:
         args.stt, args.llm = "test-whisper", "test-tiny"
@@ -465,14 +497,16 @@ def main(argv=None) -> int:
     # transcript -> distinct prompt, so only the template text before the
     # transcript can hit the prefix cache), drawn up front for the warmup and
     # timed rounds; each stream's command count cycles through the mix
-    n_per_stream = args.warmup + args.steps
+    win_steps = args.window_steps if (args.mode == "hub" and args.bypass) else 0
+    n_per_stream = args.warmup + args.steps + win_steps
     uniq = []
     if args.mode in ("closed", "hub"):
         counts = [mix[(ci + k) % len(mix)] for ci in range(B) for k in range(n_per_stream)]
         uniq = make_unique(args.seed, counts, offset=info.rank * B * n_per_stream)
 
-    def next_utt(ci: int, k: int, record: bool):
-        return uniq[ci * n_per_stream + k + (args.warmup if record else 0)]
+    def next_utt(ci: int, k: int, record: bool, base: int | None = None):
+        return uniq[ci * n_per_stream + k + (base if base is not None else
+                                             args.warmup if record else 0)]
 
     async def run_closed(n: int, record: bool) -> None:
         """--mode closed (default): B concurrent relay streams per GPU, each a
@@ -500,10 +534,11 @@ def main(argv=None) -> int:
         hub = loop.run_until_complete(_start_hub(args, pipe, port, info))
         cmd_counter = loop.run_until_complete(CommandCounter.start(f"nats://127.0.0.1:{port}"))
 
-    async def run_hub(n: int, record: bool) -> None:
+    async def run_hub(n: int, record: bool, base: int | None = None) -> None:
         """--mode hub: B relays per GPU, each a closed loop of gRPC StreamAudio
         calls (wake-word chunk, 100 ms speech chunks, end of speech) into the
-        served hub; latency = first chunk sent -> response received."""
+        served hub; latency = first chunk sent -> response received. ``base``:
+        index of the first utterance of each relay's list (distinct ones)."""
         import grpc
 
         from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
@@ -512,7 +547,7 @@ def main(argv=None) -> int:
         async def client(ci: int, ch) -> None:
             call = stream_audio_stub(ch)
             for k in range(n):
-                u = next_utt(ci, k, record)
+                u = next_utt(ci, k, record, base)
                 relay = f"relay-{info.rank}-{ci}"
                 hints[relay] = u.text
                 data = np.ascontiguousarray(u.pcm, dtype="<i2").tobytes()
@@ -549,12 +584,16 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     s0 = dict(llm.stats)
+    if hub is not None:
+        hub[0].processor.job_sink = all_jobs      # per-phase timestamps of the timed utterances
     t0 = time.perf_counter()
     loop.run_until_complete(run(args.steps, True))
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
+    if hub is not None:
+        hub[0].processor.job_sink = None
 
     if hub is not None:
         recs_local = loop.run_until_complete(cmd_counter.records(hub[0], hub_recs))
@@ -565,6 +604,23 @@ def main(argv=None) -> int:
     if hub is not None:
         stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub[0], recs_local,
                                                                             args)
+    window = None
+    if hub is not None and win_steps > 0:
+        # secondary: the same served path with every relay waiting out the
+        # reference's arbitration window (audio_service.go:408-502)
+        svc = hub[0].audio_service
+        svc.single_relay_bypass = False
+        pdist.barrier(info)
+        tw = time.perf_counter()
+        loop.run_until_complete(run_hub(win_steps, False, args.warmup + args.steps))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        pdist.barrier(info)
+        tw = pdist.max_over_ranks(info, time.perf_counter() - tw)
+        window = {"window_ms": args.window_ms, "utterances_per_sec": round(info.world * B * win_steps / tw, 3),
+                  "utterances": info.world * B * win_steps,
+                  "note": "after the timed steps, single-relay bypass off: every utterance waits "
+                          "out the arbitration window before STT"}
     def _mean_ms(a, b):
         v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
         return round(float(np.mean(v)) * 1e3, 2) if v else None
@@ -626,6 +682,7 @@ def main(argv=None) -> int:
             "llm_stats": llm.stats,
             "stt_stats": stt.stats,
             "hub": hub_stats,
+            "window_300ms": window,
             "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v)
                                   for k, v in ops._FSPLITS.items()},
             "init_s": round(t_init, 2),

@@ -16,8 +16,10 @@
 //     go to f32 slabs part[S][Mpad][N] that the NEXT kernel sums in its prologue
 //     (slab_ops.hip) - deterministic, no atomics, no extra launch.
 #include "common.h"
-#include "attn_decode.h"
 #include <stdlib.h>
+
+// launch priority of the calling host thread (attn_decode.hip)
+extern thread_local int g_loqa_launch_prio;
 
 typedef float float4v_ __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -413,18 +415,6 @@ struct FusedParams {
   int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
   int wr;                 // waves along the rows (1, or 4 with S == 1; any S with xl)
   int xl;                 // x through LDS (wr == 4; Mpad 32 / 64 / 128)
-  // qkv + decode attention in ONE launch (mode 3, see ATTD below): 0 = off
-  int att;
-  long long q_bytes, kv_bytes;       // sizes of q_out and of one layer's K (= V) cache
-  const int* cu_q; const int* ctx_lens; const int* block_tables;
-  int max_blocks, att_B, split_keys, num_splits;
-  float att_scale; float* part_o; float* part_ml; int* att_counters;
-  void* att_out; long long att_ld;
-  int* att_sync;                     // [ready per kv head | work | exit | error], zeroed, left zero
-  // mode 4 (act) + att: attention over contiguous K / V rows (Whisper
-  // cross-attention over the encoder output): q = this GEMM's output
-  const void* att_k; const void* att_v; long long att_kv_stride; const int* att_kv_start;
-  int att_workers;                   // >= the GEMM's blocks: the rest are attention-only blocks
 };
 
 struct FusedArgs {
@@ -436,86 +426,8 @@ struct FusedArgs {
   bf16_t* residual; float* rowsq_out; float* rowsum_out;                      // EPI_RESID
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
-  AttnDecArgs att; int att_B; int* att_sync; long long q_bytes, kv_bytes;     // ATTD
-  int att_need;                                 // ready tiles per kv head
-  int gemm_x;                                   // GEMM blocks along x (the rest: attention only)
-  int att_extra;                                // attention-only blocks (after the GEMM's)
   int prio;                                     // s_setprio 3 for the launch (attn_decode.h)
 };
-
-// ---------------------------------------------------------------------------
-// qkv -> decode attention hand-off (ATTD = head dim, 0 = off; mode EPI_ROPE;
-// mode EPI_ACT: a q projection -> attention over contiguous K / V rows, the
-// Whisper cross-attention, where only the q tiles are waited for):
-// the q / K / V rows of the step go out with write-through (sc1) stores and
-// each row tile then bumps its kv head's ready counter (release: sc1 stores,
-// vmcnt(0), relaxed agent atomic - guide §6 Guideline 16). Every workgroup of
-// the grid, once its tiles are done, turns into an attention worker: it takes
-// (split, kv head, sequence) items from a work counter, waits for the item's
-// kv head to be complete ((G + 2) x D / (16 RT) tiles) and runs the
-// decode-attention body of attn_decode.h, reading the handed-off rows with
-// sc1 loads (an agent acquire fence here invalidated the L2 under every
-// concurrent kernel: measured 45 vs 30 us per layer alone) - the launch
-// boundary between qkv and attention disappears and the attention of a head
-// starts as soon as ITS tiles are in. Workers only wait for tiles of the same
-// grid whose workgroups hold no dependency (they are producers that have not
-// yet been dispatched at worst), so every wait ends; the spin is bounded
-// anyway (error word). The last workgroup out resets the counters (graph
-// replays). The attention arithmetic is attn_decode_kernel's, bit for bit.
-#define ATT_SPIN_LIMIT (1 << 20)
-
-template <int D>
-__device__ __forceinline__ void attn_fused_phase(const FusedArgs& a, DecSmem<D>& sm, int* sflag) {
-  int* sync = a.att_sync;
-  const int Hkv = a.att.Hkv, Bq = a.att_B, ns = a.att.num_splits;
-  const int n_items = ns * Hkv * Bq;
-  const int need = a.att_need;
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0)
-      sflag[0] = __hip_atomic_fetch_add(&sync[64], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int item = __builtin_amdgcn_readfirstlane(sflag[0]);   // uniform: scalar tile math
-    if (item >= n_items) break;
-    const int kvh = item % Hkv, rest = item / Hkv;
-    const int b = rest % Bq, split = rest / Bq;
-    if (threadIdx.x == 0) {
-      unsigned spins = __hip_atomic_load(&sync[66], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           ? ATT_SPIN_LIMIT : 0u;
-      while (__hip_atomic_load(&sync[kvh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        if (++spins > ATT_SPIN_LIMIT) {
-          __hip_atomic_store(&sync[66], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);   // ~0.2 us between polls: hundreds of pollers share a line
-      }
-    }
-    __syncthreads();
-    // no acquire fence (on this chip an agent-scope acquire invalidates the
-    // L2 under every other workgroup's feet): the handed-off q / K / V rows
-    // are read with sc1 buffer loads instead
-    attn_decode_body<D, 0, 1, 1>(a.att, split, kvh, b, sm);
-  }
-  if (threadIdx.x == 0) {
-    const int e = __hip_atomic_fetch_add(&sync[65], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (e == (int)(gridDim.x * gridDim.y) - 1) {
-      for (int k = 0; k < Hkv; ++k) __hip_atomic_store(&sync[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[64], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[65], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// an 8-byte store, write-through (sc1) when the attention phase reads it
-template <int SC1>
-__device__ __forceinline__ void st_u2(bf16_t* base, size_t elem, uint2 v, long long nbytes) {
-  if constexpr (SC1) {
-    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2_{v.x, v.y}, r, (unsigned)(elem * 2), 0, 16);
-  } else {
-    *reinterpret_cast<uint2*>(base + elem) = v;
-  }
-}
 
 // WR: waves along the rows. WR = 1: the 4 waves split the tile's K range
 // (LDS reduce); WR = 4: every wave owns its own (16 * RT)-row tile over the
@@ -533,7 +445,7 @@ struct FusedSmem {
 
 // One (16 * RT * WR)-row output tile of the fused GEMM (a workgroup's whole
 // GEMM work; `return` = this workgroup's GEMM part is done)
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int ATTD>
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL>
 __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs, const int bx,
                                                   const int by) {
   constexpr int WK = 4 / WR;                     // waves along K
@@ -921,11 +833,11 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
           w2.x = pack_bf16x2(ov[0], ov[1]);
           w2.y = pack_bf16x2(ov[2], ov[3]);
           if (!isk) {
-            st_u2<ATTD != 0>(a.q_out, (size_t)m * a.H * D + head * D + c, w2, a.q_bytes);
+            *reinterpret_cast<uint2*>(a.q_out + (size_t)m * a.H * D + head * D + c) = w2;
           } else {
             if (slot < 0) continue;
             const int bb = slot / a.blk, o = slot - bb * a.blk;
-            st_u2<ATTD != 0>(a.kc, (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c, w2, a.kv_bytes);
+            *reinterpret_cast<uint2*>(a.kc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c) = w2;
           }
         } else {
           if (slot < 0) continue;
@@ -935,21 +847,8 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
           uint2 w2;
           w2.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
           w2.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-          st_u2<ATTD != 0>(a.vc, (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c, w2, a.kv_bytes);
+          *reinterpret_cast<uint2*>(a.vc + (((size_t)bb * a.Hkv + head) * a.blk + o) * D + c) = w2;
         }
-      }
-    }
-    if constexpr (ATTD != 0) {
-      // this row tile is in: bump its kv head's ready counter (after the
-      // write-through stores have completed)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        const int pt0 = tile * RT;
-        const int G = a.H / a.Hkv;
-        const int kvh = pt0 < nq_t ? (pt0 / tph) / G
-                        : pt0 < nq_t + nk_t ? (pt0 - nq_t) / tph
-                                            : ((pt0 - nq_t - nk_t) * 16) / D;
-        __hip_atomic_fetch_add(&a.att_sync[kvh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   } else if constexpr (MODE == EPI_ACT) {
@@ -982,44 +881,19 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
         uint2 w2;
         w2.x = pack_bf16x2(o[0], o[1]);
         w2.y = pack_bf16x2(o[2], o[3]);
-        st_u2<ATTD != 0>(a.out, (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq, w2, a.q_bytes);
-      }
-    }
-    if constexpr (ATTD != 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        const int kvh = ((tile * 16 * RT) / ATTD) / (a.att.Hq / a.att.Hkv);
-        __hip_atomic_fetch_add(&a.att_sync[kvh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<uint2*>(a.out + (size_t)m * a.ldo + tile * (16 * RT) + i * 16 + nq) = w2;
       }
     }
   }
 }
 
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int ATTD = 0>
-__global__ __launch_bounds__(256, ATTD ? 2 : 1) void skinny_fused_kernel(FusedArgs a) {
-  static_assert(!ATTD || ((MODE == EPI_ROPE || MODE == EPI_ACT) && !XL),
-                "attention hand-off: qkv (RoPE) or q projection (act) mode");
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0>
+__global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   constexpr int NSM = FusedSmem<RT, MT, WR>::NSM;
-  // ATTD: the attention phase's LDS aliases the reduce / prologue area (one
-  // __shared__ array; the phase starts behind a workgroup barrier), + a flag word
-  constexpr int ATT_F = ATTD ? (int)(sizeof(DecSmem<ATTD ? ATTD : 64>) / 4) + 4 : 0;
-  constexpr int SMF = NSM > ATT_F ? NSM : ATT_F;
-  __shared__ __attribute__((aligned(16))) float smem[SMF];
+  __shared__ __attribute__((aligned(16))) float smem[NSM];
   __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   if (a.prio) __builtin_amdgcn_s_setprio(3);     // kernel argument: wave-uniform
-  if constexpr (ATTD == 0) {
-    skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, 0>(a, smem, xs, blockIdx.x, blockIdx.y);
-  } else {
-    // 1-D grid: blocks [0, gemm_x * S) are the GEMM's (x fastest, then the K
-    // split), the rest attention workers only. Dispatched in linear order,
-    // every GEMM block of an XCD is placed before any attention-only block
-    // of that XCD, so those never hold a slot a producer waits for
-    const int id = blockIdx.x;
-    if (id < a.gemm_x * a.S)
-      skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL, ATTD>(a, smem, xs, id % a.gemm_x, id / a.gemm_x);
-    attn_fused_phase<ATTD>(a, *reinterpret_cast<DecSmem<ATTD>*>(smem),
-                           reinterpret_cast<int*>(smem) + (SMF - 1));
-  }
+  skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL>(a, smem, xs, blockIdx.x, blockIdx.y);
 }
 
 // Deep prefetch (LOQA_FUSED_DEEP bit mask, Mpad 16): bit 0 - a wave's whole k
@@ -1141,40 +1015,6 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
   }
 }
 
-// qkv + attention (ATTD): RT 1 / 2, WR 1 / 4, Mpad 16 / 32 / 64, no XL, the
-// plain prefetch-group choice of launch_fused
-template <int RT, int MT, int WR, int MODE, int NORM, int ATTD>
-static int launch_attd(const FusedArgs& a, hipStream_t st) {
-  constexpr int WK = 4 / WR;
-  dim3 grid(a.gemm_x * a.S + a.att_extra);
-  const int kw = a.K / 32 / (a.S * WK);
-  if (MT <= 2 && kw % 4 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, (MT <= 2 ? 4 : 2), WR, MODE, NORM, 0, ATTD>), grid,
-                       dim3(256), 0, st, a);
-  else if (kw % 2 == 0)
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 2, WR, MODE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 1, WR, MODE, NORM, 0, ATTD>), grid, dim3(256), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-template <int MODE, int NORM, int ATTD>
-static int dispatch_attd(const FusedArgs& a, int rt, int wr, hipStream_t st) {
-#define LQ_ATTD_MT(RT_, WR_)                                           \
-  switch (a.Mpad) {                                                    \
-    case 16: return launch_attd<RT_, 1, WR_, MODE, NORM, ATTD>(a, st);       \
-    case 32: return launch_attd<RT_, 2, WR_, MODE, NORM, ATTD>(a, st);       \
-    default: return launch_attd<RT_, 4, WR_, MODE, NORM, ATTD>(a, st);       \
-  }
-  if (rt == 1) {
-    if (wr == 4) { LQ_ATTD_MT(1, 4) }
-    LQ_ATTD_MT(1, 1)
-  }
-  if (wr == 4) { LQ_ATTD_MT(2, 4) }
-  LQ_ATTD_MT(2, 1)
-#undef LQ_ATTD_MT
-}
-
 // mode: 1 silu (out [Mpad, ldo >= N/2]), 2 residual (+bias) + row sum-of-squares
 // (+ row sums), 3 (RoPE if cs) + paged KV append + q, 4 act(bias + x W^T) -> out
 // (act 0 identity, 1 GELU-erf). norm: 1 RMSNorm / 2 LayerNorm of x (the bf16
@@ -1206,67 +1046,6 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   a.prio = g_loqa_launch_prio;
-  if (p->att) {
-    // GEMM + decode attention in one launch. rope: the attention reads the q
-    // rows this launch writes (row stride H * D) and the paged caches it
-    // appends to; act: q = the output rows (stride ldo), K / V contiguous rows
-    // at per-sequence starts (cross-attention, not causal)
-    const bool rope = p->mode == EPI_ROPE;
-    if ((!rope && p->mode != EPI_ACT) || p->xl || p->rt > 2 || p->att != p->D ||
-        (p->D != 64 && p->D != 128) || p->H % p->Hkv ||
-        !p->att_sync || !p->cu_q || !p->ctx_lens || !p->part_o || !p->part_ml ||
-        !p->att_counters || !p->att_out || p->att_B < 1 || p->Hkv > 64 || p->num_splits < 1 ||
-        p->split_keys % DEC_TILE || p->q_bytes <= 0 || p->q_bytes >= (1ll << 31) ||
-        (rope && (!p->block_tables || p->blk < 16 || (p->blk & (p->blk - 1)) || p->kv_bytes <= 0 ||
-                  p->kv_bytes >= (1ll << 31))) ||
-        (!rope && (p->act > 1 || N != p->H * p->D || !p->att_k || !p->att_v || !p->att_kv_start ||
-                   p->att_kv_stride % 8 || p->ldo % 8)) ||
-        (p->norm != NORM_RMS && p->norm != NORM_LN) || (p->norm == NORM_LN && p->D != 64))
-      return (int)hipErrorInvalidValue;
-    // the whole grid must be resident at once (workers wait on tiles of the
-    // same grid): <= one workgroup per CU although two fit (launch bounds
-    // 256 x 2), so two such launches on concurrent streams (the Whisper and
-    // Llama decoders) are resident together as well
-    static int ncu = 0;
-    if (ncu <= 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return (int)hipErrorInvalidValue;
-    }
-    if ((long long)(N / (16 * p->rt * p->wr)) * S > ncu) return (int)hipErrorInvalidValue;
-    const float sl2 = p->att_scale * 1.4426950408889634f;
-    const int G = p->H / p->Hkv, tile_rows = 16 * p->rt;
-    if (rope)
-      a.att = AttnDecArgs{a.q_out, (long long)p->H * p->D, a.kc, a.vc, 0, nullptr, p->cu_q, p->ctx_lens,
-                          p->block_tables, p->max_blocks, p->blk, p->H, p->Hkv, sl2, 1, p->split_keys,
-                          p->num_splits, p->part_o, p->part_ml, Mpad, p->att_counters,
-                          (bf16_t*)p->att_out, p->att_ld, p->q_bytes, p->kv_bytes};
-    else
-      a.att = AttnDecArgs{a.out, p->ldo, (const bf16_t*)p->att_k, (const bf16_t*)p->att_v,
-                          p->att_kv_stride, p->att_kv_start, p->cu_q, p->ctx_lens, nullptr, 0, 0, p->H,
-                          p->Hkv, sl2, 0, p->split_keys, p->num_splits, p->part_o, p->part_ml, Mpad,
-                          p->att_counters, (bf16_t*)p->att_out, p->att_ld, p->q_bytes, 0};
-    // tiles per kv head: its G q heads (+ its k and v rows in rope mode)
-    a.att_need = (rope ? G + 2 : G) * p->D / tile_rows;
-    a.att_B = p->att_B;
-    a.gemm_x = N / (16 * p->rt * p->wr);
-    a.att_extra = p->att_workers > a.gemm_x * S ? p->att_workers - a.gemm_x * S : 0;
-    a.att_sync = p->att_sync;
-    a.q_bytes = p->q_bytes;
-    a.kv_bytes = p->kv_bytes;
-    if (rope) {
-      if (p->D == 128) {
-        if (p->norm == NORM_RMS) return dispatch_attd<EPI_ROPE, NORM_RMS, 128>(a, p->rt, p->wr, st);
-        return (int)hipErrorInvalidValue;
-      }
-      if (p->norm == NORM_RMS) return dispatch_attd<EPI_ROPE, NORM_RMS, 64>(a, p->rt, p->wr, st);
-      return dispatch_attd<EPI_ROPE, NORM_LN, 64>(a, p->rt, p->wr, st);
-    }
-    // act mode: the Whisper q projection (LayerNorm prologue, D = 64) only
-    if (p->D == 64 && p->norm == NORM_LN) return dispatch_attd<EPI_ACT, NORM_LN, 64>(a, p->rt, p->wr, st);
-    return (int)hipErrorInvalidValue;
-  }
   switch (p->mode) {
     case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, p->xl, st);
     case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, p->xl, st);

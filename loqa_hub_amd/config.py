@@ -210,6 +210,9 @@ class GPUConfig:
     stt_checkpoint: str = ""          # safetensors file/dir (HF naming); "" = seeded random init
     llm_checkpoint: str = ""
     tts_checkpoint: str = ""          # HF VITS / MMS-TTS dir; "" = the random-init HUB_TTS_MODEL
+    # what a TTS_FORMAT the GPU voice cannot encode (mp3, opus, aac, flac) gets:
+    # "wav" = WAV, labelled wav, logged + counted; "error" = the synthesis fails
+    tts_format_policy: str = "wav"
     # tokenizer.json of a checkpoint ("": the one in / beside the checkpoint;
     # no checkpoint: the synthetic tokenizer of the random-init weights)
     stt_tokenizer: str = ""
@@ -399,6 +402,7 @@ def load(env=None) -> Config:
             stt_checkpoint=env_str(e, "", "HUB_STT_CHECKPOINT"),
             llm_checkpoint=env_str(e, "", "HUB_LLM_CHECKPOINT"),
             tts_checkpoint=env_str(e, "", "HUB_TTS_CHECKPOINT"),
+            tts_format_policy=env_str(e, "wav", "HUB_TTS_FORMAT_POLICY"),
             stt_tokenizer=env_str(e, "", "HUB_STT_TOKENIZER"),
             llm_tokenizer=env_str(e, "", "HUB_LLM_TOKENIZER"),
         ),

@@ -168,9 +168,16 @@ class PcmStager:
         self._h2d = h2d_stream
         self._pending: list = []      # (event, pinned host tail) until the copy is done
         if h2d_stream is not None:
-            _lib.check(_lib.runtime().loqa_stager_set_stream(self._h, h2d_stream.cuda_stream, 1),
-                       "stager_set_stream")
-            self.stream_in = True
+            # stream-in needs a device mirror per slot (hipMalloc): on a GPU
+            # whose HBM is nearly full (a 70B shard) that can fail - the stager
+            # then stays in whole-utterance mode instead of failing every relay
+            rc = _lib.runtime().loqa_stager_set_stream(self._h, h2d_stream.cuda_stream, 1)
+            if rc == 0:
+                self.stream_in = True
+            else:
+                self._h2d = None
+                log.warning("PCM stream-in disabled (device mirrors not allocated, hip error %d): "
+                            "whole-utterance uploads", rc)
 
     def acquire_index(self) -> int:
         with self._lock:

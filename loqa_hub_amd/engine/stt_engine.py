@@ -45,10 +45,15 @@ PCM_STREAM_IN = os.environ.get("LOQA_PCM_STREAM_IN", "1") != "0"
 # PREV_TOKENS tokens, fed 4 per step like the SOT prompt); the texts are joined.
 MAX_WINDOWS = int(os.environ.get("LOQA_STT_MAX_WINDOWS", "20"))
 PREV_TOKENS = int(os.environ.get("LOQA_STT_PREV_TOKENS", "32"))
+# admissions that may pass a waiting item that does not fit yet (FIFO otherwise)
+HOL_BYPASS = int(os.environ.get("LOQA_STT_HOL_BYPASS", "16"))
 
 
-def n_windows(n_samples: int) -> int:
-    return max(1, min(MAX_WINDOWS, -(-n_samples // N_SAMPLES)))
+def n_windows(n_samples: int, cap: int = MAX_WINDOWS) -> int:
+    """30 s windows of an utterance, at most ``cap`` (an engine passes
+    min(MAX_WINDOWS, max_batch): every window holds a cross-attention slot, so
+    a longer utterance is truncated like one past MAX_WINDOWS, not rejected)."""
+    return max(1, min(cap, -(-n_samples // N_SAMPLES)))
 
 
 @dataclass(eq=False)
@@ -216,13 +221,13 @@ class STTEngine:
         lens = []
         for r in reqs:
             n = self._n_samples(r)
-            w = n_windows(n)
+            w = n_windows(n, self.max_windows)
             if n > w * N_SAMPLES:
                 self.stats["long_form_dropped_samples"] = \
                     self.stats.get("long_form_dropped_samples", 0) + n - w * N_SAMPLES
-                log.error("utterance of %.1f s exceeds %d windows (LOQA_STT_MAX_WINDOWS): "
-                          "the last %.1f s are not transcribed", n / 16000, MAX_WINDOWS,
-                          (n - w * N_SAMPLES) / 16000)
+                log.error("utterance of %.1f s exceeds %d windows (LOQA_STT_MAX_WINDOWS, "
+                          "max_batch): the last %.1f s are not transcribed", n / 16000,
+                          self.max_windows, (n - w * N_SAMPLES) / 16000)
             lens.append(min(n, w * N_SAMPLES))
             r.windows = w
         for r, n in zip(reqs, lens):
@@ -604,7 +609,11 @@ class STTEngine:
 
     def rows_needed(self, reqs: list[STTRequest]) -> int:
         """Encoder rows / cross-attention slots of ``reqs`` (one per 30 s window)."""
-        return sum(n_windows(self._n_samples(r)) for r in reqs)
+        return sum(n_windows(self._n_samples(r), self.max_windows) for r in reqs)
+
+    @property
+    def max_windows(self) -> int:
+        return max(1, min(MAX_WINDOWS, self.max_batch))
 
     def _encode(self, reqs: list[STTRequest], slots: list[int],
                 device_pcm: torch.Tensor | None = None) -> None:
@@ -813,6 +822,7 @@ class STTEngine:
         waiting: list[tuple] = []          # (reqs, cb, fut) not yet admitted (no free slot)
         encoding: list[tuple] = []         # (reqs, future) on the encoder worker
         cells: dict[int, list] = {}
+        head_bypass = 0                     # admissions that passed the blocked head
         # the encoder runs on its own worker thread + stream, overlapped with
         # the running decoder batch (an arrival's encode no longer stalls every
         # live transcription); requests join at the next step boundary after
@@ -838,9 +848,29 @@ class STTEngine:
             try:
                 new: list[STTRequest] = []
                 n_rows = 0
-                while waiting and self.rows_needed(waiting[0][0]) <= len(self._free_slots) - n_rows:
-                    reqs, cb, fut = waiting.pop(0)
-                    n_rows += self.rows_needed(reqs)
+                # FIFO, except that items which fit may pass a head that does
+                # not (a long-form utterance waiting for many free slots), at
+                # most HOL_BYPASS times per head so it is never starved
+                i = 0
+                while i < len(waiting):
+                    need = self.rows_needed(waiting[i][0])
+                    if need > len(self._free_slots) - n_rows:
+                        if i == 0 and head_bypass < HOL_BYPASS:
+                            i = 1
+                            continue
+                        if i == 0:
+                            break
+                        i += 1
+                        continue
+                    reqs, cb, fut = waiting.pop(i)
+                    if i == 0:
+                        head_bypass = 0
+                    else:
+                        head_bypass += 1
+                        self.stats["hol_bypass"] = self.stats.get("hol_bypass", 0) + 1
+                        if head_bypass >= HOL_BYPASS:
+                            i = len(waiting)      # the head goes next
+                    n_rows += need
                     if not reqs:
                         fut.set_result(reqs)
                         continue

@@ -3,13 +3,24 @@
 
 Concurrent ``synthesize`` calls (the progressive pipeline's phrase workers of
 every live session) are micro-batched into one padded VITS forward; each
-result is returned as a WAV (PCM16 mono, 22 050 Hz) or raw PCM. ``speed`` maps
-to the duration length scale (1 / speed), as in the reference's request body.
+result is returned as a WAV (PCM16 mono, the voice's sample rate) or raw PCM.
+``speed`` maps to the duration length scale (1 / speed), as in the reference's
+request body.
+
+``response_format`` (``openai_tts_client.go:39-46``; the status manager asks
+for ``mp3``, ``status_manager.go:441-462``): ``wav`` and ``pcm`` are produced
+as asked. No compressed-audio encoder ships in this image, so ``mp3``,
+``opus``, ``aac`` and ``flac`` follow ``format_policy``: ``"wav"`` (default)
+returns WAV, logs the downgrade once per format and counts it in
+``stats["format_downgrades"]``; ``"error"`` raises
+:class:`UnsupportedAudioFormat`. Either way ``TTSResult.format`` names the
+container the bytes are really in, and the hub labels the audio with it.
 """
 from __future__ import annotations
 
 import asyncio
 import io
+import logging
 import struct
 import threading
 import time
@@ -22,6 +33,15 @@ from ..models.configs import VitsConfig
 from ..models.vits import VitsGraphRunner, VitsModel, VitsWeights, text_to_ids
 from ..utils.faults import faults
 
+log = logging.getLogger("loqa.tts")
+
+SUPPORTED_FORMATS = ("wav", "pcm")
+_CONTENT_TYPES = {"wav": "audio/wav", "pcm": "audio/pcm"}
+
+
+class UnsupportedAudioFormat(ValueError):
+    """A response_format the on-GPU TTS cannot encode (format_policy "error")."""
+
 
 def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
     data = np.ascontiguousarray(pcm, dtype="<i2").tobytes()
@@ -32,11 +52,17 @@ def pcm16_to_wav(pcm: np.ndarray, sample_rate: int) -> bytes:
 
 class VitsTTSEngine:
     def __init__(self, cfg: VitsConfig | None, device, *, seed: int = 0, batch_window: float = 0.003,
-                 max_batch: int = 32, use_graphs: bool = True, checkpoint: str | None = None):
+                 max_batch: int = 32, use_graphs: bool = True, checkpoint: str | None = None,
+                 format_policy: str = "wav"):
         """``checkpoint``: a Hugging Face VITS / MMS-TTS directory (config.json,
         safetensors, vocab.json; models/loader.py ``load_vits``) — its config
         and vocabulary replace ``cfg`` and the character table; None: the
-        random-init voice of ``cfg``."""
+        random-init voice of ``cfg``. ``format_policy``: what an unsupported
+        response_format gets - "wav" (a logged, counted downgrade) or "error"."""
+        if format_policy not in ("wav", "error"):
+            raise ValueError(f"format_policy must be 'wav' or 'error', not {format_policy!r}")
+        self.format_policy = format_policy
+        self._downgrade_logged: set[str] = set()
         self.device = torch.device(device)
         self.vocab = None
         if checkpoint:
@@ -57,7 +83,8 @@ class VitsTTSEngine:
         self._gpu_lock = threading.Lock()
         self._stream = None            # the placed TTS stream (utils/streams.py), created lazily
         self._seed = seed
-        self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0, "launch_s": 0.0}
+        self.stats = {"batches": 0, "phrases": 0, "samples": 0, "gpu_s": 0.0, "launch_s": 0.0,
+                      "format_downgrades": 0}
 
     # ---------------------------------------------------------------- batch
     # ---------------------------------------------------------------- voices
@@ -153,10 +180,27 @@ class VitsTTSEngine:
         return torch.cuda.stream(self._stream)
 
     # ------------------------------------------------------ TextToSpeech API
+    def output_format(self, requested: str | None) -> str:
+        """The container a request for ``requested`` gets (see module doc)."""
+        fmt = (requested or "wav").lower()
+        if fmt in SUPPORTED_FORMATS:
+            return fmt
+        if self.format_policy == "error":
+            raise UnsupportedAudioFormat(
+                f"on-GPU TTS cannot encode {fmt!r} (supported: {', '.join(SUPPORTED_FORMATS)})")
+        self.stats["format_downgrades"] += 1
+        if fmt not in self._downgrade_logged:
+            self._downgrade_logged.add(fmt)
+            log.warning("TTS response_format %r is not available on the GPU backend (no %s "
+                        "encoder); returning WAV and labelling the audio 'wav'", fmt, fmt)
+        return "wav"
+
     async def synthesize(self, text: str, options: TTSOptions | None = None) -> TTSResult:
         if not text:
             raise ValueError("text cannot be empty")
         faults().check("tts_error")
+        # decided before any GPU work: an "error" policy rejects at once
+        fmt = self.output_format(options.response_format if options else None)
         speed = options.speed if options and options.speed > 0 else 1.0
         spk = self.speaker_id(options.voice if options else None)
         loop = asyncio.get_running_loop()
@@ -165,12 +209,11 @@ class VitsTTSEngine:
         if len(self._pending) >= self.max_batch or self._flusher is None or self._flusher.done():
             self._flusher = loop.create_task(self._flush())
         pcm = await fut
-        fmt = (options.response_format if options and options.response_format else "wav")
         if fmt == "pcm":
-            data, ctype = pcm.astype("<i2").tobytes(), "audio/pcm"
+            data = pcm.astype("<i2").tobytes()
         else:
-            data, ctype = pcm16_to_wav(pcm, self.cfg.sample_rate), "audio/wav"
-        return TTSResult(data, ctype, len(data), self.cfg.sample_rate)
+            data = pcm16_to_wav(pcm, self.cfg.sample_rate)
+        return TTSResult(data, _CONTENT_TYPES[fmt], len(data), self.cfg.sample_rate, format=fmt)
 
     async def _flush(self) -> None:
         await asyncio.sleep(self.batch_window)

@@ -38,6 +38,11 @@ class TTSResult:
     content_type: str
     length: int
     sample_rate: int = 0
+    # the container the bytes are actually in ("wav", "pcm", "mp3", ...): what
+    # a consumer labels the audio with (gRPC AudioResponse.audio_format, the
+    # NATS audio message), which can differ from the requested response_format
+    # when the backend cannot produce that one (engine/tts_engine.py)
+    format: str = ""
 
 
 class TextToSpeech(Protocol):
@@ -112,7 +117,9 @@ class OpenAITTSClient:
                 raise RuntimeError(f"TTS request failed with status {r.status}: "
                                    f"{r.body.decode(errors='replace')}")
             ctype = r.headers.get("Content-Type", "")
-            return TTSResult(r.body, ctype, len(r.body))
+            fmt = (options.response_format if options and options.response_format
+                   else self.cfg.response_format)
+            return TTSResult(r.body, ctype, len(r.body), format=fmt)
         finally:
             self._sem.release()
 

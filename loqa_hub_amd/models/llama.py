@@ -493,13 +493,6 @@ class LlamaModel:
         return ops.skinny_gemm(hf, w.lm_head_p, 1,
                                max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
 
-    def _prefetch_stream(self, device):
-        st = getattr(self, "_pf_stream", None)
-        if st is None:
-            from ..utils.streams import placed_stream
-            st = self._pf_stream = placed_stream(device, "prefetch")
-        return st
-
     def forward_decode_fused(self, meta: StepMeta, k_cache: torch.Tensor, v_cache: torch.Tensor,
                              attn_ws: ops.AttnWorkspace | None, scratch: ops.FusedScratch,
                              split_keys: int = 128) -> torch.Tensor:
@@ -527,18 +520,9 @@ class LlamaModel:
         # grouped kernels' row limit: plain varlen flash attention then
         grouped = (H // Hkv) * meta.max_q <= 128
         # decode rows (the split-key kernel's <= 32 query rows per kv head): qkv
-        # and attention through skinny_fused(attn=), one launch with FUSE_QKV_ATTN
+        # and attention through skinny_fused(attn=)
         dec_attn = (H // Hkv) * meta.max_q <= 32 and attn_ws is not None
         ao = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device) if dec_attn else None
-        # Infinity Cache prefetch (ops.L3_PREFETCH): once a layer's qkv GEMM is
-        # done, a side stream reads that layer's o / gate|up / down and the next
-        # layer's qkv weights while the attention and all-reduces (latency
-        # chains) leave HBM idle; nothing waits for it except the step's end
-        pf = ops.L3_PREFETCH and residual.is_cuda
-        if pf:
-            main = torch.cuda.current_stream(residual.device)
-            side = self._prefetch_stream(residual.device)
-            side.wait_stream(main)
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
             if dec_attn:
@@ -562,13 +546,6 @@ class LlamaModel:
                                      grouped=grouped, split_keys=split_keys,
                                      num_splits=num_splits if grouped else 1,
                                      workspace=attn_ws, max_k=meta.max_ctx)
-            if pf:
-                ev = torch.cuda.Event()
-                ev.record(main)
-                nxt = w.decode_layers[li + 1]["wqkv_f"] if li + 1 < len(w.layers) else None
-                with torch.cuda.stream(side):
-                    side.wait_event(ev)
-                    ops.l3_prefetch([P["wo"], P["w_gate_up_f"], P["w_down"], nxt])
             if tp.world == 1:
                 ops.skinny_fused(attn, P["wo"], "resid", scratch, residual=residual)
             else:
@@ -585,8 +562,6 @@ class LlamaModel:
                 pd = tp.partial_out(1, Mpad, d, residual.device)
                 ops.skinny_fused(a, P["w_down"], "act", scratch, out=pd, act="f32")
                 tp.resid_epilogue(1, pd, residual, scratch)
-        if pf:
-            main.wait_stream(side)      # join the side stream (graph capture needs it)
         if ops.FUSED_EMBED:
             hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
         else:

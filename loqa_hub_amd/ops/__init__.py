@@ -166,10 +166,6 @@ class AttnWorkspace:
         # split-arrival tickets of the decode kernel's in-launch combine, one per
         # (sequence, kv head); the last arriving split resets its counter
         self.counters = torch.zeros(max_tokens * n_heads, dtype=torch.int32, device=device)
-        # hand-off words of the fused qkv + attention launch (skinny_fused(attn=)):
-        # per-kv-head ready counts [0, 64), work 64, exit 65, error 66; zero on
-        # entry and left zero (the error word is sticky)
-        self.sync = torch.zeros(128, dtype=torch.int32, device=device)
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Tensor, *,
@@ -1029,36 +1025,6 @@ def expand_sample(stats: torch.Tensor, cum: torch.Tensor, flen: torch.Tensor, F:
     return z
 
 
-# ------------------------------------------------------ Infinity Cache prefetch
-# Weight prefetch into the die-level cache on a side stream during the decode
-# layer's latency-bound phases (csrc/kernels/l3_prefetch.hip); off by default
-# until measured (docs/PERF.md)
-L3_PREFETCH = os.environ.get("LOQA_L3_PREFETCH", "0") == "1"
-L3_PREFETCH_WGS = int(os.environ.get("LOQA_L3_PREFETCH_WGS", "128"))
-_L3_SINKS: dict = {}
-
-
-def l3_prefetch(tensors: list, wgs: int | None = None) -> None:
-    """Read ``tensors`` (device, contiguous; <= 8) front to back on the current
-    stream so their bytes sit in the Infinity Cache for a later consumer. A
-    pure read - nothing waits for it. No-op off the GPU."""
-    ts = [t.wp if isinstance(t, FusedLinear) else t for t in tensors if t is not None]
-    if not ts or not _gpu(ts[0]):
-        return
-    assert len(ts) <= 8
-    dev = ts[0].device
-    sink = _L3_SINKS.get(dev)
-    if sink is None:
-        sink = _L3_SINKS[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
-    for t in ts:
-        assert t.is_contiguous() and (t.numel() * t.element_size()) % 16 == 0
-    n = len(ts)
-    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
-    sizes = (ctypes.c_longlong * n)(*[t.numel() * t.element_size() for t in ts])
-    check(kernels().loqa_l3_prefetch(ptrs, sizes, n, wgs or L3_PREFETCH_WGS, ptr(sink),
-                                     torch.cuda.current_stream(dev).cuda_stream), "l3_prefetch")
-
-
 # ------------------------------------------------------------ fused decode GEMMs
 class FusedScratch:
     """Device state shared by the fused decode GEMMs of one engine: split-K
@@ -1223,40 +1189,34 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     ``attn`` (mode "rope"): the step's causal decode attention over the paged
     caches (keys of :func:`attention`: cu_q, ctx_lens, block_tables, max_q,
     split_keys, num_splits, workspace, max_k, scale, out) follows the GEMM and
-    its output is returned. With ``FUSE_QKV_ATTN`` and a supported shape both
-    run in ONE launch (the GEMM's workgroups turn into attention workers as
-    their tiles complete, gemm_skinny.hip ATTD), bit-identical to the two
-    launches; otherwise the two launches."""
+    its output is returned (mode "act": attention over contiguous K / V rows,
+    keys k, v, kv_start). Two launches: the one-launch hand-off was measured
+    slower in every configuration and removed (docs/PERF.md, round 5)."""
     if attn is not None:
         assert mode in ("rope", "act")
         rope = mode == "rope"
         if not rope and out is None:
             out = torch.empty(x.shape[0], wp.shape[0] * 16 if not isinstance(wp, FusedLinear)
                               else wp.N, dtype=torch.bfloat16, device=x.device)
-        fused = _gpu(x) and _attd_plan(x, wp, scratch, splits, rt, wr, xl,
-                                       q_out if rope else out, k_cache if rope else attn["k"],
-                                       n_heads, n_kv, head_dim, attn, norm, mode, act)
-        if not fused:
-            qq = skinny_fused(x, wp, mode, scratch, splits=splits, norm=norm, eps=eps,
-                              rowsq_tiles=rowsq_tiles, rt=rt, positions=positions, cos_sin=cos_sin,
-                              q_out=q_out, k_cache=k_cache, v_cache=v_cache, slots=slots,
-                              n_heads=n_heads, n_kv=n_kv, head_dim=head_dim, bias=bias,
-                              colsum=colsum, wr=wr, xl=xl, out=out, act=act)
-            if rope:
-                return attention(q_out, k_cache, v_cache, attn["cu_q"], n_heads=n_heads,
-                                 n_kv=n_kv, head_dim=head_dim, causal=True, max_q=attn["max_q"],
-                                 ctx_lens=attn["ctx_lens"], block_tables=attn["block_tables"],
-                                 scale=attn.get("scale"), grouped=True,
-                                 split_keys=attn["split_keys"], num_splits=attn["num_splits"],
-                                 workspace=attn["workspace"], out=attn.get("out"),
-                                 max_k=attn.get("max_k"))
-            return attention(qq, attn["k"], attn["v"], attn["cu_q"], n_heads=n_heads, n_kv=n_kv,
-                             head_dim=head_dim, causal=False, max_q=attn["max_q"],
-                             cu_k=attn["kv_start"], ctx_lens=attn["ctx_lens"],
+        qq = skinny_fused(x, wp, mode, scratch, splits=splits, norm=norm, eps=eps,
+                          rowsq_tiles=rowsq_tiles, rt=rt, positions=positions, cos_sin=cos_sin,
+                          q_out=q_out, k_cache=k_cache, v_cache=v_cache, slots=slots,
+                          n_heads=n_heads, n_kv=n_kv, head_dim=head_dim, bias=bias,
+                          colsum=colsum, wr=wr, xl=xl, out=out, act=act)
+        if rope:
+            return attention(q_out, k_cache, v_cache, attn["cu_q"], n_heads=n_heads,
+                             n_kv=n_kv, head_dim=head_dim, causal=True, max_q=attn["max_q"],
+                             ctx_lens=attn["ctx_lens"], block_tables=attn["block_tables"],
                              scale=attn.get("scale"), grouped=True,
                              split_keys=attn["split_keys"], num_splits=attn["num_splits"],
-                             workspace=attn["workspace"], out=attn.get("out"))
-        splits, rt, wr, xl = fused
+                             workspace=attn["workspace"], out=attn.get("out"),
+                             max_k=attn.get("max_k"))
+        return attention(qq, attn["k"], attn["v"], attn["cu_q"], n_heads=n_heads, n_kv=n_kv,
+                         head_dim=head_dim, causal=False, max_q=attn["max_q"],
+                         cu_k=attn["kv_start"], ctx_lens=attn["ctx_lens"],
+                         scale=attn.get("scale"), grouped=True,
+                         split_keys=attn["split_keys"], num_splits=attn["num_splits"],
+                         workspace=attn["workspace"], out=attn.get("out"))
     if isinstance(wp, FusedLinear):
         lin = wp
         wp = lin.wp
@@ -1326,101 +1286,18 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
     p.rt, p.wr, p.xl = rt, wr, int(bool(xl))
-    if attn is not None:
-        ws = attn["workspace"]
-        bt = attn.get("block_tables")
-        aout = attn.get("out")
-        if aout is None:
-            aout = torch.empty(Mpad, n_heads * head_dim, dtype=torch.bfloat16, device=x.device)
-        if mode == "rope":
-            p.att, p.q_bytes, p.kv_bytes = head_dim, q_out.numel() * 2, k_cache.numel() * 2
-            p.block_tables, p.max_blocks = ptr(bt), bt.shape[1]
-        else:
-            p.att, p.q_bytes, p.kv_bytes = head_dim, out.numel() * 2, 0
-            k, v = attn["k"], attn["v"]
-            p.att_k, p.att_v, p.att_kv_stride = ptr(k), ptr(v), k.stride(0)
-            p.att_kv_start = ptr(attn["kv_start"])
-        p.cu_q, p.ctx_lens = ptr(attn["cu_q"]), ptr(attn["ctx_lens"])
-        p.att_B = attn["cu_q"].numel() - 1
-        # one attention worker per (split, kv head, sequence) item, as the
-        # standalone kernel's grid: the GEMM's blocks plus attention-only ones
-        p.att_workers = min(ATTD_MAX_WORKERS, attn["num_splits"] * n_kv * p.att_B)
-        p.split_keys, p.num_splits = attn["split_keys"], attn["num_splits"]
-        sc = attn.get("scale")
-        p.att_scale = sc if sc is not None else 1.0 / math.sqrt(head_dim)
-        p.part_o, p.part_ml, p.att_counters = ptr(ws.part_o), ptr(ws.part_ml), ptr(ws.counters)
-        p.att_out, p.att_ld, p.att_sync = ptr(aout), aout.stride(0), ptr(ws.sync)
-        check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused(attn)")
-        return aout
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out
     return q_out if mode == "rope" else residual
 
 
-# qkv + decode attention in one launch (skinny_fused(attn=...)): off by default
-# until it measures faster in the pipeline (docs/PERF.md)
 def set_launch_priority(prio: int) -> None:
     """Wave issue priority (s_setprio 3) of the decode attention and fused
     GEMM kernels this host THREAD launches or captures from now on (0 =
     default); the STT decoder thread sets it under ``LOQA_STT_WAVE_PRIO``."""
     if torch.cuda.is_available():
         kernels().loqa_set_launch_prio(int(prio))
-
-
-FUSE_QKV_ATTN = os.environ.get("LOQA_FUSE_QKV_ATTN", "0") == "1"
-ATTD_MAX_WORKERS = int(os.environ.get("LOQA_ATTD_WORKERS", "2048"))
-_NUM_CUS: list = []
-
-
-def _attd_plan(x, wp, scratch, splits, rt, wr, xl, q_out, k_cache, H, Hkv, D, attn, norm,
-               mode="rope", act="none"):
-    """(splits, rt, wr, xl) of a supported fused GEMM + attention launch, or
-    None. rope: qkv + paged causal attention; act: q projection + attention
-    over contiguous K / V rows (``k_cache`` = the K rows)."""
-    if not FUSE_QKV_ATTN:
-        return None
-    lin = wp if isinstance(wp, FusedLinear) else None
-    w = lin.wp if lin is not None else wp
-    nrm = _NORMS[lin.norm if (lin is not None and norm is None) else norm]
-    Mpad, K = x.shape
-    N = w.shape[0] * 16
-    tuned = _FSPLITS.get((mode, N, K, Mpad))
-    free = splits is None and rt is None and wr is None and xl is None
-    S = splits or (tuned[0] if tuned else choose_splits(N, K, Mpad))
-    rt = rt or (tuned[1] if tuned else 2)
-    if xl is None:
-        xl = tuned[3] if (tuned and not splits and len(tuned) > 3) else 0
-    if wr is None:
-        wr = tuned[2] if (tuned and not splits and len(tuned) > 2) else 1
-    if wr != 1 and (S != 1 or N % (64 * rt)):
-        wr = 1
-    if not _NUM_CUS:
-        _NUM_CUS.append(torch.cuda.get_device_properties(x.device).multi_processor_count)
-    if free and (xl or (N // (16 * rt * wr)) * S > _NUM_CUS[0]):
-        # the tuned layout would not be resident at once: 32-row tiles, no split
-        S, rt, wr, xl = 1, 2, 1, 0
-    G = H // Hkv
-    ws = attn["workspace"]
-    ok = (Mpad in (16, 32, 64) and not xl and rt in (1, 2) and D in (64, 128) and H % Hkv == 0
-          and Hkv <= 64 and G * attn["max_q"] <= 32 and attn["split_keys"] % 32 == 0
-          and q_out.numel() * 2 < (1 << 31) and ws.max_splits >= attn["num_splits"]
-          and ws.max_tokens >= Mpad and (attn["cu_q"].numel() - 1) * Hkv <= ws.counters.numel()
-          and (N // (16 * rt * wr)) * S <= _NUM_CUS[0])
-    if mode == "rope":
-        bt = attn["block_tables"]
-        ok = ok and ((nrm == 1 and D in (64, 128)) or (nrm == 2 and D == 64)) \
-            and bt is not None and k_cache.dim() == 4 and k_cache.shape[2] >= 16 \
-            and k_cache.shape[2] & (k_cache.shape[2] - 1) == 0 and q_out.is_contiguous() \
-            and q_out.shape[1] == H * D and k_cache.numel() * 2 < (1 << 31)
-    else:
-        v = attn["v"]
-        ok = ok and nrm == 2 and D == 64 and act in ("none", "gelu") and N == H * D \
-            and q_out.stride(0) % 8 == 0 and k_cache.stride(0) == v.stride(0) \
-            and k_cache.stride(0) % 8 == 0 and attn.get("kv_start") is not None
-    if ok and mode == "rope" and attn.get("max_k") is not None:
-        assert attn["max_k"] <= bt.shape[1] * k_cache.shape[2], "context exceeds block table"
-    return (S, rt, wr, 0) if ok else None
 
 
 def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, positions,

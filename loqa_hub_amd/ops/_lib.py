@@ -40,14 +40,6 @@ class FusedParams(ctypes.Structure):
         ("vc", c_void_p), ("slots", c_void_p),
         ("H", c_int), ("Hkv", c_int), ("D", c_int), ("blk", c_int),
         ("rt", c_int), ("wr", c_int), ("xl", c_int),
-        ("att", c_int), ("q_bytes", c_ll), ("kv_bytes", c_ll),
-        ("cu_q", c_void_p), ("ctx_lens", c_void_p), ("block_tables", c_void_p),
-        ("max_blocks", c_int), ("att_B", c_int), ("split_keys", c_int), ("num_splits", c_int),
-        ("att_scale", c_float), ("part_o", c_void_p), ("part_ml", c_void_p),
-        ("att_counters", c_void_p), ("att_out", c_void_p), ("att_ld", c_ll),
-        ("att_sync", c_void_p),
-        ("att_k", c_void_p), ("att_v", c_void_p), ("att_kv_stride", c_ll), ("att_kv_start", c_void_p),
-        ("att_workers", c_int),
     ]
 
 
@@ -153,7 +145,6 @@ _KERNEL_SIGS = {
 _CAR_SIGS = {
     "loqa_car_create": ([c_int, c_int, c_ll, c_ll], c_void_p),
     "loqa_car_inbuf": ([c_void_p, c_int], c_void_p),
-    "loqa_l3_prefetch": ([c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p], c_int),
     "loqa_set_launch_prio": ([c_int], None),
     "loqa_car_resid": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
     "loqa_car_argmax": ([c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -57,6 +57,43 @@ SHM_SLOTS = int(os.environ.get("LOQA_DP_SHM_SLOTS", "48"))
 SHM_SLOT_BYTES = 480000 * 2          # one 30 s window of PCM16
 
 
+def create_pcm_rings(n: int, slots: int, slot_bytes: int, shm_dir: str = "/dev/shm") -> list:
+    """One shared-memory PCM ring per worker, every page reserved up front, or
+    [] (inline pickled PCM) when the space is not there. A POSIX segment is a
+    sparse file: without the reservation a tmpfs limit (a container's default
+    64 MB /dev/shm) would surface as SIGBUS on the first touch past it - in the
+    front end's event loop copying PCM in, or in a worker pinning the ring."""
+    from multiprocessing import shared_memory
+    size = slots * slot_bytes
+    try:
+        st = os.statvfs(shm_dir)
+        free = st.f_bavail * st.f_frsize
+    except OSError:
+        free = None
+    if free is not None and free < n * size + (16 << 20):
+        log.warning("PCM rings need %.0f MB of %s, %.0f MB free: sending PCM inline",
+                    n * size / 1e6, shm_dir, free / 1e6)
+        return []
+    made: list = []
+    try:
+        for _ in range(n):
+            m = shared_memory.SharedMemory(create=True, size=size)
+            made.append(m)
+            fd = getattr(m, "_fd", -1)
+            if fd >= 0 and hasattr(os, "posix_fallocate"):
+                os.posix_fallocate(fd, 0, size)   # ENOSPC here, not SIGBUS later
+    except OSError as e:
+        log.warning("PCM ring allocation failed (%s): sending PCM inline", e)
+        for m in made:
+            try:
+                m.close()
+                m.unlink()
+            except OSError:
+                pass
+        return []
+    return made
+
+
 class _WorkerPcmRing:
     """Worker side of its shared-memory PCM ring (mapped, and pinned on a GPU)."""
 
@@ -320,12 +357,11 @@ class DPVoiceProcessor:
     async def start(self) -> None:
         ctx = mp.get_context("spawn")
         if SHM_SLOTS > 0 and "pcm_shm" not in self.spec:
-            from multiprocessing import shared_memory
-            self._shm = [shared_memory.SharedMemory(create=True, size=SHM_SLOTS * SHM_SLOT_BYTES)
-                         for _ in range(self.n)]
-            self._shm_free = [list(range(SHM_SLOTS)) for _ in range(self.n)]
-            self.spec["pcm_shm"] = [m.name for m in self._shm]
-            self.spec["pcm_shm_slot_bytes"] = SHM_SLOT_BYTES
+            self._shm = create_pcm_rings(self.n, SHM_SLOTS, SHM_SLOT_BYTES)
+            if self._shm:
+                self._shm_free = [list(range(SHM_SLOTS)) for _ in range(self.n)]
+                self.spec["pcm_shm"] = [m.name for m in self._shm]
+                self.spec["pcm_shm_slot_bytes"] = SHM_SLOT_BYTES
         self._req_qs = [ctx.Queue() for _ in range(self.n)]
         self._resp_q = ctx.Queue()
         self._procs = [ctx.Process(target=_worker_main, args=(r, self.spec, self._req_qs[r],

@@ -57,7 +57,8 @@ def build_tts(cfg: Config, device: str = "cuda:0"):
         win = float(os.environ.get("LOQA_TTS_BATCH_WINDOW_MS", "3")) / 1e3
         ckpt = cfg.gpu.tts_checkpoint or None
         return VitsTTSEngine(None if ckpt else vits_config(cfg.gpu.tts_model), device,
-                             seed=cfg.gpu.seed, batch_window=win, checkpoint=ckpt)
+                             seed=cfg.gpu.seed, batch_window=win, checkpoint=ckpt,
+                             format_policy=cfg.gpu.tts_format_policy)
     if b in ("http", "openai"):
         from .llm.tts import OpenAITTSClient
         return OpenAITTSClient(cfg.tts)

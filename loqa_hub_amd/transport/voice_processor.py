@@ -90,6 +90,9 @@ class GPUVoiceProcessor:
         self.stats = {"utterances": 0, "errors": 0, "bridge_sessions": 0, "bridge_ack": 0,
                       "bridge_fallback": 0, "interrupted": 0,
                       "progressive": 0, "first_audio_ms_sum": 0.0, "first_audio_n": 0}
+        # a list that collects every finished PipelineJob (phase timestamps for
+        # a benchmark's per-phase breakdown); None: not collected
+        self.job_sink: list | None = None
 
     def attach_publisher(self, publisher) -> None:
         self.publisher = publisher
@@ -152,6 +155,8 @@ class GPUVoiceProcessor:
                 self.streaming.begin_speech_session(speech.session_id, speech)
         try:
             await self.pipeline.submit(j)
+            if self.job_sink is not None:
+                self.job_sink.append(j)
             if "enc0" in j.t and "start" in j.t:
                 # process() runs at end of speech: the gap until the encoder
                 # (upload + log-mel) starts on this utterance
@@ -248,7 +253,7 @@ class GPUVoiceProcessor:
                 return
             try:
                 t = await self.tts.synthesize(r.response_text, opts)
-                r.audio, r.audio_format = t.audio, opts.response_format or self.tts_format
+                r.audio, r.audio_format = t.audio, t.format or opts.response_format or self.tts_format
                 if t.sample_rate:
                     r.audio_sample_rate = t.sample_rate
                     r.audio_duration = len(t.audio) / 2 / t.sample_rate
@@ -315,6 +320,6 @@ class ServiceVoiceProcessor:
         from ..llm.tts import TTSOptions
         try:
             t = await self.tts.synthesize(r.response_text, TTSOptions(response_format=self.tts_format))
-            r.audio, r.audio_format = t.audio, self.tts_format
+            r.audio, r.audio_format = t.audio, t.format or self.tts_format
         except Exception as e:  # noqa: BLE001
             log.warning("TTS failed: %s", e)

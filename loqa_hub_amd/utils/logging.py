@@ -77,19 +77,36 @@ def initialize(level: str | None = None, fmt: str | None = None, stream=None) ->
 
 
 class _DeferredHandler(logging.handlers.QueueHandler):
-    """Enqueue the raw record (the stock QueueHandler formats it in the
-    caller's thread first); a QueueListener thread formats and writes it."""
+    """DEBUG / INFO: the record is enqueued with its message already rendered
+    (so mutable args show their state at the call) and a QueueListener thread
+    formats and writes it. WARNING and above are written synchronously, in the
+    caller's thread: those are the lines that explain a failure, and a process
+    killed by the DP watchdog or aborted by a GPU fault must not lose them in
+    the queue (ERROR stack traces then also show the caller's stack)."""
 
     def __init__(self, target: logging.Handler):
         import queue as _q
         super().__init__(_q.SimpleQueue())
+        self.target = target
         self.listener = logging.handlers.QueueListener(self.queue, target,
                                                        respect_handler_level=True)
         self.listener.start()
         import atexit
         atexit.register(self.listener.stop)
 
+    def emit(self, record: logging.LogRecord) -> None:
+        if record.levelno >= logging.WARNING:
+            self.target.handle(record)
+            try:
+                self.target.flush()
+            except Exception:  # noqa: BLE001
+                pass
+            return
+        super().emit(record)
+
     def prepare(self, record: logging.LogRecord) -> logging.LogRecord:
+        record.msg = record.getMessage()
+        record.args = None
         if record.exc_info and not record.exc_text:
             record.exc_text = logging.Formatter().formatException(record.exc_info)
         return record

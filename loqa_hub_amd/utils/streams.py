@@ -71,8 +71,7 @@ def aligned_pool_stream(device: torch.device, priority: int, slot: int):
 # The PCM stream-in copies (engine/pcm_staging.py) take the old prefill
 # worker's slot 3: a queue of their own beside the decoders (the copies run on
 # the DMA engine and hold no CU).
-DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3, "tts": 29, "h2d": 3,
-                 "prefetch": 27}
+DEFAULT_SLOTS = {"llm": 2, "stt": 30, "encoder": 28, "prefill": 3, "tts": 29, "h2d": 3}
 
 
 def init_pools(device: torch.device) -> None:

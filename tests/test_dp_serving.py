@@ -149,3 +149,66 @@ def test_dp_pcm_shared_memory_ring(monkeypatch):
     assert [r.transcription for r in res] == [hashlib.sha1(p.tobytes()).hexdigest() for p in pcms]
     assert st["pcm_shm_sent"] == len(pcms) - 1 and st["pcm_inline_sent"] == 1
     assert free == [[0, 1, 2], [0, 1, 2]]
+
+
+def test_dp_pcm_rings_fall_back_when_shm_is_short(monkeypatch):
+    """a POSIX segment is sparse, so a tmpfs limit surfaces as
+    SIGBUS on first touch. The rings are reserved up front: too little free
+    /dev/shm, or a failed reservation, means inline PCM (no rings, no leak)."""
+    import collections
+    import os as _os
+
+    from loqa_hub_amd.parallel import dp_serving as dps
+    FakeSt = collections.namedtuple("FakeSt", "f_bavail f_frsize")
+    monkeypatch.setattr(dps.os, "statvfs", lambda p: FakeSt(64 << 20 >> 12, 4096))   # 64 MB free
+    assert dps.create_pcm_rings(2, 48, dps.SHM_SLOT_BYTES) == []
+    monkeypatch.setattr(dps.os, "statvfs", lambda p: FakeSt(1 << 40 >> 12, 4096))
+    made = []
+    real_fallocate = getattr(_os, "posix_fallocate", None)
+
+    def failing(fd, off, size):
+        made.append(fd)
+        if len(made) == 2:
+            raise OSError(28, "No space left on device")
+        if real_fallocate:
+            real_fallocate(fd, off, size)
+    monkeypatch.setattr(dps.os, "posix_fallocate", failing, raising=False)
+    assert dps.create_pcm_rings(3, 2, 4096) == []
+    assert len(made) == 2
+    monkeypatch.setattr(dps.os, "posix_fallocate", real_fallocate, raising=False)
+    rings = dps.create_pcm_rings(2, 2, 4096)
+    try:
+        assert len(rings) == 2 and all(m.size >= 8192 for m in rings)
+    finally:
+        for m in rings:
+            m.close()
+            m.unlink()
+
+
+def test_pcm_stager_stream_in_failure_degrades(monkeypatch):
+    """when the device mirrors of stream-in cannot be allocated
+    (HBM nearly full), the stager logs and stays in whole-utterance mode
+    instead of raising from its constructor (which failed every relay)."""
+    from loqa_hub_amd.engine import pcm_staging
+
+    class FakeRuntime:
+        destroyed = 0
+
+        def loqa_stager_create(self, n, cap, own):
+            return 1234
+
+        def loqa_stager_set_stream(self, h, stream, on):
+            return 2                      # hipErrorOutOfMemory
+
+        def loqa_stager_destroy(self, h):
+            FakeRuntime.destroyed += 1
+
+    fake = FakeRuntime()
+    monkeypatch.setattr(pcm_staging._lib, "runtime", lambda: fake)
+
+    class Stream:
+        cuda_stream = 99
+    st = pcm_staging.PcmStager(4, 1600, h2d_stream=Stream())
+    assert st.stream_in is False and st._h2d is None
+    st.close()
+    assert FakeRuntime.destroyed == 1

@@ -257,6 +257,40 @@ def test_bench_cpu_smoke_dp4_gloo():
     assert out["command_count_match_rate"] == 1.0
 
 
+def test_bench_cpu_smoke_dp8_gloo():
+    """Eight ranks - the width the driver launches on an 8-GPU node
+    (torchrun --nproc-per-node 8): per-rank served hubs (the default hub mode,
+    gRPC relays), one NATS broker, records gathered to rank 0."""
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+                "8", "--master-addr", "127.0.0.1", "--master-port", "29565", "bench.py",
+                "--cpu-smoke", "--gpus", "8", "--steps", "1", "--warmup", "0",
+                "--batch-per-gpu", "1", "--window-steps", "0"], timeout=900)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["config"]["mode"] == "hub" and out["config"]["global_batch"] == 8
+    assert out["queue_success_rate"] == 1.0 and out["command_count_match_rate"] == 1.0
+
+
+def test_bench_rank_without_device_fails_fast(monkeypatch):
+    """A GPU run whose rank has no device of its own exits 2 with a message
+    before any collective (VERDICT r5 #7)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = type("A", (), {"cpu_smoke": False, "gpus": 8})()
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 4)
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    monkeypatch.setenv("RANK", "5")
+    monkeypatch.delenv("LOQA_DIST_SHARE_GPU", raising=False)
+    assert "has no GPU" in bench.rank_device_problem(args)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert bench.rank_device_problem(args) is None
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 0)
+    assert "no GPU visible" in bench.rank_device_problem(args)
+    args.cpu_smoke = True
+    assert bench.rank_device_problem(args) is None
+
+
 def test_bench_gpus_guard():
     """--gpus must match the launch: a torchrun job of the wrong size exits 2;
     without torchrun, --gpus 2 relaunches the bench under torch.distributed.run."""
@@ -277,10 +311,17 @@ def test_bench_gpus_guard():
 def test_bench_cpu_smoke_hub_mode():
     """--mode hub: relays over gRPC into the served hub (arbitration, bridge,
     voice events) on the same pipeline."""
-    out = _run([sys.executable, "bench.py", "--cpu-smoke", "--mode", "hub", "--steps", "1",
-                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "10"])
+    out = _run([sys.executable, "bench.py", "--cpu-smoke", "--steps", "1",
+                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "10",
+                "--window-steps", "1"])
+    # hub mode + single-relay bypass are the defaults; the window_300ms pass
+    # (bypass off) adds one utterance per relay after the timed step
     assert out["config"]["mode"] == "hub" and out["queue_success_rate"] == 1.0
     assert out["hub"]["voice_events"] == 2 and out["hub"]["audio_service"]["processed"] == 2
+    svc = out["hub"]["audio_service"]
+    assert svc["bypassed"] == 2
+    w = out["window_300ms"]
+    assert w["utterances"] == 2 and w["utterances_per_sec"] > 0 and w["window_ms"] == 10
 
 
 def test_whisper_fast_decode_matches_eager_cpu():
@@ -358,6 +399,38 @@ def test_vits_tts_cpu():
         assert r2.content_type == "audio/pcm" and len(r2.audio) % 2 == 0
     asyncio.run(go())
     assert e.stats["batches"] >= 2
+
+
+def test_vits_tts_response_format_cpu():
+    """response_format (openai_tts_client.go:39-46): wav / pcm as asked; a
+    format the GPU voice cannot encode (the status manager's mp3,
+    status_manager.go:441-462) is a counted, logged downgrade to WAV labelled
+    "wav" by default, an error under format_policy="error"."""
+    import asyncio
+    import pytest as _pt
+    from loqa_hub_amd.engine.tts_engine import UnsupportedAudioFormat, VitsTTSEngine, wav_info
+    from loqa_hub_amd.llm.tts import TTSOptions
+    from loqa_hub_amd.models.configs import VITS_CONFIGS
+    e = VitsTTSEngine(VITS_CONFIGS["test-vits"], "cpu")
+
+    async def go():
+        w, p, m, o = await asyncio.gather(
+            e.synthesize("hello", TTSOptions(response_format="wav")),
+            e.synthesize("hello", TTSOptions(response_format="pcm")),
+            e.synthesize("hello", TTSOptions("af_bella", 1.1, "mp3", True)),
+            e.synthesize("hello", TTSOptions(response_format="opus")))
+        assert (w.format, w.content_type) == ("wav", "audio/wav") and wav_info(w.audio)[0] == 22050
+        assert (p.format, p.content_type) == ("pcm", "audio/pcm")
+        for r in (m, o):   # never mp3 / opus bytes under a wav label or vice versa
+            assert (r.format, r.content_type) == ("wav", "audio/wav") and r.audio[:4] == b"RIFF"
+    asyncio.run(go())
+    assert e.stats["format_downgrades"] == 2
+    strict = VitsTTSEngine(VITS_CONFIGS["test-vits"], "cpu", format_policy="error")
+    with _pt.raises(UnsupportedAudioFormat):
+        asyncio.run(strict.synthesize("hello", TTSOptions(response_format="mp3")))
+    assert asyncio.run(strict.synthesize("hi", TTSOptions(response_format="PCM"))).format == "pcm"
+    with _pt.raises(ValueError):
+        VitsTTSEngine(VITS_CONFIGS["test-vits"], "cpu", format_policy="mp3")
 
 
 def test_vits_padding_is_inert_cpu():
@@ -664,7 +737,8 @@ def test_bench_cpu_smoke_hub_mode_bypass():
     utterance waits for the arbitration window (the window here is 5 s: a
     run that waited would time out of the smoke's budget)."""
     out = _run([sys.executable, "bench.py", "--cpu-smoke", "--mode", "hub", "--steps", "1",
-                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "5000", "--bypass"])
+                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "5000", "--bypass",
+                "--window-steps", "0"])
     svc = out["hub"]["audio_service"]
     assert out["queue_success_rate"] == 1.0 and svc["processed"] == 2
     assert svc.get("bypassed", 0) == svc.get("windows", 0) > 0

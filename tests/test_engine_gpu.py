@@ -626,24 +626,3 @@ def test_whisper_large_v3_fused_graph_decode_vs_fp32_gpu():
         errs.append(_rel_max(out[0, :V].float(), want))
     print("whisper-large-v3 x2 fused graph decode: max rel logit err per step", max(errs))
     assert max(errs) <= 2e-2, errs
-
-
-def test_llm_l3_prefetch_same_tokens_gpu():
-    """The Infinity Cache weight prefetch (a side-stream read during each
-    layer's attention / all-reduce) changes no output: graph-replayed and
-    pipelined decode give the same tokens with it on and off."""
-    from loqa_hub_amd import ops
-    cfg = llama_config("test-tiny")
-    n_list = [1, 2, 3, 2]
-    old = ops.L3_PREFETCH
-    try:
-        ops.L3_PREFETCH = False
-        ref = _sched_outputs(LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True), n_list)
-        ops.L3_PREFETCH = True
-        got = _sched_outputs(LLMEngine(cfg, "cuda", max_seqs=8, use_graphs=True), n_list)
-        w = [torch.randn(1000, 64, device="cuda").bfloat16() for _ in range(3)]
-        ops.l3_prefetch(w, wgs=8)
-        torch.cuda.synchronize()
-    finally:
-        ops.L3_PREFETCH = old
-    assert got == ref

@@ -168,3 +168,14 @@ def test_hub_served_dp_cpu(tmp_path, streaming):
     res = _served(tmp_path, "cpu", streaming=streaming, dp=2, relays=relays)
     _check_served(*res, streaming=streaming, relays=relays)
     assert sorted(res[4]["dp_workers"]) == [0, 1]      # both workers served one
+
+
+def test_hub_served_dp8_cpu(tmp_path):
+    """The served DP hub at the driver's 8-rank width: eight
+    spawned workers, each the real per-GPU composition on the CPU engines
+    (tiny models), eight relays in their own groups - every worker is up,
+    every relay is answered and every utterance is a voice event."""
+    relays = tuple(f"relay-{i}" for i in range(8))
+    res = _served(tmp_path, "cpu", streaming=False, dp=8, relays=relays)
+    _check_served(*res, streaming=False, relays=relays)
+    assert len(res[4]["dp_workers"]) == 8

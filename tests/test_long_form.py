@@ -57,6 +57,32 @@ def test_stt_long_form_free_decoding_cpu():
     assert abs(r.rms - want) <= 1e-4 * want
 
 
+def test_stt_windows_capped_by_max_batch_and_hol_bypass_cpu():
+    """an utterance needing more 30 s windows than the engine has
+    cross-attention slots is truncated (like one past LOQA_STT_MAX_WINDOWS),
+    not rejected; and a short utterance may pass a long-form one that waits
+    for free slots (bounded, so the long one is never starved)."""
+    from loqa_hub_amd.engine.stt_engine import STTRequest
+    eng = _stt(torch.device("cpu"), "test-whisper")        # max_batch 4
+    u = make_long_utterance(2, 2, seconds=150)            # 5 windows > 4 slots
+    r = STTRequest(u.pcm, max_new_tokens=2)
+    assert eng.rows_needed([r]) == 4
+    out = eng.submit_batch([r]).result(timeout=300)
+    assert out[0].windows == 4 and out[0].t_done > 0
+    assert eng.stats["long_form_dropped_samples"] == len(u.pcm) - 4 * 480000
+    # a 3-window item at the head cannot start while 2 slots are held; the
+    # 1-window items behind it pass it
+    s = make_utterance(0, 1, 2)
+    a = eng.submit_batch([STTRequest(make_long_utterance(3, 2, seconds=40).pcm, max_new_tokens=40),
+                          STTRequest(s.pcm, max_new_tokens=40)])   # 3 rows, takes 3 of 4
+    b = eng.submit_batch([STTRequest(make_long_utterance(4, 2, seconds=80).pcm, max_new_tokens=2)])
+    c = eng.submit_batch([STTRequest(s.pcm, transcript=s.text)])
+    for f in (a, b, c):
+        f.result(timeout=300)
+    eng.stop()
+    assert sorted(eng._free_slots) == [0, 1, 2, 3]
+
+
 def _long_pipeline(device, stt_name, llm_name, graphs):
     from loqa_hub_amd.engine.llm_engine import LLMEngine
     from loqa_hub_amd.engine.pipeline import PipelineJob, VoicePipeline

@@ -181,3 +181,30 @@ def test_gpu_voice_processor_batches_on_cpu(tmp_path):
         assert all(r.command in ("voice_command_success", "no_speech", "error",
                                  "confirmation_needed") for r in res)
     asyncio.run(go())
+
+
+def test_deferred_logging_keeps_failures_and_call_time_args(monkeypatch, capsys):
+    """with the async log handler, WARNING+ lines are written
+    before the call returns (a process killed right after keeps them), and a
+    deferred INFO line renders its args as they were at the call."""
+    import logging as _logging
+
+    from loqa_hub_amd.utils import logging as lg
+    monkeypatch.setenv("LOQA_LOG_ASYNC", "1")
+    root = _logging.getLogger(lg.ROOT)
+    try:
+        lg.initialize("info", "console")
+        h = root.handlers[0]
+        assert isinstance(h, lg._DeferredHandler)
+        h.listener.stop()                 # nothing deferred is written from here on
+        lg.get("t").error("gpu fault on %s", "rank3")
+        assert "gpu fault on rank3" in capsys.readouterr().err
+        box = ["before"]
+        lg.get("t").info("state=%s", box)
+        box[0] = "after"
+        rec = h.queue.get_nowait()
+        assert rec.getMessage() == "state=['before']"
+        h.listener.start()                # its atexit stop() needs a running thread
+    finally:
+        for x in list(root.handlers):
+            root.removeHandler(x)
