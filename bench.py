@@ -96,8 +96,11 @@ def start_broker() -> tuple[int, threading.Thread]:
     return box["port"], t
 
 
-async def _start_hub(args, pipe, nats_port: int, info):
-    """The served hub of --mode hub on this rank's GPU pipeline."""
+async def _start_hub(args, pipe, nats_port: int, info, texts: dict):
+    """The served hub of --mode hub on this rank's GPU pipeline. ``texts``:
+    relay -> its utterances' transcripts in sending order (the teacher-forcing
+    hints of the random-init Whisper; each processed utterance takes the next)."""
+    import collections
     import tempfile
 
     from loqa_hub_amd import config as cfgmod
@@ -108,15 +111,19 @@ async def _start_hub(args, pipe, nats_port: int, info):
                        "ARBITRATION_SCOPE": "per_relay_group",
                        "ARBITRATION_WINDOW_DURATION": f"{args.window_ms}ms",
                        "ARBITRATION_SINGLE_RELAY_BYPASS": "true" if args.bypass else "false"})
-    hints: dict[str, str] = {}
+    fifo = {r: collections.deque(t) for r, t in texts.items()}
+
+    def hint(relay: str):
+        q = fifo.get(relay)
+        return q.popleft() if q else None
     srv = HubServer(cfg, skills_dir=os.path.join(os.path.dirname(db), "skills"),
                     skills_config_store=os.path.join(os.path.dirname(db), "skillcfg"),
-                    transcript_hints=hints.get)
+                    transcript_hints=hint)
     await srv._connect_nats()
     srv.processor = GPUVoiceProcessor(pipe, max_batch=pipe.max_batch,
                                       bridge=build_bridge(srv.skills), batch_window=0.002)
     await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
-    return srv, hints
+    return srv
 
 
 class CommandCounter:
@@ -529,50 +536,31 @@ def main(argv=None) -> int:
     recs_local: list[list[float]] = []
     hub_recs: dict[str, list] = {}
 
-    hub = None
+    hub = relays = None
     if args.mode == "hub":
-        hub = loop.run_until_complete(_start_hub(args, pipe, port, info))
-        cmd_counter = loop.run_until_complete(CommandCounter.start(f"nats://127.0.0.1:{port}"))
+        # the relays are devices of their own: a separate process drives them
+        # over gRPC (transport/relay_sim.py), so their client work shares no
+        # GIL with this hub's scheduler threads
+        from loqa_hub_amd.transport.relay_sim import RelayProcess, relay_name, relay_utterances
+        ru = relay_utterances(args.seed, mix, B, n_per_stream, info.rank)
+        texts = {relay_name(info.rank, ci): [u.text for u in ru[ci]] for ci in range(B)}
+        hub = loop.run_until_complete(_start_hub(args, pipe, port, info, texts))
+        relays = RelayProcess(port=hub.grpc_port, nats_url=f"nats://127.0.0.1:{port}",
+                              rank=info.rank, relays=B, seed=args.seed, mix=args.mix,
+                              per_relay=n_per_stream, paced=args.paced,
+                              cwd=os.path.dirname(os.path.abspath(__file__)))
 
     async def run_hub(n: int, record: bool, base: int | None = None) -> None:
         """--mode hub: B relays per GPU, each a closed loop of gRPC StreamAudio
         calls (wake-word chunk, 100 ms speech chunks, end of speech) into the
-        served hub; latency = first chunk sent -> response received. ``base``:
-        index of the first utterance of each relay's list (distinct ones)."""
-        import grpc
-
-        from loqa_hub_amd.transport.audio_proto import AudioChunk, stream_audio_stub
-        srv, hints = hub
-
-        async def client(ci: int, ch) -> None:
-            call = stream_audio_stub(ch)
-            for k in range(n):
-                u = next_utt(ci, k, record, base)
-                relay = f"relay-{info.rank}-{ci}"
-                hints[relay] = u.text
-                data = np.ascontiguousarray(u.pcm, dtype="<i2").tobytes()
-                wake, rest = data[:9600], data[9600:]
-                step_b = 3200
-
-                async def chunks():
-                    yield AudioChunk(relay_id=relay, audio_data=wake, sample_rate=16000,
-                                     is_wake_word=True)
-                    for o in range(0, max(len(rest), 1), step_b):
-                        if args.paced:          # a real relay: one 100 ms chunk per 100 ms
-                            await asyncio.sleep(step_b / 32000)
-                        yield AudioChunk(relay_id=relay, audio_data=rest[o:o + step_b],
-                                         sample_rate=16000,
-                                         is_end_of_speech=o + step_b >= len(rest))
-                t_s = time.perf_counter()
-                got = [r async for r in call(chunks())]
-                lat = (time.perf_counter() - t_s) * 1e3
-                if args.paced:                  # latency after the relay stopped speaking
-                    lat -= 1e3 * (-(-max(len(rest), 1) // step_b)) * step_b / 32000
-                ok = bool(got) and got[-1].success
-                if record:
-                    hub_recs.setdefault(relay, []).append([u.n_commands, float(ok), lat])
-        async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
-            await asyncio.gather(*[client(ci, ch) for ci in range(B)])
+        served hub, driven by the relay simulator process; latency = first
+        chunk sent -> response received (relay side). ``base``: index of the
+        first utterance of each relay's list (distinct utterances)."""
+        b0 = base if base is not None else (args.warmup if record else 0)
+        out = await relays.run(b0, n)
+        if record:
+            for relay, expected, ok, lat, rid in out:
+                hub_recs.setdefault(relay, []).append([expected, ok, lat, rid])
 
     def run(n: int, record: bool):
         if args.mode == "hub":
@@ -585,7 +573,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize(dev)
     s0 = dict(llm.stats)
     if hub is not None:
-        hub[0].processor.job_sink = all_jobs      # per-phase timestamps of the timed utterances
+        hub.processor.job_sink = all_jobs         # per-phase timestamps of the timed utterances
     t0 = time.perf_counter()
     loop.run_until_complete(run(args.steps, True))
     if dev.type == "cuda":
@@ -593,34 +581,33 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(info, time.perf_counter() - t0)
     if hub is not None:
-        hub[0].processor.job_sink = None
+        hub.processor.job_sink = None
 
     if hub is not None:
-        recs_local = loop.run_until_complete(cmd_counter.records(hub[0], hub_recs))
+        # commands each timed utterance actually published on loqa.voice.commands
+        # (observed by the relay process over NATS, keyed by the response's
+        # request id) - the parsed command count, not the expected one
+        # (the gRPC response carries no request id, as the reference's
+        # sendSuccessResponse sets none: utterances are matched to the voice
+        # events, one per processed utterance, in order per relay)
+        per_req = loop.run_until_complete(relays.counts())
+        from loqa_hub_amd.storage.voice_events_store import ListOptions
+        evs = hub.events.list(ListOptions(sort_by="timestamp", sort_order="ASC"))
+        by_relay: dict[str, list[str]] = {}
+        for ev in evs:
+            by_relay.setdefault(ev.relay_id, []).append(ev.request_id)
+        recs_local = []
+        for relay, recs in hub_recs.items():
+            rids = by_relay.get(relay, [])[-len(recs):]
+            rids = [""] * (len(recs) - len(rids)) + rids
+            for (exp, ok, lat, _), rid in zip(recs, rids):
+                recs_local.append([float(per_req.get(rid, 0)), float(exp), ok, lat])
     if args.mode in ("closed", "hub") and recs_local:
         step.records.append(gather_records(info, torch.tensor(recs_local, dtype=torch.float64)).cpu())
     stats = added_command_stats(all_jobs)
     hub_stats = None
     if hub is not None:
-        stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub[0], recs_local,
-                                                                            args)
-    window = None
-    if hub is not None and win_steps > 0:
-        # secondary: the same served path with every relay waiting out the
-        # reference's arbitration window (audio_service.go:408-502)
-        svc = hub[0].audio_service
-        svc.single_relay_bypass = False
-        pdist.barrier(info)
-        tw = time.perf_counter()
-        loop.run_until_complete(run_hub(win_steps, False, args.warmup + args.steps))
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        pdist.barrier(info)
-        tw = pdist.max_over_ranks(info, time.perf_counter() - tw)
-        window = {"window_ms": args.window_ms, "utterances_per_sec": round(info.world * B * win_steps / tw, 3),
-                  "utterances": info.world * B * win_steps,
-                  "note": "after the timed steps, single-relay bypass off: every utterance waits "
-                          "out the arbitration window before STT"}
+        stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub, recs_local, args)
     def _mean_ms(a, b):
         v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
         return round(float(np.mean(v)) * 1e3, 2) if v else None
@@ -640,6 +627,25 @@ def main(argv=None) -> int:
                            / args.steps * 1e3, 2),
         "llm_mixed_steps": (llm.stats.get("mixed_steps", 0) - s0.get("mixed_steps", 0)) / args.steps,
     }
+    # counters as of the end of the timed steps (the window pass below runs more)
+    llm_stats_t, stt_stats_t = dict(llm.stats), dict(stt.stats)
+    window = None
+    if hub is not None and win_steps > 0:
+        # secondary: the same served path with every relay waiting out the
+        # reference's arbitration window (audio_service.go:408-502)
+        svc = hub.audio_service
+        svc.single_relay_bypass = False
+        pdist.barrier(info)
+        tw = time.perf_counter()
+        loop.run_until_complete(run_hub(win_steps, False, args.warmup + args.steps))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        pdist.barrier(info)
+        tw = pdist.max_over_ranks(info, time.perf_counter() - tw)
+        window = {"window_ms": args.window_ms, "utterances_per_sec": round(info.world * B * win_steps / tw, 3),
+                  "utterances": info.world * B * win_steps,
+                  "note": "after the timed steps, single-relay bypass off: every utterance waits "
+                          "out the arbitration window before STT"}
     recs = torch.cat(step.records, 0) if step.records else torch.zeros(0, 4)
     total_utts = info.world * B * args.steps
     value = total_utts / elapsed
@@ -679,8 +685,8 @@ def main(argv=None) -> int:
             "queue_success_rate": round(ok, 4),
             "command_count_match_rate": round(cmd_match, 4),
             "phase_ms_per_step": phase_ms,
-            "llm_stats": llm.stats,
-            "stt_stats": stt.stats,
+            "llm_stats": llm_stats_t,
+            "stt_stats": stt_stats_t,
             "hub": hub_stats,
             "window_300ms": window,
             "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v)
@@ -689,8 +695,8 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     if hub is not None:
-        loop.run_until_complete(cmd_counter.close())
-        loop.run_until_complete(hub[0].stop())
+        relays.close()
+        loop.run_until_complete(hub.stop())
     loop.run_until_complete(nats.close())
     pdist.shutdown(info)
     if broker is not None:

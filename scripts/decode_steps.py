@@ -18,6 +18,10 @@ ENGINES = {
             "skinny_gemm_kernel<2, 1, 4>"),
     "stt": (re.compile(r"skinny_fused_kernel<\d, \d, 2, |attn_decode_kernel<64|skinny_gemm_kernel<2, 1, 2>"),
             "skinny_gemm_kernel<2, 1, 2>"),
+    # a tensor-parallel rank's graph-replayed decode step alone on the GPU
+    # (scripts/config5_projection.py): every kernel, a step ends at the
+    # vocab-parallel argmax combine
+    "tp": (re.compile(r"."), "car_argmax_kernel"),
 }
 
 
@@ -36,7 +40,8 @@ def main(path, engine="llm"):
             steps.append(cur)
             cur = []
     # decode steps only (tuning sweeps and prefill chunks have other shapes)
-    steps = [s for s in steps if 100 <= len(s) <= 400]
+    lo, hi = (100, 400) if engine != "tp" else (50, 2000)
+    steps = [s for s in steps if lo <= len(s) <= hi]
     if not steps:
         print(f"{engine}: no steps found")
         return
