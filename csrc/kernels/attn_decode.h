@@ -18,13 +18,14 @@ __device__ __forceinline__ float16v mfma32d(const bf16x8& a, const bf16x8& b, co
 // The V tiles are dead once the key loop ends, so the merge buffer aliases them:
 // 51 KB (D = 128) instead of 92 KB lets three workgroups share a CU, so a
 // 512-workgroup grid is resident in one round instead of two.
-template <int D>
+// NW waves per workgroup (4; 8 for the single-pass form, see attn_decode.hip)
+template <int D, int NW = DEC_WAVES>
 struct DecSmem {
   union {
-    bf16_t v[DEC_WAVES][DEC_TILE][D + 32];        // per-wave V tile (padded rows)
-    float o[DEC_WAVES - 1][D / 32][16][64];        // O^T partials of waves 1..3
+    bf16_t v[NW][DEC_TILE][D + 32];               // per-wave V tile (padded rows)
+    float o[NW - 1][D / 32][16][64];               // O^T partials of waves 1..NW-1
   };
-  float ml[DEC_WAVES][2][64];                      // (m, l) per wave per lane
+  float ml[NW][2][64];                             // (m, l) per wave per lane
 };
 
 // K/V source: paged caches [nb, Hkv, blk, D] via block_tables, or (block_tables
@@ -41,6 +42,7 @@ struct AttnDecArgs {
   // one K (= V) cache, for the write-through-coherent buffer loads
   long long q_bytes, kv_bytes;
   int prio;      // wave issue priority of the launch (loqa_set_launch_prio), 0 = default
+  long long o_bytes;   // bytes of out (OSC1 write-through stores)
 };
 
 // Launch priority of the calling host thread: kernels launched (or captured)
@@ -67,9 +69,21 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* base, size_t elem, long long
 // One workgroup's work item (split, kv head, sequence) - the body of the
 // standalone kernel, whose grid is (splits, kv heads, sequences); 256
 // threads, 4 waves.
-template <int D, int PF, int LOOP = 0, int SC1 = 0>
+// output store: plain, or write-through (OSC1: the attention runs as a
+// prologue item of the GEMM that consumes its output in the same launch)
+template <int OSC1>
+__device__ __forceinline__ void st_attn_out(bf16_t* base, long long nbytes, size_t elem, uint2 v) {
+  if constexpr (OSC1) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2_{v.x, v.y}, r, (unsigned)(elem * 2), 0, 16);
+  } else {
+    *reinterpret_cast<uint2*>(base + elem) = v;
+  }
+}
+
+template <int D, int PF, int LOOP = 0, int SC1 = 0, int NW = DEC_WAVES, int OSC1 = 0>
 __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int split, const int kvh,
-                                                 const int b, DecSmem<D>& sm) {
+                                                 const int b, DecSmem<D, NW>& sm) {
   const bf16_t* __restrict__ q = A.q;
   const long long q_stride = A.q_stride;
   const bf16_t* __restrict__ kc = A.kc;
@@ -155,7 +169,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
       bi0 = kt / blk;
       base0 = nbt0;
       base1 = (blk < DEC_TILE && bi0 + 1 < max_blocks) ? nbt1 : base0;
-      const int bn = min((kt + DEC_WAVES * DEC_TILE) / blk, max_blocks - 1);
+      const int bn = min((kt + NW * DEC_TILE) / blk, max_blocks - 1);
       nbt0 = bt[bn];
       nbt1 = bt[min(bn + 1, max_blocks - 1)];
     }
@@ -252,7 +266,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
     __builtin_amdgcn_wave_barrier();
   };
 
-  constexpr int STEP = DEC_WAVES * DEC_TILE;
+  constexpr int STEP = NW * DEC_TILE;
   int kt = kbeg + wave * DEC_TILE;
   if constexpr (PF) {
     // ping-pong: the next tile's K / V are requested before this tile is
@@ -304,7 +318,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
   if (wave == 0) {
     float mstar = m_run;
 #pragma unroll
-    for (int w = 1; w < DEC_WAVES; ++w) mstar = fmaxf(mstar, sm.ml[w][0][lane]);
+    for (int w = 1; w < NW; ++w) mstar = fmaxf(mstar, sm.ml[w][0][lane]);
     const float s0 = exp2f(m_run - mstar);
     float l = l_run * s0;
 #pragma unroll
@@ -312,7 +326,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[dt][j] *= s0;
 #pragma unroll
-    for (int w = 1; w < DEC_WAVES; ++w) {
+    for (int w = 1; w < NW; ++w) {
       const float sw = exp2f(sm.ml[w][0][lane] - mstar);
       l += sm.ml[w][1][lane] * sw;
 #pragma unroll
@@ -323,7 +337,7 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
     const size_t tok = (size_t)(q0 + qi);
     if (nsplit == 1) {
       if (!row_valid) return;
-      bf16_t* orow = out + tok * (size_t)o_stride + (size_t)head * D;
+      const size_t orow = tok * (size_t)o_stride + (size_t)head * D;
       const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
@@ -331,7 +345,8 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
         for (int g4 = 0; g4 < 4; ++g4) {
           float f[4] = {acc[dt][4 * g4] * inv, acc[dt][4 * g4 + 1] * inv, acc[dt][4 * g4 + 2] * inv,
                         acc[dt][4 * g4 + 3] * inv};
-          *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * h) = make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+          st_attn_out<OSC1>(out, A.o_bytes, orow + 32 * dt + 8 * g4 + 4 * h,
+                            make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3])));
         }
       return;
     }
@@ -441,12 +456,12 @@ __device__ __forceinline__ void attn_decode_body(const AttnDecArgs& A, const int
       }
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    bf16_t* orow = out + tokr * (size_t)o_stride + (size_t)hr * D + c0;
+    const size_t orow = tokr * (size_t)o_stride + (size_t)hr * D + c0;
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      *reinterpret_cast<uint2*>(orow + 4 * k) =
-          make_uint2(pack_bf16x2(o[4 * k] * inv, o[4 * k + 1] * inv),
-                     pack_bf16x2(o[4 * k + 2] * inv, o[4 * k + 3] * inv));
+      st_attn_out<OSC1>(out, A.o_bytes, orow + 4 * k,
+                        make_uint2(pack_bf16x2(o[4 * k] * inv, o[4 * k + 1] * inv),
+                                   pack_bf16x2(o[4 * k + 2] * inv, o[4 * k + 3] * inv)));
   }
 }
 

@@ -29,12 +29,21 @@ thread_local int g_loqa_launch_prio = 0;
 
 extern "C" void loqa_set_launch_prio(int prio) { g_loqa_launch_prio = prio; }
 
-template <int D, int PF>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(AttnDecArgs a) {
+template <int D, int PF, int NW = DEC_WAVES, int OCC = 2>
+__global__ __launch_bounds__(NW * 64, OCC) void attn_decode_kernel(AttnDecArgs a) {
   if (a.prio) __builtin_amdgcn_s_setprio(3);     // kernel argument: wave-uniform
-  __shared__ __attribute__((aligned(16))) DecSmem<D> sm;
-  attn_decode_body<D, PF>(a, blockIdx.x, blockIdx.y, blockIdx.z, sm);
+  __shared__ __attribute__((aligned(16))) DecSmem<D, NW> sm;
+  attn_decode_body<D, PF, 0, 0, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z, sm);
 }
+
+// Single-pass form (waves = 8): a workgroup of 8 waves covers 256 keys per
+// pass and, for the short contexts of an intent parse (<= 512 keys), the
+// whole context in ONE split - no partial publish, ticket or last-arriver
+// merge (the split combine's three dependent memory round trips), the 8
+// waves' states merged through LDS only. With PF the second tile of a wave
+// is requested before the first is consumed. For a tensor-parallel rank
+// (one kv head per rank: 8 sequences -> 8 workgroups) the combine was the
+// larger part of the kernel.
 
 // q: [Tq, >=Hq*D] bf16; K/V paged caches [nb, Hkv, blk, D] (block_tables) or
 // contiguous rows (kv_stride, kv_start); out [Tq, Hq*D] bf16.
@@ -46,7 +55,7 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
                                 const int* block_tables, int max_blocks, int blk, int B, int max_q,
                                 int Hq, int Hkv, int D, float scale, int causal, int split_keys,
                                 int num_splits, float* part_o, float* part_ml, int total_q,
-                                int* counters, hipStream_t s) {
+                                int* counters, int waves, int pf, hipStream_t s) {
   if (B <= 0 || total_q <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv || (Hq / Hkv) * max_q > 32 || split_keys % DEC_TILE || num_splits < 1 ||
       (D != 64 && D != 128) || !part_o || !part_ml || !counters)
@@ -58,7 +67,24 @@ extern "C" int loqa_attn_decode(const void* q, long long q_stride, const void* k
   const AttnDecArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, kv_stride,
                       kv_start, cu_q, ctx_lens, block_tables, max_blocks, blk, Hq, Hkv, sl2, causal,
                       split_keys, num_splits, part_o, part_ml, total_q, counters, (bf16_t*)o,
-                      o_stride, 0, 0, g_loqa_launch_prio};
+                      o_stride, 0, 0, g_loqa_launch_prio, 0};
+  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
+  if (waves == 8) {   // 512 threads: 2 waves per SIMD, 256 registers each (no PF at D = 128)
+    if (D == 128)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 0, 8, 1>), grid, dim3(512), 0, s, a);
+    else if (pf)
+      hipLaunchKernelGGL((attn_decode_kernel<64, 1, 8, 1>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_decode_kernel<64, 0, 8, 1>), grid, dim3(512), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  if (pf) {           // 4 waves, one per SIMD: the whole register file for the prefetch
+    if (D == 128)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 1, 4, 1>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_decode_kernel<64, 1, 4, 1>), grid, dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
   if (D == 128)
     hipLaunchKernelGGL((attn_decode_kernel<128, 0>), grid, dim3(256), 0, s, a);
   else

@@ -16,6 +16,8 @@
 //     go to f32 slabs part[S][Mpad][N] that the NEXT kernel sums in its prologue
 //     (slab_ops.hip) - deterministic, no atomics, no extra launch.
 #include "common.h"
+#include "attn_decode.h"
+#include "car_common.h"
 #include <stdlib.h>
 
 // launch priority of the calling host thread (attn_decode.hip)
@@ -39,6 +41,25 @@ __device__ __forceinline__ bf16x8 ldx(const bf16_t* p) {
   return *reinterpret_cast<bf16x8*>(&v);
 }
 
+// Source of the activation fragments: plain loads, or (XS = 1) sc1 buffer
+// loads - x was stored write-through by a prologue item of the SAME launch
+// (guide §6 Guideline 16: every handed-off byte read with sc1, no acquire)
+struct XSrc {
+  const bf16_t* x0;                 // x base (offsets are taken from it)
+  __amdgpu_buffer_rsrc_t r;
+};
+
+template <int XS>
+__device__ __forceinline__ bf16x8 ldx_s(const bf16_t* p, const XSrc& xs) {
+  if constexpr (XS) {
+    const u32x4 v = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(xs.r, (unsigned)((p - xs.x0) * 2), 0, 16));
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    return ldx(p);
+  }
+}
+
 // workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
 // for its outstanding global loads (__syncthreads' release fence would drain
 // the weight prefetch)
@@ -55,16 +76,28 @@ struct Frag {
 };
 
 template <int RT, int MT, int U>
-__device__ __forceinline__ void load_frag(Frag<RT, MT, U>& f, const bf16_t* wp, size_t tile_stride,
-                                          const bf16_t* xp, long long ldx_, int ks) {
+__device__ __forceinline__ void load_frag_w(Frag<RT, MT, U>& f, const bf16_t* wp, size_t tile_stride, int ks) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int i = 0; i < RT; ++i) f.a[u][i] = ldw(wp + (size_t)i * tile_stride + (size_t)(ks + u) * 512);
+}
+
+template <int RT, int MT, int U, int XS = 0>
+__device__ __forceinline__ void load_frag_x(Frag<RT, MT, U>& f, const bf16_t* xp, long long ldx_, int ks,
+                                            const XSrc& xs) {
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int j = 0; j < MT; ++j) f.b[u][j] = ldx(xp + (size_t)j * 16 * ldx_ + (size_t)(ks + u) * 32);
+    for (int j = 0; j < MT; ++j) f.b[u][j] = ldx_s<XS>(xp + (size_t)j * 16 * ldx_ + (size_t)(ks + u) * 32, xs);
+}
+
+template <int RT, int MT, int U, int XS = 0>
+__device__ __forceinline__ void load_frag(Frag<RT, MT, U>& f, const bf16_t* wp, size_t tile_stride,
+                                          const bf16_t* xp, long long ldx_, int ks,
+                                          const XSrc& xs = XSrc{}) {
+  load_frag_w(f, wp, tile_stride, ks);
+  load_frag_x<RT, MT, U, XS>(f, xp, ldx_, ks, xs);
 }
 
 template <int RT, int MT, int U>
@@ -84,28 +117,28 @@ __device__ __forceinline__ void mma_frag(const Frag<RT, MT, U>& f, float4v_ (&ac
 // consumer block a join point of the refill / no-refill paths, and hipcc's
 // waitcnt pass then takes the stricter count of the two (vmcnt(0)) - every
 // iteration drained the prefetch and only ONE group was ever in flight.
-template <int RT, int MT, int U>
+template <int RT, int MT, int U, int XS = 0>
 __device__ __forceinline__ void stream_k(Frag<RT, MT, U>& f0, Frag<RT, MT, U>& f1,
                                          float4v_ (&acc)[RT][MT], const bf16_t* wp,
                                          size_t tile_stride, const bf16_t* xp, long long ldx_,
-                                         int ks0, int ng, int rot) {
+                                         int ks0, int ng, int rot, const XSrc& xs = XSrc{}) {
   auto ks = [&](int g) { int q = g + rot; q -= q >= ng ? ng : 0; return ks0 + q * U; };
   // sched_barrier(0) pins each phase: without it the machine scheduler sinks
   // the refill loads between the MFMAs to save registers, collapsing the
   // prefetch distance to 3-5 loads
   int g = 0;
   for (; g + 2 < ng; g += 2) {
-    load_frag(f1, wp, tile_stride, xp, ldx_, ks(g + 1));
+    load_frag<RT, MT, U, XS>(f1, wp, tile_stride, xp, ldx_, ks(g + 1), xs);
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f0, acc);
     __builtin_amdgcn_sched_barrier(0);
-    load_frag(f0, wp, tile_stride, xp, ldx_, ks(g + 2));
+    load_frag<RT, MT, U, XS>(f0, wp, tile_stride, xp, ldx_, ks(g + 2), xs);
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f1, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
   if (g + 1 < ng) {
-    load_frag(f1, wp, tile_stride, xp, ldx_, ks(g + 1));
+    load_frag<RT, MT, U, XS>(f1, wp, tile_stride, xp, ldx_, ks(g + 1), xs);
     __builtin_amdgcn_sched_barrier(0);
     mma_frag(f0, acc);
     mma_frag(f1, acc);
@@ -415,6 +448,15 @@ struct FusedParams {
   int rt;                 // output tile rows / 16 (1, 2; 4 at Mpad 64)
   int wr;                 // waves along the rows (1, or 4 with S == 1; any S with xl)
   int xl;                 // x through LDS (wr == 4; Mpad 32 / 64 / 128)
+  // prologue items (see PRO below): 0 none, 1 the residual all-reduce of the
+  // previous row-parallel GEMM (x = the residual it updates), 2 the decode
+  // attention whose output is x
+  int pro; int* pro_ctr; int pro_wgs;
+  void* car; int car_which, car_nblk;                // pro 1: all-reduce handle, input buffer, blocks
+  const void* att_q; long long att_q_stride; const void* att_kc; const void* att_vc;   // pro 2
+  const int* att_cu_q; const int* att_ctx; const int* att_bt; int att_max_blocks, att_blk;
+  int att_B, att_Hq, att_Hkv, att_split_keys, att_num_splits, att_total_q;
+  float att_scale; float* att_part_o; float* att_part_ml; int* att_counters;
 };
 
 struct FusedArgs {
@@ -427,7 +469,30 @@ struct FusedArgs {
   const int* positions; const float2* cs; bf16_t* q_out; bf16_t* kc; bf16_t* vc;
   const int* slots; int H, Hkv, D, blk;                                       // EPI_ROPE
   int prio;                                     // s_setprio 3 for the launch (attn_decode.h)
+  // PRO: [0, pro_items) tickets run items, the next pro_gx * S take tiles
+  int pro_items, pro_gx, pro_tiles; int* pro_ctr;
+  long long x_bytes, rs_bytes;                  // sc1 loads of x / the row statistics
+  CarPeers car_peers; long long car_in_off, car_res_off, car_st_off;   // PRO_CAR
+  int car_rank, car_world, car_nblk;
+  AttnDecArgs att; int att_ns;                  // PRO_ATT
 };
+
+enum { PRO_NONE = 0, PRO_CAR = 1, PRO_ATT = 2 };
+#define PRO_SPIN_LIMIT (1 << 24)
+
+// the tiles' wait for every prologue item of the launch (bounded spin; a
+// failed collective still counts its item, and the step's argmax turns the
+// sticky error word into error tokens)
+__device__ __forceinline__ void pro_gate(const FusedArgs& a) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(&a.pro_ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.pro_items) {
+      if (++spins > PRO_SPIN_LIMIT) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  lds_barrier();       // not __syncthreads: that would drain the weight prefetch
+}
 
 // WR: waves along the rows. WR = 1: the 4 waves split the tile's K range
 // (LDS reduce); WR = 4: every wave owns its own (16 * RT)-row tile over the
@@ -445,7 +510,7 @@ struct FusedSmem {
 
 // One (16 * RT * WR)-row output tile of the fused GEMM (a workgroup's whole
 // GEMM work; `return` = this workgroup's GEMM part is done)
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL>
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int PRO = 0>
 __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs, const int bx,
                                                   const int by) {
   constexpr int WK = 4 / WR;                     // waves along K
@@ -476,9 +541,19 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
   // (a k-start rotation per workgroup measured 5-10 % SLOWER on every shape:
   // the in-step x reuse across neighbouring workgroups in L2 matters more)
   const int rot = 0;
+  constexpr int XS = PRO != PRO_NONE;
+  XSrc xsrc{a.x, __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0,
+                                                    (int)(XS ? a.x_bytes : 0), 0x00020000)};
   if constexpr (XL) {
     load_xc<MT * 16, U>(xr, a.x, a.ldx, ks0);      // x first: storing it waits for x only
     load_w(w0, wp, tile_stride, ks0);
+  } else if constexpr (PRO != PRO_NONE) {
+    // the first weight group streams while the prologue items (the residual
+    // all-reduce, or the attention producing x) finish; x and the row
+    // statistics only after them, with sc1 loads
+    load_frag_w(f0, wp, tile_stride, ks0 + rot * U);
+    pro_gate(a);
+    load_frag_x<RT, MT, (XL ? 1 : U), 1>(f0, xp, a.ldx, ks0 + rot * U, xsrc);
   } else {
     load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + rot * U);
   }
@@ -572,7 +647,14 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
       for (int i = 0; i < 16; ++i) {
         const int t = base + g + i * G;
         const bool ok = t < a.rowstat_tiles;
-        vq[i] = ok ? a.rowsq_in[(size_t)t * Mp + m] : 0.f;
+        if constexpr (PRO != PRO_NONE)
+          vq[i] = ok ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                           __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.rowsq_in), 0,
+                                                             (int)a.rs_bytes, 0x00020000),
+                           (unsigned)(((size_t)t * Mp + m) * 4), 0, 16))
+                     : 0.f;
+        else
+          vq[i] = ok ? a.rowsq_in[(size_t)t * Mp + m] : 0.f;
         if constexpr (NORM == NORM_LN) vs[i] = ok ? a.rowsum_in[(size_t)t * Mp + m] : 0.f;
       }
 #pragma unroll
@@ -613,7 +695,7 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
     stream_k_xl(w0, w1, xr, acc, wp, tile_stride, a.x, a.ldx, xs, ks0, ng, lane);
     if constexpr (MODE == EPI_ROPE && !EARLY_EPI) load_rope_ops();
   } else {
-    stream_k(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, ng, rot);
+    stream_k<RT, MT, (XL ? 1 : U), XS>(f0, f1, acc, wp, tile_stride, xp, a.ldx, ks0, ng, rot, xsrc);
   }
 
   if constexpr (WK > 1) {
@@ -887,13 +969,67 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
   }
 }
 
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0>
+// PRO (prologue items): a launch whose input x is produced by a short
+// latency-bound step - the tensor-parallel residual all-reduce of the
+// previous row-parallel GEMM (PRO_CAR, x = the residual it updates, its
+// statistics tiles = this GEMM's norm prologue) or the decode attention
+// (PRO_ATT, x = its output) - runs that step INSIDE this launch: workgroups
+// draw tickets from a counter; the first pro_items tickets run the items
+// (all-reduce blocks / attention items, their results stored write-through),
+// later tickets take GEMM tiles, whose weight stream starts at once and which
+// wait for every item (pro_gate) before reading x with sc1 loads. The kernel
+// boundary and the GEMM's first-load latency disappear behind the step; a
+// tile never waits for work that is not already running (items are taken
+// first), so any grid size is deadlock-free on its own GPU. The last
+// workgroup out resets the counters (graph replays).
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int PRO = PRO_NONE>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   constexpr int NSM = FusedSmem<RT, MT, WR>::NSM;
-  __shared__ __attribute__((aligned(16))) float smem[NSM];
+  constexpr int ASM = PRO == PRO_ATT ? (int)(sizeof(DecSmem<128>) / 4) : 0;
+  constexpr int SMF = (NSM > ASM ? NSM : ASM) + 4;
+  __shared__ __attribute__((aligned(16))) float smem[SMF];
   __shared__ __attribute__((aligned(16))) bf16_t xs[XL ? U * MT * 16 * XROW : 8];
   if (a.prio) __builtin_amdgcn_s_setprio(3);     // kernel argument: wave-uniform
-  skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL>(a, smem, xs, blockIdx.x, blockIdx.y);
+  if constexpr (PRO == PRO_NONE) {
+    skinny_fused_tile<RT, MT, U, WR, MODE, NORM, XL>(a, smem, xs, blockIdx.x, blockIdx.y);
+  } else {
+    int* sflag = reinterpret_cast<int*>(smem) + (SMF - 1);
+    for (;;) {
+      __syncthreads();                            // smem / sflag of the previous item
+      if (threadIdx.x == 0)
+        sflag[0] = __hip_atomic_fetch_add(&a.pro_ctr[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int t = __builtin_amdgcn_readfirstlane(sflag[0]);
+      if (t < a.pro_items) {
+        if constexpr (PRO == PRO_CAR) {
+          car_resid_block<1, 1>(a.car_peers, a.car_in_off, a.car_res_off, a.car_st_off,
+                                const_cast<bf16_t*>(a.x), const_cast<float*>(a.rowsq_in), a.Mpad, a.K,
+                                a.car_rank, a.car_world, t, a.car_nblk);
+        } else {
+          const int split = t % a.att_ns, rest = t / a.att_ns;
+          attn_decode_body<128, 0, 1, 0, DEC_WAVES, 1>(a.att, split, rest % a.att.Hkv, rest / a.att.Hkv,
+                                                       *reinterpret_cast<DecSmem<128>*>(smem));
+        }
+        // the item's write-through stores are complete -> count it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+          __hip_atomic_fetch_add(&a.pro_ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      const int g = t - a.pro_items;
+      if (g < a.pro_tiles) {
+        skinny_fused_tile<RT, MT, U, WR, MODE, NORM, 0, PRO>(a, smem, xs, g % a.pro_gx, g / a.pro_gx);
+        continue;
+      }
+      // exit ticket: the last workgroup out leaves the counters zeroed
+      if (threadIdx.x == 0 && g - a.pro_tiles == (int)gridDim.x - 1) {
+        __hip_atomic_store(&a.pro_ctr[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.pro_ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
+  }
 }
 
 // Deep prefetch (LOQA_FUSED_DEEP bit mask, Mpad 16): bit 0 - a wave's whole k
@@ -928,6 +1064,13 @@ static int launch_fused(const FusedArgs& a, hipStream_t st) {
     // whose <= 256 workgroups hold one 4-wave group per CU - bytes in flight
     // per CU, not occupancy, bound them
     if ((g_fused_deep & 4) && kw % 8 == 0 && a.N <= 6144 && a.K <= 4096) {
+      hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 8, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    // bit 3 (value 8): any grid of at most one workgroup per CU (a tensor-
+    // parallel rank's shard GEMMs: 80-256 workgroups, nothing beside them) -
+    // twice the bytes in flight per CU
+    if ((g_fused_deep & 8) && kw % 8 == 0 && (long long)grid.x * grid.y <= 256) {
       hipLaunchKernelGGL((skinny_fused_kernel<RT, 1, 8, WR, MODE, NORM>), grid, dim3(256), 0, st, a);
       return (int)hipGetLastError();
     }
@@ -1015,6 +1158,85 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
   }
 }
 
+// prologue-item launches (PRO_CAR / PRO_ATT): WR 1, no XL, Mpad 16 / 32,
+// 4-step prefetch groups; a 1-D grid of at most ``wgs`` workgroups that draw
+// items and tiles from the ticket counter
+template <int RT, int MT, int MODE, int NORM, int PRO>
+static int launch_pro(const FusedArgs& a, int wgs, hipStream_t st) {
+  hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 4, 1, MODE, NORM, 0, PRO>), dim3(wgs), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, int NORM, int PRO>
+static int dispatch_pro(const FusedArgs& a, int rt, int wgs, hipStream_t st) {
+  if (a.Mpad == 16) return rt == 1 ? launch_pro<1, 1, MODE, NORM, PRO>(a, wgs, st)
+                                   : launch_pro<2, 1, MODE, NORM, PRO>(a, wgs, st);
+  return rt == 1 ? launch_pro<1, 2, MODE, NORM, PRO>(a, wgs, st) : launch_pro<2, 2, MODE, NORM, PRO>(a, wgs, st);
+}
+
+static int fused_prologue(const FusedParams* p, FusedArgs& a, hipStream_t st) {
+  const int Mpad = p->Mpad, N = p->N, K = p->K, S = p->S;
+  if (p->xl || p->wr != 1 || (Mpad != 16 && Mpad != 32) || (p->rt != 1 && p->rt != 2) ||
+      (K / 32 / (S * 4)) % 4 || !p->pro_ctr)
+    return (int)hipErrorInvalidValue;
+  static int ncu = 0;
+  if (ncu <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return (int)hipErrorInvalidValue;
+  }
+  a.pro_ctr = p->pro_ctr;
+  a.pro_gx = N / (16 * p->rt);
+  a.pro_tiles = a.pro_gx * S;
+  a.x_bytes = (long long)Mpad * p->ldx * 2;
+  a.rs_bytes = (long long)(p->rowstat_tiles > 0 ? p->rowstat_tiles : 1) * Mpad * 4;
+  if (p->pro == PRO_CAR) {
+    // x = the residual [Mpad, d = K] the all-reduce updates; its statistics
+    // tiles (world x nblk) are this GEMM's norm input
+    if ((p->mode != EPI_SILU && p->mode != EPI_ROPE) || p->norm != NORM_RMS || !p->car || p->car_nblk < 1 ||
+        p->car_nblk > CAR_MAX_BLOCKS || p->ldx != K)
+      return (int)hipErrorInvalidValue;
+    size_t in_bytes = 0;
+    const int rc = car_prologue_args(p->car, p->car_which, &a.car_peers, &a.car_in_off, &a.car_res_off,
+                                     &a.car_st_off, &a.car_rank, &a.car_world, &in_bytes);
+    if (rc) return rc;
+    const int cw = K / a.car_world / p->car_nblk, vpr = cw / 4;
+    if (K % (a.car_world * p->car_nblk) || cw % 8 || vpr > 64 || (vpr & (vpr - 1)) ||
+        (size_t)Mpad * K * 4 > in_bytes || p->rowstat_tiles != a.car_world * p->car_nblk)
+      return (int)hipErrorInvalidValue;
+    a.car_nblk = p->car_nblk;
+    a.pro_items = p->car_nblk;
+  } else if (p->pro == PRO_ATT) {
+    // x = the attention output [Mpad, Hq * 128] (row stride ldx)
+    if ((p->mode != EPI_ACT && p->mode != EPI_RESID) || p->norm != NORM_NONE || !p->att_q || !p->att_kc ||
+        !p->att_vc || !p->att_cu_q || !p->att_ctx || !p->att_bt || !p->att_part_o || !p->att_part_ml ||
+        !p->att_counters || p->att_Hkv < 1 || p->att_Hq % p->att_Hkv || p->att_Hq * 128 != K ||
+        p->att_blk < 16 || (p->att_blk & (p->att_blk - 1)) || p->att_split_keys % DEC_TILE ||
+        p->att_num_splits < 1 || p->att_B < 1 || p->att_total_q > Mpad)
+      return (int)hipErrorInvalidValue;
+    a.att = AttnDecArgs{(const bf16_t*)p->att_q, p->att_q_stride, (const bf16_t*)p->att_kc,
+                        (const bf16_t*)p->att_vc, 0, nullptr, p->att_cu_q, p->att_ctx, p->att_bt,
+                        p->att_max_blocks, p->att_blk, p->att_Hq, p->att_Hkv,
+                        p->att_scale * 1.4426950408889634f, 1, p->att_split_keys, p->att_num_splits,
+                        p->att_part_o, p->att_part_ml, p->att_total_q, p->att_counters,
+                        const_cast<bf16_t*>(a.x), p->ldx, 0, 0, 0, a.x_bytes};
+    a.att_ns = p->att_num_splits;
+    a.pro_items = p->att_num_splits * p->att_Hkv * p->att_B;
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  const int cap = p->pro_wgs > 0 ? p->pro_wgs : ncu;
+  const int total = a.pro_items + a.pro_tiles;
+  const int wgs = total < cap ? total : cap;
+  if (p->pro == PRO_CAR) {
+    if (p->mode == EPI_SILU) return dispatch_pro<EPI_SILU, NORM_RMS, PRO_CAR>(a, p->rt, wgs, st);
+    return dispatch_pro<EPI_ROPE, NORM_RMS, PRO_CAR>(a, p->rt, wgs, st);
+  }
+  if (p->mode == EPI_ACT) return dispatch_pro<EPI_ACT, NORM_NONE, PRO_ATT>(a, p->rt, wgs, st);
+  return dispatch_pro<EPI_RESID, NORM_NONE, PRO_ATT>(a, p->rt, wgs, st);
+}
+
 // mode: 1 silu (out [Mpad, ldo >= N/2]), 2 residual (+bias) + row sum-of-squares
 // (+ row sums), 3 (RoPE if cs) + paged KV append + q, 4 act(bias + x W^T) -> out
 // (act 0 identity, 1 GELU-erf). norm: 1 RMSNorm / 2 LayerNorm of x (the bf16
@@ -1046,6 +1268,7 @@ extern "C" int loqa_skinny_fused(const FusedParams* p, hipStream_t st) {
               p->rowsum_out, p->positions, (const float2*)p->cs, (bf16_t*)p->q_out,
               (bf16_t*)p->kc, (bf16_t*)p->vc, p->slots, p->H, p->Hkv, p->D, p->blk};
   a.prio = g_loqa_launch_prio;
+  if (p->pro) return fused_prologue(p, a, st);
   switch (p->mode) {
     case EPI_SILU: return dispatch_norm<EPI_SILU>(a, p->norm, p->rt, p->wr, p->xl, st);
     case EPI_RESID: return dispatch_norm<EPI_RESID>(a, p->norm, p->rt, p->wr, p->xl, st);

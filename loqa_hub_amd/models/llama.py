@@ -257,13 +257,16 @@ class LlamaWeights:
         """Measure the split-K of each fused decode GEMM shape (layer-0 weights)."""
         P, D = self.decode_layers[0], self.cfg.head_dim
         pf = bool(getattr(self, "compact", False))
+        # TP ranks with prologue launches: qkv / o / gate|up tuned over the
+        # layouts those launches run (same order with or without them)
+        pc = self.tp.world > 1 and ops.TP_PROLOGUE
         ops.tune_fused(P["wqkv_f"], "rope", norm="rms", heads=(self.h, self.hkv, D),
-                       cos_sin=self.cos_sin, prefill=pf)
-        ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms", prefill=pf)
+                       cos_sin=self.cos_sin, prefill=pf, pro_compat=pc)
+        ops.tune_fused(P["w_gate_up_f"], "silu", norm="rms", prefill=pf, pro_compat=pc)
         # TP: the row-parallel projections emit bf16 partials ("act" epilogue)
         # that the all-reduce kernel adds to the residual stream
         mode = "resid" if self.tp.world == 1 else "act"
-        ops.tune_fused(P["wo"], mode, prefill=pf)
+        ops.tune_fused(P["wo"], mode, prefill=pf, pro_compat=pc)
         ops.tune_fused(P["w_down"], mode, prefill=pf)
 
     @classmethod
@@ -523,6 +526,11 @@ class LlamaModel:
         # and attention through skinny_fused(attn=)
         dec_attn = (H // Hkv) * meta.max_q <= 32 and attn_ws is not None
         ao = torch.empty(Mpad, H * D, dtype=torch.bfloat16, device=residual.device) if dec_attn else None
+        car = tp.car if tp.world > 1 else None
+        if (car is not None and dec_attn and ops.TP_PROLOGUE and Mpad in (16, 32)
+                and residual.is_cuda and D == 128):
+            return self._decode_fused_tp_prologue(meta, k_cache, v_cache, attn_ws, scratch, residual, q,
+                                                  ao, num_splits, split_keys, car)
         for li, L in enumerate(w.layers):
             P = w.decode_layers[li]
             if dec_attn:
@@ -562,6 +570,52 @@ class LlamaModel:
                 pd = tp.partial_out(1, Mpad, d, residual.device)
                 ops.skinny_fused(a, P["w_down"], "act", scratch, out=pd, act="f32")
                 tp.resid_epilogue(1, pd, residual, scratch)
+        if ops.FUSED_EMBED:
+            hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
+        else:
+            hf = ops.rmsnorm(residual.index_select(0, meta.logit_idx), w.final_norm, cfg.norm_eps)
+        return ops.skinny_gemm(hf, w.lm_head_p, 1,
+                               max_wgs=getattr(w, "max_wgs", ops.MAX_DECODE_WGS))[0][:, :w.v]
+
+    def _decode_fused_tp_prologue(self, meta, k_cache, v_cache, attn_ws, scratch, residual, q, ao,
+                                  num_splits, split_keys, car) -> torch.Tensor:
+        """The tensor-parallel decode step with every latency-bound step run as
+        the prologue of the GEMM that consumes it (ops.skinny_fused
+        ``prologue``; gemm_skinny.hip PRO): 4 launches per layer instead of 7 -
+        qkv (+ the previous layer's down all-reduce) -> o (+ the decode
+        attention) -> gate|up (+ the o all-reduce) -> down. Each GEMM's weight
+        stream starts while its prologue's flag exchanges and KV reads are in
+        flight; numerics are those of the 7-launch step (same arithmetic, same
+        order)."""
+        cfg, w, tp = self.cfg, self.w, self.w.tp
+        H, Hkv, D, d = w.h, w.hkv, cfg.head_dim, cfg.d_model
+        Mpad = meta.tokens.numel()
+        nb = car.resid_blocks(d)
+        pw = car.prologue_wgs(d)
+        att = dict(kind="attn", q=q, cu_q=meta.cu_q, ctx_lens=meta.ctx_lens,
+                   block_tables=meta.block_tables, n_heads=H, n_kv=Hkv, max_q=meta.max_q,
+                   split_keys=split_keys, num_splits=num_splits, workspace=attn_ws,
+                   max_k=meta.max_ctx, pro_wgs=pw)
+        for li in range(len(w.layers)):
+            P = w.decode_layers[li]
+            pro = None
+            if li > 0:        # the previous layer's down all-reduce -> this qkv
+                pro = dict(kind="car", car=car, which=1, nblk=nb, pro_wgs=pw)
+                scratch.stat_tiles = tp.world * nb
+            ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True, eps=cfg.norm_eps,
+                             positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
+                             k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
+                             n_heads=H, n_kv=Hkv, head_dim=D, prologue=pro)
+            po = tp.partial_out(0, Mpad, d, residual.device)
+            ops.skinny_fused(ao, P["wo"], "act", scratch, out=po, act="f32",
+                             prologue=dict(att, k_cache=k_cache[li], v_cache=v_cache[li]))
+            scratch.stat_tiles = tp.world * nb
+            a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
+                                 eps=cfg.norm_eps,
+                                 prologue=dict(kind="car", car=car, which=0, nblk=nb, pro_wgs=pw))
+            pd = tp.partial_out(1, Mpad, d, residual.device)
+            ops.skinny_fused(a, P["w_down"], "act", scratch, out=pd, act="f32")
+        tp.resid_epilogue(1, pd, residual, scratch)
         if ops.FUSED_EMBED:
             hf = ops.rmsnorm(residual, w.final_norm, cfg.norm_eps, row_idx=meta.logit_idx)
         else:

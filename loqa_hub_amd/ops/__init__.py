@@ -168,6 +168,14 @@ class AttnWorkspace:
         self.counters = torch.zeros(max_tokens * n_heads, dtype=torch.int32, device=device)
 
 
+# decode attention (attn_decode.hip): splits of at least this many keys run on
+# 8-wave workgroups (0: always 4 waves)
+ATTN8_MIN_KEYS = int(os.environ.get("LOQA_ATTN8_MIN_KEYS", "0"))
+# splits of at least this many keys (and more than one tile per wave) prefetch
+# a wave's next K / V tile (4 waves: one per SIMD; 0: never)
+ATTN_PF_MIN_KEYS = int(os.environ.get("LOQA_ATTN_PF_MIN_KEYS", "0"))
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Tensor, *,
               n_heads: int, n_kv: int, head_dim: int, causal: bool, max_q: int,
               cu_k: torch.Tensor | None = None, ctx_lens: torch.Tensor | None = None,
@@ -224,12 +232,16 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_q: torch.Ten
         assert workspace.max_tokens >= Tq and B * n_kv <= workspace.counters.numel()
         assert not paged or (blk >= 16 and blk & (blk - 1) == 0)
         kv_stride = 0 if paged else k.stride(0)
+        # a split of >= ATTN8_MIN_KEYS keys runs on 8 waves (256 keys per
+        # pass); with more than 256 keys a wave also prefetches its next tile
+        waves = 8 if (ATTN8_MIN_KEYS and split_keys >= ATTN8_MIN_KEYS) else 4
+        pf = int(split_keys > 32 * waves and ATTN_PF_MIN_KEYS and split_keys >= ATTN_PF_MIN_KEYS)
         check(kernels().loqa_attn_decode(
             ptr(q), q.stride(0), ptr(k), ptr(v), kv_stride, None if paged else ptr(cu_k),
             ptr(out), out.stride(0), ptr(cu_q), ptr(ctx_lens),
             ptr(block_tables) if paged else None, max_blocks, blk, B, max_q, n_heads, n_kv,
             head_dim, scale, int(causal), split_keys, num_splits, ptr(workspace.part_o),
-            ptr(workspace.part_ml), Tq, ptr(workspace.counters), stream_ptr(q)),
+            ptr(workspace.part_ml), Tq, ptr(workspace.counters), waves, pf, stream_ptr(q)),
             "attn_decode")
         return out
     if grouped:
@@ -533,7 +545,8 @@ class contended_tuning:
 
 
 def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies: int = 1,
-                      wr4: bool = False, fewest: bool = True, xl: str = "no") -> tuple:
+                      wr4: bool = False, fewest: bool = True, xl: str = "no",
+                      splits: list | None = None) -> tuple:
     """(split-K, tile rows / 16, waves along rows) for a fused-epilogue GEMM,
     measured: ``run(s, rt, wr, i)`` launches it on weight copy ``i`` (the graph
     cycles through ``ncopies`` copies so every call streams COLD weights, as a
@@ -554,7 +567,7 @@ def tune_fused_splits(key: tuple, run, K: int, reps: int = 8, rts=(2,), ncopies:
         return ov
     N = key[1]
     cands = [] if xl == "only" else \
-        [(s, rt, 1) for rt in rts for s in SPLIT_CANDIDATES if K % (s * 128) == 0]
+        [(s, rt, 1) for rt in rts for s in (splits or SPLIT_CANDIDATES) if K % (s * 128) == 0]
     if wr4 and xl != "only":
         cands += [(1, rt, 4) for rt in rts if N % (64 * rt) == 0]
     if xl != "no":
@@ -1039,6 +1052,9 @@ class FusedScratch:
         self.rowsq = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
         self.rowsum = torch.zeros(max_tiles * max_rows, dtype=torch.float32, device=device)
         self.stat_tiles = 0   # partial tiles written by the last residual epilogue
+        # ticket / item counters of the prologue-item launches (skinny_fused
+        # ``prologue``): zero between launches, each launch resets its own
+        self.pro_ctr = torch.zeros(2, dtype=torch.int32, device=device)
 
     def seed_stats(self, x: torch.Tensor, sums: bool = True) -> None:
         """Row statistics of ``x`` as ONE partial tile (layer 0's norm input)."""
@@ -1092,9 +1108,12 @@ class FusedLinear:
 
 def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = "none",
                heads: tuple | None = None, cos_sin=None, prefill: bool = False,
-               xl: bool = True) -> None:
+               xl: bool = True, pro_compat: bool = False) -> None:
     """Measure the split-K of one fused decode GEMM shape on dummy operands
     (``heads`` = (H, Hkv, D) for "rope"); before any graph capture.
+    ``pro_compat``: at Mpad 16 / 32 only the layouts a prologue launch runs
+    (4 waves along K, 4-step prefetch groups), so a tensor-parallel step with
+    and without prologues computes in the same order (bitwise equal).
     ``prefill``: Mpad 64 is the chunked prefill of compact weights (a whole
     weight pass per 64 tokens, on its own stream): 64-row tiles and 4 waves
     along rows are then candidates too (70B gate|up 64 tokens: 204 us vs 483 us
@@ -1150,9 +1169,11 @@ def tune_fused(wp, mode: str, *, mpads=(16, 32, 64, 128), norm=None, act: str = 
         # to 10.3 utt/s (long-lived 4-wave workgroups: the co-scheduling cliff,
         # docs/PERF.md)
         xl = "only" if Mpad == 128 else "no"
+        pc = pro_compat and Mpad in (16, 32)
         tune_fused_splits(key, lambda sp, rt, wr, i, xl_=0: skinny_fused(
             x, copies[i], mode, scr, splits=sp, rt=rt, wr=wr, norm=nrm, xl=xl_, **kw), K, rts=rts,
-            ncopies=len(copies), wr4=wide, fewest=wide, xl=xl)
+            ncopies=len(copies), wr4=wide and not pc, fewest=wide, xl=xl,
+            splits=[sp for sp in SPLIT_CANDIDATES if (K // 32 // (sp * 4)) % 4 == 0] if pc else None)
     del copies
 
 
@@ -1169,7 +1190,7 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
                  k_cache=None, v_cache=None, slots=None, n_heads: int = 0, n_kv: int = 0,
                  head_dim: int = 0, out=None, act: str = "none", bias=None, colsum=None,
                  row_sums: bool = False, wr: int | None = None, xl: int | None = None,
-                 attn: dict | None = None) -> torch.Tensor:
+                 attn: dict | None = None, prologue: dict | None = None) -> torch.Tensor:
     """Skinny GEMM with a fused epilogue and optional input norm; Mpad 16, 32,
     64 or 128 (``xl``: activations staged through LDS, 4 waves along rows,
     required at Mpad 128; chosen by the tuner at 64).
@@ -1191,7 +1212,19 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     split_keys, num_splits, workspace, max_k, scale, out) follows the GEMM and
     its output is returned (mode "act": attention over contiguous K / V rows,
     keys k, v, kv_start). Two launches: the one-launch hand-off was measured
-    slower in every configuration and removed (docs/PERF.md, round 5)."""
+    slower in every configuration and removed (docs/PERF.md, round 5).
+
+    ``prologue``: the short step that produces x runs INSIDE this launch
+    (gemm_skinny.hip PRO; the weight stream starts at once, the tiles read x
+    after every item is done). ``dict(kind="car", car=<CustomAllReduce>,
+    which=0|1, nblk=n)``: the tensor-parallel residual all-reduce of input
+    buffer ``which`` - x is the residual it updates in place, its world x nblk
+    statistics tiles are this GEMM's norm input (mode "silu" / "rope", RMSNorm).
+    ``dict(kind="attn", q=, k_cache=, v_cache=, cu_q=, ctx_lens=,
+    block_tables=, n_heads=, n_kv=, max_q=, split_keys=, num_splits=,
+    workspace=, scale=)``: paged causal decode attention whose output is x
+    (D = 128; mode "act" / "resid"). ``pro_wgs`` in the dict caps the grid
+    (the one-GPU multi-rank rehearsal)."""
     if attn is not None:
         assert mode in ("rope", "act")
         rope = mode == "rope"
@@ -1270,6 +1303,13 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
         assert residual.shape[0] >= Mpad and residual.shape[1] == N
     part = torch.empty(S, Mpad, N, dtype=torch.float32, device=x.device) if S > 1 else None
     blk = k_cache.shape[2] if k_cache is not None else 0
+    if prologue is not None and not (wr == 1 and not xl and Mpad in (16, 32) and rt in (1, 2)
+                                     and (K // 32 // (S * 4)) % 4 == 0):
+        # a layout the prologue launch form (4 waves along K, no XL, Mpad 16 /
+        # 32, 4-step prefetch groups) does not run: the prologue as its own
+        # kernel first - the same arithmetic, one more launch
+        _prologue_standalone(prologue, x, scratch)
+        prologue = None
     p = FusedParams()
     p.x, p.ldx, p.Wp, p.part, p.counters = ptr(x), x.stride(0), ptr(wp), ptr(part), \
         ptr(scratch.counters)
@@ -1286,6 +1326,8 @@ def skinny_fused(x: torch.Tensor, wp, mode: str, scratch: FusedScratch, *,
     p.kc, p.vc, p.slots = ptr(k_cache), ptr(v_cache), ptr(slots)
     p.H, p.Hkv, p.D, p.blk = n_heads, n_kv, head_dim, blk
     p.rt, p.wr, p.xl = rt, wr, int(bool(xl))
+    if prologue is not None:
+        _set_prologue(p, prologue, x, scratch, Mpad, K, rowsq_tiles)
     check(kernels().loqa_skinny_fused(ctypes.byref(p), stream_ptr(x)), "skinny_fused")
     if mode in ("silu", "act"):
         return out
@@ -1298,6 +1340,55 @@ def set_launch_priority(prio: int) -> None:
     default); the STT decoder thread sets it under ``LOQA_STT_WAVE_PRIO``."""
     if torch.cuda.is_available():
         kernels().loqa_set_launch_prio(int(prio))
+
+
+PRO_KINDS = {"car": 1, "attn": 2}
+
+
+def _prologue_standalone(pro: dict, x, scratch) -> None:
+    """The prologue of a skinny_fused launch as its own kernel (same numerics)."""
+    if pro["kind"] == "car":
+        pro["car"].resid(pro["which"], x, scratch.rowsq, pro["nblk"])
+        return
+    attention(pro["q"], pro["k_cache"], pro["v_cache"], pro["cu_q"], n_heads=pro["n_heads"],
+              n_kv=pro["n_kv"], head_dim=pro["k_cache"].shape[3], causal=True, max_q=pro["max_q"],
+              ctx_lens=pro["ctx_lens"], block_tables=pro["block_tables"], scale=pro.get("scale"),
+              grouped=True, split_keys=pro["split_keys"], num_splits=pro["num_splits"],
+              workspace=pro["workspace"], out=x, max_k=pro.get("max_k"))
+# tensor-parallel decode steps with the all-reduces / attention as GEMM
+# prologues (models/llama.py _decode_fused_tp_prologue; grid cap:
+# CustomAllReduce.prologue_wgs)
+TP_PROLOGUE = os.environ.get("LOQA_TP_PROLOGUE", "1") == "1"
+
+
+def _set_prologue(p, pro: dict, x, scratch, Mpad: int, K: int, rowsq_tiles: int) -> None:
+    kind = PRO_KINDS[pro["kind"]]
+    assert Mpad in (16, 32), "prologue launches: Mpad 16 / 32"
+    p.pro, p.pro_ctr, p.pro_wgs = kind, ptr(scratch.pro_ctr), int(pro.get("pro_wgs", 0))
+    if kind == 1:
+        car = pro["car"]
+        assert x.stride(0) == K and rowsq_tiles == car.world * pro["nblk"]
+        p.car, p.car_which, p.car_nblk = car._h, int(pro["which"]), int(pro["nblk"])
+        return
+    q, kc, vc, ws = pro["q"], pro["k_cache"], pro["v_cache"], pro["workspace"]
+    H, Hkv = pro["n_heads"], pro["n_kv"]
+    D = kc.shape[3]
+    B = pro["cu_q"].numel() - 1
+    assert D == 128 and H * D == K and (H // Hkv) * pro["max_q"] <= 32
+    assert pro["split_keys"] % 32 == 0 and ws.max_splits >= pro["num_splits"]
+    assert ws.max_tokens >= q.shape[0] and B * Hkv <= ws.counters.numel() and q.shape[0] <= Mpad
+    bt = pro["block_tables"]
+    assert kc.is_contiguous() and vc.is_contiguous() and bt.is_contiguous()
+    if pro.get("max_k") is not None:
+        assert pro["max_k"] <= bt.shape[1] * kc.shape[2], "context exceeds block table"
+    sc = pro.get("scale")
+    p.att_q, p.att_q_stride, p.att_kc, p.att_vc = ptr(q), q.stride(0), ptr(kc), ptr(vc)
+    p.att_cu_q, p.att_ctx, p.att_bt = ptr(pro["cu_q"]), ptr(pro["ctx_lens"]), ptr(bt)
+    p.att_max_blocks, p.att_blk = bt.shape[1], kc.shape[2]
+    p.att_B, p.att_Hq, p.att_Hkv = B, H, Hkv
+    p.att_split_keys, p.att_num_splits, p.att_total_q = pro["split_keys"], pro["num_splits"], q.shape[0]
+    p.att_scale = sc if sc is not None else 1.0 / math.sqrt(D)
+    p.att_part_o, p.att_part_ml, p.att_counters = ptr(ws.part_o), ptr(ws.part_ml), ptr(ws.counters)
 
 
 def _skinny_fused_ref(x, wp, mode, scratch, nrm, eps, rowsq_tiles, residual, positions,

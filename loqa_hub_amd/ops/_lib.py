@@ -40,6 +40,15 @@ class FusedParams(ctypes.Structure):
         ("vc", c_void_p), ("slots", c_void_p),
         ("H", c_int), ("Hkv", c_int), ("D", c_int), ("blk", c_int),
         ("rt", c_int), ("wr", c_int), ("xl", c_int),
+        ("pro", c_int), ("pro_ctr", c_void_p), ("pro_wgs", c_int),
+        ("car", c_void_p), ("car_which", c_int), ("car_nblk", c_int),
+        ("att_q", c_void_p), ("att_q_stride", c_ll), ("att_kc", c_void_p), ("att_vc", c_void_p),
+        ("att_cu_q", c_void_p), ("att_ctx", c_void_p), ("att_bt", c_void_p),
+        ("att_max_blocks", c_int), ("att_blk", c_int),
+        ("att_B", c_int), ("att_Hq", c_int), ("att_Hkv", c_int), ("att_split_keys", c_int),
+        ("att_num_splits", c_int), ("att_total_q", c_int),
+        ("att_scale", c_float), ("att_part_o", c_void_p), ("att_part_ml", c_void_p),
+        ("att_counters", c_void_p),
     ]
 
 
@@ -110,7 +119,7 @@ _KERNEL_SIGS = {
     "loqa_attn_decode": [c_void_p, c_ll, c_void_p, c_void_p, c_ll, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                         c_void_p],
+                         c_int, c_int, c_void_p],
     "loqa_slab_rmsnorm": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
                           c_void_p, c_int, c_float, c_void_p],
     "loqa_slab_rope_append": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

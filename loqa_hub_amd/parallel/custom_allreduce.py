@@ -28,6 +28,8 @@ Use as ``TPGroup(rank, world, group, allreduce=CustomAllReduce(group))``.
 from __future__ import annotations
 
 import ctypes
+import os
+import socket
 
 import torch
 import torch.distributed as dist
@@ -98,6 +100,15 @@ class CustomAllReduce:
             dist.all_gather_object(handles, bytes(buf.raw), group=group)
             blob = ctypes.create_string_buffer(b"".join(handles), hs * self.world)
             _lib.check(lib.loqa_car_open(self._h, blob), "hipIpcOpenMemHandle")
+        # ranks sharing ONE physical GPU (the multi-rank rehearsal on a one-GPU
+        # box): kernels that wait on peers must then leave CU slots for them
+        ident = (socket.gethostname(), os.environ.get("HIP_VISIBLE_DEVICES",
+                                                      os.environ.get("CUDA_VISIBLE_DEVICES", "")),
+                 torch.cuda.current_device())
+        idents = [ident] if solo else [None] * self.world
+        if not solo:
+            dist.all_gather_object(idents, ident, group=group)
+        self.shared_device = len(set(idents)) < len(idents)
         self.device = torch.device("cuda", torch.cuda.current_device())
         self.calls = 0
         self.fallbacks = 0
@@ -138,6 +149,18 @@ class CustomAllReduce:
         if not p:
             raise RuntimeError("custom all-reduce: no input buffers")
         return DeviceView(p, rows, cols, self.device)
+
+    def prologue_wgs(self, d: int) -> int:
+        """Grid cap of the decode GEMMs that run this all-reduce (or the
+        attention) as their prologue (ops.skinny_fused ``prologue``): 0 (no cap)
+        on GPUs of their own; with every rank on one GPU, the ranks' waiting
+        grids plus the standalone all-reduce blocks stay well under the 256
+        one-workgroup-per-CU slots, so a rank whose items wait on a peer never
+        holds the slots that peer needs."""
+        env = int(os.environ.get("LOQA_TP_PROLOGUE_WGS", "0"))
+        if env > 0 or not self.shared_device:
+            return env
+        return max(4, (192 - self.world * self.resid_blocks(d)) // self.world)
 
     def resid_blocks(self, d: int) -> int:
         """Workgroups per rank of ``resid``: each owns a sub-slice of 64

@@ -112,6 +112,8 @@ def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
         stt_name, llm_name, streams = "whisper-base", "tinyllama", 1
     else:
         stt_name, llm_name, streams = "whisper-large-v3", "llama3-70b", 8
+    if getattr(args, "streams", 0):
+        streams = args.streams
     t0 = time.perf_counter()
     stt = STTEngine(whisper_config(stt_name), dev, seed=0, max_batch=8)
     tp = tp_info.world if tp_info is not None else 1
@@ -126,7 +128,7 @@ def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
     pipe = VoicePipeline(stt, llm, nats, min_response_tokens=8, max_batch=8)
     pipe.warmup()
     tts = None
-    if cfg_id == 5:
+    if cfg_id == 5 and not getattr(args, "no_tts", False):
         from loqa_hub_amd.engine.tts_engine import VitsTTSEngine
         tts = VitsTTSEngine(vits_config("vits-ljs"), dev, seed=0)
     init_s = time.perf_counter() - t0
@@ -158,6 +160,11 @@ def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
         else round(st["e2e_marginal_ms_per_added_command"], 2),
         "ms_per_added_command_ref_equiv": st["ref_equiv_ms_per_added_command"],
         "llm_ms_per_decode_step": round((llm.stats["decode_s"] - s0["decode_s"]) / max(1, steps) * 1e3, 3),
+        # the added command's cost in decode steps of this run (marginal ms /
+        # ms per step): what a TP=8 projection multiplies its rank step by
+        "steps_per_added_command": (None if not st["e2e_marginal_ms_per_added_command"] or not steps
+                                    else round(st["e2e_marginal_ms_per_added_command"]
+                                               / ((llm.stats["decode_s"] - s0["decode_s"]) / steps * 1e3), 2)),
         "command_count_match": float(np.mean([j.n_commands == j.n_expected for j in jobs])),
         "init_s": round(init_s, 1),
         "fused_gemm_tuning": {f"{k[0]}:{k[1]}x{k[2]}:M{k[3]}": list(v) for k, v in ops._FSPLITS.items()},
@@ -325,6 +332,10 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--config", type=int, nargs="+", default=[2, 3])
     ap.add_argument("--per-stream", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="configs 2 / 5: closed-loop streams (0: the config's own, 1 / 8)")
+    ap.add_argument("--no-tts", action="store_true",
+                    help="config 5: no progressive VITS (the LLM's steps per added command alone)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1, help="config 5: tensor-parallel degree")
     ap.add_argument("--concurrency", type=int, default=8,

@@ -75,7 +75,8 @@ def main() -> int:
     meta = eng._build_meta(d, max_q, max_ctx, True)
 
     def step():
-        logits = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch)
+        logits = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch,
+                                                eng.attn_split_keys)
         return eng._tp_argmax(logits[: a.batch], d["mask_rows"])
 
     s = torch.cuda.Stream(dev)

@@ -185,12 +185,26 @@ def test_attention_prefill_paged_with_prefix(G, D):
     assert _rel(o, orf) < 2e-2
 
 
+# decode-attention kernel forms: (8-wave min keys, prefetch min keys) -> the
+# 4-wave kernel, the 8-wave single-pass one, and the prefetching variants
+ATTN_FORMS = {"w4": (0, 0), "w8": (256, 0), "w4pf": (0, 64), "w8pf": (256, 64)}
+
+
+@pytest.fixture(params=sorted(ATTN_FORMS))
+def attn_form(request, monkeypatch):
+    w8, pf = ATTN_FORMS[request.param]
+    monkeypatch.setattr(ops, "ATTN8_MIN_KEYS", w8)
+    monkeypatch.setattr(ops, "ATTN_PF_MIN_KEYS", pf)
+    return request.param
+
+
 @pytest.mark.parametrize("split_keys", [128, 256, 512])
 @pytest.mark.parametrize("qlens,G,splits", [([1, 1, 1, 1], 4, 4), ([3, 1, 7, 2], 4, 2),
                                             ([1, 1], 1, 1), ([16, 5], 8, 3)])
-def test_attention_grouped_paged(qlens, G, splits, split_keys):
+def test_attention_grouped_paged(qlens, G, splits, split_keys, attn_form):
     """Paged GQA decode attention; split_keys 128 / 256 / 512 run the 4- and
-    8-wave kernels (one pass, several passes, one split or several)."""
+    8-wave kernels (one pass, several passes, one split or several), with and
+    without the next-tile prefetch."""
     D, Hkv, blk = 128, 2, 16
     H = Hkv * G
     ctx = [700, 65, 300, 1][: len(qlens)]
@@ -218,7 +232,7 @@ def test_attention_grouped_paged(qlens, G, splits, split_keys):
 
 
 @pytest.mark.parametrize("split_keys", [128, 256, 512, 1536])
-def test_attention_grouped_cross_starts(split_keys):
+def test_attention_grouped_cross_starts(split_keys, attn_form):
     """Whisper cross-attention: subset of utterances addressed by start/len
     (4 / 8 / 16-wave workgroups, 12 / 6 / 3 / 1 splits)."""
     D, H, T = 64, 6, 1500

@@ -48,12 +48,42 @@ def test_pmc_summary_two_passes(tmp_path):
     assert out[0].split()[0] == "kernel" and out[0].split()[-1] == "calls"
     gemm, attn = out[1].split(), out[2].split()
     assert gemm[0] == "gemm" and attn[0] == "attn"
+    # columns: kernel grid MFMA% bf16TF LDScf us fetchx2 rdreq TB/s algo meas/algo label calls
     # MFMA busy: 2 x 6144 cycles over 10 us x 2.4 GHz x 1024 SIMDs = 0.05 %
-    assert abs(float(gemm[1]) - 100 * 12288 / (10e-6 * 2.4e9 * 1024)) < 0.05
-    assert float(gemm[3]) == 0.0 and gemm[-1] == "4"
-    # fetch: 2 x 25000 KiB in 10 us
-    assert abs(float(gemm[4]) - 50000 * 1024 / 10e-6 / 1e12) < 0.01
-    assert float(attn[3]) == 1.0 and attn[-1] == "1"      # 100 extra / 100 conflict-free cycles
+    assert abs(float(gemm[2]) - 100 * 12288 / (10e-6 * 2.4e9 * 1024)) < 0.05
+    assert float(gemm[4]) == 0.0 and gemm[-1] == "4"
+    # FETCH_SIZE reports half of a streaming read's bytes on gfx950: 2 x 2 x
+    # 25000 KiB per dispatch (two instances summed), doubled -> 204.8 MB in 10 us
+    assert abs(float(gemm[6]) - 4 * 25000 * 1024 / 1e6) < 0.01
+    assert abs(float(gemm[8]) - 4 * 25000 * 1024 / 10e-6 / 1e12) < 0.01
+    assert float(attn[4]) == 1.0 and attn[-1] == "1"      # 100 extra / 100 conflict-free cycles
+
+
+def test_pmc_summary_shapes_and_rdreq(tmp_path):
+    """Rows split by grid (one template, two shapes); TCC_EA0_RDREQ_sum x 128 B
+    is the measured read bytes when present; pmc_gemm.py shapes add the
+    algorithmic bytes and the ratio."""
+    import json
+    fields = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value",
+              "Start_Timestamp", "End_Timestamp"]
+    tpl = "void skinny_fused_kernel<2, 1, 4, 1, 2, 0, 0>(FusedArgs)"
+    rows = []
+    for d, (grid, req) in enumerate([(65536, 1e6), (65536, 1e6), (32768, 5e5)]):
+        rows.append(dict(Dispatch_Id=d, Kernel_Name=tpl, Grid_Size=grid, Counter_Name="TCC_EA0_RDREQ_sum",
+                         Counter_Value=req, Start_Timestamp=0, End_Timestamp=20000))
+    pa = tmp_path / "c_counter_collection.csv"
+    _write(pa, fields, rows)
+    shapes = [{"label": "down", "mode": "resid", "grid": 65536, "algorithmic_bytes": 128e6,
+               "layout": [2, 2, 1]}]
+    sp = tmp_path / "shapes.json"
+    sp.write_text(json.dumps(shapes))
+    out = _run("scripts/pmc_summary.py", "--shapes", str(sp), str(pa))
+    # the kernel name (with spaces) fills the first 60 columns
+    big, small = out[1][61:].split(), out[2][61:].split()
+    assert big[0] == "65536" and small[0] == "32768" and big[-1] == "2"
+    assert abs(float(big[6]) - 128.0) < 1e-6             # 1e6 requests x 128 B
+    assert big[10] == "down" and abs(float(big[9]) - 1.0) < 1e-6
+    assert small[10] == "-"
 
 
 def test_kernel_summary_top_n(tmp_path):

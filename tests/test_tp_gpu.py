@@ -372,3 +372,80 @@ def test_tp_decode_bitwise_equals_emulation(tmp_path, world):
             assert torch.equal(a, b[r]), (world, r, step, (a - b[r]).abs().max().item())
         for step, (a, b) in enumerate(zip(real["tokens"], emu["tokens"])):
             assert torch.equal(a.to(torch.int32), b.to(torch.int32)), (world, r, step, a, b)
+
+
+def _solo_tp_engine(n_layers=3, world=8):
+    """One TP rank of Llama-3-8B-shaped layers with one-rank collectives (the
+    config-5 projection's setup, scripts/config5_projection.py)."""
+    from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
+    from loqa_hub_amd.models.configs import llama_config
+    from loqa_hub_amd.models.llama import TPGroup
+    from loqa_hub_amd.parallel.custom_allreduce import CustomAllReduce
+    dev = torch.device("cuda", 0)
+    cfg = llama_config("llama3-8b", n_layers=n_layers)
+    tp = TPGroup(0, world, None, CustomAllReduce(solo=True))
+    eng = LLMEngine(cfg, dev, max_seqs=8, max_seq_len=512, tp=tp, use_graphs=False, seed=5)
+    reqs = []
+    for i, ctx in enumerate([300, 17, 129, 64]):
+        r = GenRequest(list(range(5 + i, 5 + i + ctx)), [])
+        r.seq_id = eng._next_id
+        eng._next_id += 1
+        eng.kv.pool.add_seq(r.seq_id, [])
+        eng._meta([r], [r.prompt], decode=False)
+        reqs.append(r)
+    return eng, reqs
+
+
+@pytest.mark.parametrize("Mpad,per", [(16, 2), (32, 3)])
+def test_tp_prologue_step_bitwise(Mpad, per):
+    """The TP decode step with the all-reduces and the attention run as GEMM
+    prologues (4 launches per layer, gemm_skinny.hip PRO) gives BITWISE the
+    logits of the 7-launch step, eagerly and replayed from a HIP graph (the
+    launches' ticket counters reset themselves)."""
+    import numpy as np
+
+    from loqa_hub_amd import ops
+    eng, reqs = _solo_tp_engine()
+    feeds = [[7 + j for j in range(per)] for _ in reqs]
+    max_q, max_ctx, host = eng._meta(reqs, feeds, True, len(reqs), Mpad)
+    host["mask_rows"] = np.zeros(len(reqs), np.int32)
+    d = eng._to_device(host)
+    meta = eng._build_meta(d, max_q, max_ctx, True)
+    k0, v0 = eng.kv.k.clone(), eng.kv.v.clone()
+
+    def step(pro: bool):
+        old = ops.TP_PROLOGUE
+        ops.TP_PROLOGUE = pro
+        try:
+            eng.kv.k.copy_(k0)
+            eng.kv.v.copy_(v0)
+            return eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws,
+                                                  eng.scratch, 128).float().clone()
+        finally:
+            ops.TP_PROLOGUE = old
+    ref_ = step(False)
+    got = step(True)
+    assert torch.equal(got, ref_), (got - ref_).abs().max().item()
+    assert int(eng.scratch.pro_ctr.abs().sum()) == 0
+    # graph capture + replays
+    old = ops.TP_PROLOGUE
+    ops.TP_PROLOGUE = True
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step(True)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        eng.kv.k.copy_(k0)
+        eng.kv.v.copy_(v0)
+        with torch.cuda.graph(g):
+            out = eng.model.forward_decode_fused(meta, eng.kv.k, eng.kv.v, eng.attn_ws, eng.scratch, 128)
+        for _ in range(3):
+            eng.kv.k.copy_(k0)
+            eng.kv.v.copy_(v0)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out.float(), ref_)
+    finally:
+        ops.TP_PROLOGUE = old
