@@ -483,15 +483,20 @@ enum { PRO_NONE = 0, PRO_CAR = 1, PRO_ATT = 2 };
 // the tiles' wait for every prologue item of the launch (bounded spin; a
 // failed collective still counts its item, and the step's argmax turns the
 // sticky error word into error tokens)
+template <int ACQ>
 __device__ __forceinline__ void pro_gate(const FusedArgs& a) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
     while (__hip_atomic_load(&a.pro_ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.pro_items) {
       if (++spins > PRO_SPIN_LIMIT) break;
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(8);   // ~0.2 us: a few hundred pollers share one line
     }
   }
   lds_barrier();       // not __syncthreads: that would drain the weight prefetch
+  // ACQ: an agent-scope acquire (invalidates this CU's L1 and the XCD's L2)
+  // instead of sc1 loads: x and the statistics are then read with plain,
+  // L2-cached loads (the items stored them write-through)
+  if constexpr (ACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // WR: waves along the rows. WR = 1: the 4 waves split the tile's K range
@@ -510,7 +515,7 @@ struct FusedSmem {
 
 // One (16 * RT * WR)-row output tile of the fused GEMM (a workgroup's whole
 // GEMM work; `return` = this workgroup's GEMM part is done)
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int PRO = 0>
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL, int PRO = 0, int ACQ = 0>
 __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* smem, bf16_t* xs, const int bx,
                                                   const int by) {
   constexpr int WK = 4 / WR;                     // waves along K
@@ -541,7 +546,7 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
   // (a k-start rotation per workgroup measured 5-10 % SLOWER on every shape:
   // the in-step x reuse across neighbouring workgroups in L2 matters more)
   const int rot = 0;
-  constexpr int XS = PRO != PRO_NONE;
+  constexpr int XS = PRO != PRO_NONE && !ACQ;
   XSrc xsrc{a.x, __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0,
                                                     (int)(XS ? a.x_bytes : 0), 0x00020000)};
   if constexpr (XL) {
@@ -552,8 +557,8 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
     // all-reduce, or the attention producing x) finish; x and the row
     // statistics only after them, with sc1 loads
     load_frag_w(f0, wp, tile_stride, ks0 + rot * U);
-    pro_gate(a);
-    load_frag_x<RT, MT, (XL ? 1 : U), 1>(f0, xp, a.ldx, ks0 + rot * U, xsrc);
+    pro_gate<ACQ>(a);
+    load_frag_x<RT, MT, (XL ? 1 : U), XS>(f0, xp, a.ldx, ks0 + rot * U, xsrc);
   } else {
     load_frag(f0, wp, tile_stride, xp, a.ldx, ks0 + rot * U);
   }
@@ -647,7 +652,7 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
       for (int i = 0; i < 16; ++i) {
         const int t = base + g + i * G;
         const bool ok = t < a.rowstat_tiles;
-        if constexpr (PRO != PRO_NONE)
+        if constexpr (XS)
           vq[i] = ok ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.rowsq_in), 0,
                                                              (int)a.rs_bytes, 0x00020000),
@@ -982,7 +987,7 @@ __device__ __forceinline__ void skinny_fused_tile(const FusedArgs& a, float* sme
 // tile never waits for work that is not already running (items are taken
 // first), so any grid size is deadlock-free on its own GPU. The last
 // workgroup out resets the counters (graph replays).
-template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int PRO = PRO_NONE>
+template <int RT, int MT, int U, int WR, int MODE, int NORM, int XL = 0, int PRO = PRO_NONE, int ACQ = 0>
 __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
   constexpr int NSM = FusedSmem<RT, MT, WR>::NSM;
   constexpr int ASM = PRO == PRO_ATT ? (int)(sizeof(DecSmem<128>) / 4) : 0;
@@ -1019,7 +1024,7 @@ __global__ __launch_bounds__(256) void skinny_fused_kernel(FusedArgs a) {
       }
       const int g = t - a.pro_items;
       if (g < a.pro_tiles) {
-        skinny_fused_tile<RT, MT, U, WR, MODE, NORM, 0, PRO>(a, smem, xs, g % a.pro_gx, g / a.pro_gx);
+        skinny_fused_tile<RT, MT, U, WR, MODE, NORM, 0, PRO, ACQ>(a, smem, xs, g % a.pro_gx, g / a.pro_gx);
         continue;
       }
       // exit ticket: the last workgroup out leaves the counters zeroed
@@ -1161,9 +1166,18 @@ static int dispatch_norm(const FusedArgs& a, int norm, int rt, int wr, int xl, h
 // prologue-item launches (PRO_CAR / PRO_ATT): WR 1, no XL, Mpad 16 / 32,
 // 4-step prefetch groups; a 1-D grid of at most ``wgs`` workgroups that draw
 // items and tiles from the ticket counter
+static int g_pro_acq = -1;   // LOQA_PRO_ACQ: 1 = acquire + plain loads, 0 = sc1 loads
+
 template <int RT, int MT, int MODE, int NORM, int PRO>
 static int launch_pro(const FusedArgs& a, int wgs, hipStream_t st) {
-  hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 4, 1, MODE, NORM, 0, PRO>), dim3(wgs), dim3(256), 0, st, a);
+  if (g_pro_acq < 0) {
+    const char* e = getenv("LOQA_PRO_ACQ");
+    g_pro_acq = e ? atoi(e) : 0;
+  }
+  if (g_pro_acq)
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 4, 1, MODE, NORM, 0, PRO, 1>), dim3(wgs), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((skinny_fused_kernel<RT, MT, 4, 1, MODE, NORM, 0, PRO, 0>), dim3(wgs), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -51,6 +51,7 @@ class PipelineJob:
     queue: ExecutionResult | None = None
     error: str = ""
     stt_failed: bool = False
+    llm_steps: int = 0                      # decode steps the intent parse sampled in
     t: dict = field(default_factory=dict)   # stage timestamps (perf_counter)
 
     @property
@@ -335,6 +336,7 @@ class VoicePipeline:
             tracer().record("llm", t_llm, time.monotonic(), request=j.request_id)
             j.t["llm_first"] = r.t_first
             j.t["llm_done"] = r.t_done
+            j.llm_steps = r.steps
             with tracer().span("parse", request=j.request_id):
                 self.parse(j, r)
             t = asyncio.ensure_future(self.execute(j))

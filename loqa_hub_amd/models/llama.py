@@ -102,7 +102,9 @@ class TPGroup:
         if self._allreduce is not None:
             nb = self._allreduce.resid_blocks(residual.shape[1])
             self._allreduce.resid(which, residual, scratch.rowsq, nb)
-            scratch.stat_tiles = self.world * nb
+            # tiles the kernel wrote: its world (a one-rank timing handle in
+            # scripts/config5_projection.py has world 1 under a TP-8 shard)
+            scratch.stat_tiles = self._allreduce.world * nb
             return
         import torch.distributed as dist
         p = partial.float()
@@ -601,7 +603,7 @@ class LlamaModel:
             pro = None
             if li > 0:        # the previous layer's down all-reduce -> this qkv
                 pro = dict(kind="car", car=car, which=1, nblk=nb, pro_wgs=pw)
-                scratch.stat_tiles = tp.world * nb
+                scratch.stat_tiles = car.world * nb
             ops.skinny_fused(residual, P["wqkv_f"], "rope", scratch, norm=True, eps=cfg.norm_eps,
                              positions=meta.positions, cos_sin=w.cos_sin, q_out=q,
                              k_cache=k_cache[li], v_cache=v_cache[li], slots=meta.slots,
@@ -609,7 +611,7 @@ class LlamaModel:
             po = tp.partial_out(0, Mpad, d, residual.device)
             ops.skinny_fused(ao, P["wo"], "act", scratch, out=po, act="f32",
                              prologue=dict(att, k_cache=k_cache[li], v_cache=v_cache[li]))
-            scratch.stat_tiles = tp.world * nb
+            scratch.stat_tiles = car.world * nb
             a = ops.skinny_fused(residual, P["w_gate_up_f"], "silu", scratch, norm=True,
                                  eps=cfg.norm_eps,
                                  prologue=dict(kind="car", car=car, which=0, nblk=nb, pro_wgs=pw))

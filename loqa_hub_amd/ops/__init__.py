@@ -1357,8 +1357,10 @@ def _prologue_standalone(pro: dict, x, scratch) -> None:
               workspace=pro["workspace"], out=x, max_k=pro.get("max_k"))
 # tensor-parallel decode steps with the all-reduces / attention as GEMM
 # prologues (models/llama.py _decode_fused_tp_prologue; grid cap:
-# CustomAllReduce.prologue_wgs)
-TP_PROLOGUE = os.environ.get("LOQA_TP_PROLOGUE", "1") == "1"
+# CustomAllReduce.prologue_wgs). Off by default: 328 instead of 567 launches
+# per config-5 rank step, bitwise the same logits, but 7.86 vs 6.87 ms per
+# step (profiles/r6_config5_prologue_ab.txt, docs/PERF.md round 6)
+TP_PROLOGUE = os.environ.get("LOQA_TP_PROLOGUE", "0") == "1"
 
 
 def _set_prologue(p, pro: dict, x, scratch, Mpad: int, K: int, rowsq_tiles: int) -> None:

@@ -107,6 +107,13 @@ def _progressive_loop(pipe, utts, streams: int, per_stream: int, tts):
     return jobs, wall, speech
 
 
+def _slope(xs, ys):
+    """Least-squares slope of ys over xs (None with < 2 distinct xs)."""
+    if len(set(xs)) < 2:
+        return None
+    return round(float(np.polyfit(np.asarray(xs, float), np.asarray(ys, float), 1)[0]), 3)
+
+
 def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
     if cfg_id == 2:
         stt_name, llm_name, streams = "whisper-base", "tinyllama", 1
@@ -160,6 +167,12 @@ def config_2_or_5(cfg_id: int, args, dev, nats, tp_info=None) -> dict:
         else round(st["e2e_marginal_ms_per_added_command"], 2),
         "ms_per_added_command_ref_equiv": st["ref_equiv_ms_per_added_command"],
         "llm_ms_per_decode_step": round((llm.stats["decode_s"] - s0["decode_s"]) / max(1, steps) * 1e3, 3),
+        # measured: the decode steps an utterance's parse sampled in, per added
+        # command (slope over the command counts) - the step count a TP=8
+        # projection multiplies its rank step by for a single stream
+        "decode_steps_per_added_command": _slope([j.n_commands for j in jobs],
+                                                 [j.llm_steps for j in jobs]),
+        "stt_ms_per_added_command": _slope([j.n_commands for j in jobs], stt_ms),
         # the added command's cost in decode steps of this run (marginal ms /
         # ms per step): what a TP=8 projection multiplies its rank step by
         "steps_per_added_command": (None if not st["e2e_marginal_ms_per_added_command"] or not steps

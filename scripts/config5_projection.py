@@ -43,8 +43,16 @@ def main() -> int:
                     help="effective GB/s per xGMI link (low,high) for the prompt pass's two-shot "
                          "all-reduces (7 links per GPU)")
     ap.add_argument("--steps-per-command", type=float, default=40.0,
-                    help="decode steps per added command (profiles/config5_tp1_r2.json: "
-                         "1035.73 ms / 25.884 ms per step = 40; config5_tp8_share_r3.json: 38)")
+                    help="decode steps per added command with 8 loaded streams (marginal ms / ms "
+                         "per step of the 70B TP=1 8-stream run: profiles/config5_tp1_r2.json "
+                         "1035.73 / 25.884 = 40; r5_config5_tp1.json 972.93 / 24.743 = 39.3)")
+    ap.add_argument("--steps-per-command-1stream", type=float, default=None,
+                    help="measured decode steps per added command of ONE stream (the reference's "
+                         "scenario: one multi-command utterance; scripts/bench_configs.py --config 5 "
+                         "--streams 1, decode_steps_per_added_command)")
+    ap.add_argument("--stt-ms-per-command-1stream", type=float, default=0.0,
+                    help="the STT phase's growth per added command of that run (a longer "
+                         "transcript; independent of the LLM's TP degree)")
     a = ap.parse_args()
     from loqa_hub_amd.engine.llm_engine import GenRequest, LLMEngine
     from loqa_hub_amd.models.configs import llama_config
@@ -120,6 +128,12 @@ def main() -> int:
     out["steps_per_added_command"] = spc
     out["projected_ms_per_added_command"] = [round(spc * v, 1) for v in out["projected_step_ms"]]
     out["reference_bar_ms_per_added_command"] = 200.0
+    if a.steps_per_command_1stream:
+        s1 = a.steps_per_command_1stream
+        out["steps_per_added_command_1stream"] = s1
+        out["stt_ms_per_added_command_1stream"] = a.stt_ms_per_command_1stream
+        out["projected_ms_per_added_command_1stream"] = [
+            round(s1 * v + a.stt_ms_per_command_1stream, 1) for v in out["projected_step_ms"]]
     if a.prefill_rows > 0 and "wqkv" in (w.layers[0] if w.layers else {}):
         # this rank's prompt pass (hand-written GEMMs on its shards; the
         # row-parallel partials' all-reduces are no-ops on the one-rank handle

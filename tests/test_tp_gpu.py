@@ -297,8 +297,9 @@ def _decode_teacher(meta_fn, fwd_fn, add_seq, steps: int = 10):
     return out
 
 
-def _bitwise_worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOQA_NO_TUNE="1")
+def _bitwise_worker(rank, world, port, out_dir, pro=0):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOQA_NO_TUNE="1",
+                      LOQA_TP_PROLOGUE=str(pro))
     if world >= 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -347,15 +348,17 @@ def _bitwise_worker(rank, world, port, out_dir):
     os._exit(0)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_tp_decode_bitwise_equals_emulation(tmp_path, world):
+@pytest.mark.parametrize("world,pro", [(2, 0), (4, 0), (8, 0), (8, 1)])
+def test_tp_decode_bitwise_equals_emulation(tmp_path, world, pro):
     """TP=W over the real IPC collectives (W processes sharing cuda:0) vs the
     single-process TP emulation of the same W shards (parallel/tp_emulation.py):
     every logit shard of every decode step and every combined greedy token is
-    BITWISE equal (replaces round 3's 2% / 90% tolerances)."""
+    BITWISE equal (replaces round 3's 2% / 90% tolerances). ``pro``: the step
+    with the all-reduces as prologue items of the consuming GEMMs, the ranks'
+    grids capped so they are resident together (CustomAllReduce.prologue_wgs)."""
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_bitwise_worker, args=(r, world, port, str(tmp_path)))
+    procs = [ctx.Process(target=_bitwise_worker, args=(r, world, port, str(tmp_path), pro))
              for r in range(world)]
     for p in procs:
         p.start()
