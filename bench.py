@@ -121,7 +121,8 @@ async def _start_hub(args, pipe, nats_port: int, info, texts: dict):
                     transcript_hints=hint)
     await srv._connect_nats()
     srv.processor = GPUVoiceProcessor(pipe, max_batch=pipe.max_batch,
-                                      bridge=build_bridge(srv.skills), batch_window=0.002)
+                                      bridge=None if os.environ.get("LOQA_BENCH_NO_BRIDGE") == "1"
+                                      else build_bridge(srv.skills), batch_window=0.002)
     await srv.start(host="127.0.0.1", http_port=0, grpc_port=0)
     return srv
 

@@ -471,6 +471,7 @@ struct FusedArgs {
   int prio;                                     // s_setprio 3 for the launch (attn_decode.h)
   // PRO: [0, pro_items) tickets run items, the next pro_gx * S take tiles
   int pro_items, pro_gx, pro_tiles; int* pro_ctr;
+  int pro_sleep0, pro_sleep;                    // gate poll back-off: 64 x, then 8 x s_sleep units
   long long x_bytes, rs_bytes;                  // sc1 loads of x / the row statistics
   CarPeers car_peers; long long car_in_off, car_res_off, car_st_off;   // PRO_CAR
   int car_rank, car_world, car_nblk;
@@ -486,10 +487,15 @@ enum { PRO_NONE = 0, PRO_CAR = 1, PRO_ATT = 2 };
 template <int ACQ>
 __device__ __forceinline__ void pro_gate(const FusedArgs& a) {
   if (threadIdx.x == 0) {
+    // back off first: a few hundred waiting workgroups polling one counter
+    // line at agent scope would queue the items' own atomics behind them
     unsigned spins = 0;
-    while (__hip_atomic_load(&a.pro_ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.pro_items) {
-      if (++spins > PRO_SPIN_LIMIT) break;
-      __builtin_amdgcn_s_sleep(8);   // ~0.2 us: a few hundred pollers share one line
+    if (__hip_atomic_load(&a.pro_ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.pro_items) {
+      for (int i = 0; i < a.pro_sleep0; ++i) __builtin_amdgcn_s_sleep(64);
+      while (__hip_atomic_load(&a.pro_ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.pro_items) {
+        if (++spins > PRO_SPIN_LIMIT) break;
+        for (int i = 0; i < a.pro_sleep; ++i) __builtin_amdgcn_s_sleep(8);
+      }
     }
   }
   lds_barrier();       // not __syncthreads: that would drain the weight prefetch
@@ -1201,6 +1207,15 @@ static int fused_prologue(const FusedParams* p, FusedArgs& a, hipStream_t st) {
       return (int)hipErrorInvalidValue;
   }
   a.pro_ctr = p->pro_ctr;
+  static int sl0 = -1, sl = -1;
+  if (sl0 < 0) {
+    const char* e0 = getenv("LOQA_PRO_SLEEP0");
+    const char* e1 = getenv("LOQA_PRO_SLEEP");
+    sl0 = e0 ? atoi(e0) : 2;      // ~3.4 us before the first re-poll
+    sl = e1 ? atoi(e1) : 4;       // ~0.9 us between polls
+  }
+  a.pro_sleep0 = sl0;
+  a.pro_sleep = sl < 1 ? 1 : sl;
   a.pro_gx = N / (16 * p->rt);
   a.pro_tiles = a.pro_gx * S;
   a.x_bytes = (long long)Mpad * p->ldx * 2;
