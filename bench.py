@@ -172,10 +172,12 @@ class CommandCounter:
         await self.client.close()
 
 
-def hub_summary(srv, recs: list, args) -> tuple[float | None, dict]:
+def hub_summary(srv, recs: list, args, events_before: int = 0) -> tuple[float | None, dict]:
     """Served-path statistics: the end-to-end marginal cost of an added command
     (slope of the relay-side latency over the parsed command count) and the
-    hub's own counters."""
+    hub's own counters. ``voice_events``: events stored during the timed steps
+    (``events_before`` = the count when they started: warm-up utterances are
+    stored too), one per timed utterance; ``voice_events_total`` all of them."""
     from loqa_hub_amd.storage.voice_events_store import ListOptions
     r = np.array(recs, dtype=np.float64).reshape(-1, 4)
     slope = (float(np.polyfit(r[:, 0], r[:, 3], 1)[0])
@@ -183,7 +185,9 @@ def hub_summary(srv, recs: list, args) -> tuple[float | None, dict]:
     st = srv.processor.stats
     gap = (round(1e3 * st["eos_enc_gap_s"] / st["eos_enc_n"], 3)
            if st.get("eos_enc_n") else None)
-    return slope, {"voice_events": srv.events.count(ListOptions()),
+    total = srv.events.count(ListOptions())
+    return slope, {"voice_events": total - events_before, "voice_events_total": total,
+                   "timed_utterances": len(r),
                    "end_of_speech_to_encoder_ms": gap,
                    "encode_span_ms": (round(1e3 * st["enc_span_s"] / st["eos_enc_n"], 3)
                                       if st.get("eos_enc_n") and "enc_span_s" in st else None),
@@ -275,12 +279,14 @@ def run_hub_dp(args) -> int:
             async with grpc.aio.insecure_channel(f"127.0.0.1:{srv.grpc_port}") as ch:
                 await asyncio.gather(*[client(ci, ch, n, record) for ci in range(N * B)])
         try:
+            from loqa_hub_amd.storage.voice_events_store import ListOptions
             await run(args.warmup, False)
+            ev0 = srv.events.count(ListOptions())
             t0 = time.perf_counter()
             await run(args.steps, True)
             elapsed = time.perf_counter() - t0
             recs = await counter.records(srv, hub_recs)
-            slope, hub_stats = hub_summary(srv, recs, args)
+            slope, hub_stats = hub_summary(srv, recs, args, ev0)
             hub_stats["dp"] = srv.processor.metrics()
             ps = srv.processor.stats
             if args.tts and ps.get("tts_phrases"):
@@ -573,7 +579,10 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     s0 = dict(llm.stats)
+    ev0 = 0
     if hub is not None:
+        from loqa_hub_amd.storage.voice_events_store import ListOptions
+        ev0 = hub.events.count(ListOptions())     # warm-up utterances' events
         hub.processor.job_sink = all_jobs         # per-phase timestamps of the timed utterances
     t0 = time.perf_counter()
     loop.run_until_complete(run(args.steps, True))
@@ -608,7 +617,7 @@ def main(argv=None) -> int:
     stats = added_command_stats(all_jobs)
     hub_stats = None
     if hub is not None:
-        stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub, recs_local, args)
+        stats["e2e_marginal_ms_per_added_command"], hub_stats = hub_summary(hub, recs_local, args, ev0)
     def _mean_ms(a, b):
         v = [j.t[b] - j.t[a] for j in all_jobs if a in j.t and b in j.t]
         return round(float(np.mean(v)) * 1e3, 2) if v else None

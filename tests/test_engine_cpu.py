@@ -312,14 +312,16 @@ def test_bench_cpu_smoke_hub_mode():
     """--mode hub: relays over gRPC into the served hub (arbitration, bridge,
     voice events) on the same pipeline."""
     out = _run([sys.executable, "bench.py", "--cpu-smoke", "--steps", "1",
-                "--warmup", "0", "--batch-per-gpu", "2", "--window-ms", "10",
+                "--warmup", "1", "--batch-per-gpu", "2", "--window-ms", "10",
                 "--window-steps", "1"])
     # hub mode + single-relay bypass are the defaults; the window_300ms pass
     # (bypass off) adds one utterance per relay after the timed step
     assert out["config"]["mode"] == "hub" and out["queue_success_rate"] == 1.0
-    assert out["hub"]["voice_events"] == 2 and out["hub"]["audio_service"]["processed"] == 2
-    svc = out["hub"]["audio_service"]
-    assert svc["bypassed"] == 2
+    # one voice event per timed utterance (the warm-up step's are counted apart)
+    hub = out["hub"]
+    assert hub["voice_events"] == 2 == hub["timed_utterances"] and hub["voice_events_total"] == 4
+    svc = hub["audio_service"]
+    assert svc["processed"] == 4 and svc["bypassed"] == 4
     w = out["window_300ms"]
     assert w["utterances"] == 2 and w["utterances_per_sec"] > 0 and w["window_ms"] == 10
 
