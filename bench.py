@@ -5,8 +5,9 @@ BASELINE.json metric: "ms per added command (multi-cmd utterance) + utterances/s
 at 1/2/4/8 MI355X"; config 4: 64 concurrent audio streams, Whisper-large-v3 +
 Llama-3-8B intent, DP=8 (8 streams per GPU -> weak scaling: per-GPU work fixed).
 
-One step = every rank processes its batch of B utterances end to end:
-  rank-0 router scatters the step's PCM16 over RCCL -> fused PCM convert/RMS ->
+One step = every rank processes B utterances end to end (--mode batch: the
+rank-0 router scatters the step's PCM16 over RCCL; the hub / closed modes
+draw each rank's utterances locally from the shared seed) -> fused PCM convert/RMS ->
   log-mel -> Whisper-large-v3 encoder + teacher-forced greedy decode ->
   wake-word strip -> ONE grammar-constrained Llama-3-8B multi-command decode
   (verbatim reference prompt, jump-forward JSON) -> command queue with rollback
@@ -523,7 +524,7 @@ def main(argv=None) -> int:
                                              args.warmup if record else 0)]
 
     async def run_closed(n: int, record: bool) -> None:
-        """--mode closed (default): B concurrent relay streams per GPU, each a
+        """--mode closed: B concurrent relay streams per GPU, each a
         closed loop (its next utterance is sent when the previous one's reply
         is back); n utterances per stream. Arrivals are micro-batched for STT
         and join the running LLM decode batch (continuous batching)."""
