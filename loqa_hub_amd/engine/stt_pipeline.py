@@ -44,8 +44,12 @@ class STTPipeline:
         self.eng = eng
         self.inflight: collections.deque[_Step] = collections.deque()
         self.stats = eng.stats
-        for k in ("pl_steps", "pl_spec", "pl_discard"):
+        for k in ("pl_steps", "pl_spec", "pl_discard", "pl_empty"):
             self.stats.setdefault(k, 0)
+        # host time of the launch path (metadata + graph replay) and of the
+        # replay call alone: where a step-to-step gap on the STT stream comes from
+        for k in ("pl_launch_s", "pl_replay_s"):
+            self.stats.setdefault(k, 0.0)
         assert eng.RES_SLOTS >= self.DEPTH + 1
 
     # -------------------------------------------------------------- helpers
@@ -84,8 +88,14 @@ class STTPipeline:
         done = []
         if len(self.inflight) >= self.DEPTH:
             done += self._retire(self.inflight.popleft())
-        if not self._launch(live) and self.inflight:
-            done += self._retire(self.inflight.popleft())
+        t0 = time.perf_counter()
+        launched = self._launch(live)
+        self.stats["pl_launch_s"] += time.perf_counter() - t0
+        if not launched:
+            if self.inflight:
+                done += self._retire(self.inflight.popleft())
+            else:
+                self.stats["pl_empty"] += 1     # nothing to launch and nothing in flight
         return done
 
     def drain(self) -> list:
@@ -144,7 +154,9 @@ class STTPipeline:
                 i += 1
         hb["row_slot"].fill(eng.max_batch)
         hb["row_slot"][:B] = [r.slot for r in rows]
+        t_r = time.perf_counter()
         rslot = eng._replay(g)
+        self.stats["pl_replay_s"] += time.perf_counter() - t_r
         ev = torch.cuda.Event()
         ev.record()
         entries = []
