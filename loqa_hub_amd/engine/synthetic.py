@@ -20,6 +20,12 @@ CLAUSES = [
 ]
 JOINERS = [" and ", " and then ", " then ", ", and ", " after that ", " also "]
 WAKE = ["hey loqa", "loqa", "hey loqa,"]
+# a long run (make_unique past ~300 one-command utterances per rank) draws from
+# a wider pool once the base one is nearly used up: more rooms and devices and
+# a closing word, same clause shapes
+EXTRA_DEVICES = ["heater", "speaker", "radio", "ceiling fan"]
+EXTRA_LOCATIONS = ["hallway", "dining room", "basement", "porch", "attic", "study"]
+CLOSERS = ["", " please", " now", " thanks", " right now"]
 
 
 @dataclass
@@ -31,15 +37,19 @@ class SyntheticUtterance:
     wake_pcm: np.ndarray
 
 
-def utterance_text(rng: np.random.Generator, n_commands: int) -> str:
+def utterance_text(rng: np.random.Generator, n_commands: int, wide: bool = False) -> str:
+    devs = DEVICES + EXTRA_DEVICES if wide else DEVICES
+    locs = LOCATIONS + EXTRA_LOCATIONS if wide else LOCATIONS
     parts = []
     for _ in range(n_commands):
         c = CLAUSES[rng.integers(len(CLAUSES))]
-        parts.append(c.format(loc=LOCATIONS[rng.integers(len(LOCATIONS))],
-                              dev=DEVICES[rng.integers(len(DEVICES))]))
+        parts.append(c.format(loc=locs[rng.integers(len(locs))],
+                              dev=devs[rng.integers(len(devs))]))
     s = parts[0]
     for p in parts[1:]:
         s += JOINERS[rng.integers(len(JOINERS))] + p
+    if wide:
+        s += CLOSERS[rng.integers(len(CLOSERS))]
     return WAKE[rng.integers(len(WAKE))] + " " + s
 
 
@@ -65,14 +75,19 @@ def to_pcm16(x: np.ndarray) -> np.ndarray:
 
 
 def make_utterance(seed: int, index: int, n_commands: int, relay_id: str | None = None,
-                   amp: float = 0.3) -> SyntheticUtterance:
+                   amp: float = 0.3, wide: bool = False) -> SyntheticUtterance:
     rng = np.random.default_rng(seed * 100003 + index)
-    text = utterance_text(rng, n_commands)
+    text = utterance_text(rng, n_commands, wide)
+    return _voice(rng, text, n_commands, relay_id or f"relay-{index}", amp)
+
+
+def _voice(rng: np.random.Generator, text: str, n_commands: int, relay_id: str,
+           amp: float = 0.3) -> SyntheticUtterance:
+    """The audio of ``text``, drawn from ``rng`` right after the text was."""
     words = text.split()
     wake = to_pcm16(speechlike(rng, 2, amp=amp))
     body = to_pcm16(speechlike(rng, max(1, len(words) - 2), amp=amp))
-    return SyntheticUtterance(relay_id or f"relay-{index}", text, n_commands,
-                              np.concatenate([wake, body]), wake)
+    return SyntheticUtterance(relay_id, text, n_commands, np.concatenate([wake, body]), wake)
 
 
 def make_batch(seed: int, n: int, commands_mix: list[int], offset: int = 0) -> list[SyntheticUtterance]:
@@ -86,18 +101,23 @@ def make_unique(seed: int, counts: list[int], offset: int = 0,
     ``seen``) share a transcript: every LLM prompt is then distinct, so the
     prefix cache can only reuse the template text before the transcript, as
     with real traffic (a cycled set of utterances would let whole prompts hit
-    the cache)."""
+    the cache). The base pool holds ~320 one-command transcripts; once draws
+    from it keep colliding, the utterance comes from the wider pool
+    (``utterance_text(wide=True)``), so a long run never runs out."""
     seen = set() if seen is None else seen
     out = []
     for i, nc in enumerate(counts):
-        for t in range(max_tries):
-            u = make_utterance(seed + 7919 * t, offset + i, nc)
-            if u.text not in seen:
+        for t in range(2 * max_tries):
+            # the text alone first (cheap); the audio only for the accepted draw,
+            # from the same generator (as make_utterance draws it)
+            rng = np.random.default_rng((seed + 7919 * t) * 100003 + offset + i)
+            text = utterance_text(rng, nc, wide=t >= max_tries)
+            if text not in seen:
                 break
         else:
             raise RuntimeError("could not draw a distinct utterance")
-        seen.add(u.text)
-        out.append(u)
+        seen.add(text)
+        out.append(_voice(rng, text, nc, f"relay-{offset + i}"))
     return out
 
 

@@ -219,3 +219,19 @@ def test_llm_chunked_prefill_matches_cpu(pipelined, monkeypatch):
     for a, b, n in zip(got, ref, (2, 1, 1, 3, 1, 4)):
         assert len(json.loads(a)["commands"]) == n
     assert got == ref
+
+
+def test_synthetic_unique_utterances_outlast_the_base_pool():
+    """A long bench run (hundreds of steps) draws more distinct one-command
+    transcripts than the base pool holds (~320): the wider pool takes over
+    instead of failing, every transcript stays distinct, and the early draws
+    are those of the base generator (make_utterance), audio included."""
+    import numpy as np
+
+    from loqa_hub_amd.engine.synthetic import make_unique, make_utterance
+    us = make_unique(3, [1] * 420)
+    texts = [u.text for u in us]
+    assert len(set(texts)) == 420
+    first = make_utterance(3, 0, 1)
+    assert us[0].text == first.text and np.array_equal(us[0].pcm, first.pcm)
+    assert all(u.n_commands == 1 and len(u.pcm) > len(u.wake_pcm) for u in us)
