@@ -78,7 +78,6 @@ def test_llm_pipelined_decode_gpu():
 def test_llm_gpu_matches_cpu_reference_first_tokens():
     cfg = llama_config("test-tiny")
     g = LLMEngine(cfg, "cuda", max_seqs=4, use_graphs=False)
-    from loqa_hub_amd.models.llama import LlamaWeights
     c = LLMEngine(cfg, "cpu", max_seqs=4)
     # same weights on both
     c.weights.__dict__.update({k: (v.cpu() if torch.is_tensor(v) else v)
